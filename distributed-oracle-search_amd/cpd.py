@@ -1,0 +1,384 @@
+"""Python mirror of the libcpd C ABI (include/cpd_api.h) over ctypes.
+
+Host-side glue for tests, bench.py and __graft_entry__: numpy arrays in, numpy
+arrays out, CPD_E_* codes raised as CpdError.  The compute path is libcpd.so
+(HIP kernels for gfx950); there is no Python or CPU fallback here — if the
+shared library is missing, importing this module raises.
+
+Reference interfaces mirrored (the reference has no FFI; these are the
+executables' contracts):
+  partition()          <- distribution_controller / gen_distribute_conf
+                          (process_query.py:46-53)
+  Graph.build_rows()   <- make_cpd_auto's per-node row loop (README.md:82-95)
+  Index.query()        <- fifo_auto --alg table-search (make_fifos.py:20-21)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcpd.so")
+
+CPD_OK = 0
+CPD_E_ARG = -1
+CPD_E_HIP = -2
+CPD_E_OOM = -3
+CPD_E_NOROW = -4
+CPD_E_RANGE = -5
+CPD_E_IO = -6
+PART_DIV = 0
+PART_MOD = 1
+INF = 0xFFFFFFFF
+FM_ALL = 0xFFFF
+
+EXPORTED = [
+    "cpd_last_error", "cpd_version", "cpd_partition", "cpd_partition_nbuckets",
+    "cpd_dfs_preorder", "cpd_synth_road_graph", "cpd_synth_congestion",
+    "cpd_plan_create", "cpd_plan_info_get", "cpd_plan_order", "cpd_plan_export_ch",
+    "cpd_plan_save", "cpd_plan_load", "cpd_plan_free", "cpd_device_count",
+    "cpd_graph_create", "cpd_graph_set_batch", "cpd_graph_get_batch", "cpd_graph_free",
+    "cpd_build_rows", "cpd_rows_count", "cpd_rows_export", "cpd_rows_free",
+    "cpd_debug_rows", "cpd_index_create", "cpd_index_from_rows", "cpd_index_set_weights",
+    "cpd_query_batch", "cpd_query_prepare", "cpd_query_run", "cpd_query_fetch",
+    "cpd_index_free", "cpd_timing_enable", "cpd_timing_reset", "cpd_timing_get",
+]
+
+
+class CpdError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libcpd error {code}: {msg}")
+        self.code = code
+
+
+class PlanOpts(C.Structure):
+    _fields_ = [("threads", C.c_int), ("witness_settle", C.c_uint32), ("verbose", C.c_int),
+                ("no_hierarchy", C.c_int)]
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("m", C.c_uint32), ("ch_up_arcs", C.c_uint64),
+                ("ch_dn_arcs", C.c_uint64), ("levels_up", C.c_uint32),
+                ("levels_dn", C.c_uint32), ("dist_bound", C.c_uint64),
+                ("ch_seconds", C.c_double)]
+
+
+class QueryStats(C.Structure):
+    _fields_ = [("queries", C.c_uint64), ("finished", C.c_uint64), ("hops", C.c_uint64),
+                ("cost", C.c_uint64), ("kernel_ms", C.c_double)]
+
+
+class KernelTime(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_uint64), ("ms", C.c_double),
+                ("bytes", C.c_double)]
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it first (make lib, or "
+                          "__graft_entry__.build()); there is no fallback")
+    lib = C.CDLL(LIB_PATH)
+    lib.cpd_last_error.restype = C.c_char_p
+    lib.cpd_version.restype = C.c_char_p
+    for name in EXPORTED:
+        if name not in ("cpd_last_error", "cpd_version"):
+            fn = getattr(lib, name)
+            if not name.endswith("_free"):
+                fn.restype = C.c_int
+            else:
+                fn.restype = None
+    return lib
+
+
+lib = _load()
+
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+u16p = C.POINTER(C.c_uint16)
+u8p = C.POINTER(C.c_uint8)
+i32p = C.POINTER(C.c_int32)
+
+
+def _check(rc: int) -> None:
+    if rc != CPD_OK:
+        raise CpdError(rc, lib.cpd_last_error().decode())
+
+
+def _ptr(a, ctype):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctype)
+
+
+def _u32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def version() -> str:
+    return lib.cpd_version().decode()
+
+
+# --------------------------------------------------------------------------
+# host utilities
+
+def partition(nodenum: int, maxworker: int, method: str, key: int, node: int):
+    """(wid, bid, bidx) of `node` — distribution_controller semantics [U]."""
+    wid, bid, bidx = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    m = PART_MOD if method == "mod" else PART_DIV if method == "div" else -1
+    _check(lib.cpd_partition(C.c_uint32(nodenum), C.c_uint32(maxworker), C.c_int(m),
+                             C.c_uint32(key), C.c_uint32(node), C.byref(wid), C.byref(bid),
+                             C.byref(bidx)))
+    return wid.value, bid.value, bidx.value
+
+
+def owned_nodes(nodenum: int, maxworker: int, method: str, key: int, wid: int) -> np.ndarray:
+    """All nodes assigned to worker `wid` (vectorised restatement of partition())."""
+    nodes = np.arange(nodenum, dtype=np.int64)
+    if method == "mod":
+        bid = nodes % key
+    elif method == "div":
+        chunk = -(-nodenum // key)
+        bid = nodes // chunk
+    else:
+        raise ValueError("partmethod must be div or mod")
+    return nodes[(bid % maxworker) == wid].astype(np.uint32)
+
+
+def dfs_preorder(row_ptr, dst) -> np.ndarray:
+    row_ptr, dst = _u32(row_ptr), _u32(dst)
+    n = len(row_ptr) - 1
+    order = np.empty(n, dtype=np.uint32)
+    _check(lib.cpd_dfs_preorder(C.c_uint32(n), _ptr(row_ptr, u32p), _ptr(dst, u32p),
+                                _ptr(order, u32p)))
+    return order
+
+
+class RoadGraph:
+    """CSR graph (node space, file edge order) + coordinates."""
+
+    def __init__(self, row_ptr, dst, w, x=None, y=None):
+        self.row_ptr, self.dst, self.w = _u32(row_ptr), _u32(dst), _u32(w)
+        self.x, self.y = x, y
+
+    @property
+    def n(self) -> int:
+        return len(self.row_ptr) - 1
+
+    @property
+    def m(self) -> int:
+        return len(self.dst)
+
+
+def synth_road_graph(width: int, height: int, seed: int, mean_outdeg: float = 2.5) -> RoadGraph:
+    n, m = C.c_uint32(), C.c_uint32()
+    _check(lib.cpd_synth_road_graph(width, height, C.c_double(mean_outdeg), C.c_uint64(seed),
+                                    C.byref(n), C.byref(m), None, None, None, None, None))
+    rp = np.empty(n.value + 1, np.uint32)
+    dst = np.empty(m.value, np.uint32)
+    w = np.empty(m.value, np.uint32)
+    x = np.empty(n.value, np.int32)
+    y = np.empty(n.value, np.int32)
+    _check(lib.cpd_synth_road_graph(width, height, C.c_double(mean_outdeg), C.c_uint64(seed),
+                                    C.byref(n), C.byref(m), _ptr(rp, u32p), _ptr(dst, u32p),
+                                    _ptr(w, u32p), _ptr(x, i32p), _ptr(y, i32p)))
+    return RoadGraph(rp, dst, w, x, y)
+
+
+def synth_congestion(w, frac=0.1, lo=1.0, hi=3.0, seed=3) -> np.ndarray:
+    w = _u32(w)
+    out = np.empty_like(w)
+    _check(lib.cpd_synth_congestion(C.c_uint32(len(w)), _ptr(w, u32p), C.c_double(frac),
+                                    C.c_double(lo), C.c_double(hi), C.c_uint64(seed),
+                                    _ptr(out, u32p)))
+    return out
+
+
+# --------------------------------------------------------------------------
+# plan (host preprocessing)
+
+class Plan:
+    def __init__(self, g: RoadGraph | None = None, threads: int = 0, settle: int = 0,
+                 verbose: bool = False, hierarchy: bool = True, _handle=None):
+        self._h = C.c_void_p()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            opts = PlanOpts(threads, settle, int(verbose), int(not hierarchy))
+            _check(lib.cpd_plan_create(_ptr(g.row_ptr, u32p), _ptr(g.dst, u32p),
+                                       _ptr(g.w, u32p), C.c_uint32(g.n), C.c_uint32(g.m),
+                                       C.byref(opts), C.byref(self._h)))
+
+    @classmethod
+    def load(cls, path: str) -> "Plan":
+        h = C.c_void_p()
+        _check(lib.cpd_plan_load(path.encode(), C.byref(h)))
+        return cls(_handle=h)
+
+    def save(self, path: str) -> None:
+        _check(lib.cpd_plan_save(self._h, path.encode()))
+
+    def info(self) -> dict:
+        i = PlanInfo()
+        _check(lib.cpd_plan_info_get(self._h, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in PlanInfo._fields_}
+
+    def order(self) -> np.ndarray:
+        o = np.empty(self.info()["n"], np.uint32)
+        _check(lib.cpd_plan_order(self._h, _ptr(o, u32p)))
+        return o
+
+    def export_ch(self) -> dict:
+        inf = self.info()
+        n, up, dn = inf["n"], inf["ch_up_arcs"], inf["ch_dn_arcs"]
+        out = {
+            "rank": np.empty(n, np.uint32),
+            "up_off": np.empty(n + 1, np.uint64), "up_dst": np.empty(up, np.uint32),
+            "up_w": np.empty(up, np.uint32),
+            "dn_off": np.empty(n + 1, np.uint64), "dn_dst": np.empty(dn, np.uint32),
+            "dn_w": np.empty(dn, np.uint32),
+            "level_up": np.empty(n, np.uint32), "level_dn": np.empty(n, np.uint32),
+        }
+        _check(lib.cpd_plan_export_ch(
+            self._h, _ptr(out["rank"], u32p), _ptr(out["up_off"], u64p),
+            _ptr(out["up_dst"], u32p), _ptr(out["up_w"], u32p), _ptr(out["dn_off"], u64p),
+            _ptr(out["dn_dst"], u32p), _ptr(out["dn_w"], u32p), _ptr(out["level_up"], u32p),
+            _ptr(out["level_dn"], u32p)))
+        return out
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.cpd_plan_free(self._h)
+            self._h = None
+
+
+# --------------------------------------------------------------------------
+# GPU
+
+def device_count() -> int:
+    c = C.c_int()
+    _check(lib.cpd_device_count(C.byref(c)))
+    return c.value
+
+
+class Rows:
+    def __init__(self, h):
+        self._h = h
+
+    def count(self):
+        nr, tot = C.c_uint32(), C.c_uint64()
+        _check(lib.cpd_rows_count(self._h, C.byref(nr), C.byref(tot)))
+        return nr.value, tot.value
+
+    def export(self):
+        nr, tot = self.count()
+        off = np.empty(nr + 1, np.uint64)
+        runs = np.empty(tot, np.uint32)
+        _check(lib.cpd_rows_export(self._h, _ptr(off, u64p), _ptr(runs, u32p)))
+        return off, runs
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.cpd_rows_free(self._h)
+            self._h = None
+
+
+class Graph:
+    """A plan resident on one GPU."""
+
+    def __init__(self, plan: Plan, device: int = 0, batch: int = 0):
+        self._h = C.c_void_p()
+        self.plan = plan
+        _check(lib.cpd_graph_create(plan._h, C.c_int(device), C.byref(self._h)))
+        if batch:
+            _check(lib.cpd_graph_set_batch(self._h, C.c_uint32(batch)))
+
+    @property
+    def batch(self) -> int:
+        b = C.c_uint32()
+        _check(lib.cpd_graph_get_batch(self._h, C.byref(b)))
+        return b.value
+
+    def build_rows(self, targets, reuse: Rows | None = None) -> Rows:
+        t = _u32(targets)
+        h = C.c_void_p()
+        _check(lib.cpd_build_rows(self._h, _ptr(t, u32p), C.c_uint32(len(t)),
+                                  reuse._h if reuse else None, C.byref(h)))
+        if reuse is not None:
+            return reuse
+        return Rows(h)
+
+    def debug_rows(self, targets, want_dist=True, want_fm=True):
+        t = _u32(targets)
+        n = self.plan.info()["n"]
+        dist = np.empty((n, len(t)), np.uint32) if want_dist else None
+        fm = np.empty((len(t), n), np.uint16) if want_fm else None
+        _check(lib.cpd_debug_rows(self._h, _ptr(t, u32p), C.c_uint32(len(t)),
+                                  _ptr(dist, u32p), _ptr(fm, u16p)))
+        return dist, fm
+
+    def timing(self, enable: bool = True) -> None:
+        _check(lib.cpd_timing_enable(self._h, C.c_int(int(enable))))
+
+    def timing_reset(self) -> None:
+        _check(lib.cpd_timing_reset(self._h))
+
+    def timing_get(self) -> dict:
+        arr = (KernelTime * 32)()
+        cnt = C.c_int()
+        _check(lib.cpd_timing_get(self._h, arr, 32, C.byref(cnt)))
+        return {arr[i].name.decode(): {"launches": arr[i].launches, "ms": arr[i].ms,
+                                       "bytes": arr[i].bytes} for i in range(cnt.value)}
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.cpd_graph_free(self._h)
+            self._h = None
+
+
+class Index:
+    def __init__(self, graph: Graph, rows: Rows | None = None, row_targets=None,
+                 offsets=None, runs=None):
+        self.graph = graph
+        self._h = C.c_void_p()
+        if rows is not None:
+            _check(lib.cpd_index_from_rows(graph._h, rows._h, C.byref(self._h)))
+        else:
+            rt, off = _u32(row_targets), np.ascontiguousarray(offsets, np.uint64)
+            rn = _u32(runs)
+            _check(lib.cpd_index_create(graph._h, _ptr(rt, u32p), C.c_uint32(len(rt)),
+                                        _ptr(off, u64p), _ptr(rn, u32p), C.byref(self._h)))
+
+    def set_weights(self, w=None) -> None:
+        if w is None:
+            _check(lib.cpd_index_set_weights(self._h, None))
+        else:
+            w = _u32(w)
+            _check(lib.cpd_index_set_weights(self._h, _ptr(w, u32p)))
+
+    def query(self, s, t, k_moves: int = -1):
+        s, t = _u32(s), _u32(t)
+        nq = len(s)
+        cost = np.empty(nq, np.uint64)
+        hops = np.empty(nq, np.uint32)
+        fin = np.empty(nq, np.uint8)
+        st = QueryStats()
+        _check(lib.cpd_query_batch(self._h, _ptr(s, u32p), _ptr(t, u32p), C.c_uint32(nq),
+                                   C.c_int32(k_moves), _ptr(cost, u64p), _ptr(hops, u32p),
+                                   _ptr(fin, u8p), C.byref(st)))
+        return cost, hops, fin, {k: getattr(st, k) for k, _ in QueryStats._fields_}
+
+    def prepare(self, s, t) -> None:
+        s, t = _u32(s), _u32(t)
+        _check(lib.cpd_query_prepare(self._h, _ptr(s, u32p), _ptr(t, u32p), C.c_uint32(len(s))))
+
+    def run(self, k_moves: int = -1) -> dict:
+        st = QueryStats()
+        _check(lib.cpd_query_run(self._h, C.c_int32(k_moves), C.byref(st)))
+        return {k: getattr(st, k) for k, _ in QueryStats._fields_}
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib.cpd_index_free(self._h)
+            self._h = None

@@ -1,0 +1,749 @@
+// GPU half of the C ABI: graph upload, batched CPD row build, table-search
+// index, per-kernel timing.  All device work runs on one non-blocking HIP
+// stream per graph; every entry point selects the graph's device first.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "cpd_internal.hpp"
+#include "cpd_kernels.hpp"
+
+using namespace cpd;
+
+#define HIP_CHECK(expr)                                                          \
+    do {                                                                         \
+        hipError_t _e = (expr);                                                  \
+        if (_e != hipSuccess)                                                    \
+            throw ::cpd::Error(_e == hipErrorOutOfMemory ? CPD_E_OOM : CPD_E_HIP, \
+                               std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+namespace {
+
+// Owning device buffer.
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t count) {
+        if (count <= n && p) return;
+        release();
+        HIP_CHECK(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)));
+        n = count;
+    }
+    void upload(const T* src, size_t count, hipStream_t s) {
+        alloc(count);
+        if (count) HIP_CHECK(hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s));
+    }
+};
+
+struct Pending {
+    const char* name;
+    hipEvent_t a, b;
+    double bytes;
+};
+
+struct Agg {
+    uint64_t launches = 0;
+    double ms = 0.0, bytes = 0.0;
+};
+
+}  // namespace
+
+struct cpd_graph {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t n = 0, m = 0, npad = 0;
+    std::vector<uint32_t> order;       // node -> column
+    std::vector<uint32_t> inv;         // column -> node
+    std::vector<uint32_t> edge_perm;   // column-space edge -> file edge
+    std::vector<uint32_t> w_free_col;  // free-flow weights, column-space edges
+    std::vector<uint32_t> rowc_host;   // column-space row_ptr (host copy)
+    // column-space CSR of the original graph
+    DevBuf<uint32_t> row_ptr, dst, w;
+    // sweeps: level-ordered node lists, per-slot arc offsets, (col, w) arcs
+    DevBuf<uint32_t> asc_nodes, asc_off, asc_arcs;
+    DevBuf<uint32_t> dsc_nodes, dsc_off, dsc_arcs;
+    std::vector<uint32_t> asc_lvl, dsc_lvl;         // level -> first slot
+    std::vector<double> asc_lvl_arcs, dsc_lvl_arcs;  // arcs per level (bytes model)
+    uint64_t ch_arcs = 0;
+    bool has_ch = false;
+    // batch workspace
+    uint32_t B = 0, cap = 0;
+    DevBuf<uint32_t> dist, tgt, scratch, counts;
+    DevBuf<uint16_t> fm;
+    DevBuf<uint64_t> off_dev;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<Pending> pending;
+    std::map<std::string, Agg> agg;
+
+    ~cpd_graph() {
+        if (hipSetDevice(device) == hipSuccess) {
+            if (stream) (void)hipStreamSynchronize(stream);
+            for (auto& p : pending) {
+                (void)hipEventDestroy(p.a);
+                (void)hipEventDestroy(p.b);
+            }
+            for (auto e : ev_pool) (void)hipEventDestroy(e);
+            if (stream) (void)hipStreamDestroy(stream);
+        }
+    }
+
+    hipEvent_t get_event() {
+        if (ev_pool.empty()) {
+            hipEvent_t e;
+            HIP_CHECK(hipEventCreate(&e));
+            return e;
+        }
+        hipEvent_t e = ev_pool.back();
+        ev_pool.pop_back();
+        return e;
+    }
+    // Bracket a launch with events when timing is on.
+    template <class F>
+    void timed(const char* name, double bytes, F&& launch) {
+        if (!timing) {
+            launch();
+            return;
+        }
+        hipEvent_t a = get_event(), b = get_event();
+        HIP_CHECK(hipEventRecord(a, stream));
+        launch();
+        HIP_CHECK(hipEventRecord(b, stream));
+        pending.push_back({name, a, b, bytes});
+    }
+    void sync() {
+        HIP_CHECK(hipStreamSynchronize(stream));
+        for (auto& p : pending) {
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+            Agg& g = agg[p.name];
+            g.launches++;
+            g.ms += ms;
+            g.bytes += p.bytes;
+            ev_pool.push_back(p.a);
+            ev_pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+    void select() const { HIP_CHECK(hipSetDevice(device)); }
+
+    void reserve_batch(uint32_t want) {
+        if (want == 0) {
+            size_t free_b = 0, total_b = 0;
+            HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            // per target: dist 4n + fm 2npad + scratch 4cap(<= n/4 typical)
+            double per = 4.0 * n + 2.0 * npad + 4.0 * std::max<uint32_t>(1024, n / 4);
+            double fit = 0.4 * (double)free_b / per;
+            want = (uint32_t)std::min(8192.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
+        }
+        want = (want + 1023u) / 1024u * 1024u;
+        if (want == B && dist.p) return;
+        B = want;
+        // RLE scratch: up to 4 GiB, at least 1024 runs per row, at most n+1
+        uint64_t c = (4ull << 30) / (4ull * B);
+        cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c, 1024), (uint64_t)n + 1);
+        dist.alloc((size_t)n * B);
+        fm.alloc((size_t)B * npad);
+        tgt.alloc(B);
+        scratch.alloc((size_t)B * cap);
+        counts.alloc(B);
+        off_dev.alloc((size_t)B + 1);
+    }
+};
+
+struct cpd_rows {
+    int device = 0;
+    uint32_t nrows = 0;
+    uint64_t total = 0;
+    std::vector<uint32_t> targets;   // node ids, row order
+    std::vector<uint64_t> offsets;   // host copy, nrows+1
+    DevBuf<uint32_t> runs;
+    DevBuf<uint64_t> off;
+};
+
+struct cpd_index {
+    cpd_graph* g = nullptr;
+    uint32_t nrows = 0;
+    uint64_t total = 0;
+    std::vector<uint32_t> row_of_col;   // host copy
+    std::vector<uint64_t> offsets;      // host copy
+    DevBuf<uint32_t> d_row_of_col, runs, w_sel;
+    DevBuf<uint64_t> off;
+    bool custom_w = false;
+    // query workspace
+    uint32_t nq = 0;
+    DevBuf<uint32_t> qs, qt, hops;
+    DevBuf<uint64_t> cost;
+    DevBuf<uint8_t> fin;
+    DevBuf<unsigned long long> agg;
+};
+
+namespace {
+
+void require_device() {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0)
+        throw Error(CPD_E_HIP, "no HIP device available (libcpd has no CPU fallback)");
+}
+
+// Build the level-ordered sweep arrays in column space.
+void build_sweep(const cpd_plan& p, bool ascend, std::vector<uint32_t>& nodes,
+                 std::vector<uint32_t>& off, std::vector<uint32_t>& arcs,
+                 std::vector<uint32_t>& lvl_first, std::vector<double>& lvl_arcs) {
+    const Hierarchy& H = p.ch;
+    const uint32_t n = p.n;
+    const std::vector<uint32_t>& level = ascend ? H.level_up : H.level_dn;
+    const uint32_t nlev = ascend ? H.nlev_up : H.nlev_dn;
+    // ascend reads each node's DOWN arcs; descend reads its UP arcs
+    const std::vector<uint64_t>& aoff = ascend ? H.dn_off : H.up_off;
+    const std::vector<uint32_t>& adst = ascend ? H.dn_dst : H.up_dst;
+    const std::vector<uint32_t>& aw = ascend ? H.dn_w : H.up_w;
+    CPD_REQUIRE(aoff[n] < 0xFFFFFFFFull, CPD_E_RANGE, "hierarchy has >= 2^32 arcs");
+    // counting sort by (level, column)
+    std::vector<uint32_t> cnt(nlev + 1, 0);
+    for (uint32_t v = 0; v < n; ++v) cnt[level[v] + 1]++;
+    for (uint32_t l = 0; l < nlev; ++l) cnt[l + 1] += cnt[l];
+    lvl_first.assign(cnt.begin(), cnt.end());
+    nodes.assign(n, 0);
+    std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
+    for (uint32_t c = 0; c < n; ++c) {  // columns ascending inside a level
+        uint32_t v = p.inv[c];
+        nodes[pos[level[v]]++] = c;
+    }
+    off.assign(n + 1, 0);
+    arcs.clear();
+    arcs.reserve(2 * aoff[n]);
+    lvl_arcs.assign(nlev, 0.0);
+    std::vector<std::pair<uint32_t, uint32_t>> tmp;
+    for (uint32_t s = 0; s < n; ++s) {
+        uint32_t v = p.inv[nodes[s]];
+        tmp.clear();
+        for (uint64_t e = aoff[v]; e < aoff[v + 1]; ++e) tmp.push_back({p.order[adst[e]], aw[e]});
+        std::sort(tmp.begin(), tmp.end());
+        for (auto& a : tmp) {
+            arcs.push_back(a.first);
+            arcs.push_back(a.second);
+        }
+        off[s + 1] = off[s] + (uint32_t)tmp.size();
+        lvl_arcs[level[v]] += (double)tmp.size();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpd_device_count(int* count) {
+    return guarded([&] {
+        CPD_REQUIRE(count, CPD_E_ARG, "null count");
+        hipError_t e = hipGetDeviceCount(count);
+        if (e != hipSuccess) *count = 0;
+    });
+}
+
+int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
+    return guarded([&] {
+        CPD_REQUIRE(p && out, CPD_E_ARG, "graph: null argument");
+        *out = nullptr;
+        require_device();
+        auto g = std::make_unique<cpd_graph>();
+        g->device = device;
+        g->select();
+        HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+        const uint32_t n = p->n, m = p->m;
+        g->n = n;
+        g->m = m;
+        g->npad = (n + 511u) / 512u * 512u;
+        g->order = p->order;
+        g->inv = p->inv;
+        // column-space CSR, per-node out-edge order preserved (moves = file order)
+        g->rowc_host.assign(n + 1, 0);
+        for (uint32_t c = 0; c < n; ++c) {
+            uint32_t v = p->inv[c];
+            g->rowc_host[c + 1] = g->rowc_host[c] + (p->row_ptr[v + 1] - p->row_ptr[v]);
+        }
+        std::vector<uint32_t> dstc(m);
+        g->edge_perm.resize(m);
+        g->w_free_col.resize(m);
+        for (uint32_t c = 0; c < n; ++c) {
+            uint32_t v = p->inv[c];
+            uint32_t b = p->row_ptr[v], k = p->row_ptr[v + 1] - b;
+            for (uint32_t i = 0; i < k; ++i) {
+                uint32_t e = g->rowc_host[c] + i;
+                g->edge_perm[e] = b + i;
+                dstc[e] = p->order[p->dst[b + i]];
+                g->w_free_col[e] = p->w[b + i];
+            }
+        }
+        hipStream_t s = g->stream;
+        g->row_ptr.upload(g->rowc_host.data(), n + 1, s);
+        g->dst.upload(dstc.data(), m, s);
+        g->w.upload(g->w_free_col.data(), m, s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        g->has_ch = !p->ch.rank.empty();
+        if (!g->has_ch) {  // query-only graph (fifo_auto)
+            *out = g.release();
+            return;
+        }
+        std::vector<uint32_t> nodes, off, arcs;
+        build_sweep(*p, true, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs);
+        g->asc_nodes.upload(nodes.data(), nodes.size(), s);
+        g->asc_off.upload(off.data(), off.size(), s);
+        g->asc_arcs.upload(arcs.data(), arcs.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        g->ch_arcs = arcs.size() / 2;
+        build_sweep(*p, false, nodes, off, arcs, g->dsc_lvl, g->dsc_lvl_arcs);
+        g->dsc_nodes.upload(nodes.data(), nodes.size(), s);
+        g->dsc_off.upload(off.data(), off.size(), s);
+        g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
+        HIP_CHECK(hipStreamSynchronize(s));
+        g->ch_arcs += arcs.size() / 2;
+        *out = g.release();
+    });
+}
+
+int cpd_graph_set_batch(cpd_graph* g, uint32_t batch) {
+    return guarded([&] {
+        CPD_REQUIRE(g, CPD_E_ARG, "null graph");
+        CPD_REQUIRE(batch % 1024u == 0, CPD_E_ARG, "batch must be a multiple of 1024");
+        g->select();
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        g->reserve_batch(batch);
+    });
+}
+
+int cpd_graph_get_batch(const cpd_graph* g, uint32_t* batch) {
+    return guarded([&] {
+        CPD_REQUIRE(g && batch, CPD_E_ARG, "null argument");
+        *batch = g->B;
+    });
+}
+
+void cpd_graph_free(cpd_graph* g) { delete g; }
+
+}  // extern "C"
+
+namespace {
+
+// Distances + first-move sets for `k` targets (columns already in g->tgt,
+// padded to a multiple of 1024 with valid columns).
+void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
+    const uint32_t B = g->B, n = g->n;
+    const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
+    const uint32_t active = slabs * 1024u;
+    // ascending sweep: each level reads lower levels' rows
+    for (size_t l = 0; l + 1 < g->asc_lvl.size(); ++l) {
+        uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
+        if (!cnt) continue;
+        double bytes = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active +
+                       8.0 * g->asc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
+        g->timed("sweep_up", bytes, [&] {
+            launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt, g->dist.p,
+                         g->tgt.p, B, slabs, g->stream);
+        });
+    }
+    for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
+        uint32_t s0 = g->dsc_lvl[l], cnt = g->dsc_lvl[l + 1] - s0;
+        if (!cnt) continue;
+        double bytes = (4.0 * g->dsc_lvl_arcs[l] + 8.0 * cnt) * active +
+                       8.0 * g->dsc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
+        g->timed("sweep_down", bytes, [&] {
+            launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
+                         g->tgt.p, B, slabs, g->stream);
+        });
+    }
+    const uint32_t fslabs = (k + 255u) / 256u;
+    double fbytes = (4.0 * n + 4.0 * g->m + 2.0 * g->npad) * (fslabs * 256.0) +
+                    (4.0 * (n + 1) + 8.0 * g->m) * fslabs;
+    g->timed("first_moves", fbytes, [&] {
+        launch_first_moves(g->row_ptr.p, g->dst.p, g->w.p, g->dist.p, g->tgt.p, B, k, n,
+                           g->npad, g->fm.p, g->stream);
+    });
+}
+
+void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k) {
+    CPD_REQUIRE(g->has_ch, CPD_E_ARG,
+                "graph was created from a plan without hierarchy: it can serve queries "
+                "but not build rows");
+    std::vector<uint32_t> cols(g->B);
+    for (uint32_t i = 0; i < k; ++i) {
+        CPD_REQUIRE(targets[i] < g->n, CPD_E_ARG,
+                    "target " + std::to_string(targets[i]) + " out of range");
+        cols[i] = g->order[targets[i]];
+    }
+    for (uint32_t i = k; i < g->B; ++i) cols[i] = cols[0];  // padding lanes
+    g->tgt.upload(cols.data(), g->B, g->stream);
+}
+
+// Build rows for one batch of k <= B targets; append to r (device).
+void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r) {
+    upload_targets(g, targets, k);
+    run_sweeps_and_fm(g, k);
+    const uint32_t cap = g->cap, npad = g->npad;
+    g->timed("rle_rows", 2.0 * npad * k, [&] {
+        launch_rle(g->fm.p, npad, k, g->scratch.p, cap, g->counts.p, g->stream);
+    });
+    std::vector<uint32_t> counts(k);
+    HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
+                             hipMemcpyDeviceToHost, g->stream));
+    g->sync();
+    // compact offsets for this batch, appended after r->total
+    std::vector<uint64_t> off(k + 1);
+    off[0] = r->total;
+    for (uint32_t i = 0; i < k; ++i) off[i + 1] = off[i] + counts[i];
+    uint64_t new_total = off[k];
+    if (new_total > r->runs.n) {  // grow, preserving the rows already built
+        size_t want = std::max<size_t>(new_total, r->runs.n + r->runs.n / 2);
+        uint32_t* np = nullptr;
+        HIP_CHECK(hipMalloc(&np, std::max<size_t>(want, 1) * sizeof(uint32_t)));
+        if (r->total)
+            HIP_CHECK(hipMemcpyAsync(np, r->runs.p, r->total * sizeof(uint32_t),
+                                     hipMemcpyDeviceToDevice, g->stream));
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        r->runs.release();
+        r->runs.p = np;
+        r->runs.n = want;
+    }
+    g->off_dev.upload(off.data(), k + 1, g->stream);
+    // rows that fit the scratch cap: one compaction launch
+    double cbytes = 8.0 * (double)(new_total - r->total);
+    g->timed("compact_rows", cbytes, [&] {
+        launch_compact(g->scratch.p, cap, g->off_dev.p, k, r->runs.p, g->stream);
+    });
+    // rows past the cap (rare): re-run the scan alone into a full-size buffer
+    std::vector<uint32_t> big;
+    for (uint32_t i = 0; i < k; ++i)
+        if (counts[i] > cap) big.push_back(i);
+    if (!big.empty()) {
+        DevBuf<uint32_t> full, cnt1;
+        full.alloc((size_t)g->n + 1);
+        cnt1.alloc(1);
+        for (uint32_t i : big) {
+            launch_rle(g->fm.p + (size_t)i * npad, npad, 1, full.p, g->n + 1, cnt1.p, g->stream);
+            HIP_CHECK(hipMemcpyAsync(r->runs.p + off[i], full.p, counts[i] * sizeof(uint32_t),
+                                     hipMemcpyDeviceToDevice, g->stream));
+        }
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+    }
+    g->sync();
+    r->offsets.insert(r->offsets.end(), off.begin() + 1, off.end());
+    r->targets.insert(r->targets.end(), targets, targets + k);
+    r->nrows += k;
+    r->total = new_total;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
+                   cpd_rows* reuse, cpd_rows** out) {
+    return guarded([&] {
+        CPD_REQUIRE(g && out && (targets || ntargets == 0), CPD_E_ARG, "build: null argument");
+        *out = nullptr;
+        g->select();
+        if (!g->B) g->reserve_batch(0);
+        cpd_rows* r = reuse ? reuse : new cpd_rows();
+        std::unique_ptr<cpd_rows> owned(reuse ? nullptr : r);
+        r->device = g->device;
+        r->nrows = 0;
+        r->total = 0;
+        r->targets.clear();
+        r->offsets.assign(1, 0);
+        for (uint32_t b = 0; b < ntargets; b += g->B) {
+            uint32_t k = std::min(g->B, ntargets - b);
+            build_batch(g, targets + b, k, r);
+        }
+        r->off.upload(r->offsets.data(), r->offsets.size(), g->stream);
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        owned.release();
+        *out = r;
+    });
+}
+
+int cpd_rows_count(const cpd_rows* r, uint32_t* nrows, uint64_t* total_runs) {
+    return guarded([&] {
+        CPD_REQUIRE(r, CPD_E_ARG, "null rows");
+        if (nrows) *nrows = r->nrows;
+        if (total_runs) *total_runs = r->total;
+    });
+}
+
+int cpd_rows_export(const cpd_rows* r, uint64_t* offsets, uint32_t* runs) {
+    return guarded([&] {
+        CPD_REQUIRE(r, CPD_E_ARG, "null rows");
+        HIP_CHECK(hipSetDevice(r->device));
+        if (offsets) std::memcpy(offsets, r->offsets.data(), (r->nrows + 1) * sizeof(uint64_t));
+        if (runs && r->total)
+            HIP_CHECK(hipMemcpy(runs, r->runs.p, r->total * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    });
+}
+
+void cpd_rows_free(cpd_rows* r) {
+    if (r) (void)hipSetDevice(r->device);
+    delete r;
+}
+
+int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uint32_t* dist,
+                   uint16_t* fm) {
+    return guarded([&] {
+        CPD_REQUIRE(g && targets, CPD_E_ARG, "debug: null argument");
+        g->select();
+        if (!g->B) g->reserve_batch(0);
+        CPD_REQUIRE(ntargets > 0 && ntargets <= g->B, CPD_E_ARG, "debug: 0 < ntargets <= batch");
+        upload_targets(g, targets, ntargets);
+        run_sweeps_and_fm(g, ntargets);
+        g->sync();
+        const uint32_t n = g->n, B = g->B;
+        if (dist) {
+            std::vector<uint32_t> h((size_t)n * B);
+            HIP_CHECK(hipMemcpy(h.data(), g->dist.p, h.size() * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost));
+            for (uint32_t v = 0; v < n; ++v)
+                for (uint32_t i = 0; i < ntargets; ++i)
+                    dist[(size_t)v * ntargets + i] = h[(size_t)g->order[v] * B + i];
+        }
+        if (fm) {
+            std::vector<uint16_t> h((size_t)ntargets * g->npad);
+            HIP_CHECK(hipMemcpy(h.data(), g->fm.p, h.size() * sizeof(uint16_t),
+                                hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < ntargets; ++i)
+                for (uint32_t v = 0; v < n; ++v)
+                    fm[(size_t)i * n + v] = h[(size_t)i * g->npad + g->order[v]];
+        }
+    });
+}
+
+// ---------------------------------------------------------------------------
+// Index + queries
+
+int cpd_index_create(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows,
+                     const uint64_t* offsets, const uint32_t* runs, cpd_index** out) {
+    return guarded([&] {
+        CPD_REQUIRE(g && out && row_targets && offsets, CPD_E_ARG, "index: null argument");
+        *out = nullptr;
+        g->select();
+        auto ix = std::make_unique<cpd_index>();
+        ix->g = g;
+        ix->nrows = nrows;
+        ix->row_of_col.assign(g->n, CPD_INF);
+        CPD_REQUIRE(offsets[0] == 0, CPD_E_ARG, "index: offsets[0] must be 0");
+        for (uint32_t i = 0; i < nrows; ++i) {
+            CPD_REQUIRE(row_targets[i] < g->n, CPD_E_ARG, "index: row target out of range");
+            CPD_REQUIRE(offsets[i + 1] > offsets[i], CPD_E_ARG, "index: empty or unsorted row");
+            ix->row_of_col[g->order[row_targets[i]]] = i;
+        }
+        ix->total = offsets[nrows];
+        CPD_REQUIRE(ix->total == 0 || runs, CPD_E_ARG, "index: null runs");
+        // every run must name a legal column; a row must start at column 0
+        for (uint32_t i = 0; i < nrows; ++i) {
+            CPD_REQUIRE((runs[offsets[i]] >> 4) == 0, CPD_E_ARG, "index: row does not start at column 0");
+            for (uint64_t e = offsets[i] + 1; e < offsets[i + 1]; ++e)
+                CPD_REQUIRE((runs[e] >> 4) > (runs[e - 1] >> 4) && (runs[e] >> 4) < g->n,
+                            CPD_E_ARG, "index: run columns must increase and be < n");
+        }
+        ix->offsets.assign(offsets, offsets + nrows + 1);
+        ix->d_row_of_col.upload(ix->row_of_col.data(), g->n, g->stream);
+        ix->off.upload(offsets, (size_t)nrows + 1, g->stream);
+        ix->runs.upload(runs, ix->total, g->stream);
+        ix->agg.alloc(3);
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        *out = ix.release();
+    });
+}
+
+int cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out) {
+    return guarded([&] {
+        CPD_REQUIRE(g && r && out, CPD_E_ARG, "index: null argument");
+        CPD_REQUIRE(r->device == g->device, CPD_E_ARG, "index: rows live on another device");
+        *out = nullptr;
+        g->select();
+        auto ix = std::make_unique<cpd_index>();
+        ix->g = g;
+        ix->nrows = r->nrows;
+        ix->total = r->total;
+        ix->row_of_col.assign(g->n, CPD_INF);
+        for (uint32_t i = 0; i < r->nrows; ++i) ix->row_of_col[g->order[r->targets[i]]] = i;
+        ix->offsets = r->offsets;
+        ix->d_row_of_col.upload(ix->row_of_col.data(), g->n, g->stream);
+        ix->off.upload(r->offsets.data(), r->offsets.size(), g->stream);
+        ix->runs.alloc(r->total);
+        if (r->total)
+            HIP_CHECK(hipMemcpyAsync(ix->runs.p, r->runs.p, r->total * sizeof(uint32_t),
+                                     hipMemcpyDeviceToDevice, g->stream));
+        ix->agg.alloc(3);
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        *out = ix.release();
+    });
+}
+
+int cpd_index_set_weights(cpd_index* ix, const uint32_t* w) {
+    return guarded([&] {
+        CPD_REQUIRE(ix, CPD_E_ARG, "null index");
+        cpd_graph* g = ix->g;
+        g->select();
+        if (!w) {
+            ix->custom_w = false;
+            return;
+        }
+        std::vector<uint32_t> wc(g->m);
+        for (uint32_t e = 0; e < g->m; ++e) wc[e] = w[g->edge_perm[e]];
+        ix->w_sel.upload(wc.data(), g->m, g->stream);
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        ix->custom_w = true;
+    });
+}
+
+int cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint32_t nq) {
+    return guarded([&] {
+        CPD_REQUIRE(ix && (nq == 0 || (s && t)), CPD_E_ARG, "query: null argument");
+        cpd_graph* g = ix->g;
+        g->select();
+        std::vector<uint32_t> sc(nq), tc(nq);
+        for (uint32_t q = 0; q < nq; ++q) {
+            CPD_REQUIRE(s[q] < g->n && t[q] < g->n, CPD_E_ARG, "query node out of range");
+            tc[q] = g->order[t[q]];
+            sc[q] = g->order[s[q]];
+            if (ix->row_of_col[tc[q]] == CPD_INF)
+                throw Error(CPD_E_NOROW, "target " + std::to_string(t[q]) +
+                                             " has no CPD row in this index");
+        }
+        ix->qs.upload(sc.data(), nq, g->stream);
+        ix->qt.upload(tc.data(), nq, g->stream);
+        ix->cost.alloc(nq);
+        ix->hops.alloc(nq);
+        ix->fin.alloc(nq);
+        ix->nq = nq;
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+    });
+}
+
+int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
+    return guarded([&] {
+        CPD_REQUIRE(ix, CPD_E_ARG, "null index");
+        cpd_graph* g = ix->g;
+        g->select();
+        const uint32_t nq = ix->nq;
+        HIP_CHECK(hipMemsetAsync(ix->agg.p, 0, 3 * sizeof(unsigned long long), g->stream));
+        hipEvent_t a = g->get_event(), b = g->get_event();
+        HIP_CHECK(hipEventRecord(a, g->stream));
+        const uint32_t* w = ix->custom_w ? ix->w_sel.p : g->w.p;
+        if (nq)
+            launch_table_search(g->row_ptr.p, g->dst.p, w, ix->d_row_of_col.p, ix->off.p,
+                                ix->runs.p, ix->qs.p, ix->qt.p, nq, k_moves, g->n, ix->cost.p,
+                                ix->hops.p, ix->fin.p, ix->agg.p, g->stream);
+        HIP_CHECK(hipEventRecord(b, g->stream));
+        unsigned long long hagg[3] = {0, 0, 0};
+        HIP_CHECK(hipMemcpyAsync(hagg, ix->agg.p, sizeof hagg, hipMemcpyDeviceToHost, g->stream));
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+        g->ev_pool.push_back(a);
+        g->ev_pool.push_back(b);
+        if (g->timing) {
+            Agg& ag = g->agg["table_search"];
+            ag.launches++;
+            ag.ms += ms;
+            // SURVEY.md §8(d) B_q = 8 + 12 + 8 + L * (4 ceil(log2 R) + 16)
+            double mean_log = 0.0;
+            if (ix->nrows) {
+                double s = 0.0;
+                for (uint32_t i = 0; i < ix->nrows; ++i)
+                    s += std::ceil(std::log2((double)std::max<uint64_t>(
+                        2, ix->offsets[i + 1] - ix->offsets[i])));
+                mean_log = s / ix->nrows;
+            }
+            ag.bytes += 28.0 * nq + (double)hagg[1] * (4.0 * mean_log + 16.0);
+        }
+        if (st) {
+            st->queries = nq;
+            st->finished = hagg[0];
+            st->hops = hagg[1];
+            st->cost = hagg[2];
+            st->kernel_ms = ms;
+        }
+    });
+}
+
+int cpd_query_fetch(cpd_index* ix, uint64_t* cost, uint32_t* hops, uint8_t* finished) {
+    return guarded([&] {
+        CPD_REQUIRE(ix, CPD_E_ARG, "null index");
+        ix->g->select();
+        const uint32_t nq = ix->nq;
+        if (cost && nq) HIP_CHECK(hipMemcpy(cost, ix->cost.p, nq * 8ull, hipMemcpyDeviceToHost));
+        if (hops && nq) HIP_CHECK(hipMemcpy(hops, ix->hops.p, nq * 4ull, hipMemcpyDeviceToHost));
+        if (finished && nq) HIP_CHECK(hipMemcpy(finished, ix->fin.p, nq, hipMemcpyDeviceToHost));
+    });
+}
+
+int cpd_query_batch(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint32_t nq,
+                    int32_t k_moves, uint64_t* cost, uint32_t* hops, uint8_t* finished,
+                    cpd_query_stats* st) {
+    int rc = cpd_query_prepare(ix, s, t, nq);
+    if (rc) return rc;
+    rc = cpd_query_run(ix, k_moves, st);
+    if (rc) return rc;
+    return cpd_query_fetch(ix, cost, hops, finished);
+}
+
+void cpd_index_free(cpd_index* ix) {
+    if (ix && ix->g) (void)hipSetDevice(ix->g->device);
+    delete ix;
+}
+
+// ---------------------------------------------------------------------------
+// Timing
+
+int cpd_timing_enable(cpd_graph* g, int enable) {
+    return guarded([&] {
+        CPD_REQUIRE(g, CPD_E_ARG, "null graph");
+        g->timing = enable != 0;
+    });
+}
+
+int cpd_timing_reset(cpd_graph* g) {
+    return guarded([&] {
+        CPD_REQUIRE(g, CPD_E_ARG, "null graph");
+        g->agg.clear();
+    });
+}
+
+int cpd_timing_get(const cpd_graph* g, cpd_kernel_time* out, int max, int* count) {
+    return guarded([&] {
+        CPD_REQUIRE(g && count, CPD_E_ARG, "null argument");
+        int k = 0;
+        for (auto& kv : g->agg) {
+            if (out && k < max) {
+                std::memset(out[k].name, 0, sizeof out[k].name);
+                std::strncpy(out[k].name, kv.first.c_str(), sizeof out[k].name - 1);
+                out[k].launches = kv.second.launches;
+                out[k].ms = kv.second.ms;
+                out[k].bytes = kv.second.bytes;
+            }
+            ++k;
+        }
+        *count = std::min(k, out ? max : k);
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,352 @@
+// File formats on the drop-in boundary — see cpd_io.hpp.
+#include "cpd_io.hpp"
+
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <memory>
+
+#include "cpd_internal.hpp"
+
+namespace cpd {
+namespace io {
+namespace {
+
+std::string slurp(const std::string& path) {
+    std::FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) throw Error(CPD_E_IO, "cannot open " + path);
+    std::string s;
+    char buf[1 << 16];
+    size_t k;
+    while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, k);
+    std::fclose(f);
+    return s;
+}
+
+// Minimal tokenizer over one line.
+struct Line {
+    const char* p;
+    const char* e;
+    bool word(std::string& out) {
+        while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) ++p;
+        if (p >= e) return false;
+        const char* b = p;
+        while (p < e && *p != ' ' && *p != '\t' && *p != '\r') ++p;
+        out.assign(b, p);
+        return true;
+    }
+    bool i64(int64_t& v) {
+        while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) ++p;
+        if (p >= e) return false;
+        bool neg = false;
+        if (*p == '-' || *p == '+') neg = *p++ == '-';
+        if (p >= e || *p < '0' || *p > '9') return false;
+        int64_t r = 0;
+        while (p < e && *p >= '0' && *p <= '9') r = r * 10 + (*p++ - '0');
+        v = neg ? -r : r;
+        return true;
+    }
+};
+
+template <class F>
+void for_lines(const std::string& s, F&& f) {
+    size_t i = 0, lineno = 0;
+    while (i < s.size()) {
+        size_t j = s.find('\n', i);
+        if (j == std::string::npos) j = s.size();
+        f(Line{s.data() + i, s.data() + j}, lineno++);
+        i = j + 1;
+    }
+}
+
+uint32_t to_u32(int64_t v, const std::string& what) {
+    if (v < 0 || v > 0xFFFFFFFFll) throw Error(CPD_E_IO, what + " out of range");
+    return (uint32_t)v;
+}
+
+const char kBucketMagic[8] = {'D', 'O', 'S', 'C', 'P', 'D', '0', '1'};
+const char kOrderMagic[8] = {'D', 'O', 'S', 'O', 'R', 'D', '0', '1'};
+
+}  // namespace
+
+XYGraph read_xy(const std::string& path) {
+    std::string s = slurp(path);
+    XYGraph g;
+    int64_t hn = -1, hm = -1;
+    struct E { uint32_t a, b, w; };
+    std::vector<E> edges;
+    std::vector<std::pair<uint32_t, std::pair<int32_t, int32_t>>> verts;
+    for_lines(s, [&](Line ln, size_t lineno) {
+        std::string tag;
+        Line probe = ln;
+        if (!probe.word(tag)) return;
+        if (tag == "nodes") {
+            int64_t n, m;
+            std::string et;
+            if (!probe.i64(n) || !probe.word(et) || et != "edges" || !probe.i64(m))
+                throw Error(CPD_E_IO, path + ": bad header line " + std::to_string(lineno + 1));
+            hn = n;
+            hm = m;
+            edges.reserve((size_t)m);
+        } else if (tag == "v") {
+            int64_t id, x, y;
+            if (!probe.i64(id) || !probe.i64(x) || !probe.i64(y))
+                throw Error(CPD_E_IO, path + ": bad v line " + std::to_string(lineno + 1));
+            verts.push_back({to_u32(id, "node id"), {(int32_t)x, (int32_t)y}});
+        } else if (tag == "e") {
+            int64_t a, b, w;
+            if (!probe.i64(a) || !probe.i64(b) || !probe.i64(w))
+                throw Error(CPD_E_IO, path + ": bad e line " + std::to_string(lineno + 1));
+            edges.push_back({to_u32(a, "edge tail"), to_u32(b, "edge head"), to_u32(w, "edge cost")});
+        }
+        // anything else (comments) is ignored
+    });
+    if (hn < 0) throw Error(CPD_E_IO, path + ": missing 'nodes N edges M' header");
+    if (hm != (int64_t)edges.size())
+        throw Error(CPD_E_IO, path + ": header says " + std::to_string(hm) + " edges, file has " +
+                                  std::to_string(edges.size()));
+    g.n = (uint32_t)hn;
+    g.m = (uint32_t)edges.size();
+    g.x.assign(g.n, 0);
+    g.y.assign(g.n, 0);
+    for (auto& v : verts) {
+        if (v.first >= g.n) throw Error(CPD_E_IO, path + ": vertex id out of range");
+        g.x[v.first] = v.second.first;
+        g.y[v.first] = v.second.second;
+    }
+    g.row_ptr.assign(g.n + 1, 0);
+    for (auto& e : edges) {
+        if (e.a >= g.n || e.b >= g.n) throw Error(CPD_E_IO, path + ": edge endpoint out of range");
+        g.row_ptr[e.a + 1]++;
+    }
+    for (uint32_t v = 0; v < g.n; ++v) g.row_ptr[v + 1] += g.row_ptr[v];
+    g.dst.resize(g.m);
+    g.w.resize(g.m);
+    std::vector<uint32_t> pos(g.row_ptr.begin(), g.row_ptr.end() - 1);
+    for (auto& e : edges) {  // stable: file order within a node
+        uint32_t p = pos[e.a]++;
+        g.dst[p] = e.b;
+        g.w[p] = e.w;
+    }
+    return g;
+}
+
+void write_xy(const std::string& path, uint32_t n, const uint32_t* row_ptr, const uint32_t* dst,
+              const uint32_t* w, const int32_t* x, const int32_t* y) {
+    std::FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw Error(CPD_E_IO, "cannot write " + path);
+    std::unique_ptr<std::FILE, int (*)(std::FILE*)> guard(f, std::fclose);
+    std::vector<char> buf(1 << 20);
+    std::setvbuf(f, buf.data(), _IOFBF, buf.size());
+    std::fprintf(f, "c cpd-mi355x xy graph\nc nodes are 0-based; edges grouped by tail in out-edge order\nc\n");
+    std::fprintf(f, "nodes %u edges %u\n", n, row_ptr[n]);
+    for (uint32_t v = 0; v < n; ++v)
+        std::fprintf(f, "v %u %d %d\n", v, x ? x[v] : 0, y ? y[v] : 0);
+    for (uint32_t v = 0; v < n; ++v)
+        for (uint32_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e)
+            std::fprintf(f, "e %u %u %u\n", v, dst[e], w[e]);
+    if (std::ferror(f)) throw Error(CPD_E_IO, "write failed: " + path);
+}
+
+std::vector<uint32_t> read_diff(const std::string& path, const XYGraph& g) {
+    std::vector<uint32_t> w = g.w;
+    if (path.empty() || path == "-") return w;
+    std::string s = slurp(path);
+    for_lines(s, [&](Line ln, size_t lineno) {
+        Line probe = ln;
+        std::string tag;
+        Line save = probe;
+        if (!probe.word(tag)) return;
+        Line nums = (tag == "e") ? probe : save;
+        if (tag != "e" && !(tag[0] >= '0' && tag[0] <= '9')) return;  // comment / header
+        int64_t a, b, c;
+        if (!nums.i64(a) || !nums.i64(b) || !nums.i64(c))
+            throw Error(CPD_E_IO, path + ": bad diff line " + std::to_string(lineno + 1));
+        uint32_t ua = to_u32(a, "diff tail"), ub = to_u32(b, "diff head");
+        if (ua >= g.n || ub >= g.n) throw Error(CPD_E_IO, path + ": diff node out of range");
+        bool found = false;
+        for (uint32_t e = g.row_ptr[ua]; e < g.row_ptr[ua + 1]; ++e)
+            if (g.dst[e] == ub) {
+                w[e] = to_u32(c, "diff cost");
+                found = true;
+                break;
+            }
+        if (!found)
+            throw Error(CPD_E_IO, path + ": diff line " + std::to_string(lineno + 1) +
+                                      " names a missing edge");
+    });
+    return w;
+}
+
+void write_diff(const std::string& path, const XYGraph& g, const std::vector<uint32_t>& wc) {
+    std::FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw Error(CPD_E_IO, "cannot write " + path);
+    std::unique_ptr<std::FILE, int (*)(std::FILE*)> guard(f, std::fclose);
+    std::fprintf(f, "c cpd-mi355x congestion diff: e from to new_cost\n");
+    for (uint32_t v = 0; v < g.n; ++v)
+        for (uint32_t e = g.row_ptr[v]; e < g.row_ptr[v + 1]; ++e)
+            if (wc[e] != g.w[e]) std::fprintf(f, "e %u %u %u\n", v, g.dst[e], wc[e]);
+}
+
+Pairs read_scen(const std::string& path) {
+    std::string s = slurp(path);
+    Pairs q;
+    for_lines(s, [&](Line ln, size_t lineno) {
+        if (ln.p >= ln.e || *ln.p != 'q') return;  // read_p2p: line[0] == "q"
+        ++ln.p;
+        int64_t a, b;
+        if (!ln.i64(a) || !ln.i64(b))
+            throw Error(CPD_E_IO, path + ": bad q line " + std::to_string(lineno + 1));
+        q.push_back({to_u32(a, "query source"), to_u32(b, "query target")});
+    });
+    return q;
+}
+
+void write_scen(const std::string& path, const Pairs& q) {
+    std::FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw Error(CPD_E_IO, "cannot write " + path);
+    std::unique_ptr<std::FILE, int (*)(std::FILE*)> guard(f, std::fclose);
+    std::fprintf(f, "p aux sp p2p %zu\n", q.size());
+    for (auto& p : q) std::fprintf(f, "q %u %u\n", p.first, p.second);
+}
+
+Pairs read_query_file(const std::string& path) {
+    std::string s = slurp(path);
+    Pairs q;
+    int64_t expect = -1;
+    for_lines(s, [&](Line ln, size_t lineno) {
+        int64_t a, b;
+        if (expect < 0) {
+            if (!ln.i64(a)) throw Error(CPD_E_IO, path + ": missing query count");
+            expect = a;
+            q.reserve((size_t)a);
+            return;
+        }
+        if (!ln.i64(a)) return;  // blank
+        if (!ln.i64(b)) throw Error(CPD_E_IO, path + ": bad query line " + std::to_string(lineno + 1));
+        q.push_back({to_u32(a, "query source"), to_u32(b, "query target")});
+    });
+    if (expect < 0) expect = 0;
+    if ((int64_t)q.size() != expect)
+        throw Error(CPD_E_IO, path + ": header says " + std::to_string(expect) + " queries, file has " +
+                                  std::to_string(q.size()));
+    return q;
+}
+
+uint64_t graph_fingerprint(uint32_t n, const uint32_t* row_ptr, const uint32_t* dst,
+                           const uint32_t* w) {
+    uint64_t h = 1469598103934665603ull;
+    auto mixin = [&](const void* p, size_t bytes) {
+        const unsigned char* c = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < bytes; ++i) h = (h ^ c[i]) * 1099511628211ull;
+    };
+    mixin(&n, 4);
+    mixin(row_ptr, (size_t)(n + 1) * 4);
+    mixin(dst, (size_t)row_ptr[n] * 4);
+    mixin(w, (size_t)row_ptr[n] * 4);
+    return h;
+}
+
+std::string xy_stem(const std::string& xy_path) {
+    size_t s = xy_path.find_last_of('/');
+    return s == std::string::npos ? xy_path : xy_path.substr(s + 1);
+}
+
+std::string bucket_path(const std::string& outdir, const std::string& xy_path,
+                        const std::string& method, uint32_t key, uint32_t bid) {
+    return outdir + "/" + xy_stem(xy_path) + "-" + method + "-" + std::to_string(key) + "-" +
+           std::to_string(bid) + ".cpd";
+}
+
+std::string order_path(const std::string& outdir, const std::string& xy_path) {
+    return outdir + "/" + xy_stem(xy_path) + ".order";
+}
+
+void write_bucket(const std::string& path, const CpdBucket& b) {
+    std::string tmp = path + ".tmp";
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) throw Error(CPD_E_IO, "cannot write " + tmp);
+        uint32_t nrows = (uint32_t)b.targets.size();
+        uint64_t total = b.offsets.empty() ? 0 : b.offsets.back();
+        f.write(kBucketMagic, 8);
+        uint32_t h32[6] = {b.n, nrows, b.bid, b.method, b.key, b.maxworker};
+        f.write(reinterpret_cast<const char*>(h32), sizeof h32);
+        f.write(reinterpret_cast<const char*>(&total), 8);
+        f.write(reinterpret_cast<const char*>(&b.fingerprint), 8);
+        f.write(reinterpret_cast<const char*>(b.targets.data()), nrows * 4ull);
+        f.write(reinterpret_cast<const char*>(b.offsets.data()), (nrows + 1) * 8ull);
+        f.write(reinterpret_cast<const char*>(b.runs.data()), total * 4ull);
+        if (!f) throw Error(CPD_E_IO, "write failed: " + tmp);
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path);
+}
+
+CpdBucket read_bucket(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw Error(CPD_E_IO, "cannot open " + path);
+    char magic[8];
+    f.read(magic, 8);
+    if (!f || std::memcmp(magic, kBucketMagic, 8) != 0) throw Error(CPD_E_IO, path + ": not a CPD bucket file");
+    CpdBucket b;
+    uint32_t h32[6];
+    uint64_t total = 0;
+    f.read(reinterpret_cast<char*>(h32), sizeof h32);
+    f.read(reinterpret_cast<char*>(&total), 8);
+    f.read(reinterpret_cast<char*>(&b.fingerprint), 8);
+    if (!f) throw Error(CPD_E_IO, path + ": truncated header");
+    b.n = h32[0];
+    uint32_t nrows = h32[1];
+    b.bid = h32[2];
+    b.method = h32[3];
+    b.key = h32[4];
+    b.maxworker = h32[5];
+    b.targets.resize(nrows);
+    b.offsets.resize((size_t)nrows + 1);
+    b.runs.resize(total);
+    f.read(reinterpret_cast<char*>(b.targets.data()), nrows * 4ull);
+    f.read(reinterpret_cast<char*>(b.offsets.data()), (nrows + 1) * 8ull);
+    f.read(reinterpret_cast<char*>(b.runs.data()), total * 4ull);
+    if (!f) throw Error(CPD_E_IO, path + ": truncated body");
+    if (b.offsets[0] != 0 || b.offsets[nrows] != total) throw Error(CPD_E_IO, path + ": bad offsets");
+    return b;
+}
+
+void write_order(const std::string& path, uint64_t fp, const std::vector<uint32_t>& order) {
+    std::string tmp = path + ".tmp." + std::to_string(::getpid());
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) throw Error(CPD_E_IO, "cannot write " + tmp);
+        uint32_t n = (uint32_t)order.size();
+        f.write(kOrderMagic, 8);
+        f.write(reinterpret_cast<const char*>(&n), 4);
+        f.write(reinterpret_cast<const char*>(&fp), 8);
+        f.write(reinterpret_cast<const char*>(order.data()), n * 4ull);
+        if (!f) throw Error(CPD_E_IO, "write failed: " + tmp);
+    }
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path);
+}
+
+std::vector<uint32_t> read_order(const std::string& path, uint64_t fp) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw Error(CPD_E_IO, "cannot open " + path);
+    char magic[8];
+    uint32_t n = 0;
+    uint64_t got = 0;
+    f.read(magic, 8);
+    f.read(reinterpret_cast<char*>(&n), 4);
+    f.read(reinterpret_cast<char*>(&got), 8);
+    if (!f || std::memcmp(magic, kOrderMagic, 8) != 0) throw Error(CPD_E_IO, path + ": not an order file");
+    if (got != fp) throw Error(CPD_E_IO, path + ": built for a different graph");
+    std::vector<uint32_t> order(n);
+    f.read(reinterpret_cast<char*>(order.data()), n * 4ull);
+    if (!f) throw Error(CPD_E_IO, path + ": truncated");
+    return order;
+}
+
+}  // namespace io
+}  // namespace cpd

@@ -1,0 +1,64 @@
+// File formats on the drop-in boundary (host C++; used by bin/* tools).
+//
+//   .xy    graph: 3 comment lines, "nodes N edges M" on line 4 (read by
+//          process_query.get_node_num, process_query.py:126-130), then
+//          "v id x y" and "e from to cost" lines.  Out-edge k of a node is its
+//          k-th "e" line (file order) [U: warthog xy_graph].
+//   .diff  congested weights: "e from to cost" (or "from to cost") lines, each
+//          replacing the weight of the first from->to edge [U].
+//   .scen  scenario: "q s t" lines (process_query.read_p2p, :22-32).
+//   query  "{n}\n" then n lines "s t" (process_query.send_queries, :93-96).
+//   .cpd   one file per partition bucket (README.md:86-93 "one or more CPDs"),
+//          our own layout == the HBM layout, so a load is one read + one copy.
+//   .order the DFS column order shared by every bucket of a graph.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace cpd {
+namespace io {
+
+struct XYGraph {
+    uint32_t n = 0, m = 0;
+    std::vector<uint32_t> row_ptr, dst, w;
+    std::vector<int32_t> x, y;
+};
+
+XYGraph read_xy(const std::string& path);
+void write_xy(const std::string& path, uint32_t n, const uint32_t* row_ptr,
+              const uint32_t* dst, const uint32_t* w, const int32_t* x, const int32_t* y);
+
+// Weights after applying a .diff to `g` ("-" or "" = free-flow copy).
+std::vector<uint32_t> read_diff(const std::string& path, const XYGraph& g);
+void write_diff(const std::string& path, const XYGraph& g, const std::vector<uint32_t>& w_cong);
+
+using Pairs = std::vector<std::pair<uint32_t, uint32_t>>;
+Pairs read_scen(const std::string& path);
+void write_scen(const std::string& path, const Pairs& q);
+Pairs read_query_file(const std::string& path);
+
+uint64_t graph_fingerprint(uint32_t n, const uint32_t* row_ptr, const uint32_t* dst,
+                           const uint32_t* w);
+
+struct CpdBucket {
+    uint32_t n = 0, bid = 0, method = 0, key = 0, maxworker = 0;
+    uint64_t fingerprint = 0;
+    std::vector<uint32_t> targets;
+    std::vector<uint64_t> offsets;
+    std::vector<uint32_t> runs;
+};
+
+std::string xy_stem(const std::string& xy_path);
+std::string bucket_path(const std::string& outdir, const std::string& xy_path,
+                        const std::string& method, uint32_t key, uint32_t bid);
+std::string order_path(const std::string& outdir, const std::string& xy_path);
+
+void write_bucket(const std::string& path, const CpdBucket& b);
+CpdBucket read_bucket(const std::string& path);
+void write_order(const std::string& path, uint64_t fingerprint, const std::vector<uint32_t>& order);
+std::vector<uint32_t> read_order(const std::string& path, uint64_t fingerprint);
+
+}  // namespace io
+}  // namespace cpd

@@ -1,0 +1,33 @@
+// Host-callable launchers for the gfx950 kernels in cpd_kernels.hip.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+
+namespace cpd {
+
+// One CH sweep level: `count` node slots starting at `slot0` of the
+// level-ordered node list; grid (count, slabs) x 256 threads, one slab =
+// 1024 targets of the B-wide batch row.
+void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
+                  const uint32_t* arcs /* (col, w) pairs */, uint32_t slot0, uint32_t count, uint32_t* dist,
+                  const uint32_t* tgt, uint32_t B, uint32_t slabs, hipStream_t s);
+
+void launch_first_moves(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
+                        const uint32_t* dist, const uint32_t* tgt, uint32_t B,
+                        uint32_t rows, uint32_t n, uint32_t npad, uint16_t* fm,
+                        hipStream_t s);
+
+void launch_rle(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* runs,
+                uint32_t cap, uint32_t* counts, hipStream_t s);
+
+void launch_compact(const uint32_t* scratch, uint32_t cap, const uint64_t* off,
+                    uint32_t nrows, uint32_t* out, hipStream_t s);
+
+void launch_table_search(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
+                         const uint32_t* row_of_col, const uint64_t* offsets,
+                         const uint32_t* runs, const uint32_t* qs, const uint32_t* qt,
+                         uint32_t nq, int32_t kmoves, uint32_t n, uint64_t* cost,
+                         uint32_t* hops, uint8_t* fin, unsigned long long* agg,
+                         hipStream_t s);
+
+}  // namespace cpd

@@ -1,0 +1,190 @@
+// cpd_plan: the once-per-graph host preprocessing (column order + hierarchy).
+#include <cstring>
+#include <fstream>
+#include <memory>
+
+#include "cpd_internal.hpp"
+
+using namespace cpd;
+
+namespace {
+
+const char kPlanMagic[8] = {'D', 'O', 'S', 'P', 'L', 'A', 'N', '1'};
+
+template <class T>
+void put_vec(std::ofstream& f, const std::vector<T>& v) {
+    uint64_t k = v.size();
+    f.write(reinterpret_cast<const char*>(&k), sizeof k);
+    if (k) f.write(reinterpret_cast<const char*>(v.data()), k * sizeof(T));
+}
+
+template <class T>
+void get_vec(std::ifstream& f, std::vector<T>& v) {
+    uint64_t k = 0;
+    f.read(reinterpret_cast<char*>(&k), sizeof k);
+    CPD_REQUIRE(f && k < (1ull << 40), CPD_E_IO, "plan file truncated");
+    v.resize(k);
+    if (k) f.read(reinterpret_cast<char*>(v.data()), k * sizeof(T));
+    CPD_REQUIRE(f, CPD_E_IO, "plan file truncated");
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpd_plan_create(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
+                    uint32_t n, uint32_t m, const cpd_plan_opts* opts, cpd_plan** out) {
+    return guarded([&] {
+        CPD_REQUIRE(out, CPD_E_ARG, "plan: null output");
+        *out = nullptr;
+        check_csr(n, m, row_ptr, dst, w);
+        auto p = std::make_unique<cpd_plan>();
+        p->n = n;
+        p->m = m;
+        p->row_ptr.assign(row_ptr, row_ptr + n + 1);
+        p->dst.assign(dst, dst + m);
+        p->w.assign(w, w + m);
+        p->order.resize(n);
+        dfs_preorder(n, row_ptr, dst, p->order.data());
+        p->inv.resize(n);
+        for (uint32_t v = 0; v < n; ++v) p->inv[p->order[v]] = v;
+        p->dist_bound = distance_bound(n, row_ptr, dst, w);
+        CPD_REQUIRE(p->dist_bound < 0xFFFFFFFFull, CPD_E_RANGE,
+                    "graph distances may reach 2^32-1; the u32 distance path "
+                    "cannot represent them");
+        int threads = opts ? opts->threads : 0;
+        uint32_t settle = opts ? opts->witness_settle : 0;
+        int verbose = opts ? opts->verbose : 0;
+        if (!(opts && opts->no_hierarchy)) {
+            double t0 = now_seconds();
+            p->ch = build_hierarchy(n, row_ptr, dst, w, threads, settle, verbose);
+            p->ch_seconds = now_seconds() - t0;
+        }
+        *out = p.release();
+    });
+}
+
+int cpd_plan_info_get(const cpd_plan* p, cpd_plan_info* info) {
+    return guarded([&] {
+        CPD_REQUIRE(p && info, CPD_E_ARG, "plan info: null argument");
+        info->n = p->n;
+        info->m = p->m;
+        CPD_REQUIRE(p->ch.up_off.empty() || p->ch.up_off.size() == (size_t)p->n + 1, CPD_E_ARG,
+                    "plan hierarchy inconsistent");
+        info->ch_up_arcs = p->ch.up_off.empty() ? 0 : p->ch.up_off[p->n];
+        info->ch_dn_arcs = p->ch.dn_off.empty() ? 0 : p->ch.dn_off[p->n];
+        info->levels_up = p->ch.nlev_up;
+        info->levels_dn = p->ch.nlev_dn;
+        info->dist_bound = p->dist_bound;
+        info->ch_seconds = p->ch_seconds;
+    });
+}
+
+int cpd_plan_order(const cpd_plan* p, uint32_t* order) {
+    return guarded([&] {
+        CPD_REQUIRE(p && order, CPD_E_ARG, "plan order: null argument");
+        std::memcpy(order, p->order.data(), p->n * sizeof(uint32_t));
+    });
+}
+
+int cpd_plan_export_ch(const cpd_plan* p, uint32_t* rank, uint64_t* up_off,
+                       uint32_t* up_dst, uint32_t* up_w, uint64_t* dn_off,
+                       uint32_t* dn_dst, uint32_t* dn_w, uint32_t* level_up,
+                       uint32_t* level_dn) {
+    return guarded([&] {
+        CPD_REQUIRE(p, CPD_E_ARG, "plan export: null plan");
+        CPD_REQUIRE(!p->ch.rank.empty(), CPD_E_ARG, "plan has no hierarchy");
+        const Hierarchy& H = p->ch;
+        auto cp = [](auto* dstp, const auto& v) {
+            if (dstp && !v.empty()) std::memcpy(dstp, v.data(), v.size() * sizeof(v[0]));
+        };
+        cp(rank, H.rank);
+        cp(up_off, H.up_off);
+        cp(up_dst, H.up_dst);
+        cp(up_w, H.up_w);
+        cp(dn_off, H.dn_off);
+        cp(dn_dst, H.dn_dst);
+        cp(dn_w, H.dn_w);
+        cp(level_up, H.level_up);
+        cp(level_dn, H.level_dn);
+    });
+}
+
+int cpd_plan_save(const cpd_plan* p, const char* path) {
+    return guarded([&] {
+        CPD_REQUIRE(p && path, CPD_E_ARG, "plan save: null argument");
+        std::string tmp = std::string(path) + ".tmp";
+        {
+            std::ofstream f(tmp, std::ios::binary);
+            CPD_REQUIRE(f, CPD_E_IO, std::string("cannot write ") + tmp);
+            f.write(kPlanMagic, 8);
+            uint32_t hdr[4] = {p->n, p->m, p->ch.nlev_up, p->ch.nlev_dn};
+            f.write(reinterpret_cast<const char*>(hdr), sizeof hdr);
+            f.write(reinterpret_cast<const char*>(&p->dist_bound), 8);
+            f.write(reinterpret_cast<const char*>(&p->ch_seconds), 8);
+            put_vec(f, p->row_ptr);
+            put_vec(f, p->dst);
+            put_vec(f, p->w);
+            put_vec(f, p->order);
+            const Hierarchy& H = p->ch;
+            put_vec(f, H.rank);
+            put_vec(f, H.up_off);
+            put_vec(f, H.up_dst);
+            put_vec(f, H.up_w);
+            put_vec(f, H.dn_off);
+            put_vec(f, H.dn_dst);
+            put_vec(f, H.dn_w);
+            put_vec(f, H.level_up);
+            put_vec(f, H.level_dn);
+            CPD_REQUIRE(f, CPD_E_IO, "plan write failed");
+        }
+        CPD_REQUIRE(std::rename(tmp.c_str(), path) == 0, CPD_E_IO, "plan rename failed");
+    });
+}
+
+int cpd_plan_load(const char* path, cpd_plan** out) {
+    return guarded([&] {
+        CPD_REQUIRE(path && out, CPD_E_ARG, "plan load: null argument");
+        *out = nullptr;
+        std::ifstream f(path, std::ios::binary);
+        CPD_REQUIRE(f, CPD_E_IO, std::string("cannot open ") + path);
+        char magic[8];
+        f.read(magic, 8);
+        CPD_REQUIRE(f && std::memcmp(magic, kPlanMagic, 8) == 0, CPD_E_IO,
+                    "not a plan file");
+        auto p = std::make_unique<cpd_plan>();
+        uint32_t hdr[4];
+        f.read(reinterpret_cast<char*>(hdr), sizeof hdr);
+        f.read(reinterpret_cast<char*>(&p->dist_bound), 8);
+        f.read(reinterpret_cast<char*>(&p->ch_seconds), 8);
+        p->n = hdr[0];
+        p->m = hdr[1];
+        p->ch.nlev_up = hdr[2];
+        p->ch.nlev_dn = hdr[3];
+        get_vec(f, p->row_ptr);
+        get_vec(f, p->dst);
+        get_vec(f, p->w);
+        get_vec(f, p->order);
+        Hierarchy& H = p->ch;
+        get_vec(f, H.rank);
+        get_vec(f, H.up_off);
+        get_vec(f, H.up_dst);
+        get_vec(f, H.up_w);
+        get_vec(f, H.dn_off);
+        get_vec(f, H.dn_dst);
+        get_vec(f, H.dn_w);
+        get_vec(f, H.level_up);
+        get_vec(f, H.level_dn);
+        CPD_REQUIRE(p->row_ptr.size() == (size_t)p->n + 1 && p->order.size() == p->n &&
+                        (H.level_dn.size() == p->n || H.level_dn.empty()),
+                    CPD_E_IO, "plan file inconsistent");
+        check_csr(p->n, p->m, p->row_ptr.data(), p->dst.data(), p->w.data());
+        p->inv.resize(p->n);
+        for (uint32_t v = 0; v < p->n; ++v) p->inv[p->order[v]] = v;
+        *out = p.release();
+    });
+}
+
+void cpd_plan_free(cpd_plan* p) { delete p; }
+
+}  // extern "C"

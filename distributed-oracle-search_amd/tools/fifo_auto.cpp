@@ -1,0 +1,262 @@
+// bin/fifo_auto — drop-in for warthog's resident query server with
+// `--alg table-search` (make_fifos.py:20-21, README.md:107-111):
+//
+//   fifo_auto --input X.xy DIFF --partmethod {div|mod} --partkey K
+//             --workerid I --maxworker W --outdir D --alg table-search
+//             [--partition M] [--device G] [--fifo PATH] [--once]
+//
+// Loads the CPD buckets this worker owns onto its GPU, then serves requests on
+// /tmp/worker{I}.fifo (process_query.py:86).  A request is what
+// process_query.send_remote pipes in (process_query.py:66-79,89):
+//     {worker JSON config}\n<query file> <answer fifo> <diff file>\n
+// read until the writer closes.  The query file holds "{n}\n" + n "s t" lines
+// (process_query.py:93-96).  The answer is ONE line of 10 comma-separated
+// values on the answer FIFO (process_query.py:199-208):
+//     n_expanded,n_inserted,n_touched,n_updated,n_surplus,plen,finished,
+//     t_receive,t_astar,t_search
+// For table-search: n_expanded = plen = moves walked, finished = queries that
+// reached t, t_receive = read + upload ns, t_search = extraction kernel ns,
+// the A*-only fields are 0.  With "debug": true in the config, per-query
+// results are written to <query file>.res ("s t cost moves finished").
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "cli.hpp"
+#include "cpd_io.hpp"
+
+static double now() {
+    using namespace std::chrono;
+    return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+static volatile sig_atomic_t g_stop = 0;
+static void on_signal(int) { g_stop = 1; }
+
+// Value of a top-level key in the worker config (json.dumps output), as text.
+static std::string json_field(const std::string& js, const std::string& key) {
+    std::string pat = "\"" + key + "\"";
+    size_t p = js.find(pat);
+    if (p == std::string::npos) return "";
+    p = js.find(':', p + pat.size());
+    if (p == std::string::npos) return "";
+    ++p;
+    while (p < js.size() && js[p] == ' ') ++p;
+    size_t e = p;
+    while (e < js.size() && js[e] != ',' && js[e] != '}') ++e;
+    std::string v = js.substr(p, e - p);
+    while (!v.empty() && v.back() == ' ') v.pop_back();
+    return v;
+}
+
+static std::string read_all(const std::string& path) {
+    int fd = -1;
+    while ((fd = ::open(path.c_str(), O_RDONLY)) < 0) {
+        if (errno != EINTR || g_stop) return "";
+    }
+    std::string s;
+    char buf[4096];
+    for (;;) {
+        ssize_t k = ::read(fd, buf, sizeof buf);
+        if (k > 0) s.append(buf, (size_t)k);
+        else if (k == 0) break;
+        else if (errno != EINTR) break;
+    }
+    ::close(fd);
+    return s;
+}
+
+static bool write_answer(const std::string& path, const std::string& line) {
+    // process_query.send_remote mkfifo's the answer before writing the request
+    // (process_query.py:72-73); tolerate a late mkfifo for up to 10 s
+    for (int i = 0; i < 1000; ++i) {
+        struct stat st;
+        if (::stat(path.c_str(), &st) == 0) break;
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+    int fd = ::open(path.c_str(), O_WRONLY);
+    if (fd < 0) return false;
+    std::string out = line + "\n";
+    const char* p = out.data();
+    size_t left = out.size();
+    while (left) {
+        ssize_t k = ::write(fd, p, left);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            ::close(fd);
+            return false;
+        }
+        p += k;
+        left -= (size_t)k;
+    }
+    ::close(fd);
+    return true;
+}
+
+int main(int argc, char** argv) {
+    cli::Args a(argc, argv);
+    const auto& inputs = a.list("input");
+    std::string method = a.str_any({"partmethod", "partition"});
+    long long key = a.num("partkey", -1), wid = a.num("workerid", -1), W = a.num("maxworker", -1);
+    std::string alg = a.str("alg", "table-search");
+    if (inputs.empty() || method.empty() || key <= 0 || wid < 0 || W <= 0 || wid >= W) {
+        std::fprintf(stderr,
+                     "usage: fifo_auto --input X.xy [DIFF] --partmethod {div|mod} --partkey K "
+                     "--workerid I --maxworker W --outdir D --alg table-search\n");
+        return 2;
+    }
+    if (alg != "table-search") {
+        std::fprintf(stderr, "fifo_auto: only --alg table-search is implemented (got '%s')\n",
+                     alg.c_str());
+        return 2;
+    }
+    int mcode = cli::method_code(method);
+    std::string xy = inputs[0];
+    std::string outdir = a.str("outdir", ".");
+    std::string fifo = a.str("fifo", "/tmp/worker" + std::to_string(wid) + ".fifo");
+    bool once = a.has("once");
+    signal(SIGINT, on_signal);
+    signal(SIGTERM, on_signal);
+    signal(SIGPIPE, SIG_IGN);
+
+    cpd_index* ix = nullptr;
+    cpd_graph* dg = nullptr;
+    cpd_plan* plan = nullptr;
+    cpd::io::XYGraph g;
+    std::map<std::string, std::vector<uint32_t>> diff_cache;
+    std::string active_diff = "-";
+    try {
+        double t0 = now();
+        g = cpd::io::read_xy(xy);
+        uint64_t fp = cpd::io::graph_fingerprint(g.n, g.row_ptr.data(), g.dst.data(), g.w.data());
+        if (inputs.size() > 1) diff_cache[inputs[1]] = cpd::io::read_diff(inputs[1], g);
+        cpd_plan_opts o{};
+        o.no_hierarchy = 1;  // queries need the CSR + column order only
+        cli::check(cpd_plan_create(g.row_ptr.data(), g.dst.data(), g.w.data(), g.n, g.m, &o, &plan),
+                   "plan");
+        std::vector<uint32_t> order(g.n);
+        cli::check(cpd_plan_order(plan, order.data()), "order");
+        std::vector<uint32_t> stored = cpd::io::read_order(cpd::io::order_path(outdir, xy), fp);
+        if (stored != order) throw std::runtime_error("stored column order differs from this build's");
+        // this worker's buckets, concatenated
+        uint32_t nb = 0;
+        cli::check(cpd_partition_nbuckets(g.n, mcode, (uint32_t)key, &nb), "buckets");
+        std::vector<uint32_t> targets, runs;
+        std::vector<uint64_t> offsets{0};
+        for (uint32_t b = 0; b < nb; ++b) {
+            if (b % (uint32_t)W != (uint32_t)wid) continue;
+            auto bk = cpd::io::read_bucket(cpd::io::bucket_path(outdir, xy, method, (uint32_t)key, b));
+            if (bk.fingerprint != fp || bk.key != (uint32_t)key || bk.method != (uint32_t)mcode)
+                throw std::runtime_error("bucket " + std::to_string(b) + " was built for another graph/partition");
+            uint64_t base = runs.size();
+            targets.insert(targets.end(), bk.targets.begin(), bk.targets.end());
+            for (size_t r = 1; r < bk.offsets.size(); ++r) offsets.push_back(base + bk.offsets[r]);
+            runs.insert(runs.end(), bk.runs.begin(), bk.runs.end());
+        }
+        int ndev = 0;
+        cli::check(cpd_device_count(&ndev), "device count");
+        if (ndev == 0) throw std::runtime_error("no GPU visible (this build has no CPU path)");
+        int device = (int)a.num("device", wid % ndev);
+        cli::check(cpd_graph_create(plan, device, &dg), "graph upload");
+        cli::check(cpd_index_create(dg, targets.data(), (uint32_t)targets.size(), offsets.data(),
+                                    runs.data(), &ix),
+                   "index");
+        std::printf("fifo_auto: worker %lld: %zu rows, %zu runs on device %d, ready in %.3fs; "
+                    "listening on %s\n",
+                    wid, targets.size(), runs.size(), device, now() - t0, fifo.c_str());
+        std::fflush(stdout);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "fifo_auto: %s\n", e.what());
+        return 1;
+    }
+
+    if (::mkfifo(fifo.c_str(), 0666) != 0 && errno != EEXIST) {
+        std::fprintf(stderr, "fifo_auto: mkfifo %s: %s\n", fifo.c_str(), std::strerror(errno));
+        return 1;
+    }
+    while (!g_stop) {
+        std::string msg = read_all(fifo);
+        if (g_stop) break;
+        if (msg.empty()) continue;
+        size_t nl = msg.find('\n');
+        std::string conf = msg.substr(0, nl);
+        if (conf == "quit" || conf == "exit") break;
+        std::string rest = nl == std::string::npos ? "" : msg.substr(nl + 1);
+        char qfile[4096] = {0}, answer[4096] = {0}, dname[4096] = {0};
+        int got = std::sscanf(rest.c_str(), "%4095s %4095s %4095s", qfile, answer, dname);
+        if (got < 2) {
+            std::fprintf(stderr, "fifo_auto: malformed request: %s\n", msg.c_str());
+            continue;
+        }
+        std::string diff = got >= 3 ? dname : "-";
+        int k_moves = -1;
+        std::string km = json_field(conf, "k_moves");
+        if (!km.empty()) k_moves = std::atoi(km.c_str());
+        bool debug = json_field(conf, "debug") == "true";
+        std::string line = "0,0,0,0,0,0,0,0,0,0";
+        try {
+            double t0 = now();
+            auto q = cpd::io::read_query_file(qfile);
+            if (diff != active_diff) {
+                if (diff == "-" ) {
+                    cli::check(cpd_index_set_weights(ix, nullptr), "weights");
+                } else {
+                    auto it = diff_cache.find(diff);
+                    if (it == diff_cache.end())
+                        it = diff_cache.emplace(diff, cpd::io::read_diff(diff, g)).first;
+                    cli::check(cpd_index_set_weights(ix, it->second.data()), "weights");
+                }
+                active_diff = diff;
+            }
+            std::vector<uint32_t> s(q.size()), t(q.size());
+            for (size_t i = 0; i < q.size(); ++i) {
+                s[i] = q[i].first;
+                t[i] = q[i].second;
+            }
+            int rc = cpd_query_prepare(ix, s.data(), t.data(), (uint32_t)q.size());
+            if (rc != CPD_OK) throw std::runtime_error(cpd_last_error());
+            double t_receive = now() - t0;
+            cpd_query_stats st{};
+            rc = cpd_query_run(ix, k_moves, &st);
+            if (rc != CPD_OK) throw std::runtime_error(cpd_last_error());
+            if (debug) {
+                std::vector<uint64_t> cost(q.size());
+                std::vector<uint32_t> hops(q.size());
+                std::vector<uint8_t> fin(q.size());
+                cli::check(cpd_query_fetch(ix, cost.data(), hops.data(), fin.data()), "fetch");
+                std::string res = std::string(qfile) + ".res";
+                if (std::FILE* f = std::fopen(res.c_str(), "w")) {
+                    for (size_t i = 0; i < q.size(); ++i)
+                        std::fprintf(f, "%u %u %llu %u %u\n", s[i], t[i], (unsigned long long)cost[i],
+                                     hops[i], fin[i]);
+                    std::fclose(f);
+                }
+            }
+            char buf[512];
+            std::snprintf(buf, sizeof buf, "%llu,0,0,0,0,%llu,%llu,%lld,0,%lld",
+                          (unsigned long long)st.hops, (unsigned long long)st.hops,
+                          (unsigned long long)st.finished, (long long)(t_receive * 1e9),
+                          (long long)(st.kernel_ms * 1e6));
+            line = buf;
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "fifo_auto: request failed: %s\n", e.what());
+        }
+        if (!write_answer(answer, line))
+            std::fprintf(stderr, "fifo_auto: cannot write answer to %s\n", answer);
+        if (once) break;
+    }
+    cpd_index_free(ix);
+    cpd_graph_free(dg);
+    cpd_plan_free(plan);
+    return 0;
+}

@@ -1,0 +1,233 @@
+/*
+ * cpd_api.h — C ABI of the MI355X-native CPD engine (libcpd.so).
+ *
+ * The reference (eggeek/distributed-oracle-search) has no in-process FFI: its
+ * hot path lives in the warthog executables `make_cpd_auto` and
+ * `fifo_auto --alg table-search` (un-vendored submodule `pathfinding/`,
+ * README.md:6-7, install.sh:3-7), driven over a process boundary by
+ * make_cpds.py:20, make_fifos.py:21 and process_query.py:46,86-89.  This
+ * header is the boundary our replacement executables (bin/make_cpd_auto,
+ * bin/fifo_auto, bin/gen_distribute_conf) call, and the one a maintainer would
+ * bind from Python (ctypes) or any other FFI.  Every
+ * signature is plain C: pointers, sizes, status codes.  No torch types.
+ *
+ * Each entry point names the reference interface it replaces.  [U] marks
+ * upstream-warthog behaviour that cannot be verified here (source absent,
+ * SURVEY.md §0, §8c).
+ *
+ * Conventions
+ *   - Node ids are the 0-based ids of the .xy file.  A "column" is a node's
+ *     position in the DFS-preorder column order (warthog
+ *     cpd::compute_dfs_preorder [U]); CPD runs store column indices.
+ *   - Out-edge k of node n is the k-th `e n ...` line of the .xy file (file
+ *     order); first moves are these k (0..14; 15 is reserved).
+ *   - A run is `(start_column << 4) | move` (warthog rle_run32 [U]).
+ *   - Every function returns CPD_OK (0) or a negative CPD_E_* code and sets a
+ *     thread-local message readable with cpd_last_error().
+ *   - Functions marked [host] never touch a GPU and work without one.
+ *     Functions marked [gpu] fail loudly (CPD_E_HIP) when no gfx950 device is
+ *     present; there is no CPU fallback in this library.
+ */
+#ifndef CPD_API_H
+#define CPD_API_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPD_OK          0
+#define CPD_E_ARG      -1   /* bad argument / malformed input            */
+#define CPD_E_HIP      -2   /* HIP runtime error or no usable device     */
+#define CPD_E_OOM      -3   /* host or device allocation failed          */
+#define CPD_E_NOROW    -4   /* a query's target has no row in the index  */
+#define CPD_E_RANGE    -5   /* value out of supported range (degree>15,
+                               distances >= 2^32-1, N >= 2^28)            */
+#define CPD_E_IO       -6   /* file open/read/write/format error         */
+
+#define CPD_PART_DIV    0
+#define CPD_PART_MOD    1
+
+#define CPD_MAX_DEGREE 15u          /* 4-bit move field, 0xF reserved [U] */
+#define CPD_INF        0xFFFFFFFFu  /* unreachable distance              */
+#define CPD_FM_ALL     0xFFFFu      /* wildcard first-move set           */
+
+typedef struct cpd_plan  cpd_plan;   /* host-side preprocessing of one graph     */
+typedef struct cpd_graph cpd_graph;  /* a plan resident on one GPU               */
+typedef struct cpd_rows  cpd_rows;   /* a batch of built CPD rows (device)       */
+typedef struct cpd_index cpd_index;  /* CPD rows loaded for table-search (device) */
+
+/* Thread-local description of the last error. Never NULL. */
+const char* cpd_last_error(void);
+/* Library version string, e.g. "cpd-mi355x 0.1 gfx950". */
+const char* cpd_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* [host] Partitioner — replaces warthog util/distribution_controller.h,
+ * exposed by ./bin/gen_distribute_conf (README.md:31-34,75-80;
+ * process_query.py:46-53).  node -> (worker id, bucket id, index in bucket).
+ *   mod: bid = node % key, bidx = node / key
+ *   div: chunk = ceil(nodenum / key), bid = node / chunk, bidx = node % chunk
+ *   both: wid = bid % maxworker                                   [U]        */
+int cpd_partition(uint32_t nodenum, uint32_t maxworker, int method,
+                  uint32_t key, uint32_t node,
+                  uint32_t* wid, uint32_t* bid, uint32_t* bidx);
+/* Number of buckets a (nodenum, method, key) partition has. */
+int cpd_partition_nbuckets(uint32_t nodenum, int method, uint32_t key,
+                           uint32_t* nbuckets);
+
+/* [host] DFS-preorder column order — replaces warthog
+ * cpd::compute_dfs_preorder [U]: iterative DFS from node 0 (then from every
+ * still-unvisited node in id order), out-edges pushed in file order, so the
+ * last out-edge is explored first.  order[node] = column.                    */
+int cpd_dfs_preorder(uint32_t n, const uint32_t* row_ptr, const uint32_t* dst,
+                     uint32_t* order);
+
+/* [host] Synthetic grid-perturbed road graph.  W x H lattice,
+ * jittered coordinates, random spanning tree kept bidirectional (strongly
+ * connected), extra lattice edges (a share of them one-way) up to a mean
+ * out-degree `mean_outdeg`; weights ceil(euclid * speed * asym / 10) in
+ * [1, 65535]; node ids randomly permuted; out-edge order shuffled.
+ * Call once with row_ptr == NULL to get *n and *m, then again with buffers
+ * row_ptr[n+1], dst[m], w[m], x[n], y[n] (x / y may be NULL).               */
+int cpd_synth_road_graph(uint32_t width, uint32_t height, double mean_outdeg,
+                         uint64_t seed, uint32_t* n, uint32_t* m,
+                         uint32_t* row_ptr, uint32_t* dst, uint32_t* w,
+                         int32_t* x, int32_t* y);
+/* [host] Congested weights (the `.diff` stand-in): a share
+ * `frac` of the edges get w * U[lo, hi] rounded up; others unchanged.        */
+int cpd_synth_congestion(uint32_t m, const uint32_t* w, double frac, double lo,
+                         double hi, uint64_t seed, uint32_t* w_out);
+
+/* ------------------------------------------------------------------------ */
+/* [host] Preprocessing plan — the part of warthog's make_cpd_auto that runs
+ * once per graph (graph load, column order) [U], plus what the GPU build needs
+ * instead of a per-row Dijkstra: a contraction hierarchy (CH) with its
+ * up/down sweep levels (GPHAST-style one-to-all sweeps).                     */
+typedef struct cpd_plan_opts {
+    int      threads;          /* OpenMP threads for the CH build (0 = all)  */
+    uint32_t witness_settle;   /* witness-search settle limit (0 = default)  */
+    int      verbose;          /* print CH progress to stderr                */
+    int      no_hierarchy;     /* skip the CH: the plan can serve queries
+                                  (fifo_auto) but cannot build rows         */
+} cpd_plan_opts;
+
+typedef struct cpd_plan_info {
+    uint32_t n, m;
+    uint64_t ch_up_arcs;       /* arcs v->x with rank(x) > rank(v)           */
+    uint64_t ch_dn_arcs;       /* arcs u->v with rank(v) < rank(u)           */
+    uint32_t levels_up;        /* launches of the upward sweep               */
+    uint32_t levels_dn;        /* launches of the downward sweep             */
+    uint64_t dist_bound;       /* proven upper bound on any finite distance  */
+    double   ch_seconds;       /* wall time of the CH build                  */
+} cpd_plan_info;
+
+int  cpd_plan_create(const uint32_t* row_ptr, const uint32_t* dst,
+                     const uint32_t* w, uint32_t n, uint32_t m,
+                     const cpd_plan_opts* opts, cpd_plan** out);
+int  cpd_plan_info_get(const cpd_plan* p, cpd_plan_info* info);
+int  cpd_plan_order(const cpd_plan* p, uint32_t* order /* n */);
+/* Export the hierarchy in NODE space (for CPU-side checks):
+ * rank[n]; up CSR (up_off[n+1], up_dst, up_w); down CSR (dn_off[n+1],
+ * dn_dst, dn_w); level_up[n], level_dn[n].  Any pointer may be NULL.        */
+int  cpd_plan_export_ch(const cpd_plan* p, uint32_t* rank,
+                        uint64_t* up_off, uint32_t* up_dst, uint32_t* up_w,
+                        uint64_t* dn_off, uint32_t* dn_dst, uint32_t* dn_w,
+                        uint32_t* level_up, uint32_t* level_dn);
+int  cpd_plan_save(const cpd_plan* p, const char* path);
+int  cpd_plan_load(const char* path, cpd_plan** out);
+void cpd_plan_free(cpd_plan* p);
+
+/* ------------------------------------------------------------------------ */
+/* [gpu] Devices and graphs. */
+int  cpd_device_count(int* count);
+/* Upload a plan to `device` (column-space CSR, CH arcs, levels). */
+int  cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out);
+/* Batch width (rows built per sweep, multiple of 1024; 0 = auto from HBM). */
+int  cpd_graph_set_batch(cpd_graph* g, uint32_t batch);
+int  cpd_graph_get_batch(const cpd_graph* g, uint32_t* batch);
+void cpd_graph_free(cpd_graph* g);
+
+/* ------------------------------------------------------------------------ */
+/* [gpu] CPD row build — replaces the per-source loop of warthog
+ * make_cpd_auto (README.md:82-95; make_cpds.py:20): for each target t, the
+ * distances d(n,t) for all n (reverse search: rows are keyed by target
+ * because queries are routed to the worker owning t, process_query.py:56-57),
+ * the first-move sets FM_t(n) = {k : w(n->v_k) + d(v_k,t) = d(n,t)}
+ * (t itself and unreachable nodes: wildcard), and the greedy run-length row
+ * over the DFS column order with the lowest-set-bit tie-break
+ * (warthog graph_oracle::add_row [U]).  Rows stay in HBM; export copies them
+ * to the host.  `reuse` (may be NULL) recycles a previous result's buffers. */
+int  cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
+                    cpd_rows* reuse, cpd_rows** out);
+int  cpd_rows_count(const cpd_rows* r, uint32_t* nrows, uint64_t* total_runs);
+int  cpd_rows_export(const cpd_rows* r, uint64_t* offsets /* nrows+1 */,
+                     uint32_t* runs /* total_runs */);
+void cpd_rows_free(cpd_rows* r);
+
+/* [gpu] Inspection (tests): distances d(n,t) in NODE order, n-major
+ * (dist[node * ntargets + i]), and first-move sets fm[i * n + node].
+ * ntargets <= batch.  Either output may be NULL.                            */
+int  cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
+                    uint32_t* dist, uint16_t* fm);
+
+/* ------------------------------------------------------------------------ */
+/* [gpu] Table-search index — replaces fifo_auto's CPD load + `--alg
+ * table-search` extraction (make_fifos.py:20-21; README.md:110).            */
+int  cpd_index_create(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows,
+                      const uint64_t* offsets, const uint32_t* runs,
+                      cpd_index** out);
+/* Same, straight from device-resident rows (no host round trip). */
+int  cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out);
+/* Edge weights used for path cost (m entries, original edge order):
+ * NULL restores the free-flow weights; otherwise e.g. the .diff weights
+ * (process_query.py:89,178 sends the diff name with every batch).           */
+int  cpd_index_set_weights(cpd_index* ix, const uint32_t* w);
+
+typedef struct cpd_query_stats {
+    uint64_t queries;
+    uint64_t finished;      /* queries whose walk reached t                  */
+    uint64_t hops;          /* sum of moves taken (n_expanded / plen)        */
+    uint64_t cost;          /* sum of path costs                             */
+    double   kernel_ms;     /* device time of the extraction kernel          */
+} cpd_query_stats;
+
+/* Walk each query s -> t by repeated get_move(t, cur) (binary search in
+ * row(t) at column(cur), warthog graph_oracle::get_move [U]) and sum the
+ * selected weights.  k_moves < 0: walk to t (process_query.py:153 sends -1);
+ * otherwise stop after k moves.  cost/hops/finished may be NULL.
+ * Returns CPD_E_NOROW if some t has no row in this index.                    */
+int  cpd_query_batch(cpd_index* ix, const uint32_t* s, const uint32_t* t,
+                     uint32_t nq, int32_t k_moves, uint64_t* cost,
+                     uint32_t* hops, uint8_t* finished, cpd_query_stats* st);
+/* The same in three steps, so that a caller can keep the queries resident in
+ * HBM and time the extraction alone: prepare uploads (s, t) as columns,
+ * run launches the kernel (stats only), fetch copies per-query results.     */
+int  cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t,
+                       uint32_t nq);
+int  cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st);
+int  cpd_query_fetch(cpd_index* ix, uint64_t* cost, uint32_t* hops,
+                     uint8_t* finished);
+void cpd_index_free(cpd_index* ix);
+
+/* ------------------------------------------------------------------------ */
+/* [gpu] Per-kernel device timing (HIP events on the library's stream).      */
+typedef struct cpd_kernel_time {
+    char     name[32];
+    uint64_t launches;
+    double   ms;            /* summed device time                            */
+    double   bytes;         /* summed algorithmic bytes      */
+} cpd_kernel_time;
+
+int  cpd_timing_enable(cpd_graph* g, int enable);
+int  cpd_timing_reset(cpd_graph* g);
+/* Fills up to `max` entries, returns the number in *count. */
+int  cpd_timing_get(const cpd_graph* g, cpd_kernel_time* out, int max,
+                    int* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CPD_API_H */

@@ -1,0 +1,169 @@
+"""GPU parity: libcpd (HIP, gfx950) against the CPU oracle, bit-exact.
+
+Integer work, so the bar is exact equality: distances, first-move sets, RLE
+row words, per-query costs/hops/finished flags.  Inputs are seeded synthetic
+road graphs plus hand-built edge cases (unreachable nodes, degree-15 nodes,
+self loops, parallel edges, zero weights, a single node).
+"""
+import numpy as np
+import pytest
+
+import cpd
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph_from_edges(n, edges):
+    """edges: list of (a, b, w) in file order."""
+    rp = np.zeros(n + 1, np.uint32)
+    for a, _, _ in edges:
+        rp[a + 1] += 1
+    rp = np.cumsum(rp).astype(np.uint32)
+    pos = rp[:-1].copy()
+    dst = np.zeros(len(edges), np.uint32)
+    w = np.zeros(len(edges), np.uint32)
+    for a, b, c in edges:
+        dst[pos[a]] = b
+        w[pos[a]] = c
+        pos[a] += 1
+    return cpd.RoadGraph(rp, dst, w)
+
+
+def _irregular_graph():
+    rng = np.random.default_rng(5)
+    n = 300
+    edges = []
+    for a in range(n):
+        k = 15 if a == 17 else int(rng.integers(0, 5))
+        for _ in range(k):
+            b = int(rng.integers(0, n))
+            edges.append((a, b, int(rng.integers(0, 4))))  # zero weights too
+    edges.append((3, 3, 1))        # self loop
+    edges.append((5, 9, 2))        # parallel edge pair
+    edges.append((5, 9, 1))
+    # nodes 290..299: sources only / sinks only -> unreachable pairs
+    edges = [e for e in edges if not (e[1] >= 290)]
+    return _graph_from_edges(n, edges)
+
+
+GRAPHS = {
+    "synth": lambda: cpd.synth_road_graph(40, 30, seed=7),
+    "ties": lambda: (lambda g: cpd.RoadGraph(g.row_ptr, g.dst, (g.w % 3 + 1), g.x, g.y))(
+        cpd.synth_road_graph(24, 24, seed=11)),
+    "irregular": _irregular_graph,
+    "single": lambda: _graph_from_edges(1, []),
+}
+
+
+@pytest.fixture(scope="module", params=sorted(GRAPHS))
+def setup(request):
+    g = GRAPHS[request.param]()
+    plan = cpd.Plan(g)
+    dev = cpd.Graph(plan, batch=1024)
+    return request.param, g, plan, dev
+
+
+def test_distances_and_first_moves(setup):
+    name, g, plan, dev = setup
+    rng = np.random.default_rng(1)
+    targets = rng.choice(g.n, size=min(g.n, 37), replace=False).astype(np.uint32)
+    dist, fm = dev.debug_rows(targets)
+    for i, t in enumerate(targets):
+        ref = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, t)
+        np.testing.assert_array_equal(dist[:, i], ref, err_msg=f"{name} dist t={t}")
+        ref_fm = oracle.first_moves(g.row_ptr, g.dst, g.w, t)
+        np.testing.assert_array_equal(fm[i], ref_fm, err_msg=f"{name} fm t={t}")
+
+
+def test_rows_bit_exact(setup):
+    name, g, plan, dev = setup
+    targets = np.arange(g.n, dtype=np.uint32)[::-1].copy()  # all rows, reversed order
+    rows = dev.build_rows(targets)
+    off, runs = rows.export()
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    np.testing.assert_array_equal(off, ref_off, err_msg=name)
+    np.testing.assert_array_equal(runs, ref_runs, err_msg=name)
+
+
+def test_queries_free_flow_and_congested(setup):
+    name, g, plan, dev = setup
+    rng = np.random.default_rng(2)
+    targets = rng.choice(g.n, size=min(g.n, 50), replace=False).astype(np.uint32)
+    rows = dev.build_rows(targets)
+    off, runs = rows.export()
+    ix = cpd.Index(dev, rows=rows)
+    nq = 4000
+    s = rng.integers(0, g.n, nq).astype(np.uint32)
+    t = targets[rng.integers(0, len(targets), nq)]
+    cost, hops, fin, st = ix.query(s, t)
+    rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, plan.order(), targets, off, runs, s, t)
+    np.testing.assert_array_equal(cost, rc)
+    np.testing.assert_array_equal(hops, rh)
+    np.testing.assert_array_equal(fin, rf)
+    assert st["hops"] == int(rh.sum()) and st["finished"] == int(rf.sum())
+    assert st["cost"] == int(rc.sum())
+    # free-flow cost of a finished walk is the shortest distance
+    for q in range(0, nq, 97):
+        d = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, t[q])[s[q]]
+        if d != oracle.INF:
+            assert fin[q] == 1 and cost[q] == d
+    # congested weights: same walk, other weights
+    wc = cpd.synth_congestion(g.w, frac=0.3, lo=1.0, hi=3.0, seed=3)
+    ix.set_weights(wc)
+    cost2, hops2, fin2, _ = ix.query(s, t)
+    rc2, rh2, rf2 = oracle.table_search(g.row_ptr, g.dst, wc, plan.order(), targets, off, runs, s, t)
+    np.testing.assert_array_equal(cost2, rc2)
+    np.testing.assert_array_equal(hops2, rh2)
+    ix.set_weights(None)
+    cost3, _, _, _ = ix.query(s, t)
+    np.testing.assert_array_equal(cost3, rc)
+    # k_moves cut-off
+    cost4, hops4, fin4, _ = ix.query(s, t, k_moves=3)
+    rc4, rh4, rf4 = oracle.table_search(g.row_ptr, g.dst, g.w, plan.order(), targets, off, runs,
+                                        s, t, k_moves=3)
+    np.testing.assert_array_equal(cost4, rc4)
+    np.testing.assert_array_equal(hops4, rh4)
+    np.testing.assert_array_equal(fin4, rf4)
+
+
+def test_index_from_host_arrays_and_norow():
+    g = GRAPHS["synth"]()
+    plan = cpd.Plan(g)
+    dev = cpd.Graph(plan, batch=1024)
+    targets = np.arange(0, g.n, 7, dtype=np.uint32)
+    rows = dev.build_rows(targets)
+    off, runs = rows.export()
+    a = cpd.Index(dev, rows=rows)
+    b = cpd.Index(dev, row_targets=targets, offsets=off, runs=runs)
+    rng = np.random.default_rng(4)
+    s = rng.integers(0, g.n, 1000).astype(np.uint32)
+    t = targets[rng.integers(0, len(targets), 1000)]
+    ca = a.query(s, t)
+    cb = b.query(s, t)
+    for x, y in zip(ca[:3], cb[:3]):
+        np.testing.assert_array_equal(x, y)
+    with pytest.raises(cpd.CpdError) as ei:
+        a.query(np.array([0], np.uint32), np.array([1], np.uint32))  # node 1: no row
+    assert ei.value.code == cpd.CPD_E_NOROW
+    # empty batch
+    c, h, f, st = a.query(np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+    assert len(c) == 0 and st["queries"] == 0
+
+
+def test_multi_batch_and_reuse():
+    """ntargets > batch: rows are built in several sweeps and appended in order."""
+    g = cpd.synth_road_graph(50, 50, seed=9)
+    plan = cpd.Plan(g)
+    dev = cpd.Graph(plan, batch=1024)
+    rng = np.random.default_rng(6)
+    targets = rng.integers(0, g.n, 2500).astype(np.uint32)  # duplicates allowed
+    rows = dev.build_rows(targets)
+    off, runs = rows.export()
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    np.testing.assert_array_equal(off, ref_off)
+    np.testing.assert_array_equal(runs, ref_runs)
+    rows2 = dev.build_rows(targets[:100], reuse=rows)
+    off2, runs2 = rows2.export()
+    np.testing.assert_array_equal(off2, ref_off[:101])
+    np.testing.assert_array_equal(runs2, ref_runs[: int(ref_off[100])])
