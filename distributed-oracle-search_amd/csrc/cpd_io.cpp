@@ -137,10 +137,10 @@ XYGraph read_xy(const std::string& path) {
 
 void write_xy(const std::string& path, uint32_t n, const uint32_t* row_ptr, const uint32_t* dst,
               const uint32_t* w, const int32_t* x, const int32_t* y) {
+    std::vector<char> buf(1 << 20);  // outlives the FILE (closed by guard first)
     std::FILE* f = std::fopen(path.c_str(), "wb");
     if (!f) throw Error(CPD_E_IO, "cannot write " + path);
     std::unique_ptr<std::FILE, int (*)(std::FILE*)> guard(f, std::fclose);
-    std::vector<char> buf(1 << 20);
     std::setvbuf(f, buf.data(), _IOFBF, buf.size());
     std::fprintf(f, "c cpd-mi355x xy graph\nc nodes are 0-based; edges grouped by tail in out-edge order\nc\n");
     std::fprintf(f, "nodes %u edges %u\n", n, row_ptr[n]);

@@ -1,0 +1,51 @@
+"""Seeded test graphs shared by the CPU and GPU suites."""
+import numpy as np
+
+import cpd
+
+
+def graph_from_edges(n, edges):
+    """edges: list of (a, b, w) in file order."""
+    rp = np.zeros(n + 1, np.uint32)
+    for a, _, _ in edges:
+        rp[a + 1] += 1
+    rp = np.cumsum(rp).astype(np.uint32)
+    pos = rp[:-1].copy()
+    dst = np.zeros(len(edges), np.uint32)
+    w = np.zeros(len(edges), np.uint32)
+    for a, b, c in edges:
+        dst[pos[a]] = b
+        w[pos[a]] = c
+        pos[a] += 1
+    return cpd.RoadGraph(rp, dst, w)
+
+
+def irregular_graph():
+    """Unreachable pairs, a degree-15 node, a self loop, parallel and 0-weight edges."""
+    rng = np.random.default_rng(5)
+    n = 300
+    edges = []
+    for a in range(n):
+        k = 15 if a == 17 else int(rng.integers(0, 5))
+        for _ in range(k):
+            b = int(rng.integers(0, n))
+            edges.append((a, b, int(rng.integers(0, 4))))
+    edges.append((3, 3, 1))        # self loop
+    edges.append((5, 9, 2))        # parallel edge pair
+    edges.append((5, 9, 1))
+    edges = [e for e in edges if not (e[1] >= 290)]   # nodes 290.. are never entered
+    return graph_from_edges(n, edges)
+
+
+def tie_graph():
+    """Tiny weights -> many equal-cost paths (multi-bit first-move sets)."""
+    g = cpd.synth_road_graph(24, 24, seed=11)
+    return cpd.RoadGraph(g.row_ptr, g.dst, (g.w % 3 + 1).astype(np.uint32), g.x, g.y)
+
+
+GRAPHS = {
+    "synth": lambda: cpd.synth_road_graph(40, 30, seed=7),
+    "ties": tie_graph,
+    "irregular": irregular_graph,
+    "single": lambda: graph_from_edges(1, []),
+}

@@ -10,50 +10,9 @@ import pytest
 
 import cpd
 import oracle
+from graphs import GRAPHS
 
 pytestmark = pytest.mark.gpu
-
-
-def _graph_from_edges(n, edges):
-    """edges: list of (a, b, w) in file order."""
-    rp = np.zeros(n + 1, np.uint32)
-    for a, _, _ in edges:
-        rp[a + 1] += 1
-    rp = np.cumsum(rp).astype(np.uint32)
-    pos = rp[:-1].copy()
-    dst = np.zeros(len(edges), np.uint32)
-    w = np.zeros(len(edges), np.uint32)
-    for a, b, c in edges:
-        dst[pos[a]] = b
-        w[pos[a]] = c
-        pos[a] += 1
-    return cpd.RoadGraph(rp, dst, w)
-
-
-def _irregular_graph():
-    rng = np.random.default_rng(5)
-    n = 300
-    edges = []
-    for a in range(n):
-        k = 15 if a == 17 else int(rng.integers(0, 5))
-        for _ in range(k):
-            b = int(rng.integers(0, n))
-            edges.append((a, b, int(rng.integers(0, 4))))  # zero weights too
-    edges.append((3, 3, 1))        # self loop
-    edges.append((5, 9, 2))        # parallel edge pair
-    edges.append((5, 9, 1))
-    # nodes 290..299: sources only / sinks only -> unreachable pairs
-    edges = [e for e in edges if not (e[1] >= 290)]
-    return _graph_from_edges(n, edges)
-
-
-GRAPHS = {
-    "synth": lambda: cpd.synth_road_graph(40, 30, seed=7),
-    "ties": lambda: (lambda g: cpd.RoadGraph(g.row_ptr, g.dst, (g.w % 3 + 1), g.x, g.y))(
-        cpd.synth_road_graph(24, 24, seed=11)),
-    "irregular": _irregular_graph,
-    "single": lambda: _graph_from_edges(1, []),
-}
 
 
 @pytest.fixture(scope="module", params=sorted(GRAPHS))

@@ -1,0 +1,137 @@
+"""The CPU oracle, pinned before it is trusted.
+
+- distances against scipy.sparse.csgraph.dijkstra (independent implementation);
+- hand-worked known-answer vectors for first-move sets, RLE rows, get_move and
+  table-search (tests/golden/known_answers.json, derived by hand below);
+- structural properties of every RLE row (run starts strictly increase from
+  column 0; every column's move is one of its optimal first moves; greedy
+  maximality: no run can absorb the next column).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+from scipy.sparse import csr_matrix
+from scipy.sparse.csgraph import dijkstra
+
+import cpd
+import oracle
+
+KA = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
+
+
+def _csr(g):
+    rows = np.repeat(np.arange(g.n), np.diff(g.row_ptr.astype(np.int64)))
+    # scipy keeps the minimum over duplicate entries only via min-reduction; build
+    # explicitly so parallel edges keep the lightest weight
+    best = {}
+    for a, b, w in zip(rows, g.dst, g.w):
+        if a == b:
+            continue
+        best[(a, b)] = min(best.get((a, b), w), w)
+    if not best:
+        return csr_matrix((g.n, g.n))
+    ab = np.array(list(best.keys()))
+    w = np.array(list(best.values()), np.float64)
+    # scipy treats explicit zeros as missing: nudge zero weights, compare after rounding
+    return csr_matrix((np.where(w == 0, 1e-9, w), (ab[:, 0], ab[:, 1])), shape=(g.n, g.n))
+
+
+@pytest.fixture(scope="module")
+def graphs():
+    from graphs import GRAPHS  # the same cases as the GPU suite
+    return {k: f() for k, f in GRAPHS.items()}
+
+
+def test_distances_match_scipy(graphs):
+    rng = np.random.default_rng(0)
+    for name, g in graphs.items():
+        A = _csr(g).T.tocsr()
+        for t in rng.choice(g.n, size=min(g.n, 12), replace=False):
+            ref = dijkstra(A, indices=[t])[0]
+            got = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, t).astype(np.float64)
+            got[got == oracle.INF] = np.inf
+            np.testing.assert_array_equal(got, np.round(ref), err_msg=f"{name} t={t}")
+
+
+def _check_row(g, order, t, runs):
+    fm = oracle.first_moves(g.row_ptr, g.dst, g.w, t)
+    n = g.n
+    starts = runs >> 4
+    assert starts[0] == 0 and np.all(np.diff(starts.astype(np.int64)) > 0)
+    inv = np.empty(n, np.int64)
+    inv[order] = np.arange(n)
+    run_of_col = np.searchsorted(starts, np.arange(n), side="right") - 1
+    moves = (runs & 0xF)[run_of_col]
+    f = fm[inv].astype(np.int64)
+    assert np.all((f >> moves) & 1), "a column's move is not an optimal first move"
+    # greedy maximality: run r's AND with the first column of run r+1 is empty
+    for r in range(len(runs) - 1):
+        a, b = int(starts[r]), int(starts[r + 1])
+        acc = np.bitwise_and.reduce(f[a:b + 1])
+        assert acc == 0
+
+
+def test_rle_rows_properties(graphs):
+    rng = np.random.default_rng(3)
+    for name, g in graphs.items():
+        order = oracle.dfs_preorder(g.row_ptr, g.dst)
+        targets = rng.choice(g.n, size=min(g.n, 10), replace=False)
+        off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, targets)
+        for i, t in enumerate(targets):
+            row = runs[off[i]:off[i + 1]]
+            _check_row(g, order, t, row)
+            # get_move == the move of the run covering each column
+            for col in (0, g.n // 2, g.n - 1):
+                j = np.searchsorted(row >> 4, col, side="right") - 1
+                assert oracle.get_move(row, col) == (row[j] & 0xF)
+
+
+def _ka_graph(case):
+    from graphs import graph_from_edges
+    return graph_from_edges(case["n"], [tuple(e) for e in case["edges"]])
+
+
+@pytest.mark.parametrize("case", KA["cases"], ids=lambda c: c["name"])
+def test_known_answers(case):
+    g = _ka_graph(case)
+    order = oracle.dfs_preorder(g.row_ptr, g.dst)
+    assert order.tolist() == case["order"]
+    for t_s, exp in case["rows"].items():
+        t = int(t_s)
+        assert oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, t).tolist() == exp["dist"]
+        assert oracle.first_moves(g.row_ptr, g.dst, g.w, t).tolist() == exp["fm"]
+        off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, [t])
+        assert runs.tolist() == exp["runs"]
+    for q in case["queries"]:
+        targets = sorted({int(k) for k in case["rows"]})
+        off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, targets)
+        cost, hops, fin = oracle.table_search(g.row_ptr, g.dst, g.w, order, targets, off, runs,
+                                              [q["s"]], [q["t"]])
+        assert [int(cost[0]), int(hops[0]), int(fin[0])] == [q["cost"], q["hops"], q["finished"]]
+
+
+def test_free_flow_extraction_is_shortest(graphs):
+    rng = np.random.default_rng(8)
+    for name, g in graphs.items():
+        order = oracle.dfs_preorder(g.row_ptr, g.dst)
+        targets = rng.choice(g.n, size=min(g.n, 8), replace=False).astype(np.uint32)
+        off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, targets)
+        s = rng.integers(0, g.n, 300).astype(np.uint32)
+        t = targets[rng.integers(0, len(targets), 300)]
+        cost, hops, fin = oracle.table_search(g.row_ptr, g.dst, g.w, order, targets, off, runs, s, t)
+        for q in range(300):
+            d = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, t[q])[s[q]]
+            if d == oracle.INF:
+                continue
+            if np.all(g.w > 0):
+                assert fin[q] == 1 and cost[q] == d, (name, q)
+
+
+def test_missing_row_raises():
+    g = cpd.synth_road_graph(5, 5, seed=1)
+    order = oracle.dfs_preorder(g.row_ptr, g.dst)
+    off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, [3])
+    with pytest.raises(KeyError):
+        oracle.table_search(g.row_ptr, g.dst, g.w, order, [3], off, runs, [0], [4])
