@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py — MI355X CPD build (sources/s, GTEPS) and table-search (queries/s).
+
+Workload (BASELINE.json configs[3]; melb-both.xy is a missing blob, so the
+1M-node synthetic road graph the north star names is the headline graph):
+  synthetic grid-perturbed road graph, 1000 x 1000 lattice (1M nodes, 2.5M
+  edges), seed 1; partition `div 8` over the ranks (distribution_controller
+  semantics), one rank per GPU.  A step = one batch of `--batch` CPD rows built
+  from the rank's own targets: two CH sweeps, first-move sets and the RLE rows,
+  all resident in HBM (weak scaling: every rank builds the same number of rows
+  per step; no collective on the data path).  After the timed steps each rank
+  runs `--queries` table-search queries against its last batch of rows.
+
+One JSON line on rank 0: value = rows/s over all ranks; roofline for the
+dominant kernel from HIP events; cpu_baseline = the C oracle (OpenMP) on a
+bounded sample of the same workload, rank 0 at N = 1 only.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1 is launched by torch.distributed.run; RANK/LOCAL_RANK/WORLD_SIZE)
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "distributed-oracle-search_amd")
+METRIC = "CPD build sources/sec + GTEPS; table-search queries/sec; % HBM roofline"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1000, help="lattice side (nodes = width^2)")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--partmethod", default="div")
+    ap.add_argument("--partkey", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=4096, help="rows per step (multiple of 1024)")
+    ap.add_argument("--queries", type=int, default=1_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--cpu-rows-per-thread", type=int, default=4)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
+    ap.add_argument("--cache", default=os.environ.get("CPD_BENCH_CACHE", "/tmp/cpd-bench-cache"))
+    return ap.parse_args()
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world == 1:
+        # not under torch.distributed.run: launch ourselves that way (a child,
+        # before anything touches the GPU)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+               "--master-port", os.environ.get("MASTER_PORT", "29517"), __file__] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch  # first: libcpd then binds to the same HIP runtime
+    import torch.distributed as dist
+
+    sys.path.insert(0, PKG)
+    import cpd
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def allreduce(vals, op):
+        if world == 1:
+            return vals
+        t = torch.tensor(vals, dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=op)
+        return t.tolist()
+
+    # ---- graph + host preprocessing (cached, built once per node) ----------
+    t0 = time.time()
+    g = cpd.synth_road_graph(args.width, args.width, seed=args.seed)
+    os.makedirs(args.cache, exist_ok=True)
+    plan_path = os.path.join(args.cache, f"synth{args.width}-s{args.seed}.plan")
+    if local == 0 and not os.path.exists(plan_path):
+        log(f"building hierarchy for {g.n} nodes / {g.m} edges ...")
+        p = cpd.Plan(g)
+        p.save(plan_path)
+    if world > 1:
+        dist.barrier()
+    plan = cpd.Plan.load(plan_path)
+    pinfo = plan.info()
+    assert pinfo["n"] == g.n and pinfo["m"] == g.m
+    t_setup = time.time() - t0
+    log(f"rank {rank}: plan ready in {t_setup:.1f}s (hierarchy build {pinfo['ch_seconds']:.1f}s, "
+        f"{pinfo['ch_up_arcs'] + pinfo['ch_dn_arcs']} arcs, levels {pinfo['levels_up']}+"
+        f"{pinfo['levels_dn']})")
+
+    dev = cpd.Graph(plan, device=local, batch=args.batch)
+    B = dev.batch
+    owned = cpd.owned_nodes(g.n, world, args.partmethod, args.partkey, rank)
+    if len(owned) == 0:
+        raise SystemExit(f"rank {rank} owns no targets")
+
+    def batch(i):
+        idx = (np.arange(B, dtype=np.int64) + i * B) % len(owned)
+        return owned[idx]
+
+    rows = None
+    for i in range(args.warmup):
+        rows = dev.build_rows(batch(i), reuse=rows)
+    dev.timing(not args.no_timing)
+    dev.timing_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        rows = dev.build_rows(batch(args.warmup + i), reuse=rows)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    (elapsed_max,) = allreduce([elapsed], dist.ReduceOp.MAX if world > 1 else None)
+    kt = dev.timing_get()
+    dev.timing(False)
+    nrows, nruns = rows.count()
+    last_targets = batch(args.warmup + args.steps - 1)
+
+    # ---- table-search on the last batch's rows ------------------------------
+    ix = cpd.Index(dev, rows=rows)
+    rng = np.random.default_rng(100 + rank)
+    nq = args.queries
+    qs = rng.integers(0, g.n, nq).astype(np.uint32)
+    qt = last_targets[rng.integers(0, len(last_targets), nq)]
+    ix.prepare(qs, qt)
+    ix.run()  # warm
+    q_ms, q_hops, q_fin = 0.0, 0, 0
+    reps = 3
+    for _ in range(reps):
+        st = ix.run()
+        q_ms += st["kernel_ms"]
+        q_hops += st["hops"]
+        q_fin += st["finished"]
+    q_sum = allreduce([float(nq * reps), q_ms, float(q_hops)], dist.ReduceOp.SUM if world > 1 else None)
+    (q_ms_max,) = allreduce([q_ms], dist.ReduceOp.MAX if world > 1 else None)
+
+    # ---- CPU baseline + full-size parity sample (rank 0, N = 1) -------------
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        sample = batch(0)[: threads * args.cpu_rows_per_thread]
+        order = plan.order()
+        tc = time.perf_counter()
+        ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, sample, threads=threads)
+        cpu_s = time.perf_counter() - tc
+        grows = dev.build_rows(sample)
+        goff, gruns = grows.export()
+        parity = bool(np.array_equal(goff, ref_off) and np.array_equal(gruns, ref_runs))
+        cq = 20000
+        cs = rng.integers(0, g.n, cq).astype(np.uint32)
+        ct = sample[rng.integers(0, len(sample), cq)]
+        tq = time.perf_counter()
+        rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, order, sample, ref_off, ref_runs,
+                                         cs, ct, threads=threads)
+        cpu_q_s = time.perf_counter() - tq
+        gix = cpd.Index(dev, rows=grows)
+        gc, gh, gf, _ = gix.query(cs, ct)
+        parity = parity and bool(np.array_equal(gc, rc) and np.array_equal(gh, rh))
+        cpu = {"value": round(len(sample) / cpu_s, 3), "unit": "sources/s", "cores": threads,
+               "kind": "port",
+               "sample": f"{len(sample)} CPD rows of the same graph and partition (reverse Dijkstra "
+                         f"+ first moves + RLE, C oracle, OpenMP {threads} threads, {cpu_s:.1f}s); "
+                         f"table-search {cq} queries in {cpu_q_s:.2f}s",
+               "queries_per_s": round(cq / cpu_q_s, 1)}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    total_rows = world * args.steps * B
+    value = total_rows / elapsed_max
+    roof = None
+    if kt:
+        name, k = max(kt.items(), key=lambda kv: kv[1]["ms"])
+        achieved = k["bytes"] / (k["ms"] / 1e3) / 1e9 if k["ms"] > 0 else 0.0
+        roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": None, "launches": k["launches"],
+                "avg_launch_us": round(k["ms"] * 1e3 / max(1, k["launches"]), 3),
+                "bytes_per_launch": round(k["bytes"] / max(1, k["launches"]), 1)}
+    qps = q_sum[0] / (q_ms_max / 1e3) if q_ms_max > 0 else 0.0
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "sources/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded grid-perturbed road graph; melb-both.xy blob is missing)",
+        "config": {"workload": f"synthetic-{g.n // 1000}k-road cpd-build {args.partmethod} "
+                               f"{args.partkey} + table-search",
+                   "graph": f"grid-perturbed {args.width}x{args.width} seed {args.seed}",
+                   "nodes": g.n, "edges": g.m, "rows_per_step_per_gpu": B,
+                   "partition": f"{args.partmethod} {args.partkey}",
+                   "parallelism": f"target-partition x{world} (no collective)"},
+        "gteps": round(value * g.m / 1e9, 3),
+        "queries_per_s": round(qps, 1),
+        "query_mean_moves": round(q_sum[2] / max(1.0, q_sum[0]), 1),
+        "mean_runs_per_row": round(nruns / max(1, nrows), 1),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "parity_sample_bit_exact": parity,
+        "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                        "GBps": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] else 0}
+                    for k, v in kt.items()},
+        "hierarchy": {"arcs": pinfo["ch_up_arcs"] + pinfo["ch_dn_arcs"],
+                      "levels": [pinfo["levels_up"], pinfo["levels_dn"]],
+                      "build_s": round(pinfo["ch_seconds"], 1)},
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

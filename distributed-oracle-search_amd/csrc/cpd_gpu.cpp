@@ -85,10 +85,10 @@ struct cpd_graph {
     uint64_t ch_arcs = 0;
     bool has_ch = false;
     // batch workspace
-    uint32_t B = 0, cap = 0;
-    DevBuf<uint32_t> dist, tgt, scratch, counts;
+    uint32_t B = 0;
+    DevBuf<uint32_t> dist, tgt, counts;
     DevBuf<uint16_t> fm;
-    DevBuf<uint64_t> off_dev;
+    DevBuf<uint64_t> row_off;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -150,23 +150,18 @@ struct cpd_graph {
         if (want == 0) {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-            // per target: dist 4n + fm 2npad + scratch 4cap(<= n/4 typical)
-            double per = 4.0 * n + 2.0 * npad + 4.0 * std::max<uint32_t>(1024, n / 4);
+            // per target: dist 4n + fm 2npad + output runs (<= 4n, ~2.5n typical)
+            double per = 4.0 * n + 2.0 * npad + 4.0 * n;
             double fit = 0.4 * (double)free_b / per;
             want = (uint32_t)std::min(8192.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
         }
         want = (want + 1023u) / 1024u * 1024u;
         if (want == B && dist.p) return;
         B = want;
-        // RLE scratch: up to 4 GiB, at least 1024 runs per row, at most n+1
-        uint64_t c = (4ull << 30) / (4ull * B);
-        cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c, 1024), (uint64_t)n + 1);
         dist.alloc((size_t)n * B);
         fm.alloc((size_t)B * npad);
         tgt.alloc(B);
-        scratch.alloc((size_t)B * cap);
         counts.alloc(B);
-        off_dev.alloc((size_t)B + 1);
     }
 };
 
@@ -198,6 +193,12 @@ struct cpd_index {
 };
 
 namespace {
+
+// Host mirror of the kernels' tiled first-move row layout (cpd_kernels.hip).
+uint32_t fm_pos_host(uint32_t c) {
+    const uint32_t r = c & (kFmTile - 1u);
+    return (c & ~(kFmTile - 1u)) + ((r >> 3) & 3u) * 512u + (r >> 5) * 8u + (r & 7u);
+}
 
 void require_device() {
     int count = 0;
@@ -273,7 +274,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         const uint32_t n = p->n, m = p->m;
         g->n = n;
         g->m = m;
-        g->npad = (n + 511u) / 512u * 512u;
+        g->npad = (n + kFmTile - 1u) / kFmTile * kFmTile;
         g->order = p->order;
         g->inv = p->inv;
         // column-space CSR, per-node out-edge order preserved (moves = file order)
@@ -399,15 +400,15 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k) {
 void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r) {
     upload_targets(g, targets, k);
     run_sweeps_and_fm(g, k);
-    const uint32_t cap = g->cap, npad = g->npad;
-    g->timed("rle_rows", 2.0 * npad * k, [&] {
-        launch_rle(g->fm.p, npad, k, g->scratch.p, cap, g->counts.p, g->stream);
+    const uint32_t npad = g->npad;
+    g->timed("rle_count", 2.0 * npad * k + 4.0 * k, [&] {
+        launch_rle_count(g->fm.p, npad, k, g->counts.p, g->stream);
     });
     std::vector<uint32_t> counts(k);
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, g->stream));
     g->sync();
-    // compact offsets for this batch, appended after r->total
+    // row offsets for this batch, appended after r->total
     std::vector<uint64_t> off(k + 1);
     off[0] = r->total;
     for (uint32_t i = 0; i < k; ++i) off[i + 1] = off[i] + counts[i];
@@ -424,27 +425,11 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
         r->runs.p = np;
         r->runs.n = want;
     }
-    g->off_dev.upload(off.data(), k + 1, g->stream);
-    // rows that fit the scratch cap: one compaction launch
-    double cbytes = 8.0 * (double)(new_total - r->total);
-    g->timed("compact_rows", cbytes, [&] {
-        launch_compact(g->scratch.p, cap, g->off_dev.p, k, r->runs.p, g->stream);
+    g->row_off.upload(off.data(), k + 1, g->stream);
+    double ebytes = 2.0 * npad * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
+    g->timed("rle_emit", ebytes, [&] {
+        launch_rle_emit(g->fm.p, npad, k, g->row_off.p, r->runs.p, g->stream);
     });
-    // rows past the cap (rare): re-run the scan alone into a full-size buffer
-    std::vector<uint32_t> big;
-    for (uint32_t i = 0; i < k; ++i)
-        if (counts[i] > cap) big.push_back(i);
-    if (!big.empty()) {
-        DevBuf<uint32_t> full, cnt1;
-        full.alloc((size_t)g->n + 1);
-        cnt1.alloc(1);
-        for (uint32_t i : big) {
-            launch_rle(g->fm.p + (size_t)i * npad, npad, 1, full.p, g->n + 1, cnt1.p, g->stream);
-            HIP_CHECK(hipMemcpyAsync(r->runs.p + off[i], full.p, counts[i] * sizeof(uint32_t),
-                                     hipMemcpyDeviceToDevice, g->stream));
-        }
-        HIP_CHECK(hipStreamSynchronize(g->stream));
-    }
     g->sync();
     r->offsets.insert(r->offsets.end(), off.begin() + 1, off.end());
     r->targets.insert(r->targets.end(), targets, targets + k);
@@ -529,7 +514,7 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
                                 hipMemcpyDeviceToHost));
             for (uint32_t i = 0; i < ntargets; ++i)
                 for (uint32_t v = 0; v < n; ++v)
-                    fm[(size_t)i * n + v] = h[(size_t)i * g->npad + g->order[v]];
+                    fm[(size_t)i * n + v] = h[(size_t)i * g->npad + fm_pos_host(g->order[v])];
         }
     });
 }

@@ -22,6 +22,18 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t d, uint32_t w) {
     return (s < d) ? INF : s;  // d == INF or overflow -> INF
 }
 
+// First-move rows are stored tiled for the RLE scan: a 2048-column tile holds,
+// for each of 4 chunk slots q and 64 lanes, 8 columns — lane l's 32 columns
+// (32l .. 32l+31 of the tile) are 4 uint4 at q*64 + l, so each of the scan's
+// 4 loads is one fully coalesced 1-KiB wave access.
+constexpr uint32_t kSeg = 32;          // columns per lane
+constexpr uint32_t kTile = 64 * kSeg;  // columns per wave tile
+
+__device__ __forceinline__ uint32_t fm_pos(uint32_t c) {
+    const uint32_t r = c & (kTile - 1u);
+    return (c & ~(kTile - 1u)) + ((r >> 3) & 3u) * 512u + (r >> 5) * 8u + (r & 7u);
+}
+
 __device__ __forceinline__ void min4(uint4& acc, const uint4 d, uint32_t w) {
     acc.x = min(acc.x, sat_add(d.x, w));
     acc.y = min(acc.y, sat_add(d.y, w));
@@ -76,10 +88,10 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
     d4[(size_t)v * B4 + l4] = acc;
 }
 
-// First-move sets.  Block (x = 64-column tile, y = 256-target slab); thread =
-// one target, walks the tile's 64 columns: fm = bits k with
+// First-move sets.  Block (x = 64-column group, y = 256-target slab); thread =
+// one target, walks the group's 64 columns: fm = bits k with
 // w_k + d(dst_k) == d(c) (wildcard at the target and unreachable columns),
-// then writes the 128-B row segment fm[target][c0 .. c0+64).
+// then stores them into the target's tiled row (fm_pos).
 __global__ __launch_bounds__(256) void first_moves(const uint32_t* __restrict__ row_ptr,
                                                    const uint32_t* __restrict__ dst,
                                                    const uint32_t* __restrict__ w,
@@ -112,107 +124,117 @@ __global__ __launch_bounds__(256) void first_moves(const uint32_t* __restrict__ 
         }
         packed[p] = two;
     }
-    uint4* out = reinterpret_cast<uint4*>(fm + (size_t)j * npad + c0);
+    // tiled store: the thread's 64 columns are two lane segments of 32
+    uint16_t* rowp = fm + (size_t)j * npad;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-        out[q] = make_uint4(packed[4 * q], packed[4 * q + 1], packed[4 * q + 2], packed[4 * q + 3]);
+        *reinterpret_cast<uint4*>(rowp + fm_pos(c0 + 8u * q)) =
+            make_uint4(packed[4 * q], packed[4 * q + 1], packed[4 * q + 2], packed[4 * q + 3]);
 }
 
-__device__ __forceinline__ uint32_t pick8(const uint32_t (&v)[8], int j) {
-    uint32_t r = v[0];
+// One lane's greedy pass over its 32 columns (warthog graph_oracle::add_row
+// [U]: keep S = AND of the current run's first-move sets; a column that would
+// empty S ends the run — word (head << 4 | lowest bit of S) — and starts a new
+// one at that column).  v holds the segment's 32 u16 sets, two per register.
+template <bool EMIT>
+__device__ __forceinline__ void seg_pass(const uint32_t (&v)[16], uint32_t c0, uint32_t& h,
+                                         uint32_t& S, uint32_t& cnt, uint32_t* stage) {
 #pragma unroll
-    for (int k = 1; k < 8; ++k) r = (j == k) ? v[k] : r;
-    return r;
-}
-
-// Greedy RLE of one row per wave (warthog graph_oracle::add_row [U]).  A chunk
-// is 512 columns: lane l holds columns 8l..8l+7 (one 16-B load).  Given the
-// running intersection S, the first column where S & AND(cols) becomes 0 is
-// found with a lane-local prefix AND, a wave-wide exclusive AND-scan of the
-// lane totals and a ballot; the run is emitted, S restarts at that column and
-// the chunk is rescanned past it.  Output: runs[row*cap + i], counts[row]
-// (the true count, even past `cap`; the host re-runs overflowing rows).
-__global__ __launch_bounds__(256) void rle_rows(const uint16_t* __restrict__ fm,
-                                                uint32_t npad, uint32_t nrows,
-                                                uint32_t* __restrict__ runs,
-                                                uint32_t cap,
-                                                uint32_t* __restrict__ counts) {
-    const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (row >= nrows) return;
-    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(fm + (size_t)row * npad);
-    uint32_t* __restrict__ out = runs + (size_t)row * cap;
-    uint32_t S = 0xFFFFu, head = 0, cnt = 0;
-    const uint32_t nchunks = npad / 512u;
-    uint4 q = src[lane];
-    for (uint32_t ch = 0; ch < nchunks; ++ch) {
-        const uint4 cur = q;
-        if (ch + 1 < nchunks) q = src[(size_t)(ch + 1) * 64u + lane];
-        uint32_t v[8] = {cur.x & 0xFFFFu, cur.x >> 16, cur.y & 0xFFFFu, cur.y >> 16,
-                         cur.z & 0xFFFFu, cur.z >> 16, cur.w & 0xFFFFu, cur.w >> 16};
-        int p = 0;  // first local column not yet consumed
-        for (;;) {
-            uint32_t P[8];
-            uint32_t acc = 0xFFFFu;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t val = (lane * 8 + j < p) ? 0xFFFFu : v[j];
-                acc &= val;
-                P[j] = acc;
-            }
-            uint32_t x = acc;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(x, off, 64);
-                if (lane >= off) x &= y;
-            }
-            uint32_t E = __shfl_up(x, 1, 64);
-            if (lane == 0) E = 0xFFFFu;
-            const uint32_t base = S & E;
-            const unsigned long long mask = __ballot((base & acc) == 0u);
-            if (mask == 0ull) {
-                S &= __shfl(x, 63, 64);
-                break;
-            }
-            const int L = __ffsll(mask) - 1;
-            int j0 = 7;
-            uint32_t before = base;
-#pragma unroll
-            for (int j = 7; j >= 0; --j)
-                if ((base & P[j]) == 0u) j0 = j;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < j0) before = base & P[j];
-            const uint32_t bval = pick8(v, j0);
-            j0 = __shfl(j0, L, 64);
-            before = __shfl(before, L, 64);
-            const uint32_t newS = __shfl(bval, L, 64);
-            const int bl = L * 8 + j0;
-            if (lane == 0 && cnt < cap) out[cnt] = (head << 4) | (uint32_t)__builtin_ctz(before);
-            ++cnt;
-            head = ch * 512u + (uint32_t)bl;
-            S = newS;
-            p = bl + 1;
-            if (p >= 512) break;
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t f = (k & 1) ? (v[k >> 1] >> 16) : (v[k >> 1] & 0xFFFFu);
+        const bool brk = (S & f) == 0u;
+        if (EMIT) {
+            if (brk) stage[cnt] = (h << 4) | (uint32_t)__builtin_ctz(S);
         }
+        cnt += brk ? 1u : 0u;
+        h = brk ? c0 + (uint32_t)k : h;
+        S = brk ? f : (S & f);
+    }
+}
+
+// Greedy RLE, one row per wave, 2048-column tiles (lane l owns columns
+// 32l..32l+31 of the tile).  The scan is sequential by definition, so each
+// lane first speculates a fresh run at its segment start, then re-runs from
+// its predecessor's end state until no lane's input changes: with typical
+// run lengths every lane resynchronises inside its own segment and two passes
+// suffice; the loop is exact for any input (at most 64 rounds).
+// COUNT: counts[row] = runs in the row.  EMIT: runs written at off[row],
+// staged per tile in LDS and stored coalesced.
+template <bool EMIT>
+__global__ __launch_bounds__(256) void rle_scan(const uint16_t* __restrict__ fm, uint32_t npad,
+                                                uint32_t nrows, uint32_t* __restrict__ counts,
+                                                const uint64_t* __restrict__ off,
+                                                uint32_t* __restrict__ runs) {
+    __shared__ uint32_t stage_all[EMIT ? 4 * kTile : 1];
+    const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (row >= nrows) return;
+    uint32_t* stage = stage_all + (EMIT ? (threadIdx.x >> 6) * kTile : 0);
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(fm + (size_t)row * npad);
+    uint32_t* __restrict__ out = EMIT ? runs + off[row] : nullptr;
+    uint32_t carry_h = 0, carry_S = 0xFFFFu, total = 0;
+    const uint32_t ntiles = npad / kTile;
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        uint32_t v[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 x = src[(size_t)t * 256u + q * 64u + lane];
+            v[4 * q] = x.x;
+            v[4 * q + 1] = x.y;
+            v[4 * q + 2] = x.z;
+            v[4 * q + 3] = x.w;
+        }
+        const uint32_t c0 = t * kTile + lane * kSeg;
+        // speculative pass: a run starts at the segment (lane 0: true carry)
+        uint32_t in_h = lane == 0 ? carry_h : c0, in_S = lane == 0 ? carry_S : 0xFFFFu;
+        uint32_t eh = in_h, eS = in_S, cnt = 0;
+        seg_pass<false>(v, c0, eh, eS, cnt, nullptr);
+        for (int round = 0; round < 64; ++round) {
+            uint32_t nh = __shfl_up(eh, 1, 64), nS = __shfl_up(eS, 1, 64);
+            if (lane == 0) {
+                nh = carry_h;
+                nS = carry_S;
+            }
+            const bool need = nh != in_h || nS != in_S;
+            if (!__any(need)) break;
+            if (need) {
+                in_h = nh;
+                in_S = nS;
+                eh = nh;
+                eS = nS;
+                cnt = 0;
+                seg_pass<false>(v, c0, eh, eS, cnt, nullptr);
+            }
+        }
+        // inclusive scan of per-lane run counts
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += y;
+        }
+        const uint32_t tile_total = __shfl(incl, 63, 64);
+        if (EMIT) {
+            uint32_t h = in_h, S = in_S, k = 0;
+            seg_pass<true>(v, c0, h, S, k, stage + (incl - cnt));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t i = lane; i < tile_total; i += 64u) out[total + i] = stage[i];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        total += tile_total;
+        carry_h = __shfl(eh, 63, 64);
+        carry_S = __shfl(eS, 63, 64);
     }
     if (lane == 0) {
-        if (cnt < cap) out[cnt] = (head << 4) | (uint32_t)__builtin_ctz(S);
-        ++cnt;
-        counts[row] = cnt;
+        if (EMIT)
+            out[total] = (carry_h << 4) | (uint32_t)__builtin_ctz(carry_S);
+        else
+            counts[row] = total + 1;  // + the final run
     }
-}
-
-// Copy each row's runs from the scratch slab to its compact offset.
-__global__ __launch_bounds__(256) void compact_rows(const uint32_t* __restrict__ scratch,
-                                                    uint32_t cap,
-                                                    const uint64_t* __restrict__ off,
-                                                    uint32_t* __restrict__ out) {
-    const uint32_t row = blockIdx.x;
-    const uint64_t b = off[row], e = off[row + 1];
-    const uint32_t len = (uint32_t)(e - b);
-    const uint32_t* s = scratch + (size_t)row * cap;
-    for (uint32_t i = threadIdx.x; i < len; i += 256u) out[b + i] = s[i];
 }
 
 // Table-search extraction, one lane per query.  cur/t are columns; the run for
@@ -319,14 +341,15 @@ void launch_first_moves(const uint32_t* row_ptr, const uint32_t* dst, const uint
     kern::first_moves<<<grid, 256, 0, s>>>(row_ptr, dst, w, dist, tgt, B, n, npad, fm);
 }
 
-void launch_rle(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* runs,
-                uint32_t cap, uint32_t* counts, hipStream_t s) {
-    kern::rle_rows<<<(nrows + 3u) / 4u, 256, 0, s>>>(fm, npad, nrows, runs, cap, counts);
+void launch_rle_count(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* counts,
+                      hipStream_t s) {
+    kern::rle_scan<false><<<(nrows + 3u) / 4u, 256, 0, s>>>(fm, npad, nrows, counts, nullptr,
+                                                            nullptr);
 }
 
-void launch_compact(const uint32_t* scratch, uint32_t cap, const uint64_t* off,
-                    uint32_t nrows, uint32_t* out, hipStream_t s) {
-    kern::compact_rows<<<nrows, 256, 0, s>>>(scratch, cap, off, out);
+void launch_rle_emit(const uint16_t* fm, uint32_t npad, uint32_t nrows, const uint64_t* off,
+                     uint32_t* runs, hipStream_t s) {
+    kern::rle_scan<true><<<(nrows + 3u) / 4u, 256, 0, s>>>(fm, npad, nrows, nullptr, off, runs);
 }
 
 void launch_table_search(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,

@@ -17,11 +17,15 @@ void launch_first_moves(const uint32_t* row_ptr, const uint32_t* dst, const uint
                         uint32_t rows, uint32_t n, uint32_t npad, uint16_t* fm,
                         hipStream_t s);
 
-void launch_rle(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* runs,
-                uint32_t cap, uint32_t* counts, hipStream_t s);
+// Row width of the tiled first-move rows: npad is a multiple of this.
+constexpr uint32_t kFmTile = 2048;
 
-void launch_compact(const uint32_t* scratch, uint32_t cap, const uint64_t* off,
-                    uint32_t nrows, uint32_t* out, hipStream_t s);
+// Greedy RLE scan, one wave per row: runs per row, then the runs themselves
+// written at off[row] (uint64 offsets into `runs`).
+void launch_rle_count(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* counts,
+                      hipStream_t s);
+void launch_rle_emit(const uint16_t* fm, uint32_t npad, uint32_t nrows, const uint64_t* off,
+                     uint32_t* runs, hipStream_t s);
 
 void launch_table_search(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
                          const uint32_t* row_of_col, const uint64_t* offsets,
