@@ -31,7 +31,7 @@ METRIC = "CPD build sources/sec + GTEPS; table-search queries/sec; % HBM rooflin
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -40,19 +40,114 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--partmethod", default="div")
     ap.add_argument("--partkey", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=4096, help="rows per step (multiple of 1024)")
+    ap.add_argument("--batch", type=int, default=8192, help="rows per step (multiple of 1024)")
     ap.add_argument("--queries", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
-    ap.add_argument("--cpu-rows-per-thread", type=int, default=4)
+    ap.add_argument("--cpu-rows-per-thread", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--cache", default=os.environ.get("CPD_BENCH_CACHE", "/tmp/cpd-bench-cache"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
+
+# --------------------------------------------------------------------------
+# distributed plumbing (importable; tests/test_bench_dist.py runs it on gloo)
+
+class Comm:
+    """Barrier / reductions over torch.distributed.  Only the bench harness
+    uses them (timing and a handful of counters); nothing on the data path."""
+
+    def __init__(self, world, rank, local, device=None):
+        self.world, self.rank, self.local, self.device = world, rank, local, device
+
+    def barrier(self):
+        import torch
+        if self.device is not None:
+            torch.cuda.synchronize()
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def reduce(self, vals, op):
+        if self.world == 1:
+            return list(vals)
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor(vals, dtype=torch.float64, device=self.device or "cpu")
+        dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
+        return t.tolist()
+
+
+def shard_targets(nodenum, world, method, key, rank):
+    """The rank's targets: distribution_controller partition, worker = rank."""
+    sys.path.insert(0, PKG)
+    import cpd
+    return cpd.owned_nodes(nodenum, world, method, key, rank)
+
+
+def batch_of(owned, B, i):
+    """Step i's targets: the next B of the rank's own, wrapping around."""
+    import numpy as np
+    idx = (np.arange(B, dtype=np.int64) + i * B) % len(owned)
+    return owned[idx]
+
+
+def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows, nruns,
+             kt, cpu, parity, pinfo):
+    """Rank 0's JSON line.  value = rows built by ALL ranks / max rank time."""
+    n, m = graph_info
+    total_rows = world * args.steps * B
+    value = total_rows / elapsed_max
+    roof = None
+    if kt:
+        name, k = max(kt.items(), key=lambda kv: kv[1]["ms"])
+        achieved = k["bytes"] / (k["ms"] / 1e3) / 1e9 if k["ms"] > 0 else 0.0
+        roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": None, "launches": k["launches"],
+                "avg_launch_us": round(k["ms"] * 1e3 / max(1, k["launches"]), 3),
+                "bytes_per_launch": round(k["bytes"] / max(1, k["launches"]), 1)}
+    qps = q_totals[0] / (q_ms_max / 1e3) if q_ms_max > 0 else 0.0
+    return {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "sources/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded grid-perturbed road graph; melb-both.xy blob is missing)",
+        "config": {"workload": f"synthetic-{n // 1000}k-road cpd-build {args.partmethod} "
+                               f"{args.partkey} + table-search",
+                   "graph": f"grid-perturbed {args.width}x{args.width} seed {args.seed}",
+                   "nodes": n, "edges": m, "rows_per_step_per_gpu": B,
+                   "partition": f"{args.partmethod} {args.partkey}",
+                   "parallelism": f"target-partition x{world} (no collective)"},
+        "gteps": round(value * m / 1e9, 3),
+        "queries_per_s": round(qps, 1),
+        "query_mean_moves": round(q_totals[2] / max(1.0, q_totals[0]), 1),
+        "mean_runs_per_row": round(nruns / max(1, nrows), 1),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "parity_sample_bit_exact": parity,
+        "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
+                        "GBps": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] else 0}
+                    for k, v in (kt or {}).items()},
+        "hierarchy": {"arcs": pinfo["ch_up_arcs"] + pinfo["ch_dn_arcs"],
+                      "levels": [pinfo["levels_up"], pinfo["levels_dn"]],
+                      "build_s": round(pinfo["ch_seconds"], 1)} if pinfo else None,
+    }
+
+
+# --------------------------------------------------------------------------
 
 def main():
     args = parse()
@@ -77,18 +172,7 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-
-    def allreduce(vals, op):
-        if world == 1:
-            return vals
-        t = torch.tensor(vals, dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=op)
-        return t.tolist()
+    comm = Comm(world, rank, local, device=f"cuda:{local}")
 
     # ---- graph + host preprocessing (cached, built once per node) ----------
     t0 = time.time()
@@ -97,44 +181,37 @@ def main():
     plan_path = os.path.join(args.cache, f"synth{args.width}-s{args.seed}.plan")
     if local == 0 and not os.path.exists(plan_path):
         log(f"building hierarchy for {g.n} nodes / {g.m} edges ...")
-        p = cpd.Plan(g)
-        p.save(plan_path)
-    if world > 1:
-        dist.barrier()
+        cpd.Plan(g).save(plan_path)
+    comm.barrier()
     plan = cpd.Plan.load(plan_path)
     pinfo = plan.info()
     assert pinfo["n"] == g.n and pinfo["m"] == g.m
-    t_setup = time.time() - t0
-    log(f"rank {rank}: plan ready in {t_setup:.1f}s (hierarchy build {pinfo['ch_seconds']:.1f}s, "
-        f"{pinfo['ch_up_arcs'] + pinfo['ch_dn_arcs']} arcs, levels {pinfo['levels_up']}+"
-        f"{pinfo['levels_dn']})")
+    log(f"rank {rank}: plan ready in {time.time() - t0:.1f}s (hierarchy build "
+        f"{pinfo['ch_seconds']:.1f}s, {pinfo['ch_up_arcs'] + pinfo['ch_dn_arcs']} arcs, levels "
+        f"{pinfo['levels_up']}+{pinfo['levels_dn']})")
 
     dev = cpd.Graph(plan, device=local, batch=args.batch)
     B = dev.batch
-    owned = cpd.owned_nodes(g.n, world, args.partmethod, args.partkey, rank)
+    owned = shard_targets(g.n, world, args.partmethod, args.partkey, rank)
     if len(owned) == 0:
         raise SystemExit(f"rank {rank} owns no targets")
 
-    def batch(i):
-        idx = (np.arange(B, dtype=np.int64) + i * B) % len(owned)
-        return owned[idx]
-
     rows = None
     for i in range(args.warmup):
-        rows = dev.build_rows(batch(i), reuse=rows)
+        rows = dev.build_rows(batch_of(owned, B, i), reuse=rows)
     dev.timing(not args.no_timing)
     dev.timing_reset()
-    barrier()
+    comm.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        rows = dev.build_rows(batch(args.warmup + i), reuse=rows)
-    barrier()
+        rows = dev.build_rows(batch_of(owned, B, args.warmup + i), reuse=rows)
+    comm.barrier()
     elapsed = time.perf_counter() - t0
-    (elapsed_max,) = allreduce([elapsed], dist.ReduceOp.MAX if world > 1 else None)
+    (elapsed_max,) = comm.reduce([elapsed], "MAX")
     kt = dev.timing_get()
     dev.timing(False)
     nrows, nruns = rows.count()
-    last_targets = batch(args.warmup + args.steps - 1)
+    last_targets = batch_of(owned, B, args.warmup + args.steps - 1)
 
     # ---- table-search on the last batch's rows ------------------------------
     ix = cpd.Index(dev, rows=rows)
@@ -144,15 +221,14 @@ def main():
     qt = last_targets[rng.integers(0, len(last_targets), nq)]
     ix.prepare(qs, qt)
     ix.run()  # warm
-    q_ms, q_hops, q_fin = 0.0, 0, 0
+    q_ms, q_hops = 0.0, 0
     reps = 3
     for _ in range(reps):
         st = ix.run()
         q_ms += st["kernel_ms"]
         q_hops += st["hops"]
-        q_fin += st["finished"]
-    q_sum = allreduce([float(nq * reps), q_ms, float(q_hops)], dist.ReduceOp.SUM if world > 1 else None)
-    (q_ms_max,) = allreduce([q_ms], dist.ReduceOp.MAX if world > 1 else None)
+    q_totals = comm.reduce([float(nq * reps), q_ms, float(q_hops)], "SUM")
+    (q_ms_max,) = comm.reduce([q_ms], "MAX")
 
     # ---- CPU baseline + full-size parity sample (rank 0, N = 1) -------------
     cpu = None
@@ -161,7 +237,7 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        sample = batch(0)[: threads * args.cpu_rows_per_thread]
+        sample = batch_of(owned, B, 0)[: threads * args.cpu_rows_per_thread]
         order = plan.order()
         tc = time.perf_counter()
         ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, sample, threads=threads)
@@ -186,57 +262,10 @@ def main():
                          f"table-search {cq} queries in {cpu_q_s:.2f}s",
                "queries_per_s": round(cq / cpu_q_s, 1)}
 
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
-
-    total_rows = world * args.steps * B
-    value = total_rows / elapsed_max
-    roof = None
-    if kt:
-        name, k = max(kt.items(), key=lambda kv: kv[1]["ms"])
-        achieved = k["bytes"] / (k["ms"] / 1e3) / 1e9 if k["ms"] > 0 else 0.0
-        roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None, "launches": k["launches"],
-                "avg_launch_us": round(k["ms"] * 1e3 / max(1, k["launches"]), 3),
-                "bytes_per_launch": round(k["bytes"] / max(1, k["launches"]), 1)}
-    qps = q_sum[0] / (q_ms_max / 1e3) if q_ms_max > 0 else 0.0
-    out = {
-        "metric": METRIC,
-        "value": round(value, 2),
-        "unit": "sources/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u32",
-        "data": "synthetic (seeded grid-perturbed road graph; melb-both.xy blob is missing)",
-        "config": {"workload": f"synthetic-{g.n // 1000}k-road cpd-build {args.partmethod} "
-                               f"{args.partkey} + table-search",
-                   "graph": f"grid-perturbed {args.width}x{args.width} seed {args.seed}",
-                   "nodes": g.n, "edges": g.m, "rows_per_step_per_gpu": B,
-                   "partition": f"{args.partmethod} {args.partkey}",
-                   "parallelism": f"target-partition x{world} (no collective)"},
-        "gteps": round(value * g.m / 1e9, 3),
-        "queries_per_s": round(qps, 1),
-        "query_mean_moves": round(q_sum[2] / max(1.0, q_sum[0]), 1),
-        "mean_runs_per_row": round(nruns / max(1, nrows), 1),
-        "roofline": roof,
-        "cpu_baseline": cpu,
-        "parity_sample_bit_exact": parity,
-        "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
-                        "GBps": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] else 0}
-                    for k, v in kt.items()},
-        "hierarchy": {"arcs": pinfo["ch_up_arcs"] + pinfo["ch_dn_arcs"],
-                      "levels": [pinfo["levels_up"], pinfo["levels_dn"]],
-                      "build_s": round(pinfo["ch_seconds"], 1)},
-    }
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        out = assemble(args, world, (g.n, g.m), B, elapsed_max, q_totals, q_ms_max, nrows, nruns,
+                       kt, cpu, parity, pinfo)
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

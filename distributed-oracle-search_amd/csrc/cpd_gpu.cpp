@@ -81,7 +81,9 @@ struct cpd_graph {
     DevBuf<uint32_t> asc_nodes, asc_off, asc_arcs;
     DevBuf<uint32_t> dsc_nodes, dsc_off, dsc_arcs;
     std::vector<uint32_t> asc_lvl, dsc_lvl;         // level -> first slot
-    std::vector<double> asc_lvl_arcs, dsc_lvl_arcs;  // arcs per level (bytes model)
+    // bytes model: gathered arcs and own-row reads per level
+    std::vector<double> asc_lvl_arcs, dsc_lvl_arcs, dsc_lvl_reads;
+    std::vector<uint32_t> asc_off_host;
     uint64_t ch_arcs = 0;
     bool has_ch = false;
     // batch workspace
@@ -117,7 +119,8 @@ struct cpd_graph {
         ev_pool.pop_back();
         return e;
     }
-    // Bracket a launch with events when timing is on.
+    // Time one launch when timing is on: the events are attached to the
+    // kernel's own dispatch packet (hipExtLaunchKernelGGL, see launchers).
     template <class F>
     void timed(const char* name, double bytes, F&& launch) {
         if (!timing) {
@@ -125,9 +128,9 @@ struct cpd_graph {
             return;
         }
         hipEvent_t a = get_event(), b = get_event();
-        HIP_CHECK(hipEventRecord(a, stream));
+        set_launch_events(a, b);
         launch();
-        HIP_CHECK(hipEventRecord(b, stream));
+        HIP_CHECK(hipGetLastError());
         pending.push_back({name, a, b, bytes});
     }
     void sync() {
@@ -194,11 +197,8 @@ struct cpd_index {
 
 namespace {
 
-// Host mirror of the kernels' tiled first-move row layout (cpd_kernels.hip).
-uint32_t fm_pos_host(uint32_t c) {
-    const uint32_t r = c & (kFmTile - 1u);
-    return (c & ~(kFmTile - 1u)) + ((r >> 3) & 3u) * 512u + (r >> 5) * 8u + (r & 7u);
-}
+// Leaf flag of the level-0 shortcut (cpd_kernels.hip kLeafBit).
+constexpr uint32_t kLeafBit = 0x80000000u;
 
 void require_device() {
     int count = 0;
@@ -208,9 +208,11 @@ void require_device() {
 }
 
 // Build the level-ordered sweep arrays in column space.
+// lvl_arcs: gathered arcs per level; lvl_reads: nodes reading their own row.
 void build_sweep(const cpd_plan& p, bool ascend, std::vector<uint32_t>& nodes,
                  std::vector<uint32_t>& off, std::vector<uint32_t>& arcs,
-                 std::vector<uint32_t>& lvl_first, std::vector<double>& lvl_arcs) {
+                 std::vector<uint32_t>& lvl_first, std::vector<double>& lvl_arcs,
+                 std::vector<double>& lvl_reads) {
     const Hierarchy& H = p.ch;
     const uint32_t n = p.n;
     const std::vector<uint32_t>& level = ascend ? H.level_up : H.level_dn;
@@ -227,26 +229,32 @@ void build_sweep(const cpd_plan& p, bool ascend, std::vector<uint32_t>& nodes,
     lvl_first.assign(cnt.begin(), cnt.end());
     nodes.assign(n, 0);
     std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
+    const std::vector<uint32_t>& lup = H.level_up;  // leaf = upward level 0
     for (uint32_t c = 0; c < n; ++c) {  // columns ascending inside a level
         uint32_t v = p.inv[c];
-        nodes[pos[level[v]]++] = c;
+        // descending list: a leaf starts from the closed form, not a read
+        nodes[pos[level[v]]++] = c | (!ascend && lup[v] == 0 ? kLeafBit : 0u);
     }
     off.assign(n + 1, 0);
     arcs.clear();
     arcs.reserve(2 * aoff[n]);
     lvl_arcs.assign(nlev, 0.0);
+    lvl_reads.assign(nlev, 0.0);
     std::vector<std::pair<uint32_t, uint32_t>> tmp;
     for (uint32_t s = 0; s < n; ++s) {
-        uint32_t v = p.inv[nodes[s]];
+        uint32_t v = p.inv[nodes[s] & ~kLeafBit];
         tmp.clear();
         for (uint64_t e = aoff[v]; e < aoff[v + 1]; ++e) tmp.push_back({p.order[adst[e]], aw[e]});
         std::sort(tmp.begin(), tmp.end());
         for (auto& a : tmp) {
-            arcs.push_back(a.first);
+            // ascending arcs into leaves are evaluated in closed form
+            bool leaf = ascend && lup[p.inv[a.first]] == 0;
+            arcs.push_back(a.first | (leaf ? kLeafBit : 0u));
             arcs.push_back(a.second);
+            if (!leaf) lvl_arcs[level[v]] += 1.0;
         }
         off[s + 1] = off[s] + (uint32_t)tmp.size();
-        lvl_arcs[level[v]] += (double)tmp.size();
+        if (!ascend && !(nodes[s] & kLeafBit)) lvl_reads[level[v]] += 1.0;
     }
 }
 
@@ -307,13 +315,15 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             return;
         }
         std::vector<uint32_t> nodes, off, arcs;
-        build_sweep(*p, true, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs);
+        std::vector<double> unused;
+        build_sweep(*p, true, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs, unused);
+        g->asc_off_host = off;
         g->asc_nodes.upload(nodes.data(), nodes.size(), s);
         g->asc_off.upload(off.data(), off.size(), s);
         g->asc_arcs.upload(arcs.data(), arcs.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
         g->ch_arcs = arcs.size() / 2;
-        build_sweep(*p, false, nodes, off, arcs, g->dsc_lvl, g->dsc_lvl_arcs);
+        build_sweep(*p, false, nodes, off, arcs, g->dsc_lvl, g->dsc_lvl_arcs, g->dsc_lvl_reads);
         g->dsc_nodes.upload(nodes.data(), nodes.size(), s);
         g->dsc_off.upload(off.data(), off.size(), s);
         g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
@@ -352,12 +362,16 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
     const uint32_t B = g->B, n = g->n;
     const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
     const uint32_t active = slabs * 1024u;
-    // ascending sweep: each level reads lower levels' rows
-    for (size_t l = 0; l + 1 < g->asc_lvl.size(); ++l) {
+    // ascending sweep: each level reads lower levels' rows.  Level 0 (leaves)
+    // is never materialised (closed form, see kLeafBit), so it is skipped.
+    // Bytes per level: gathered rows 4 B x target, row writes 4 B x target,
+    // arcs 8 B and node slot 12 B per 1024-target slab.
+    for (size_t l = 1; l + 1 < g->asc_lvl.size(); ++l) {
         uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
         if (!cnt) continue;
-        double bytes = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active +
-                       8.0 * g->asc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
+        double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
+        double bytes = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + 8.0 * arcs_l * slabs +
+                       12.0 * cnt * slabs;
         g->timed("sweep_up", bytes, [&] {
             launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt, g->dist.p,
                          g->tgt.p, B, slabs, g->stream);
@@ -366,15 +380,17 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
     for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
         uint32_t s0 = g->dsc_lvl[l], cnt = g->dsc_lvl[l + 1] - s0;
         if (!cnt) continue;
-        double bytes = (4.0 * g->dsc_lvl_arcs[l] + 8.0 * cnt) * active +
+        double bytes = (4.0 * g->dsc_lvl_arcs[l] + 4.0 * g->dsc_lvl_reads[l] + 4.0 * cnt) * active +
                        8.0 * g->dsc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
         g->timed("sweep_down", bytes, [&] {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
                          g->tgt.p, B, slabs, g->stream);
         });
     }
-    const uint32_t fslabs = (k + 255u) / 256u;
-    double fbytes = (4.0 * n + 4.0 * g->m + 2.0 * g->npad) * (fslabs * 256.0) +
+    // per row: own distance 4n + neighbour distances 4m + first-move write 2npad;
+    // the CSR (row_ptr, dst, w) is read once per 1024-target slab
+    const uint32_t fslabs = (k + 1023u) / 1024u;
+    double fbytes = (4.0 * n + 4.0 * g->m + 2.0 * g->npad) * (fslabs * 1024.0) +
                     (4.0 * (n + 1) + 8.0 * g->m) * fslabs;
     g->timed("first_moves", fbytes, [&] {
         launch_first_moves(g->row_ptr.p, g->dst.p, g->w.p, g->dist.p, g->tgt.p, B, k, n,
@@ -514,7 +530,7 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
                                 hipMemcpyDeviceToHost));
             for (uint32_t i = 0; i < ntargets; ++i)
                 for (uint32_t v = 0; v < n; ++v)
-                    fm[(size_t)i * n + v] = h[(size_t)i * g->npad + fm_pos_host(g->order[v])];
+                    fm[(size_t)i * n + v] = h[(size_t)i * g->npad + g->order[v]];
         }
     });
 }

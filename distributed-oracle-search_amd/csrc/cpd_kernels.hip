@@ -6,7 +6,8 @@
 //                          16-B/lane access covers 256 targets = 1 KiB
 //   fm    [row][npad] u16  first-move sets, row-major for the RLE scan;
 //                          columns >= n are padded with the wildcard
-//   runs  [row][cap]  u32  RLE scratch, compacted afterwards
+//   runs  u32 words, rows back to back at off[row] (count pass, then emit)
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -22,17 +23,18 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t d, uint32_t w) {
     return (s < d) ? INF : s;  // d == INF or overflow -> INF
 }
 
-// First-move rows are stored tiled for the RLE scan: a 2048-column tile holds,
-// for each of 4 chunk slots q and 64 lanes, 8 columns — lane l's 32 columns
-// (32l .. 32l+31 of the tile) are 4 uint4 at q*64 + l, so each of the scan's
-// 4 loads is one fully coalesced 1-KiB wave access.
+// First-move rows are plain row-major u16 [row][npad]: the first-move kernel
+// writes each target's 32-column segment as one full 64-B line, and the RLE
+// scan's lane l reads its 32 columns as 4 x 16 B.
 constexpr uint32_t kSeg = 32;          // columns per lane
-constexpr uint32_t kTile = 64 * kSeg;  // columns per wave tile
+constexpr uint32_t kTile = 64 * kSeg;  // columns per wave tile (npad % kTile == 0)
 
-__device__ __forceinline__ uint32_t fm_pos(uint32_t c) {
-    const uint32_t r = c & (kTile - 1u);
-    return (c & ~(kTile - 1u)) + ((r >> 3) & 3u) * 512u + (r >> 5) * 8u + (r & 7u);
-}
+// Level-0 shortcut.  A node with no down-arcs ("leaf" of the upward sweep) has
+// d_up = 0 at its own target and INF elsewhere, so it is never materialised:
+// an upward-sweep arc into a leaf carries kLeafBit in its column and is
+// evaluated from the targets (no gather); a leaf in the downward node list
+// carries kLeafBit and starts from the same closed form (no read).
+constexpr uint32_t kLeafBit = 0x80000000u;
 
 __device__ __forceinline__ void min4(uint4& acc, const uint4 d, uint32_t w) {
     acc.x = min(acc.x, sat_add(d.x, w));
@@ -41,11 +43,24 @@ __device__ __forceinline__ void min4(uint4& acc, const uint4 d, uint32_t w) {
     acc.w = min(acc.w, sat_add(d.w, w));
 }
 
+__device__ __forceinline__ uint4 leaf4(const uint4 t, uint32_t col, uint32_t w) {
+    return make_uint4(t.x == col ? w : INF, t.y == col ? w : INF, t.z == col ? w : INF,
+                      t.w == col ? w : INF);
+}
+
+// Value an arc contributes: a gathered distance row, or the leaf closed form.
+__device__ __forceinline__ uint4 arc_val(const uint4* __restrict__ d4, const uint4 t, uint2 e,
+                                         uint32_t B4, uint32_t l4) {
+    if (e.x & kLeafBit) return leaf4(t, e.x & ~kLeafBit, 0u);
+    return d4[(size_t)e.x * B4 + l4];
+}
+
 // One CH sweep level.  Block (x = slot in the level, y = 1024-target slab):
 // node v = nodes[slot]; its arcs (col, w) are wave-uniform (scalar loads); each
 // lane owns 4 consecutive targets.  ASCEND: upward sweep, init 0 at the lane's
 // own target else INF.  !ASCEND: downward sweep, init = current dist (the
-// upward value).  Then acc = min(acc, w + dist[arc.col]) over the arcs.
+// upward value, or the leaf closed form).  Then acc = min(acc, w + d[arc.col])
+// over the arcs, eight gathers in flight per wave.
 template <bool ASCEND>
 __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ nodes,
                                                    const uint32_t* __restrict__ arc_off,
@@ -56,42 +71,47 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
                                                    uint32_t B4) {
     const uint32_t slot = slot0 + blockIdx.x;
     const uint32_t l4 = blockIdx.y * 256u + threadIdx.x;
-    const uint32_t v = nodes[slot];
+    const uint32_t vraw = nodes[slot];
+    const uint32_t v = vraw & ~kLeafBit;
     const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
     uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    const uint4 t = tgt4[l4];
     uint4 acc;
-    if (ASCEND) {
-        const uint4 t = tgt4[l4];
-        acc.x = (t.x == v) ? 0u : INF;
-        acc.y = (t.y == v) ? 0u : INF;
-        acc.z = (t.z == v) ? 0u : INF;
-        acc.w = (t.w == v) ? 0u : INF;
-    } else {
+    if (ASCEND || (vraw & kLeafBit))
+        acc = leaf4(t, v, 0u);
+    else
         acc = d4[(size_t)v * B4 + l4];
-    }
     uint32_t a = a0;
-    for (; a + 4 <= a1; a += 4) {
-        const uint2 e0 = arcs[a], e1 = arcs[a + 1], e2 = arcs[a + 2], e3 = arcs[a + 3];
-        const uint4 x0 = d4[(size_t)e0.x * B4 + l4];
-        const uint4 x1 = d4[(size_t)e1.x * B4 + l4];
-        const uint4 x2 = d4[(size_t)e2.x * B4 + l4];
-        const uint4 x3 = d4[(size_t)e3.x * B4 + l4];
-        min4(acc, x0, e0.y);
-        min4(acc, x1, e1.y);
-        min4(acc, x2, e2.y);
-        min4(acc, x3, e3.y);
+    for (; a + 8 <= a1; a += 8) {
+        uint2 e[8];
+        uint4 x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = arc_val(d4, t, e[i], B4, l4);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) min4(acc, x[i], e[i].y);
     }
     for (; a < a1; ++a) {
         const uint2 e = arcs[a];
-        min4(acc, d4[(size_t)e.x * B4 + l4], e.y);
+        min4(acc, arc_val(d4, t, e, B4, l4), e.y);
     }
     d4[(size_t)v * B4 + l4] = acc;
 }
 
-// First-move sets.  Block (x = 64-column group, y = 256-target slab); thread =
-// one target, walks the group's 64 columns: fm = bits k with
-// w_k + d(dst_k) == d(c) (wildcard at the target and unreachable columns),
-// then stores them into the target's tiled row (fm_pos).
+__device__ __forceinline__ uint32_t fm_bit(uint32_t dv, uint32_t w, uint32_t dn, uint32_t k) {
+    return (sat_add(dv, w) == dn ? 1u : 0u) << k;
+}
+
+__device__ __forceinline__ uint32_t fm_final(uint32_t c, uint32_t tc, uint32_t dn, uint32_t bits) {
+    return (c == tc || dn == INF) ? 0xFFFFu : bits;
+}
+
+// First-move sets.  Block (x = one 32-column lane segment, y = 1024-target
+// slab); thread = 4 consecutive targets (16-B dist accesses: 1 KiB per wave
+// instruction, like the sweeps).  For each column c: fm = bits k with
+// w_k + d(dst_k) == d(c), wildcard at the target and at unreachable columns;
+// the segment's 32 sets per target are one 64-B line of the target's row.
 __global__ __launch_bounds__(256) void first_moves(const uint32_t* __restrict__ row_ptr,
                                                    const uint32_t* __restrict__ dst,
                                                    const uint32_t* __restrict__ w,
@@ -99,37 +119,44 @@ __global__ __launch_bounds__(256) void first_moves(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ tgt,
                                                    uint32_t B, uint32_t n, uint32_t npad,
                                                    uint16_t* __restrict__ fm) {
-    const uint32_t j = blockIdx.y * 256u + threadIdx.x;
-    const uint32_t c0 = blockIdx.x * 64u;
-    const uint32_t tcol = tgt[j];
-    uint32_t packed[32];
+    const uint32_t l4 = blockIdx.y * 256u + threadIdx.x;
+    const uint32_t B4 = B / 4u;
+    const uint32_t c0 = blockIdx.x * kSeg;
+    const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
+    const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
+    uint32_t pk[4][16];
 #pragma unroll
-    for (int p = 0; p < 32; ++p) {
-        uint32_t two = 0;
+    for (int p = 0; p < 16; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t c = c0 + 2u * p + h;
-            uint32_t f = 0xFFFFu;
-            if (c < n) {
-                const uint32_t dn = dist[(size_t)c * B + j];
-                const uint32_t e0 = row_ptr[c], e1 = row_ptr[c + 1];
-                uint32_t bits = 0;
-                for (uint32_t e = e0; e < e1; ++e) {
-                    const uint32_t dv = dist[(size_t)dst[e] * B + j];
-                    bits |= (sat_add(dv, w[e]) == dn ? 1u : 0u) << (e - e0);
-                }
-                f = (c == tcol || dn == INF) ? 0xFFFFu : bits;
+    for (int cc = 0; cc < (int)kSeg; ++cc) {
+        const uint32_t c = c0 + (uint32_t)cc;
+        if (c < n) {
+            const uint4 dn = d4[(size_t)c * B4 + l4];
+            const uint32_t e0 = row_ptr[c], e1 = row_ptr[c + 1];
+            uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+            for (uint32_t e = e0; e < e1; ++e) {
+                const uint4 dv = d4[(size_t)dst[e] * B4 + l4];
+                const uint32_t we = w[e], k = e - e0;
+                b0 |= fm_bit(dv.x, we, dn.x, k);
+                b1 |= fm_bit(dv.y, we, dn.y, k);
+                b2 |= fm_bit(dv.z, we, dn.z, k);
+                b3 |= fm_bit(dv.w, we, dn.w, k);
             }
-            two |= f << (16 * h);
+            const int sh = 16 * (cc & 1);
+            const uint32_t keep = 0xFFFF0000u >> sh;  // clear this column's half
+            pk[0][cc >> 1] = (pk[0][cc >> 1] & keep) | (fm_final(c, tc.x, dn.x, b0) << sh);
+            pk[1][cc >> 1] = (pk[1][cc >> 1] & keep) | (fm_final(c, tc.y, dn.y, b1) << sh);
+            pk[2][cc >> 1] = (pk[2][cc >> 1] & keep) | (fm_final(c, tc.z, dn.z, b2) << sh);
+            pk[3][cc >> 1] = (pk[3][cc >> 1] & keep) | (fm_final(c, tc.w, dn.w, b3) << sh);
         }
-        packed[p] = two;
     }
-    // tiled store: the thread's 64 columns are two lane segments of 32
-    uint16_t* rowp = fm + (size_t)j * npad;
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-        *reinterpret_cast<uint4*>(rowp + fm_pos(c0 + 8u * q)) =
-            make_uint4(packed[4 * q], packed[4 * q + 1], packed[4 * q + 2], packed[4 * q + 3]);
+    for (int i = 0; i < 4; ++i) {
+        uint4* seg = reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * npad + c0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            seg[q] = make_uint4(pk[i][4 * q], pk[i][4 * q + 1], pk[i][4 * q + 2], pk[i][4 * q + 3]);
+    }
 }
 
 // One lane's greedy pass over its 32 columns (warthog graph_oracle::add_row
@@ -178,7 +205,7 @@ __global__ __launch_bounds__(256) void rle_scan(const uint16_t* __restrict__ fm,
         uint32_t v[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint4 x = src[(size_t)t * 256u + q * 64u + lane];
+            const uint4 x = src[(size_t)t * 256u + lane * 4u + q];  // 64 B per lane
             v[4 * q] = x.x;
             v[4 * q + 1] = x.y;
             v[4 * q + 2] = x.z;
@@ -319,7 +346,26 @@ __global__ __launch_bounds__(256) void table_search(
 }  // namespace kern
 
 // ---------------------------------------------------------------------------
-// Launchers (host side of this translation unit).
+// Launchers (host side of this translation unit).  Each launch goes through
+// hipExtLaunchKernelGGL so that, when the caller armed a start/stop event pair
+// (set_launch_events), the timestamps ride on the dispatch packet itself: exact
+// kernel time without extra barrier packets between launches.
+
+namespace {
+thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
+
+template <typename... Args, typename F>
+void launch(F kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    hipEvent_t a = g_ev_start, b = g_ev_stop;
+    g_ev_start = g_ev_stop = nullptr;
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, a, b, 0, args...);
+}
+}  // namespace
+
+void set_launch_events(hipEvent_t start, hipEvent_t stop) {
+    g_ev_start = start;
+    g_ev_stop = stop;
+}
 
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* arcs32, uint32_t slot0, uint32_t count, uint32_t* dist,
@@ -328,28 +374,31 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
     const uint4* t4 = reinterpret_cast<const uint4*>(tgt);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
     if (ascend)
-        kern::sweep_level<true><<<grid, 256, 0, s>>>(nodes, arc_off, arcs, slot0, dist, t4, B / 4u);
+        launch(kern::sweep_level<true>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, dist, t4,
+               B / 4u);
     else
-        kern::sweep_level<false><<<grid, 256, 0, s>>>(nodes, arc_off, arcs, slot0, dist, t4, B / 4u);
+        launch(kern::sweep_level<false>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, dist, t4,
+               B / 4u);
 }
 
 void launch_first_moves(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
                         const uint32_t* dist, const uint32_t* tgt, uint32_t B,
                         uint32_t rows, uint32_t n, uint32_t npad, uint16_t* fm,
                         hipStream_t s) {
-    dim3 grid(npad / 64u, (rows + 255u) / 256u);
-    kern::first_moves<<<grid, 256, 0, s>>>(row_ptr, dst, w, dist, tgt, B, n, npad, fm);
+    dim3 grid(npad / kern::kSeg, (rows + 1023u) / 1024u);
+    launch(kern::first_moves, grid, dim3(256), s, row_ptr, dst, w, dist, tgt, B, n, npad, fm);
 }
 
 void launch_rle_count(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* counts,
                       hipStream_t s) {
-    kern::rle_scan<false><<<(nrows + 3u) / 4u, 256, 0, s>>>(fm, npad, nrows, counts, nullptr,
-                                                            nullptr);
+    launch(kern::rle_scan<false>, dim3((nrows + 3u) / 4u), dim3(256), s, fm, npad, nrows, counts,
+           (const uint64_t*)nullptr, (uint32_t*)nullptr);
 }
 
 void launch_rle_emit(const uint16_t* fm, uint32_t npad, uint32_t nrows, const uint64_t* off,
                      uint32_t* runs, hipStream_t s) {
-    kern::rle_scan<true><<<(nrows + 3u) / 4u, 256, 0, s>>>(fm, npad, nrows, nullptr, off, runs);
+    launch(kern::rle_scan<true>, dim3((nrows + 3u) / 4u), dim3(256), s, fm, npad, nrows,
+           (uint32_t*)nullptr, off, runs);
 }
 
 void launch_table_search(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
@@ -358,9 +407,8 @@ void launch_table_search(const uint32_t* row_ptr, const uint32_t* dst, const uin
                          uint32_t nq, int32_t kmoves, uint32_t n, uint64_t* cost,
                          uint32_t* hops, uint8_t* fin, unsigned long long* agg,
                          hipStream_t s) {
-    kern::table_search<<<(nq + 255u) / 256u, 256, 0, s>>>(row_ptr, dst, w, row_of_col, offsets,
-                                                          runs, qs, qt, nq, kmoves, n, cost,
-                                                          hops, fin, agg);
+    launch(kern::table_search, dim3((nq + 255u) / 256u), dim3(256), s, row_ptr, dst, w, row_of_col,
+           offsets, runs, qs, qt, nq, kmoves, n, cost, hops, fin, agg);
 }
 
 }  // namespace cpd

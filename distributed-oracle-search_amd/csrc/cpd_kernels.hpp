@@ -5,6 +5,10 @@
 
 namespace cpd {
 
+// Arm a start/stop event pair for the NEXT launch on this thread (consumed by
+// it); the events record the kernel's own begin/end timestamps.
+void set_launch_events(hipEvent_t start, hipEvent_t stop);
+
 // One CH sweep level: `count` node slots starting at `slot0` of the
 // level-ordered node list; grid (count, slabs) x 256 threads, one slab =
 // 1024 targets of the B-wide batch row.

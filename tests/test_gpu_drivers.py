@@ -1,0 +1,121 @@
+"""End-to-end drop-in test on the GPU: our executables driven exactly the way
+the reference drivers drive warthog's (make_cpds.py:20, make_fifos.py:21,
+process_query.py:35-111), with `ssh host 'bash -s'` replaced by local bash
+(tests/driver_harness.py; bytes pinned by tests/golden/driver_fixtures.json).
+The answers and per-query side files are checked against the CPU oracle."""
+import os
+import select
+import subprocess
+import time
+
+import numpy as np
+import pytest
+
+import cpd
+import driver_harness as H
+import oracle
+
+pytestmark = pytest.mark.gpu
+BIN = H.BIN
+
+
+def _read_diff(path, g):
+    w = g.w.copy()
+    for line in open(path):
+        p = line.split()
+        if not p or p[0] != "e":
+            continue
+        a, b, c = map(int, p[1:4])
+        for e in range(g.row_ptr[a], g.row_ptr[a + 1]):
+            if g.dst[e] == b:
+                w[e] = c
+                break
+    return w
+
+
+def _wait_ready(proc, timeout=60):
+    t0 = time.time()
+    buf = ""
+    while time.time() - t0 < timeout:
+        r, _, _ = select.select([proc.stdout], [], [], 1.0)
+        if r:
+            line = proc.stdout.readline()
+            buf += line
+            if "listening" in line:
+                return buf
+        if proc.poll() is not None:
+            break
+    raise AssertionError(f"fifo_auto did not come up: {buf} {proc.stderr.read()}")
+
+
+@pytest.mark.parametrize("method,key", [("mod", 3), ("div", 5)])
+def test_drivers_end_to_end(tmp_path, method, key):
+    W = 3
+    prefix = str(tmp_path / "g")
+    subprocess.run([os.path.join(BIN, "gen_synth"), "--width", "30", "--height", "24", "--seed",
+                    "2", "--out", prefix, "--queries", "3000"], check=True, capture_output=True)
+    xy, diff, scen = prefix + ".xy", prefix + ".xy.diff", prefix + ".scen"
+    outdir = str(tmp_path / "index")
+    for wid in range(W):
+        p = subprocess.run([os.path.join(BIN, "make_cpd_auto"), "--input", xy, "--partmethod", method,
+                            "--partkey", str(key), "--workerid", str(wid), "--maxworker", str(W),
+                            "--outdir", outdir, "--device", "0"], capture_output=True, text=True,
+                           timeout=300)
+        assert p.returncode == 0, p.stderr
+        assert "rows/s" in p.stdout
+    g = cpd.synth_road_graph(30, 24, seed=2)
+    order = oracle.dfs_preorder(g.row_ptr, g.dst)
+    wc = _read_diff(diff, g)
+    assert np.any(wc != g.w)
+
+    procs = []
+    try:
+        for wid in range(W):
+            fifo = f"/tmp/worker{wid}.fifo"
+            if os.path.exists(fifo):
+                os.remove(fifo)
+            procs.append(subprocess.Popen(
+                [os.path.join(BIN, "fifo_auto"), "--input", xy, diff, "--partmethod", method,
+                 "--partkey", str(key), "--workerid", str(wid), "--maxworker", str(W), "--outdir",
+                 outdir, "--alg", "table-search", "--device", "0"],
+                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+        for pr in procs:
+            _wait_ready(pr)
+        nfs = str(tmp_path / "nfs")
+        os.makedirs(nfs)
+        conf = {"workers": ["localhost"] * W, "nfs": nfs, "partmethod": method, "partkey": key,
+                "xy_file": xy, "scenfile": scen, "diffs": ["-", diff]}
+        config = dict(H.DEFAULT_CONFIG, debug=True)
+        parts, stats = H.run(conf, config)
+        assert len(stats) == 2 and all(len(s) == len(parts) for s in stats)
+        for x, (dname, w_sel) in enumerate([("-", g.w), (diff, wc)]):
+            for wid, (part, row) in enumerate(zip(parts, stats[x])):
+                assert len(row) == 13, row                  # 10 stats + t_prepare, t_partition, size
+                s = np.array([q[0] for q in part], np.uint32)
+                t = np.array([q[1] for q in part], np.uint32)
+                targets = np.unique(t)
+                off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, targets)
+                rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, w_sel, order, targets, off, runs,
+                                                 s, t)
+                assert int(row[0]) == int(rh.sum())         # n_expanded = moves
+                assert int(row[5]) == int(rh.sum())         # plen
+                assert int(row[6]) == int(rf.sum()) == len(part)
+                assert row[-1] == len(part)
+                if x == 1:  # the side file holds the last experiment (congested)
+                    res = np.loadtxt(os.path.join(nfs, f"query.localhost{wid}.res"),
+                                     dtype=np.uint64, ndmin=2)
+                    np.testing.assert_array_equal(res[:, 0], s)
+                    np.testing.assert_array_equal(res[:, 2], rc)  # per-query cost
+                    np.testing.assert_array_equal(res[:, 3], rh)
+    finally:
+        for wid, pr in enumerate(procs):
+            if pr.poll() is None:
+                try:
+                    with open(f"/tmp/worker{wid}.fifo", "w") as f:
+                        f.write("quit\n")
+                    pr.wait(timeout=20)
+                except Exception:
+                    pr.kill()
+            fifo = f"/tmp/worker{wid}.fifo"
+            if os.path.exists(fifo):
+                os.remove(fifo)
