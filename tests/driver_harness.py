@@ -111,8 +111,14 @@ def send_queries(hostname, workerid, nfs, config, dname, reqs, script_dir):
     return (*res, t_prepare * 1e9, t_partition * 1e9, len(reqs))
 
 
-def run(conf, config=None):
-    """process_query.run (:132-194) for local workers."""
+def run(conf, config=None, script_dir=None):
+    """process_query.run (:132-194) for local workers.  The reference writes
+    each worker's bash script to the head node's cwd under the query file's
+    basename (process_query.py:83-84,70), so script_dir must not be the NFS
+    directory."""
+    import tempfile
+    script_dir = script_dir or tempfile.mkdtemp(prefix="head-")
+    assert os.path.realpath(script_dir) != os.path.realpath(conf["nfs"])
     config = dict(DEFAULT_CONFIG if config is None else config)
     hosts = conf["workers"]
     maxworker = len(hosts)
@@ -124,7 +130,7 @@ def run(conf, config=None):
     for dname in conf["diffs"]:
         with ThreadPoolExecutor(maxworker) as pool:
             futs = [pool.submit(send_queries, h, w, conf["nfs"], config, dname, part,
-                                conf["nfs"])
+                                script_dir)
                     for h, w, part in zip(hosts, range(maxworker), parts) if len(part) > 0]
             stats.append([f.result() for f in futs])
     return parts, stats
