@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "distributed-oracle-search_amd")
 METRIC = "CPD build sources/sec + GTEPS; table-search queries/sec; % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PLAN_TAG = "ch823"      # bump when the hierarchy builder changes (cache key)
 
 
 def parse(argv=None):
@@ -46,8 +47,80 @@ def parse(argv=None):
     ap.add_argument("--cpu-rows-per-thread", type=int, default=8)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cache", default=os.environ.get("CPD_BENCH_CACHE", "/tmp/cpd-bench-cache"))
     return ap.parse_args(argv)
+
+
+# rocprofv3 kernel names -> the library's timing names
+KERNEL_NAMES = {"sweep_level<true>": "sweep_up", "sweep_level<false>": "sweep_down",
+                "first_moves": "first_moves", "rle_scan<false>": "rle_count",
+                "rle_scan<true>": "rle_emit", "table_search": "table_search"}
+
+
+def pmc_traffic(args, plan_path):
+    """HBM traffic per launch from rocprofv3 PMC counters.
+
+    One child run per counter (MI355X_MICROARCH.md: FETCH_SIZE costs 3 and
+    WRITE_SIZE 2 of the 4 TCC slots, so they cannot share a pass), each a
+    one-step build of the same workload.  Both counters are in KiB; on gfx950
+    FETCH_SIZE reports half the bytes of a 16-B/lane streaming read, so it is
+    doubled (our kernels' loads are 16 B per lane); WRITE_SIZE is exact for
+    16-B stores.  Started before this process touches the GPU.  Returns
+    {name: {"launches", "FETCH_SIZE", "WRITE_SIZE", "bytes_per_launch"}} or None.
+    """
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    if not shutil.which("rocprofv3"):
+        return None
+    out = {}
+    base = tempfile.mkdtemp(prefix="pmc-", dir=args.cache)
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(base, counter)
+        cmd = ["rocprofv3", "--pmc", counter, "-d", d, "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "1",
+               "--warmup", "0", "--width", str(args.width), "--seed", str(args.seed),
+               "--partmethod", args.partmethod, "--partkey", str(args.partkey),
+               "--batch", str(args.batch), "--cache", args.cache]
+        try:
+            p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                               timeout=240, cwd=base)
+        except subprocess.TimeoutExpired:
+            log(f"pmc pass {counter} timed out")
+            return None
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if p.returncode != 0 or not files:
+            log(f"pmc pass {counter} failed: {p.stderr[-400:]}")
+            return None
+        for row in csv.DictReader(open(files[0])):
+            name = next((v for k, v in KERNEL_NAMES.items() if k in row["Kernel_Name"]), None)
+            if name is None:
+                continue
+            e = out.setdefault(name, {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0, "n_FETCH_SIZE": 0,
+                                      "n_WRITE_SIZE": 0})
+            e[counter] += float(row["Counter_Value"])
+            e["n_" + counter] += 1
+    for e in out.values():
+        nf, nw = max(1, e.pop("n_FETCH_SIZE")), max(1, e.pop("n_WRITE_SIZE"))
+        e["launches"] = nf
+        e["bytes_per_launch"] = 2.0 * e["FETCH_SIZE"] * 1024.0 / nf + e["WRITE_SIZE"] * 1024.0 / nw
+    shutil.rmtree(base, ignore_errors=True)
+    return out
+
+
+def pmc_child(args):
+    """One build step under the profiler (no torch: nothing else on the GPU)."""
+    sys.path.insert(0, PKG)
+    import cpd
+    plan = cpd.Plan.load(os.path.join(args.cache, f"synth{args.width}-s{args.seed}-{PLAN_TAG}.plan"))
+    n = plan.info()["n"]
+    dev = cpd.Graph(plan, device=0, batch=args.batch)
+    owned = shard_targets(n, 1, args.partmethod, args.partkey, 0)
+    dev.build_rows(batch_of(owned, dev.batch, 0))
 
 
 def log(*a):
@@ -97,8 +170,11 @@ def batch_of(owned, B, i):
 
 
 def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows, nruns,
-             kt, cpu, parity, pinfo):
-    """Rank 0's JSON line.  value = rows built by ALL ranks / max rank time."""
+             kt, cpu, parity, pinfo, traffic=None):
+    """Rank 0's JSON line.  value = rows built by ALL ranks / max rank time.
+    roofline: the kernel with the most device time; achieved = its algorithmic
+    bytes (SURVEY.md §8d model, counted per launch by libcpd) / its summed
+    event time; traffic = PMC bytes per launch of the same kernel (or None)."""
     n, m = graph_info
     total_rows = world * args.steps * B
     value = total_rows / elapsed_max
@@ -106,9 +182,12 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
     if kt:
         name, k = max(kt.items(), key=lambda kv: kv[1]["ms"])
         achieved = k["bytes"] / (k["ms"] / 1e3) / 1e9 if k["ms"] > 0 else 0.0
+        t = (traffic or {}).get(name)
         roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None, "launches": k["launches"],
+                "traffic": round(t["bytes_per_launch"], 1) if t else None,
+                "traffic_unit": "bytes/launch (PMC: 2*FETCH_SIZE + WRITE_SIZE, KiB->B)",
+                "launches": k["launches"],
                 "avg_launch_us": round(k["ms"] * 1e3 / max(1, k["launches"]), 3),
                 "bytes_per_launch": round(k["bytes"] / max(1, k["launches"]), 1)}
     qps = q_totals[0] / (q_ms_max / 1e3) if q_ms_max > 0 else 0.0
@@ -144,6 +223,9 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
         "hierarchy": {"arcs": pinfo["ch_up_arcs"] + pinfo["ch_dn_arcs"],
                       "levels": [pinfo["levels_up"], pinfo["levels_dn"]],
                       "build_s": round(pinfo["ch_seconds"], 1)} if pinfo else None,
+        "pmc_traffic_per_launch": {k: {"launches": v["launches"],
+                                       "bytes": round(v["bytes_per_launch"], 1)}
+                                   for k, v in (traffic or {}).items()},
     }
 
 
@@ -159,6 +241,9 @@ def main():
                f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
                "--master-port", os.environ.get("MASTER_PORT", "29517"), __file__] + sys.argv[1:]
         sys.exit(subprocess.call(cmd))
+    if args.pmc_child:
+        pmc_child(args)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -169,19 +254,23 @@ def main():
     sys.path.insert(0, PKG)
     import cpd
 
+    # ---- graph + host preprocessing (cached, built once per node; host only)
+    t0 = time.time()
+    g = cpd.synth_road_graph(args.width, args.width, seed=args.seed)
+    os.makedirs(args.cache, exist_ok=True)
+    plan_path = os.path.join(args.cache, f"synth{args.width}-s{args.seed}-{PLAN_TAG}.plan")
+    if local == 0 and not os.path.exists(plan_path):
+        log(f"building hierarchy for {g.n} nodes / {g.m} edges ...")
+        cpd.Plan(g).save(plan_path)
+    # PMC passes: children, before this process initialises the GPU
+    traffic = None
+    if world == 1 and not args.no_pmc:
+        traffic = pmc_traffic(args, plan_path)
+
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     comm = Comm(world, rank, local, device=f"cuda:{local}")
-
-    # ---- graph + host preprocessing (cached, built once per node) ----------
-    t0 = time.time()
-    g = cpd.synth_road_graph(args.width, args.width, seed=args.seed)
-    os.makedirs(args.cache, exist_ok=True)
-    plan_path = os.path.join(args.cache, f"synth{args.width}-s{args.seed}.plan")
-    if local == 0 and not os.path.exists(plan_path):
-        log(f"building hierarchy for {g.n} nodes / {g.m} edges ...")
-        cpd.Plan(g).save(plan_path)
     comm.barrier()
     plan = cpd.Plan.load(plan_path)
     pinfo = plan.info()
@@ -264,7 +353,7 @@ def main():
 
     if rank == 0:
         out = assemble(args, world, (g.n, g.m), B, elapsed_max, q_totals, q_ms_max, nrows, nruns,
-                       kt, cpu, parity, pinfo)
+                       kt, cpu, parity, pinfo, traffic)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

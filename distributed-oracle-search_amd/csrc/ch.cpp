@@ -18,6 +18,8 @@
 // (conservative, always correct).  The result is deterministic for any thread
 // count: every adjacency list is kept sorted and merges are grouped by owner.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -133,10 +135,15 @@ struct Contractor {
         return count;
     }
 
+    // priority = a*edge difference + b*contracted neighbours + c*depth; depth
+    // bounds the sweep levels.  8,2,3 measured best on the synthetic road
+    // graphs (fewest arcs at ~same level count; bench/DESIGN.md).
+    int64_t prio_ed = 8, prio_del = 2, prio_depth = 3;
+
     int64_t priority(uint32_t v, Witness& ws) const {
         int64_t sc = shortcuts(v, nullptr, settle_sim, nullptr, ws);
         int64_t ed = sc - (int64_t)in[v].size() - (int64_t)out[v].size();
-        return 4 * ed + 2 * (int64_t)deleted[v] + 3 * (int64_t)depth[v];
+        return prio_ed * ed + prio_del * (int64_t)deleted[v] + prio_depth * (int64_t)depth[v];
     }
 
     bool less_key(uint32_t a, uint32_t b) const {
@@ -178,6 +185,14 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
     C.depth.assign(n, 0);
     C.settle_contract = settle_limit ? settle_limit : 400;
     C.settle_sim = std::max<uint32_t>(50, C.settle_contract / 4);
+    if (const char* e = std::getenv("CPD_CH_PRIO")) {  // tuning knob: "ed,deleted,depth"
+        long a, b, c;
+        if (std::sscanf(e, "%ld,%ld,%ld", &a, &b, &c) == 3) {
+            C.prio_ed = a;
+            C.prio_del = b;
+            C.prio_depth = c;
+        }
+    }
 
     // Overlay graph: no self loops, parallel edges reduced to the lightest.
     for (uint32_t v = 0; v < n; ++v)
