@@ -10,6 +10,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "cpd_internal.hpp"
@@ -75,8 +76,25 @@ struct cpd_graph {
     std::vector<uint32_t> edge_perm;   // column-space edge -> file edge
     std::vector<uint32_t> w_free_col;  // free-flow weights, column-space edges
     std::vector<uint32_t> rowc_host;   // column-space row_ptr (host copy)
+    std::vector<uint32_t> dst_col_host;  // column-space edge heads (host copy)
     // column-space CSR of the original graph
     DevBuf<uint32_t> row_ptr, dst, w;
+    // packed fixed-stride adjacency for table-search: (dst col, w) pairs,
+    // 2^adj_shift slots per column, dst = 0xFFFFFFFF past the out-degree
+    uint32_t adj_shift = 0;
+    DevBuf<uint32_t> adj;
+
+    std::vector<uint32_t> packed_adjacency(const std::vector<uint32_t>& wcol) const {
+        const size_t stride = (size_t)1 << adj_shift;
+        std::vector<uint32_t> a(2 * stride * n, 0xFFFFFFFFu);
+        for (uint32_t c = 0; c < n; ++c)
+            for (uint32_t e = rowc_host[c]; e < rowc_host[c + 1]; ++e) {
+                size_t slot = ((size_t)c * stride + (e - rowc_host[c])) * 2;
+                a[slot] = dst_col_host[e];
+                a[slot + 1] = wcol[e];
+            }
+        return a;
+    }
     // sweeps: level-ordered node lists, per-slot arc offsets, (col, w) arcs
     DevBuf<uint32_t> asc_nodes, asc_off, asc_arcs;
     DevBuf<uint32_t> dsc_nodes, dsc_off, dsc_arcs;
@@ -184,11 +202,12 @@ struct cpd_index {
     uint64_t total = 0;
     std::vector<uint32_t> row_of_col;   // host copy
     std::vector<uint64_t> offsets;      // host copy
-    DevBuf<uint32_t> d_row_of_col, runs, w_sel;
+    DevBuf<uint32_t> d_row_of_col, runs, adj_sel;  // adj_sel: packed adjacency, custom weights
     DevBuf<uint64_t> off;
     bool custom_w = false;
-    // query workspace
+    // query workspace; queries run sorted by target row (perm[i] = caller index)
     uint32_t nq = 0;
+    std::vector<uint32_t> perm;
     DevBuf<uint32_t> qs, qt, hops;
     DevBuf<uint64_t> cost;
     DevBuf<uint8_t> fin;
@@ -291,12 +310,15 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             uint32_t v = p->inv[c];
             g->rowc_host[c + 1] = g->rowc_host[c] + (p->row_ptr[v + 1] - p->row_ptr[v]);
         }
-        std::vector<uint32_t> dstc(m);
+        std::vector<uint32_t>& dstc = g->dst_col_host;
+        dstc.resize(m);
         g->edge_perm.resize(m);
         g->w_free_col.resize(m);
+        uint32_t maxdeg = 1;
         for (uint32_t c = 0; c < n; ++c) {
             uint32_t v = p->inv[c];
             uint32_t b = p->row_ptr[v], k = p->row_ptr[v + 1] - b;
+            maxdeg = std::max(maxdeg, k);
             for (uint32_t i = 0; i < k; ++i) {
                 uint32_t e = g->rowc_host[c] + i;
                 g->edge_perm[e] = b + i;
@@ -304,10 +326,13 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 g->w_free_col[e] = p->w[b + i];
             }
         }
+        while ((1u << g->adj_shift) < maxdeg) ++g->adj_shift;
         hipStream_t s = g->stream;
         g->row_ptr.upload(g->rowc_host.data(), n + 1, s);
         g->dst.upload(dstc.data(), m, s);
         g->w.upload(g->w_free_col.data(), m, s);
+        std::vector<uint32_t> adj = g->packed_adjacency(g->w_free_col);
+        g->adj.upload(adj.data(), adj.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
         g->has_ch = !p->ch.rank.empty();
         if (!g->has_ch) {  // query-only graph (fifo_auto)
@@ -609,7 +634,8 @@ int cpd_index_set_weights(cpd_index* ix, const uint32_t* w) {
         }
         std::vector<uint32_t> wc(g->m);
         for (uint32_t e = 0; e < g->m; ++e) wc[e] = w[g->edge_perm[e]];
-        ix->w_sel.upload(wc.data(), g->m, g->stream);
+        std::vector<uint32_t> adj = g->packed_adjacency(wc);
+        ix->adj_sel.upload(adj.data(), adj.size(), g->stream);
         HIP_CHECK(hipStreamSynchronize(g->stream));
         ix->custom_w = true;
     });
@@ -620,14 +646,25 @@ int cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint3
         CPD_REQUIRE(ix && (nq == 0 || (s && t)), CPD_E_ARG, "query: null argument");
         cpd_graph* g = ix->g;
         g->select();
-        std::vector<uint32_t> sc(nq), tc(nq);
+        // counting sort by target row: a wave's lanes then walk the same row
+        std::vector<uint32_t> bucket(ix->nrows + 1, 0);
         for (uint32_t q = 0; q < nq; ++q) {
             CPD_REQUIRE(s[q] < g->n && t[q] < g->n, CPD_E_ARG, "query node out of range");
-            tc[q] = g->order[t[q]];
-            sc[q] = g->order[s[q]];
-            if (ix->row_of_col[tc[q]] == CPD_INF)
+            uint32_t r = ix->row_of_col[g->order[t[q]]];
+            if (r == CPD_INF)
                 throw Error(CPD_E_NOROW, "target " + std::to_string(t[q]) +
                                              " has no CPD row in this index");
+            bucket[r + 1]++;
+        }
+        for (uint32_t r = 0; r < ix->nrows; ++r) bucket[r + 1] += bucket[r];
+        ix->perm.resize(nq);
+        std::vector<uint32_t> sc(nq), tc(nq);
+        for (uint32_t q = 0; q < nq; ++q) {
+            uint32_t tcol = g->order[t[q]];
+            uint32_t i = bucket[ix->row_of_col[tcol]]++;
+            ix->perm[i] = q;
+            tc[i] = tcol;
+            sc[i] = g->order[s[q]];
         }
         ix->qs.upload(sc.data(), nq, g->stream);
         ix->qt.upload(tc.data(), nq, g->stream);
@@ -648,11 +685,11 @@ int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
         HIP_CHECK(hipMemsetAsync(ix->agg.p, 0, 3 * sizeof(unsigned long long), g->stream));
         hipEvent_t a = g->get_event(), b = g->get_event();
         HIP_CHECK(hipEventRecord(a, g->stream));
-        const uint32_t* w = ix->custom_w ? ix->w_sel.p : g->w.p;
+        const uint32_t* adj = ix->custom_w ? ix->adj_sel.p : g->adj.p;
         if (nq)
-            launch_table_search(g->row_ptr.p, g->dst.p, w, ix->d_row_of_col.p, ix->off.p,
-                                ix->runs.p, ix->qs.p, ix->qt.p, nq, k_moves, g->n, ix->cost.p,
-                                ix->hops.p, ix->fin.p, ix->agg.p, g->stream);
+            launch_table_search(adj, g->adj_shift, ix->d_row_of_col.p, ix->off.p, ix->runs.p,
+                                ix->qs.p, ix->qt.p, nq, k_moves, g->n, ix->cost.p, ix->hops.p,
+                                ix->fin.p, ix->agg.p, g->stream);
         HIP_CHECK(hipEventRecord(b, g->stream));
         unsigned long long hagg[3] = {0, 0, 0};
         HIP_CHECK(hipMemcpyAsync(hagg, ix->agg.p, sizeof hagg, hipMemcpyDeviceToHost, g->stream));
@@ -691,9 +728,16 @@ int cpd_query_fetch(cpd_index* ix, uint64_t* cost, uint32_t* hops, uint8_t* fini
         CPD_REQUIRE(ix, CPD_E_ARG, "null index");
         ix->g->select();
         const uint32_t nq = ix->nq;
-        if (cost && nq) HIP_CHECK(hipMemcpy(cost, ix->cost.p, nq * 8ull, hipMemcpyDeviceToHost));
-        if (hops && nq) HIP_CHECK(hipMemcpy(hops, ix->hops.p, nq * 4ull, hipMemcpyDeviceToHost));
-        if (finished && nq) HIP_CHECK(hipMemcpy(finished, ix->fin.p, nq, hipMemcpyDeviceToHost));
+        // results come back in target-sorted order; undo the permutation
+        auto fetch = [&](auto* out, auto* dev) {
+            using T = std::remove_pointer_t<decltype(out)>;
+            std::vector<T> tmp(nq);
+            HIP_CHECK(hipMemcpy(tmp.data(), dev, nq * sizeof(T), hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < nq; ++i) out[ix->perm[i]] = tmp[i];
+        };
+        if (cost && nq) fetch(cost, ix->cost.p);
+        if (hops && nq) fetch(hops, ix->hops.p);
+        if (finished && nq) fetch(finished, ix->fin.p);
     });
 }
 

@@ -268,10 +268,13 @@ __global__ __launch_bounds__(256) void rle_scan(const uint16_t* __restrict__ fm,
 // column cur is found by galloping from the previous hop's run (consecutive
 // path nodes have nearby DFS columns), then binary search inside the bracket:
 // the result is always the LAST run with start <= cur — the same run warthog's
-// get_move binary search returns [U].
+// get_move binary search returns [U].  Edges come from a packed fixed-stride
+// adjacency: edge k of column c is adj[(c << shift) + k] = (dst column, weight),
+// dst = kNoEdge past the out-degree — one 8-B load per move, no row_ptr.
+constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
+
 __global__ __launch_bounds__(256) void table_search(
-    const uint32_t* __restrict__ row_ptr, const uint32_t* __restrict__ dst,
-    const uint32_t* __restrict__ w, const uint32_t* __restrict__ row_of_col,
+    const uint2* __restrict__ adj, uint32_t shift, const uint32_t* __restrict__ row_of_col,
     const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ runs,
     const uint32_t* __restrict__ qs, const uint32_t* __restrict__ qt, uint32_t nq,
     int32_t kmoves, uint32_t n, uint64_t* __restrict__ cost_out,
@@ -317,10 +320,10 @@ __global__ __launch_bounds__(256) void table_search(
             }
             pos = lo;
             const uint32_t mv = rr[lo] & 0xFu;
-            const uint32_t e0 = row_ptr[cur];
-            if (mv >= row_ptr[cur + 1] - e0) break;
-            cost += w[e0 + mv];
-            cur = dst[e0 + mv];
+            const uint2 e = adj[((size_t)cur << shift) + mv];
+            if (e.x == kNoEdge) break;  // move past the out-degree: malformed row
+            cost += e.y;
+            cur = e.x;
             ++hops;
         }
         fin = (cur == t) ? 1u : 0u;
@@ -401,14 +404,14 @@ void launch_rle_emit(const uint16_t* fm, uint32_t npad, uint32_t nrows, const ui
            (uint32_t*)nullptr, off, runs);
 }
 
-void launch_table_search(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
-                         const uint32_t* row_of_col, const uint64_t* offsets,
-                         const uint32_t* runs, const uint32_t* qs, const uint32_t* qt,
-                         uint32_t nq, int32_t kmoves, uint32_t n, uint64_t* cost,
-                         uint32_t* hops, uint8_t* fin, unsigned long long* agg,
+void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
+                         const uint64_t* offsets, const uint32_t* runs, const uint32_t* qs,
+                         const uint32_t* qt, uint32_t nq, int32_t kmoves, uint32_t n,
+                         uint64_t* cost, uint32_t* hops, uint8_t* fin, unsigned long long* agg,
                          hipStream_t s) {
-    launch(kern::table_search, dim3((nq + 255u) / 256u), dim3(256), s, row_ptr, dst, w, row_of_col,
-           offsets, runs, qs, qt, nq, kmoves, n, cost, hops, fin, agg);
+    launch(kern::table_search, dim3((nq + 255u) / 256u), dim3(256), s,
+           reinterpret_cast<const uint2*>(adj), shift, row_of_col, offsets, runs, qs, qt, nq, kmoves,
+           n, cost, hops, fin, agg);
 }
 
 }  // namespace cpd

@@ -31,11 +31,12 @@ void launch_rle_count(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_
 void launch_rle_emit(const uint16_t* fm, uint32_t npad, uint32_t nrows, const uint64_t* off,
                      uint32_t* runs, hipStream_t s);
 
-void launch_table_search(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
-                         const uint32_t* row_of_col, const uint64_t* offsets,
-                         const uint32_t* runs, const uint32_t* qs, const uint32_t* qt,
-                         uint32_t nq, int32_t kmoves, uint32_t n, uint64_t* cost,
-                         uint32_t* hops, uint8_t* fin, unsigned long long* agg,
+// adj: packed fixed-stride adjacency, (dst column, weight) pairs, 2^shift
+// slots per column, dst = 0xFFFFFFFF past the out-degree.
+void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
+                         const uint64_t* offsets, const uint32_t* runs, const uint32_t* qs,
+                         const uint32_t* qt, uint32_t nq, int32_t kmoves, uint32_t n,
+                         uint64_t* cost, uint32_t* hops, uint8_t* fin, unsigned long long* agg,
                          hipStream_t s);
 
 }  // namespace cpd
