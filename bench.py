@@ -309,15 +309,22 @@ def main():
     qs = rng.integers(0, g.n, nq).astype(np.uint32)
     qt = last_targets[rng.integers(0, len(last_targets), nq)]
     ix.prepare(qs, qt)
-    ix.run()  # warm
-    q_ms, q_hops = 0.0, 0
-    reps = 3
-    for _ in range(reps):
-        st = ix.run()
-        q_ms += st["kernel_ms"]
-        q_hops += st["hops"]
-    q_totals = comm.reduce([float(nq * reps), q_ms, float(q_hops)], "SUM")
-    (q_ms_max,) = comm.reduce([q_ms], "MAX")
+
+    def time_queries(mode, reps=3):
+        ix.set_mode(mode)
+        ix.run()  # warm (and, for dense, expand the rows once)
+        ms, hops = 0.0, 0
+        for _ in range(reps):
+            st = ix.run()
+            ms += st["kernel_ms"]
+            hops += st["hops"]
+        tot = comm.reduce([float(nq * reps), ms, float(hops)], "SUM")
+        (ms_max,) = comm.reduce([ms], "MAX")
+        return tot, ms_max
+
+    q_rle, q_rle_ms = time_queries("rle")
+    q_totals, q_ms_max = time_queries("auto")
+    index_mode = ix.mode
 
     # ---- CPU baseline + full-size parity sample (rank 0, N = 1) -------------
     cpu = None
@@ -354,6 +361,8 @@ def main():
     if rank == 0:
         out = assemble(args, world, (g.n, g.m), B, elapsed_max, q_totals, q_ms_max, nrows, nruns,
                        kt, cpu, parity, pinfo, traffic)
+        out["query_index"] = index_mode
+        out["queries_per_s_rle"] = round(q_rle[0] / (q_rle_ms / 1e3), 1) if q_rle_ms else 0.0
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

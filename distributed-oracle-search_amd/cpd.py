@@ -44,7 +44,9 @@ EXPORTED = [
     "cpd_debug_rows", "cpd_index_create", "cpd_index_from_rows", "cpd_index_set_weights",
     "cpd_query_batch", "cpd_query_prepare", "cpd_query_run", "cpd_query_fetch",
     "cpd_index_free", "cpd_timing_enable", "cpd_timing_reset", "cpd_timing_get",
+    "cpd_index_set_mode", "cpd_index_get_mode",
 ]
+INDEX_MODES = {"auto": 0, "rle": 1, "dense": 2}
 
 
 class CpdError(RuntimeError):
@@ -349,6 +351,16 @@ class Index:
             rn = _u32(runs)
             _check(lib.cpd_index_create(graph._h, _ptr(rt, u32p), C.c_uint32(len(rt)),
                                         _ptr(off, u64p), _ptr(rn, u32p), C.byref(self._h)))
+
+    def set_mode(self, mode: str) -> None:
+        """'auto' (default), 'rle' or 'dense' — see cpd_index_set_mode."""
+        _check(lib.cpd_index_set_mode(self._h, C.c_int(INDEX_MODES[mode])))
+
+    @property
+    def mode(self) -> str:
+        m = C.c_int()
+        _check(lib.cpd_index_get_mode(self._h, C.byref(m)))
+        return {v: k for k, v in INDEX_MODES.items()}[m.value]
 
     def set_weights(self, w=None) -> None:
         if w is None:

@@ -205,6 +205,18 @@ struct cpd_index {
     DevBuf<uint32_t> d_row_of_col, runs, adj_sel;  // adj_sel: packed adjacency, custom weights
     DevBuf<uint64_t> off;
     bool custom_w = false;
+    // CPD_INDEX_AUTO / _RLE / _DENSE; dense = 4-bit move tables expanded from
+    // the RLE rows (built on first use)
+    int mode = CPD_INDEX_AUTO;
+    DevBuf<uint32_t> dense;
+    bool dense_ready = false;
+
+    bool use_dense() const {
+        if (mode == CPD_INDEX_DENSE) return true;
+        if (mode == CPD_INDEX_RLE) return false;
+        // auto: the table whose bytes are fewer (4 B per run vs n/2 B per row)
+        return nrows > 0 && 4.0 * (double)total > (double)g->npad / 2.0 * nrows;
+    }
     // query workspace; queries run sorted by target row (perm[i] = caller index)
     uint32_t nq = 0;
     std::vector<uint32_t> perm;
@@ -216,8 +228,9 @@ struct cpd_index {
 
 namespace {
 
-// Leaf flag of the level-0 shortcut (cpd_kernels.hip kLeafBit).
+// Closed-form encodings of the two lowest upward levels (cpd_kernels.hip).
 constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kL1Bit = 0x40000000u;
 
 void require_device() {
     int count = 0;
@@ -226,12 +239,30 @@ void require_device() {
         throw Error(CPD_E_HIP, "no HIP device available (libcpd has no CPU fallback)");
 }
 
-// Build the level-ordered sweep arrays in column space.
+// Nodes ordered by (level, column): node_of_slot, and lvl_first[l] = first slot.
+std::vector<uint32_t> level_order(const cpd_plan& p, const std::vector<uint32_t>& level,
+                                  uint32_t nlev, std::vector<uint32_t>& lvl_first) {
+    const uint32_t n = p.n;
+    std::vector<uint32_t> cnt(nlev + 1, 0);
+    for (uint32_t v = 0; v < n; ++v) cnt[level[v] + 1]++;
+    for (uint32_t l = 0; l < nlev; ++l) cnt[l + 1] += cnt[l];
+    lvl_first.assign(cnt.begin(), cnt.end());
+    std::vector<uint32_t> node_of_slot(n), pos(cnt.begin(), cnt.end() - 1);
+    for (uint32_t c = 0; c < n; ++c) {  // columns ascending inside a level
+        uint32_t v = p.inv[c];
+        node_of_slot[pos[level[v]]++] = v;
+    }
+    return node_of_slot;
+}
+
+// Build the level-ordered sweep arrays in column space, with the closed-form
+// encodings of cpd_kernels.hip (kLeafBit: upward level 0, kL1Bit: level 1,
+// referenced by its slot in the ASCENDING list, asc_slot[node]).
 // lvl_arcs: gathered arcs per level; lvl_reads: nodes reading their own row.
-void build_sweep(const cpd_plan& p, bool ascend, std::vector<uint32_t>& nodes,
-                 std::vector<uint32_t>& off, std::vector<uint32_t>& arcs,
-                 std::vector<uint32_t>& lvl_first, std::vector<double>& lvl_arcs,
-                 std::vector<double>& lvl_reads) {
+void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& asc_slot,
+                 std::vector<uint32_t>& nodes, std::vector<uint32_t>& off,
+                 std::vector<uint32_t>& arcs, std::vector<uint32_t>& lvl_first,
+                 std::vector<double>& lvl_arcs, std::vector<double>& lvl_reads) {
     const Hierarchy& H = p.ch;
     const uint32_t n = p.n;
     const std::vector<uint32_t>& level = ascend ? H.level_up : H.level_dn;
@@ -240,19 +271,19 @@ void build_sweep(const cpd_plan& p, bool ascend, std::vector<uint32_t>& nodes,
     const std::vector<uint64_t>& aoff = ascend ? H.dn_off : H.up_off;
     const std::vector<uint32_t>& adst = ascend ? H.dn_dst : H.up_dst;
     const std::vector<uint32_t>& aw = ascend ? H.dn_w : H.up_w;
+    const std::vector<uint32_t>& lup = H.level_up;
     CPD_REQUIRE(aoff[n] < 0xFFFFFFFFull, CPD_E_RANGE, "hierarchy has >= 2^32 arcs");
-    // counting sort by (level, column)
-    std::vector<uint32_t> cnt(nlev + 1, 0);
-    for (uint32_t v = 0; v < n; ++v) cnt[level[v] + 1]++;
-    for (uint32_t l = 0; l < nlev; ++l) cnt[l + 1] += cnt[l];
-    lvl_first.assign(cnt.begin(), cnt.end());
+    std::vector<uint32_t> node_of_slot = level_order(p, level, nlev, lvl_first);
+    // how a node is referenced: closed form (level 0 / 1 of the up sweep) or row
+    auto ref = [&](uint32_t v) -> uint32_t {
+        if (lup[v] == 0) return p.order[v] | kLeafBit;
+        if (lup[v] == 1) return asc_slot[v] | kL1Bit;
+        return p.order[v];
+    };
     nodes.assign(n, 0);
-    std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
-    const std::vector<uint32_t>& lup = H.level_up;  // leaf = upward level 0
-    for (uint32_t c = 0; c < n; ++c) {  // columns ascending inside a level
-        uint32_t v = p.inv[c];
-        // descending list: a leaf starts from the closed form, not a read
-        nodes[pos[level[v]]++] = c | (!ascend && lup[v] == 0 ? kLeafBit : 0u);
+    for (uint32_t s = 0; s < n; ++s) {
+        uint32_t v = node_of_slot[s];
+        nodes[s] = ascend ? p.order[v] : ref(v);  // descending: closed-form init
     }
     off.assign(n + 1, 0);
     arcs.clear();
@@ -261,19 +292,19 @@ void build_sweep(const cpd_plan& p, bool ascend, std::vector<uint32_t>& nodes,
     lvl_reads.assign(nlev, 0.0);
     std::vector<std::pair<uint32_t, uint32_t>> tmp;
     for (uint32_t s = 0; s < n; ++s) {
-        uint32_t v = p.inv[nodes[s] & ~kLeafBit];
+        uint32_t v = node_of_slot[s];
         tmp.clear();
         for (uint64_t e = aoff[v]; e < aoff[v + 1]; ++e) tmp.push_back({p.order[adst[e]], aw[e]});
         std::sort(tmp.begin(), tmp.end());
         for (auto& a : tmp) {
-            // ascending arcs into leaves are evaluated in closed form
-            bool leaf = ascend && lup[p.inv[a.first]] == 0;
-            arcs.push_back(a.first | (leaf ? kLeafBit : 0u));
+            // ascending arcs into upward levels 0/1 use the closed forms
+            uint32_t r = ascend ? ref(p.inv[a.first]) : a.first;
+            arcs.push_back(r);
             arcs.push_back(a.second);
-            if (!leaf) lvl_arcs[level[v]] += 1.0;
+            if (!(r & (kLeafBit | kL1Bit))) lvl_arcs[level[v]] += 1.0;
         }
         off[s + 1] = off[s] + (uint32_t)tmp.size();
-        if (!ascend && !(nodes[s] & kLeafBit)) lvl_reads[level[v]] += 1.0;
+        if (!ascend && !(nodes[s] & (kLeafBit | kL1Bit))) lvl_reads[level[v]] += 1.0;
     }
 }
 
@@ -339,16 +370,23 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             *out = g.release();
             return;
         }
-        std::vector<uint32_t> nodes, off, arcs;
+        std::vector<uint32_t> nodes, off, arcs, lvl;
         std::vector<double> unused;
-        build_sweep(*p, true, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs, unused);
+        std::vector<uint32_t> asc_slot(n);
+        {
+            std::vector<uint32_t> node_of_slot =
+                level_order(*p, p->ch.level_up, p->ch.nlev_up, lvl);
+            for (uint32_t s2 = 0; s2 < n; ++s2) asc_slot[node_of_slot[s2]] = s2;
+        }
+        build_sweep(*p, true, asc_slot, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs, unused);
         g->asc_off_host = off;
         g->asc_nodes.upload(nodes.data(), nodes.size(), s);
         g->asc_off.upload(off.data(), off.size(), s);
         g->asc_arcs.upload(arcs.data(), arcs.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
         g->ch_arcs = arcs.size() / 2;
-        build_sweep(*p, false, nodes, off, arcs, g->dsc_lvl, g->dsc_lvl_arcs, g->dsc_lvl_reads);
+        build_sweep(*p, false, asc_slot, nodes, off, arcs, g->dsc_lvl, g->dsc_lvl_arcs,
+                    g->dsc_lvl_reads);
         g->dsc_nodes.upload(nodes.data(), nodes.size(), s);
         g->dsc_off.upload(off.data(), off.size(), s);
         g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
@@ -387,11 +425,11 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
     const uint32_t B = g->B, n = g->n;
     const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
     const uint32_t active = slabs * 1024u;
-    // ascending sweep: each level reads lower levels' rows.  Level 0 (leaves)
-    // is never materialised (closed form, see kLeafBit), so it is skipped.
+    // ascending sweep: each level reads lower levels' rows.  Levels 0 and 1
+    // are never materialised (closed forms, kLeafBit / kL1Bit): not launched.
     // Bytes per level: gathered rows 4 B x target, row writes 4 B x target,
     // arcs 8 B and node slot 12 B per 1024-target slab.
-    for (size_t l = 1; l + 1 < g->asc_lvl.size(); ++l) {
+    for (size_t l = 2; l + 1 < g->asc_lvl.size(); ++l) {
         uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
         if (!cnt) continue;
         double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
@@ -399,7 +437,8 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
                        12.0 * cnt * slabs;
         g->timed("sweep_up", bytes, [&] {
             launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt, g->dist.p,
-                         g->tgt.p, B, slabs, g->stream);
+                         g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
+                         g->stream);
         });
     }
     for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
@@ -409,7 +448,8 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
                        8.0 * g->dsc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
         g->timed("sweep_down", bytes, [&] {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
-                         g->tgt.p, B, slabs, g->stream);
+                         g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
+                         g->stream);
         });
     }
     // per row: own distance 4n + neighbour distances 4m + first-move write 2npad;
@@ -437,10 +477,21 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k) {
     g->tgt.upload(cols.data(), g->B, g->stream);
 }
 
+// CPD_TRACE=1: host-side phase times of every batch on stderr.
+bool trace_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("CPD_TRACE");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
 // Build rows for one batch of k <= B targets; append to r (device).
 void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r) {
+    const double t0 = now_seconds();
     upload_targets(g, targets, k);
     run_sweeps_and_fm(g, k);
+    const double t1 = now_seconds();
     const uint32_t npad = g->npad;
     g->timed("rle_count", 2.0 * npad * k + 4.0 * k, [&] {
         launch_rle_count(g->fm.p, npad, k, g->counts.p, g->stream);
@@ -449,13 +500,16 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, g->stream));
     g->sync();
+    const double t2 = now_seconds();
     // row offsets for this batch, appended after r->total
     std::vector<uint64_t> off(k + 1);
     off[0] = r->total;
     for (uint32_t i = 0; i < k; ++i) off[i + 1] = off[i] + counts[i];
     uint64_t new_total = off[k];
     if (new_total > r->runs.n) {  // grow, preserving the rows already built
-        size_t want = std::max<size_t>(new_total, r->runs.n + r->runs.n / 2);
+        // 25% headroom: batches differ by a few runs, and re-allocating tens of
+        // GB costs ~1 s, so a reused buffer must not grow again per batch
+        size_t want = std::max<size_t>(new_total + new_total / 4, r->runs.n + r->runs.n / 2);
         uint32_t* np = nullptr;
         HIP_CHECK(hipMalloc(&np, std::max<size_t>(want, 1) * sizeof(uint32_t)));
         if (r->total)
@@ -466,12 +520,20 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
         r->runs.p = np;
         r->runs.n = want;
     }
+    const double t3 = now_seconds();
     g->row_off.upload(off.data(), k + 1, g->stream);
     double ebytes = 2.0 * npad * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
     g->timed("rle_emit", ebytes, [&] {
         launch_rle_emit(g->fm.p, npad, k, g->row_off.p, r->runs.p, g->stream);
     });
     g->sync();
+    if (trace_on())
+        std::fprintf(stderr,
+                     "[cpd] batch %u rows: launch sweeps+fm %.2f ms, to counts %.2f ms, grow %.2f "
+                     "ms, emit %.2f ms, runs %llu (cap %zu)\n",
+                     k, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3,
+                     (now_seconds() - t3) * 1e3, (unsigned long long)(new_total - r->total),
+                     r->runs.n);
     r->offsets.insert(r->offsets.end(), off.begin() + 1, off.end());
     r->targets.insert(r->targets.end(), targets, targets + k);
     r->nrows += k;
@@ -676,17 +738,63 @@ int cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint3
     });
 }
 
+}  // extern "C"
+
+namespace {
+
+// Expand the index's RLE rows into dense move tables (once per index).
+void ensure_dense(cpd_index* ix) {
+    cpd_graph* g = ix->g;
+    CPD_REQUIRE(g->npad / kFmTile < 65536u, CPD_E_RANGE, "graph too large for dense tables");
+    const size_t words = (size_t)ix->nrows * (g->npad / 8u);
+    ix->dense.alloc(words);
+    if (ix->nrows)
+        g->timed("expand_rows", 4.0 * (double)ix->total + 4.0 * (double)words + 16.0 * ix->nrows,
+                 [&] {
+                     launch_expand_rows(ix->off.p, ix->runs.p, ix->nrows, g->npad, ix->dense.p,
+                                        g->stream);
+                 });
+    g->sync();
+    ix->dense_ready = true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cpd_index_set_mode(cpd_index* ix, int mode) {
+    return guarded([&] {
+        CPD_REQUIRE(ix, CPD_E_ARG, "null index");
+        CPD_REQUIRE(mode == CPD_INDEX_AUTO || mode == CPD_INDEX_RLE || mode == CPD_INDEX_DENSE,
+                    CPD_E_ARG, "index mode must be CPD_INDEX_AUTO, _RLE or _DENSE");
+        ix->mode = mode;
+    });
+}
+
+int cpd_index_get_mode(const cpd_index* ix, int* mode) {
+    return guarded([&] {
+        CPD_REQUIRE(ix && mode, CPD_E_ARG, "null argument");
+        *mode = ix->use_dense() ? CPD_INDEX_DENSE : CPD_INDEX_RLE;
+    });
+}
+
 int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
     return guarded([&] {
         CPD_REQUIRE(ix, CPD_E_ARG, "null index");
         cpd_graph* g = ix->g;
         g->select();
         const uint32_t nq = ix->nq;
+        const bool dense = ix->use_dense();
+        if (dense && !ix->dense_ready) ensure_dense(ix);
         HIP_CHECK(hipMemsetAsync(ix->agg.p, 0, 3 * sizeof(unsigned long long), g->stream));
         hipEvent_t a = g->get_event(), b = g->get_event();
         HIP_CHECK(hipEventRecord(a, g->stream));
         const uint32_t* adj = ix->custom_w ? ix->adj_sel.p : g->adj.p;
-        if (nq)
+        if (nq && dense)
+            launch_table_search_dense(adj, g->adj_shift, ix->d_row_of_col.p, ix->dense.p, g->npad,
+                                      ix->qs.p, ix->qt.p, nq, k_moves, g->n, ix->cost.p,
+                                      ix->hops.p, ix->fin.p, ix->agg.p, g->stream);
+        else if (nq)
             launch_table_search(adj, g->adj_shift, ix->d_row_of_col.p, ix->off.p, ix->runs.p,
                                 ix->qs.p, ix->qt.p, nq, k_moves, g->n, ix->cost.p, ix->hops.p,
                                 ix->fin.p, ix->agg.p, g->stream);
@@ -699,19 +807,25 @@ int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
         g->ev_pool.push_back(a);
         g->ev_pool.push_back(b);
         if (g->timing) {
-            Agg& ag = g->agg["table_search"];
+            Agg& ag = g->agg[dense ? "table_search_dense" : "table_search"];
             ag.launches++;
             ag.ms += ms;
-            // SURVEY.md §8(d) B_q = 8 + 12 + 8 + L * (4 ceil(log2 R) + 16)
-            double mean_log = 0.0;
-            if (ix->nrows) {
-                double s = 0.0;
-                for (uint32_t i = 0; i < ix->nrows; ++i)
-                    s += std::ceil(std::log2((double)std::max<uint64_t>(
-                        2, ix->offsets[i + 1] - ix->offsets[i])));
-                mean_log = s / ix->nrows;
+            if (dense) {
+                // per query 8 (s,t) + 13 (outputs) + 4 (row); per move one
+                // 4-B move word + one 8-B packed edge
+                ag.bytes += 25.0 * nq + 12.0 * (double)hagg[1];
+            } else {
+                // SURVEY.md §8(d) B_q = 8 + 12 + 8 + L * (4 ceil(log2 R) + 16)
+                double mean_log = 0.0;
+                if (ix->nrows) {
+                    double s = 0.0;
+                    for (uint32_t i = 0; i < ix->nrows; ++i)
+                        s += std::ceil(std::log2((double)std::max<uint64_t>(
+                            2, ix->offsets[i + 1] - ix->offsets[i])));
+                    mean_log = s / ix->nrows;
+                }
+                ag.bytes += 28.0 * nq + (double)hagg[1] * (4.0 * mean_log + 16.0);
             }
-            ag.bytes += 28.0 * nq + (double)hagg[1] * (4.0 * mean_log + 16.0);
         }
         if (st) {
             st->queries = nq;

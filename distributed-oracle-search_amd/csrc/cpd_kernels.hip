@@ -29,12 +29,18 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t d, uint32_t w) {
 constexpr uint32_t kSeg = 32;          // columns per lane
 constexpr uint32_t kTile = 64 * kSeg;  // columns per wave tile (npad % kTile == 0)
 
-// Level-0 shortcut.  A node with no down-arcs ("leaf" of the upward sweep) has
-// d_up = 0 at its own target and INF elsewhere, so it is never materialised:
-// an upward-sweep arc into a leaf carries kLeafBit in its column and is
-// evaluated from the targets (no gather); a leaf in the downward node list
-// carries kLeafBit and starts from the same closed form (no read).
+// Closed forms for the two lowest upward levels, so they are never stored.
+// A level-0 node ("leaf": no down-arcs) has d_up = 0 at its own target, INF
+// elsewhere.  A level-1 node's down-arcs all end in leaves, so its d_up is
+// min(leaf form of itself, w_j + leaf form of each leaf j) — a few compares
+// against the lane's targets.  Encoding (arcs and down-sweep node slots):
+//   kLeafBit | column            -> leaf closed form
+//   kL1Bit   | ascending slot s  -> level-1 closed form over the ascending
+//                                   list's node s and its (leaf) arcs
+//   column                       -> a materialised distance row (gather)
 constexpr uint32_t kLeafBit = 0x80000000u;
+constexpr uint32_t kL1Bit = 0x40000000u;
+constexpr uint32_t kIdxMask = 0x3FFFFFFFu;
 
 __device__ __forceinline__ void min4(uint4& acc, const uint4 d, uint32_t w) {
     acc.x = min(acc.x, sat_add(d.x, w));
@@ -48,10 +54,28 @@ __device__ __forceinline__ uint4 leaf4(const uint4 t, uint32_t col, uint32_t w) 
                       t.w == col ? w : INF);
 }
 
-// Value an arc contributes: a gathered distance row, or the leaf closed form.
+// The ascending sweep's arrays, read for level-1 closed forms.
+struct Closed {
+    const uint32_t* __restrict__ nodes;
+    const uint32_t* __restrict__ off;
+    const uint2* __restrict__ arcs;
+};
+
+__device__ __forceinline__ uint4 l1_val(const Closed& cf, uint32_t s, const uint4 t) {
+    uint4 acc = leaf4(t, cf.nodes[s], 0u);
+    const uint32_t a1 = cf.off[s + 1];
+    for (uint32_t a = cf.off[s]; a < a1; ++a) {
+        const uint2 e = cf.arcs[a];  // e.x = kLeafBit | leaf column
+        min4(acc, leaf4(t, e.x & kIdxMask, 0u), e.y);
+    }
+    return acc;
+}
+
+// Value an arc contributes (before adding its weight).
 __device__ __forceinline__ uint4 arc_val(const uint4* __restrict__ d4, const uint4 t, uint2 e,
-                                         uint32_t B4, uint32_t l4) {
-    if (e.x & kLeafBit) return leaf4(t, e.x & ~kLeafBit, 0u);
+                                         uint32_t B4, uint32_t l4, const Closed& cf) {
+    if (e.x & kLeafBit) return leaf4(t, e.x & kIdxMask, 0u);
+    if (e.x & kL1Bit) return l1_val(cf, e.x & kIdxMask, t);
     return d4[(size_t)e.x * B4 + l4];
 }
 
@@ -59,8 +83,8 @@ __device__ __forceinline__ uint4 arc_val(const uint4* __restrict__ d4, const uin
 // node v = nodes[slot]; its arcs (col, w) are wave-uniform (scalar loads); each
 // lane owns 4 consecutive targets.  ASCEND: upward sweep, init 0 at the lane's
 // own target else INF.  !ASCEND: downward sweep, init = current dist (the
-// upward value, or the leaf closed form).  Then acc = min(acc, w + d[arc.col])
-// over the arcs, eight gathers in flight per wave.
+// upward value, or its closed form for levels 0/1).  Then acc = min(acc,
+// w + d[arc]) over the arcs, eight gathers in flight per wave.
 template <bool ASCEND>
 __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ nodes,
                                                    const uint32_t* __restrict__ arc_off,
@@ -68,19 +92,28 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
                                                    uint32_t slot0,
                                                    uint32_t* __restrict__ dist,
                                                    const uint4* __restrict__ tgt4,
-                                                   uint32_t B4) {
+                                                   uint32_t B4, Closed cf) {
     const uint32_t slot = slot0 + blockIdx.x;
     const uint32_t l4 = blockIdx.y * 256u + threadIdx.x;
     const uint32_t vraw = nodes[slot];
-    const uint32_t v = vraw & ~kLeafBit;
-    const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
     uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
     const uint4 t = tgt4[l4];
+    uint32_t v;
     uint4 acc;
-    if (ASCEND || (vraw & kLeafBit))
+    if (ASCEND) {
+        v = vraw;
         acc = leaf4(t, v, 0u);
-    else
+    } else if (vraw & kLeafBit) {
+        v = vraw & kIdxMask;
+        acc = leaf4(t, v, 0u);
+    } else if (vraw & kL1Bit) {
+        v = cf.nodes[vraw & kIdxMask];
+        acc = l1_val(cf, vraw & kIdxMask, t);
+    } else {
+        v = vraw;
         acc = d4[(size_t)v * B4 + l4];
+    }
+    const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
     uint32_t a = a0;
     for (; a + 8 <= a1; a += 8) {
         uint2 e[8];
@@ -88,13 +121,13 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = arc_val(d4, t, e[i], B4, l4);
+        for (int i = 0; i < 8; ++i) x[i] = arc_val(d4, t, e[i], B4, l4, cf);
 #pragma unroll
         for (int i = 0; i < 8; ++i) min4(acc, x[i], e[i].y);
     }
     for (; a < a1; ++a) {
         const uint2 e = arcs[a];
-        min4(acc, arc_val(d4, t, e, B4, l4), e.y);
+        min4(acc, arc_val(d4, t, e, B4, l4, cf), e.y);
     }
     d4[(size_t)v * B4 + l4] = acc;
 }
@@ -273,6 +306,10 @@ __global__ __launch_bounds__(256) void rle_scan(const uint16_t* __restrict__ fm,
 // dst = kNoEdge past the out-degree — one 8-B load per move, no row_ptr.
 constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
 
+// Per-wave sums of (cost, moves, finished) added to agg[2], agg[1], agg[0].
+__device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
+                           unsigned long long* __restrict__ agg);
+
 __global__ __launch_bounds__(256) void table_search(
     const uint2* __restrict__ adj, uint32_t shift, const uint32_t* __restrict__ row_of_col,
     const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ runs,
@@ -331,6 +368,95 @@ __global__ __launch_bounds__(256) void table_search(
         hops_out[q] = hops;
         fin_out[q] = (uint8_t)fin;
     }
+    wave_stats(cost, hops, fin, agg);
+}
+
+// Expand RLE rows into dense 4-bit move tables (8 columns per u32, column c at
+// bits 4*(c&7) of word c>>3).  One wave per (row, 2048-column tile): the runs
+// covering the tile (found by two wave-uniform binary searches) go to LDS,
+// then lane l resolves its 32 columns by a short LDS search and a forward walk
+// and stores 4 words (16 B).  Moves are copied, never recomputed: column c's
+// move is exactly the move of the last run starting at or before c.
+__global__ __launch_bounds__(64) void expand_rows(const uint64_t* __restrict__ offsets,
+                                                  const uint32_t* __restrict__ runs,
+                                                  uint32_t words_per_row,
+                                                  uint32_t* __restrict__ dense) {
+    __shared__ uint32_t tile_runs[kTile + 1];
+    const uint32_t row = blockIdx.x, t = blockIdx.y, lane = threadIdx.x;
+    const uint32_t* __restrict__ rr = runs + offsets[row];
+    const uint32_t R = (uint32_t)(offsets[row + 1] - offsets[row]);
+    const uint32_t c_lo = t * kTile, c_hi = c_lo + kTile;
+    // r0 = last run with start <= c_lo (start(0) = 0), r1 = first run with start >= c_hi
+    uint32_t lo = 0, hi = R;
+    while (lo + 1 < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((rr[mid] >> 4) > c_lo) hi = mid;
+        else lo = mid;
+    }
+    const uint32_t r0 = lo;
+    lo = r0;
+    hi = R;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((rr[mid] >> 4) >= c_hi) hi = mid;
+        else lo = mid + 1;
+    }
+    const uint32_t cnt = lo - r0;  // <= kTile + 1: one run per column plus the carry
+    for (uint32_t i = lane; i < cnt; i += 64u) tile_runs[i] = rr[r0 + i];
+    __syncthreads();
+    const uint32_t c0 = c_lo + lane * kSeg;
+    uint32_t a = 0, b = cnt;  // last tile run with start <= c0
+    while (a + 1 < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if ((tile_runs[mid] >> 4) > c0) b = mid;
+        else a = mid;
+    }
+    uint32_t words[4] = {0, 0, 0, 0};
+#pragma unroll 4
+    for (uint32_t k = 0; k < kSeg; ++k) {
+        const uint32_t c = c0 + k;
+        while (a + 1 < cnt && (tile_runs[a + 1] >> 4) <= c) ++a;
+        words[k >> 3] |= (tile_runs[a] & 0xFu) << (4u * (k & 7u));
+    }
+    uint4* out = reinterpret_cast<uint4*>(dense + (size_t)row * words_per_row + (c0 >> 3));
+    *out = make_uint4(words[0], words[1], words[2], words[3]);
+}
+
+// Table-search over dense move tables: one nibble load + one packed edge load
+// per move.  Same walk, same results as table_search.
+__global__ __launch_bounds__(256) void table_search_dense(
+    const uint2* __restrict__ adj, uint32_t shift, const uint32_t* __restrict__ row_of_col,
+    const uint32_t* __restrict__ dense, uint32_t words_per_row,
+    const uint32_t* __restrict__ qs, const uint32_t* __restrict__ qt, uint32_t nq,
+    int32_t kmoves, uint32_t n, uint64_t* __restrict__ cost_out,
+    uint32_t* __restrict__ hops_out, uint8_t* __restrict__ fin_out,
+    unsigned long long* __restrict__ agg) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    uint64_t cost = 0;
+    uint32_t hops = 0, fin = 0;
+    if (q < nq) {
+        const uint32_t t = qt[q];
+        uint32_t cur = qs[q];
+        const uint32_t* __restrict__ row = dense + (size_t)row_of_col[t] * words_per_row;
+        const uint32_t limit = kmoves >= 0 ? (uint32_t)kmoves : n;
+        while (cur != t && hops < limit && hops < n) {
+            const uint32_t mv = (row[cur >> 3] >> (4u * (cur & 7u))) & 0xFu;
+            const uint2 e = adj[((size_t)cur << shift) + mv];
+            if (e.x == kNoEdge) break;
+            cost += e.y;
+            cur = e.x;
+            ++hops;
+        }
+        fin = (cur == t) ? 1u : 0u;
+        cost_out[q] = cost;
+        hops_out[q] = hops;
+        fin_out[q] = (uint8_t)fin;
+    }
+    wave_stats(cost, hops, fin, agg);
+}
+
+__device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
+                           unsigned long long* __restrict__ agg) {
     // wave reduction, one atomic per wave per counter
     unsigned long long c = cost, h = hops, f = fin;
 #pragma unroll
@@ -372,16 +498,18 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop) {
 
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* arcs32, uint32_t slot0, uint32_t count, uint32_t* dist,
-                  const uint32_t* tgt, uint32_t B, uint32_t slabs, hipStream_t s) {
+                  const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
+                  const uint32_t* asc_off, const uint32_t* asc_arcs, hipStream_t s) {
     dim3 grid(count, slabs);
     const uint4* t4 = reinterpret_cast<const uint4*>(tgt);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
+    const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
     if (ascend)
         launch(kern::sweep_level<true>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, dist, t4,
-               B / 4u);
+               B / 4u, cf);
     else
         launch(kern::sweep_level<false>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, dist, t4,
-               B / 4u);
+               B / 4u, cf);
 }
 
 void launch_first_moves(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
@@ -402,6 +530,22 @@ void launch_rle_emit(const uint16_t* fm, uint32_t npad, uint32_t nrows, const ui
                      uint32_t* runs, hipStream_t s) {
     launch(kern::rle_scan<true>, dim3((nrows + 3u) / 4u), dim3(256), s, fm, npad, nrows,
            (uint32_t*)nullptr, off, runs);
+}
+
+void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,
+                        uint32_t npad, uint32_t* dense, hipStream_t s) {
+    launch(kern::expand_rows, dim3(nrows, npad / kern::kTile), dim3(64), s, offsets, runs,
+           npad / 8u, dense);
+}
+
+void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
+                               const uint32_t* dense, uint32_t npad, const uint32_t* qs,
+                               const uint32_t* qt, uint32_t nq, int32_t kmoves, uint32_t n,
+                               uint64_t* cost, uint32_t* hops, uint8_t* fin,
+                               unsigned long long* agg, hipStream_t s) {
+    launch(kern::table_search_dense, dim3((nq + 255u) / 256u), dim3(256), s,
+           reinterpret_cast<const uint2*>(adj), shift, row_of_col, dense, npad / 8u, qs, qt, nq,
+           kmoves, n, cost, hops, fin, agg);
 }
 
 void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,

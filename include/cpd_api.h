@@ -181,6 +181,19 @@ int  cpd_index_create(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows,
                       cpd_index** out);
 /* Same, straight from device-resident rows (no host round trip). */
 int  cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out);
+
+/* In-HBM representation the extraction walks.  RLE: binary search in the run
+ * rows (galloping from the previous move's run).  DENSE: the rows expanded on
+ * the GPU into 4-bit move tables (n/2 bytes per row, one load per move) —
+ * the same move for every column, so identical results.  AUTO (default)
+ * picks the smaller of the two (reverse-CPD rows on road graphs often hold
+ * more than n/8 runs, where the dense table is smaller AND faster).
+ * get_mode reports the representation AUTO resolves to.                     */
+#define CPD_INDEX_AUTO  0
+#define CPD_INDEX_RLE   1
+#define CPD_INDEX_DENSE 2
+int  cpd_index_set_mode(cpd_index* ix, int mode);
+int  cpd_index_get_mode(const cpd_index* ix, int* mode);
 /* Edge weights used for path cost (m entries, original edge order):
  * NULL restores the free-flow weights; otherwise e.g. the .diff weights
  * (process_query.py:89,178 sends the diff name with every batch).           */

@@ -45,13 +45,16 @@ def test_rows_bit_exact(setup):
     np.testing.assert_array_equal(runs, ref_runs, err_msg=name)
 
 
-def test_queries_free_flow_and_congested(setup):
+@pytest.mark.parametrize("mode", ["rle", "dense", "auto"])
+def test_queries_free_flow_and_congested(setup, mode):
     name, g, plan, dev = setup
     rng = np.random.default_rng(2)
     targets = rng.choice(g.n, size=min(g.n, 50), replace=False).astype(np.uint32)
     rows = dev.build_rows(targets)
     off, runs = rows.export()
     ix = cpd.Index(dev, rows=rows)
+    ix.set_mode(mode)
+    assert ix.mode == (mode if mode != "auto" else ix.mode)
     nq = 4000
     s = rng.integers(0, g.n, nq).astype(np.uint32)
     t = targets[rng.integers(0, len(targets), nq)]
@@ -98,6 +101,8 @@ def test_index_from_host_arrays_and_norow():
     rng = np.random.default_rng(4)
     s = rng.integers(0, g.n, 1000).astype(np.uint32)
     t = targets[rng.integers(0, len(targets), 1000)]
+    a.set_mode("rle")
+    b.set_mode("dense")
     ca = a.query(s, t)
     cb = b.query(s, t)
     for x, y in zip(ca[:3], cb[:3]):
