@@ -41,7 +41,7 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--partmethod", default="div")
     ap.add_argument("--partkey", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=8192, help="rows per step (multiple of 1024)")
+    ap.add_argument("--batch", type=int, default=16384, help="rows per step (multiple of 1024)")
     ap.add_argument("--queries", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--cpu-rows-per-thread", type=int, default=8)
@@ -107,7 +107,9 @@ def pmc_traffic(args, plan_path):
     for e in out.values():
         nf, nw = max(1, e.pop("n_FETCH_SIZE")), max(1, e.pop("n_WRITE_SIZE"))
         e["launches"] = nf
-        e["bytes_per_launch"] = 2.0 * e["FETCH_SIZE"] * 1024.0 / nf + e["WRITE_SIZE"] * 1024.0 / nw
+        e["read_bytes_per_launch"] = 2.0 * e["FETCH_SIZE"] * 1024.0 / nf
+        e["write_bytes_per_launch"] = e["WRITE_SIZE"] * 1024.0 / nw
+        e["bytes_per_launch"] = e["read_bytes_per_launch"] + e["write_bytes_per_launch"]
     shutil.rmtree(base, ignore_errors=True)
     return out
 
@@ -224,7 +226,9 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
                       "levels": [pinfo["levels_up"], pinfo["levels_dn"]],
                       "build_s": round(pinfo["ch_seconds"], 1)} if pinfo else None,
         "pmc_traffic_per_launch": {k: {"launches": v["launches"],
-                                       "bytes": round(v["bytes_per_launch"], 1)}
+                                       "bytes": round(v["bytes_per_launch"], 1),
+                                       "read": round(v["read_bytes_per_launch"], 1),
+                                       "write": round(v["write_bytes_per_launch"], 1)}
                                    for k, v in (traffic or {}).items()},
     }
 
@@ -267,10 +271,17 @@ def main():
     if world == 1 and not args.no_pmc:
         traffic = pmc_traffic(args, plan_path)
 
+    # CPD_BENCH_SHARE_GPU=1 (rehearsal on a 1-GPU box only): every rank uses
+    # GPU 0 and the harness collectives go over gloo.  Never used for numbers.
+    share = os.environ.get("CPD_BENCH_SHARE_GPU") == "1"
+    gpu = 0 if share else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    comm = Comm(world, rank, local, device=f"cuda:{local}")
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    comm = Comm(world, rank, local, device=None if share else f"cuda:{local}")
     comm.barrier()
     plan = cpd.Plan.load(plan_path)
     pinfo = plan.info()
@@ -279,7 +290,7 @@ def main():
         f"{pinfo['ch_seconds']:.1f}s, {pinfo['ch_up_arcs'] + pinfo['ch_dn_arcs']} arcs, levels "
         f"{pinfo['levels_up']}+{pinfo['levels_dn']})")
 
-    dev = cpd.Graph(plan, device=local, batch=args.batch)
+    dev = cpd.Graph(plan, device=gpu, batch=args.batch)
     B = dev.batch
     owned = shard_targets(g.n, world, args.partmethod, args.partkey, rank)
     if len(owned) == 0:

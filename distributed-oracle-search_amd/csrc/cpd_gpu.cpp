@@ -174,7 +174,7 @@ struct cpd_graph {
             // per target: dist 4n + fm 2npad + output runs (<= 4n, ~2.5n typical)
             double per = 4.0 * n + 2.0 * npad + 4.0 * n;
             double fit = 0.4 * (double)free_b / per;
-            want = (uint32_t)std::min(8192.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
+            want = (uint32_t)std::min(16384.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
         }
         want = (want + 1023u) / 1024u * 1024u;
         if (want == B && dist.p) return;
