@@ -453,13 +453,13 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
         });
     }
     // per row: own distance 4n + neighbour distances 4m + first-move write 2npad;
-    // the CSR (row_ptr, dst, w) is read once per 1024-target slab
+    // the packed adjacency (8 B per slot) is read once per 1024-target slab
     const uint32_t fslabs = (k + 1023u) / 1024u;
     double fbytes = (4.0 * n + 4.0 * g->m + 2.0 * g->npad) * (fslabs * 1024.0) +
-                    (4.0 * (n + 1) + 8.0 * g->m) * fslabs;
+                    8.0 * (double)n * (double)(1u << g->adj_shift) * fslabs;
     g->timed("first_moves", fbytes, [&] {
-        launch_first_moves(g->row_ptr.p, g->dst.p, g->w.p, g->dist.p, g->tgt.p, B, k, n,
-                           g->npad, g->fm.p, g->stream);
+        launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, g->tgt.p, B, k, n, g->npad,
+                           g->fm.p, g->stream);
     });
 }
 

@@ -145,9 +145,13 @@ __device__ __forceinline__ uint32_t fm_final(uint32_t c, uint32_t tc, uint32_t d
 // instruction, like the sweeps).  For each column c: fm = bits k with
 // w_k + d(dst_k) == d(c), wildcard at the target and at unreachable columns;
 // the segment's 32 sets per target are one 64-B line of the target's row.
-__global__ __launch_bounds__(256) void first_moves(const uint32_t* __restrict__ row_ptr,
-                                                   const uint32_t* __restrict__ dst,
-                                                   const uint32_t* __restrict__ w,
+// Edges come from the packed fixed-stride adjacency (SLOTS = 2^shift per
+// column, kNoEdge padding), so a group of G columns issues its G own-row and
+// G*SLOTS neighbour gathers back to back, with no dependent CSR lookups.
+constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
+
+template <int SLOTS, int G>
+__global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj,
                                                    const uint32_t* __restrict__ dist,
                                                    const uint32_t* __restrict__ tgt,
                                                    uint32_t B, uint32_t n, uint32_t npad,
@@ -160,27 +164,59 @@ __global__ __launch_bounds__(256) void first_moves(const uint32_t* __restrict__ 
     uint32_t pk[4][16];
 #pragma unroll
     for (int p = 0; p < 16; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
+    constexpr int KC = SLOTS < 4 ? SLOTS : 4;  // slots gathered per chunk
 #pragma unroll
-    for (int cc = 0; cc < (int)kSeg; ++cc) {
-        const uint32_t c = c0 + (uint32_t)cc;
-        if (c < n) {
-            const uint4 dn = d4[(size_t)c * B4 + l4];
-            const uint32_t e0 = row_ptr[c], e1 = row_ptr[c + 1];
-            uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-            for (uint32_t e = e0; e < e1; ++e) {
-                const uint4 dv = d4[(size_t)dst[e] * B4 + l4];
-                const uint32_t we = w[e], k = e - e0;
-                b0 |= fm_bit(dv.x, we, dn.x, k);
-                b1 |= fm_bit(dv.y, we, dn.y, k);
-                b2 |= fm_bit(dv.z, we, dn.z, k);
-                b3 |= fm_bit(dv.w, we, dn.w, k);
-            }
+    for (int cg = 0; cg < (int)kSeg; cg += G) {
+        uint4 dn[G];
+        uint2 e[G][SLOTS];  // wave-uniform: scalar registers
+        uint32_t b[G][4];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const uint32_t c = c0 + (uint32_t)(cg + j);
+            const bool ok = c < n;  // wave-uniform
+#pragma unroll
+            for (int k = 0; k < SLOTS; ++k)
+                e[j][k] = ok ? adj[(size_t)c * SLOTS + k] : make_uint2(kNoEdge, 0u);
+            dn[j] = ok ? d4[(size_t)c * B4 + l4] : make_uint4(INF, INF, INF, INF);
+            b[j][0] = b[j][1] = b[j][2] = b[j][3] = 0;
+        }
+#pragma unroll
+        for (int kb = 0; kb < SLOTS; kb += KC) {
+            bool any = false;  // edges are packed first: an empty chunk ends them all
+#pragma unroll
+            for (int j = 0; j < G; ++j) any |= e[j][kb].x != kNoEdge;
+            if (!any) break;
+            uint4 dv[G][KC];
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+#pragma unroll
+                for (int k = 0; k < KC; ++k)
+                    if (e[j][kb + k].x != kNoEdge)
+                        dv[j][k] = d4[(size_t)e[j][kb + k].x * B4 + l4];
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+#pragma unroll
+                for (int k = 0; k < KC; ++k) {
+                    if (e[j][kb + k].x == kNoEdge) continue;
+                    const uint32_t we = e[j][kb + k].y;
+                    b[j][0] |= fm_bit(dv[j][k].x, we, dn[j].x, kb + k);
+                    b[j][1] |= fm_bit(dv[j][k].y, we, dn[j].y, kb + k);
+                    b[j][2] |= fm_bit(dv[j][k].z, we, dn[j].z, kb + k);
+                    b[j][3] |= fm_bit(dv[j][k].w, we, dn[j].w, kb + k);
+                }
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const uint32_t c = c0 + (uint32_t)(cg + j);
+            if (c >= n) continue;  // stays the wildcard padding
+            const uint32_t b0 = b[j][0], b1 = b[j][1], b2 = b[j][2], b3 = b[j][3];
+            const int cc = cg + j;
             const int sh = 16 * (cc & 1);
             const uint32_t keep = 0xFFFF0000u >> sh;  // clear this column's half
-            pk[0][cc >> 1] = (pk[0][cc >> 1] & keep) | (fm_final(c, tc.x, dn.x, b0) << sh);
-            pk[1][cc >> 1] = (pk[1][cc >> 1] & keep) | (fm_final(c, tc.y, dn.y, b1) << sh);
-            pk[2][cc >> 1] = (pk[2][cc >> 1] & keep) | (fm_final(c, tc.z, dn.z, b2) << sh);
-            pk[3][cc >> 1] = (pk[3][cc >> 1] & keep) | (fm_final(c, tc.w, dn.w, b3) << sh);
+            pk[0][cc >> 1] = (pk[0][cc >> 1] & keep) | (fm_final(c, tc.x, dn[j].x, b0) << sh);
+            pk[1][cc >> 1] = (pk[1][cc >> 1] & keep) | (fm_final(c, tc.y, dn[j].y, b1) << sh);
+            pk[2][cc >> 1] = (pk[2][cc >> 1] & keep) | (fm_final(c, tc.z, dn[j].z, b2) << sh);
+            pk[3][cc >> 1] = (pk[3][cc >> 1] & keep) | (fm_final(c, tc.w, dn[j].w, b3) << sh);
         }
     }
 #pragma unroll
@@ -304,7 +340,6 @@ __global__ __launch_bounds__(256) void rle_scan(const uint16_t* __restrict__ fm,
 // get_move binary search returns [U].  Edges come from a packed fixed-stride
 // adjacency: edge k of column c is adj[(c << shift) + k] = (dst column, weight),
 // dst = kNoEdge past the out-degree — one 8-B load per move, no row_ptr.
-constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
 
 // Per-wave sums of (cost, moves, finished) added to agg[2], agg[1], agg[0].
 __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
@@ -512,12 +547,18 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                B / 4u, cf);
 }
 
-void launch_first_moves(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
-                        const uint32_t* dist, const uint32_t* tgt, uint32_t B,
-                        uint32_t rows, uint32_t n, uint32_t npad, uint16_t* fm,
-                        hipStream_t s) {
+void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* dist,
+                        const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
+                        uint32_t npad, uint16_t* fm, hipStream_t s) {
     dim3 grid(npad / kern::kSeg, (rows + 1023u) / 1024u);
-    launch(kern::first_moves, grid, dim3(256), s, row_ptr, dst, w, dist, tgt, B, n, npad, fm);
+    const uint2* adj = reinterpret_cast<const uint2*>(adj32);
+    switch (shift) {  // SLOTS = 2^shift edges per column; G columns per gather group
+        case 0: launch(kern::first_moves<1, 4>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
+        case 1: launch(kern::first_moves<2, 2>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
+        case 2: launch(kern::first_moves<4, 2>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
+        case 3: launch(kern::first_moves<8, 1>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
+        default: launch(kern::first_moves<16, 1>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
+    }
 }
 
 void launch_rle_count(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* counts,

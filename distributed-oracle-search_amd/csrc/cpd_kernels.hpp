@@ -19,10 +19,10 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
                   const uint32_t* asc_off, const uint32_t* asc_arcs, hipStream_t s);
 
-void launch_first_moves(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t* w,
-                        const uint32_t* dist, const uint32_t* tgt, uint32_t B,
-                        uint32_t rows, uint32_t n, uint32_t npad, uint16_t* fm,
-                        hipStream_t s);
+// adj: the packed fixed-stride adjacency (free-flow weights), 2^shift slots
+void launch_first_moves(const uint32_t* adj, uint32_t shift, const uint32_t* dist,
+                        const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
+                        uint32_t npad, uint16_t* fm, hipStream_t s);
 
 // Row width of the tiled first-move rows: npad is a multiple of this.
 constexpr uint32_t kFmTile = 2048;
