@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <numeric>
@@ -58,6 +59,7 @@ struct Pending {
     const char* name;
     hipEvent_t a, b;
     double bytes;
+    std::function<double()> late_bytes;  // set: bytes known only after the batch ran
 };
 
 struct Agg {
@@ -106,9 +108,17 @@ struct cpd_graph {
     bool has_ch = false;
     // batch workspace
     uint32_t B = 0;
+    uint32_t fmb = 16;  // bits per first-move set (fm_bits(adj_shift))
     DevBuf<uint32_t> dist, tgt, counts;
-    DevBuf<uint16_t> fm;
+    DevBuf<uint32_t> fm;    // [B][npad] fmb-bit sets
+    DevBuf<uint32_t> live;  // [col][B/1024] up-sweep row-stored flags
     DevBuf<uint64_t> row_off;
+    // per-level sweep counters (2 per launch: stored/own rows, gathered rows)
+    DevBuf<unsigned int> stat;
+    std::vector<unsigned int> stat_h;
+    DevBuf<uint32_t> asc_lvl_of, dsc_lvl_of;  // slot -> level
+    // lane position of each caller target in the current batch (sorted by column)
+    std::vector<uint32_t> pos_of, tgt_col;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -140,7 +150,8 @@ struct cpd_graph {
     // Time one launch when timing is on: the events are attached to the
     // kernel's own dispatch packet (hipExtLaunchKernelGGL, see launchers).
     template <class F>
-    void timed(const char* name, double bytes, F&& launch) {
+    void timed(const char* name, double bytes, F&& launch,
+               std::function<double()> late_bytes = nullptr) {
         if (!timing) {
             launch();
             return;
@@ -149,7 +160,7 @@ struct cpd_graph {
         set_launch_events(a, b);
         launch();
         HIP_CHECK(hipGetLastError());
-        pending.push_back({name, a, b, bytes});
+        pending.push_back({name, a, b, bytes, std::move(late_bytes)});
     }
     void sync() {
         HIP_CHECK(hipStreamSynchronize(stream));
@@ -159,7 +170,7 @@ struct cpd_graph {
             Agg& g = agg[p.name];
             g.launches++;
             g.ms += ms;
-            g.bytes += p.bytes;
+            g.bytes += p.late_bytes ? p.late_bytes() : p.bytes;
             ev_pool.push_back(p.a);
             ev_pool.push_back(p.b);
         }
@@ -171,8 +182,8 @@ struct cpd_graph {
         if (want == 0) {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-            // per target: dist 4n + fm 2npad + output runs (<= 4n, ~2.5n typical)
-            double per = 4.0 * n + 2.0 * npad + 4.0 * n;
+            // per target: dist 4n + fm + output runs (<= 4n, ~2.5n typical)
+            double per = 4.0 * n + fmb / 8.0 * npad + 4.0 * n;
             double fit = 0.4 * (double)free_b / per;
             want = (uint32_t)std::min(16384.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
         }
@@ -180,7 +191,8 @@ struct cpd_graph {
         if (want == B && dist.p) return;
         B = want;
         dist.alloc((size_t)n * B);
-        fm.alloc((size_t)B * npad);
+        fm.alloc((size_t)B * (npad / (32u / fmb)));
+        live.alloc((size_t)n * (B / 1024u));
         tgt.alloc(B);
         counts.alloc(B);
     }
@@ -358,6 +370,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             }
         }
         while ((1u << g->adj_shift) < maxdeg) ++g->adj_shift;
+        g->fmb = fm_bits(g->adj_shift);
         hipStream_t s = g->stream;
         g->row_ptr.upload(g->rowc_host.data(), n + 1, s);
         g->dst.upload(dstc.data(), m, s);
@@ -392,6 +405,18 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
         g->ch_arcs += arcs.size() / 2;
+        g->stat.alloc(2 * (g->asc_lvl.size() + g->dsc_lvl.size()));
+        g->stat_h.assign(g->stat.n, 0);
+        auto lvl_of = [n](const std::vector<uint32_t>& first) {
+            std::vector<uint32_t> v(n, 0);
+            for (size_t l = 0; l + 1 < first.size(); ++l)
+                for (uint32_t x = first[l]; x < first[l + 1]; ++x) v[x] = (uint32_t)l;
+            return v;
+        };
+        std::vector<uint32_t> la = lvl_of(g->asc_lvl), ld = lvl_of(g->dsc_lvl);
+        g->asc_lvl_of.upload(la.data(), n, s);
+        g->dsc_lvl_of.upload(ld.data(), n, s);
+        HIP_CHECK(hipStreamSynchronize(s));
         *out = g.release();
     });
 }
@@ -419,61 +444,124 @@ void cpd_graph_free(cpd_graph* g) { delete g; }
 
 namespace {
 
+// CPD_LIVE=0: no up-sweep row skipping; CPD_SORT=0: batches keep the caller's
+// target order (A/B measurements; results are identical either way).
+bool env_on(const char* name) {
+    const char* e = std::getenv(name);
+    return !(e && *e == '0');
+}
+bool live_on() {
+    static const bool on = env_on("CPD_LIVE");
+    return on;
+}
+bool sort_on() {
+    static const bool on = env_on("CPD_SORT");
+    return on;
+}
+
 // Distances + first-move sets for `k` targets (columns already in g->tgt,
 // padded to a multiple of 1024 with valid columns).
 void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
     const uint32_t B = g->B, n = g->n;
     const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
     const uint32_t active = slabs * 1024u;
+    uint32_t* live = live_on() ? g->live.p : nullptr;
+    unsigned int* stat = g->timing ? g->stat.p : nullptr;
+    const size_t nasc = g->asc_lvl.size();
+    if (stat) HIP_CHECK(hipMemsetAsync(stat, 0, g->stat.n * sizeof(unsigned int), g->stream));
+    const std::vector<unsigned int>& sh = g->stat_h;  // filled by the batch's D2H copy
     // ascending sweep: each level reads lower levels' rows.  Levels 0 and 1
     // are never materialised (closed forms, kLeafBit / kL1Bit): not launched.
-    // Bytes per level: gathered rows 4 B x target, row writes 4 B x target,
-    // arcs 8 B and node slot 12 B per 1024-target slab.
-    for (size_t l = 2; l + 1 < g->asc_lvl.size(); ++l) {
+    // Bytes per level: 4 B x target per gathered row and per stored row
+    // (1024 targets per live (row, slab) when skipping, else every row),
+    // arcs 8 B + their live flags 4 B and the node slot 12 B + flag 4 B per
+    // 1024-target slab.
+    for (size_t l = 2; l + 1 < nasc; ++l) {
         uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
         if (!cnt) continue;
         double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
-        double bytes = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + 8.0 * arcs_l * slabs +
-                       12.0 * cnt * slabs;
-        g->timed("sweep_up", bytes, [&] {
+        double meta = 8.0 * arcs_l * slabs + 12.0 * cnt * slabs;
+        double dense = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + meta;
+        std::function<double()> late;
+        if (live && stat)
+            late = [&sh, l, meta, arcs_l, cnt, slabs] {
+                return 4096.0 * ((double)sh[2 * l] + (double)sh[2 * l + 1]) + meta +
+                       4.0 * (arcs_l + cnt) * slabs;
+            };
+        g->timed("sweep_up", dense, [&] {
             launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt, g->dist.p,
-                         g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
+                         g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
                          g->stream);
-        });
+        }, std::move(late));
     }
     for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
         uint32_t s0 = g->dsc_lvl[l], cnt = g->dsc_lvl[l + 1] - s0;
         if (!cnt) continue;
-        double bytes = (4.0 * g->dsc_lvl_arcs[l] + 4.0 * g->dsc_lvl_reads[l] + 4.0 * cnt) * active +
-                       8.0 * g->dsc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
-        g->timed("sweep_down", bytes, [&] {
+        const size_t si = 2 * (nasc + l);
+        double base = (4.0 * g->dsc_lvl_arcs[l] + 4.0 * cnt) * active +
+                      8.0 * g->dsc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
+        double dense = base + 4.0 * g->dsc_lvl_reads[l] * active;
+        std::function<double()> late;
+        if (live && stat)
+            late = [&sh, si, base, l, g, slabs] {
+                return base + 4096.0 * (double)sh[si] + 4.0 * g->dsc_lvl_reads[l] * slabs;
+            };
+        g->timed("sweep_down", dense, [&] {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
-                         g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
+                         g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
                          g->stream);
+        }, std::move(late));
+    }
+    if (live && stat && nasc > 2) {  // row counts behind the late byte counts
+        g->timed("live_stats", 0.0, [&] {
+            launch_live_stats(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
+                              g->asc_lvl_of.p, g->asc_lvl[2], n, live, B, slabs, stat, g->stream);
+        });
+        g->timed("live_stats", 0.0, [&] {
+            launch_live_stats(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p,
+                              g->dsc_lvl_of.p, 0, n, live, B, slabs, stat + 2 * nasc, g->stream);
         });
     }
-    // per row: own distance 4n + neighbour distances 4m + first-move write 2npad;
-    // the packed adjacency (8 B per slot) is read once per 1024-target slab
+    // per row: own distance 4n + neighbour distances 4m + first-move write
+    // npad * fmb / 8; the packed adjacency (8 B per slot) is read once per
+    // 1024-target slab
     const uint32_t fslabs = (k + 1023u) / 1024u;
-    double fbytes = (4.0 * n + 4.0 * g->m + 2.0 * g->npad) * (fslabs * 1024.0) +
+    double fbytes = (4.0 * n + 4.0 * g->m + g->fmb / 8.0 * g->npad) * (fslabs * 1024.0) +
                     8.0 * (double)n * (double)(1u << g->adj_shift) * fslabs;
     g->timed("first_moves", fbytes, [&] {
         launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, g->tgt.p, B, k, n, g->npad,
                            g->fm.p, g->stream);
     });
+    if (stat)
+        HIP_CHECK(hipMemcpyAsync(g->stat_h.data(), stat, g->stat.n * sizeof(unsigned int),
+                                 hipMemcpyDeviceToHost, g->stream));
 }
 
+// Upload a batch's targets as columns.  With sorting on, lanes hold the
+// targets in column order (DFS preorder is spatially coherent, so a 1024-lane
+// slab covers one compact region and the up-sweep skips most rows);
+// g->pos_of[i] = lane of the caller's target i.
 void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k) {
     CPD_REQUIRE(g->has_ch, CPD_E_ARG,
                 "graph was created from a plan without hierarchy: it can serve queries "
                 "but not build rows");
-    std::vector<uint32_t> cols(g->B);
+    std::vector<uint32_t> cols(g->B), idx(k);
     for (uint32_t i = 0; i < k; ++i) {
         CPD_REQUIRE(targets[i] < g->n, CPD_E_ARG,
                     "target " + std::to_string(targets[i]) + " out of range");
-        cols[i] = g->order[targets[i]];
+        idx[i] = i;
+    }
+    if (sort_on())
+        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+            return g->order[targets[a]] < g->order[targets[b]];
+        });
+    g->pos_of.resize(k);
+    for (uint32_t p = 0; p < k; ++p) {
+        cols[p] = g->order[targets[idx[p]]];
+        g->pos_of[idx[p]] = p;
     }
     for (uint32_t i = k; i < g->B; ++i) cols[i] = cols[0];  // padding lanes
+    g->tgt_col = cols;
     g->tgt.upload(cols.data(), g->B, g->stream);
 }
 
@@ -493,18 +581,24 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     run_sweeps_and_fm(g, k);
     const double t1 = now_seconds();
     const uint32_t npad = g->npad;
-    g->timed("rle_count", 2.0 * npad * k + 4.0 * k, [&] {
-        launch_rle_count(g->fm.p, npad, k, g->counts.p, g->stream);
+    const double fm_row = g->fmb / 8.0 * npad;  // first-move bytes per row
+    g->timed("rle_count", fm_row * k + 4.0 * k, [&] {
+        launch_rle_count(g->fm.p, g->fmb, npad, k, g->counts.p, g->stream);
     });
     std::vector<uint32_t> counts(k);
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, g->stream));
     g->sync();
     const double t2 = now_seconds();
-    // row offsets for this batch, appended after r->total
-    std::vector<uint64_t> off(k + 1);
+    // row offsets for this batch in the caller's order, appended after
+    // r->total; counts[] and the emit kernel's offsets are per lane
+    std::vector<uint64_t> off(k + 1), lane_off(k);
     off[0] = r->total;
-    for (uint32_t i = 0; i < k; ++i) off[i + 1] = off[i] + counts[i];
+    for (uint32_t i = 0; i < k; ++i) {
+        const uint32_t p = g->pos_of[i];
+        lane_off[p] = off[i];
+        off[i + 1] = off[i] + counts[p];
+    }
     uint64_t new_total = off[k];
     if (new_total > r->runs.n) {  // grow, preserving the rows already built
         // 25% headroom: batches differ by a few runs, and re-allocating tens of
@@ -521,10 +615,10 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
         r->runs.n = want;
     }
     const double t3 = now_seconds();
-    g->row_off.upload(off.data(), k + 1, g->stream);
-    double ebytes = 2.0 * npad * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
+    g->row_off.upload(lane_off.data(), k, g->stream);
+    double ebytes = fm_row * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
     g->timed("rle_emit", ebytes, [&] {
-        launch_rle_emit(g->fm.p, npad, k, g->row_off.p, r->runs.p, g->stream);
+        launch_rle_emit(g->fm.p, g->fmb, npad, k, g->row_off.p, r->runs.p, g->stream);
     });
     g->sync();
     if (trace_on())
@@ -603,21 +697,31 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
         run_sweeps_and_fm(g, ntargets);
         g->sync();
         const uint32_t n = g->n, B = g->B;
-        if (dist) {
-            std::vector<uint32_t> h((size_t)n * B);
-            HIP_CHECK(hipMemcpy(h.data(), g->dist.p, h.size() * sizeof(uint32_t),
-                                hipMemcpyDeviceToHost));
+        // lane p holds the caller's target i = pos_of^-1(p)
+        std::vector<uint32_t> h((size_t)n * B);
+        HIP_CHECK(hipMemcpy(h.data(), g->dist.p, h.size() * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost));
+        if (dist)
             for (uint32_t v = 0; v < n; ++v)
                 for (uint32_t i = 0; i < ntargets; ++i)
-                    dist[(size_t)v * ntargets + i] = h[(size_t)g->order[v] * B + i];
-        }
+                    dist[(size_t)v * ntargets + i] = h[(size_t)g->order[v] * B + g->pos_of[i]];
         if (fm) {
-            std::vector<uint16_t> h((size_t)ntargets * g->npad);
-            HIP_CHECK(hipMemcpy(h.data(), g->fm.p, h.size() * sizeof(uint16_t),
+            // unpack fmb-bit sets; a column whose set is the wildcard (the
+            // target, unreachable columns) reports CPD_FM_ALL like the oracle
+            const uint32_t per = 32u / g->fmb, all = (1u << g->fmb) - 1u;
+            const size_t row_words = g->npad / per;
+            std::vector<uint32_t> w((size_t)B * row_words);
+            HIP_CHECK(hipMemcpy(w.data(), g->fm.p, w.size() * sizeof(uint32_t),
                                 hipMemcpyDeviceToHost));
-            for (uint32_t i = 0; i < ntargets; ++i)
-                for (uint32_t v = 0; v < n; ++v)
-                    fm[(size_t)i * n + v] = h[(size_t)i * g->npad + g->order[v]];
+            for (uint32_t i = 0; i < ntargets; ++i) {
+                const uint32_t p = g->pos_of[i];
+                for (uint32_t v = 0; v < n; ++v) {
+                    const uint32_t c = g->order[v];
+                    const uint32_t f = (w[(size_t)p * row_words + c / per] >> (g->fmb * (c % per))) & all;
+                    const bool wild = c == g->tgt_col[p] || h[(size_t)c * B + p] == CPD_INF;
+                    fm[(size_t)i * n + v] = wild ? (uint16_t)CPD_FM_ALL : (uint16_t)f;
+                }
+            }
         }
     });
 }

@@ -4,12 +4,15 @@
 // Data layout in HBM (column space = DFS-preorder position of a node):
 //   dist  [col][B]   u32   one batch row of B targets per column; a wave's
 //                          16-B/lane access covers 256 targets = 1 KiB
-//   fm    [row][npad] u16  first-move sets, row-major for the RLE scan;
-//                          columns >= n are padded with the wildcard
+//   fm    [row][npad] FMB-bit first-move sets, row-major for the RLE scan;
+//                          FMB = max(4, slots of the packed adjacency) >= the
+//                          max out-degree: 4 bits on road lattices, a quarter
+//                          of a u16; columns >= n are padded with the wildcard
 //   runs  u32 words, rows back to back at off[row] (count pass, then emit)
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 #include "cpd_kernels.hpp"
 
@@ -23,11 +26,33 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t d, uint32_t w) {
     return (s < d) ? INF : s;  // d == INF or overflow -> INF
 }
 
-// First-move rows are plain row-major u16 [row][npad]: the first-move kernel
-// writes each target's 32-column segment as one full 64-B line, and the RLE
-// scan's lane l reads its 32 columns as 4 x 16 B.
+// First-move rows are plain row-major [row][npad] FMB-bit sets: the first-move
+// kernel writes each target's 32-column segment as FMB/4 16-B stores (one
+// 16-B store at FMB = 4), and the RLE scan's lane l reads its 32 columns the
+// same way.  The wildcard is all FMB bits: every real set lies inside them
+// (FMB >= out-degree), so S & wildcard == S and lowest-bit(wildcard) == 0 as
+// with the u16 0xFFFF of the oracle — the scan's output is unchanged.
 constexpr uint32_t kSeg = 32;          // columns per lane
 constexpr uint32_t kTile = 64 * kSeg;  // columns per wave tile (npad % kTile == 0)
+
+template <int FMB>
+struct FmFmt {
+    static_assert(FMB == 4 || FMB == 8 || FMB == 16, "first-move set width");
+    static constexpr uint32_t kAll = (1u << FMB) - 1u;  // wildcard
+    static constexpr int kPer = 32 / FMB;               // columns per u32 word
+    static constexpr int kWords = (int)kSeg / kPer;     // words per 32-column segment (= FMB)
+};
+
+// Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+// one; MI355X_MICROARCH.md "Workgroup dispatch, XCD placement").  Remap so that
+// each XCD runs one contiguous range of logical blocks: neighbouring nodes and
+// column segments, which gather the same distance rows, then share an XCD's
+// 4 MiB L2.  A bijection on [0, total) for any total; speed only, never
+// correctness.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t total) {
+    const uint32_t q = total >> 3, r = total & 7u, x = b & 7u;
+    return x * q + min(x, r) + (b >> 3);
+}
 
 // Closed forms for the two lowest upward levels, so they are never stored.
 // A level-0 node ("leaf": no down-arcs) has d_up = 0 at its own target, INF
@@ -71,35 +96,57 @@ __device__ __forceinline__ uint4 l1_val(const Closed& cf, uint32_t s, const uint
     return acc;
 }
 
-// Value an arc contributes (before adding its weight).
+// Up-sweep sparsity.  d_up(x, t) is finite only for x in t's upward search
+// space, a few per cent of the (node, 1024-target slab) pairs at up-levels >= 2
+// on road graphs when a slab's targets are neighbours.  The
+// up-sweep stores a materialised row only if one of its 1024 values is finite
+// and records that in flags[col * S + slab]; readers of d_up (up-sweep
+// gathers, the down-sweep's own-row init) take INF for a row never stored.
+// flags == nullptr: every row is stored and read (no skipping).  The bytes
+// model's row counts come from live_stats (below), never from per-block
+// atomics: a level has up to ~2M blocks, and one counter word serialises them.
+struct Live {
+    uint32_t* flags;
+    uint32_t S;  // slabs per column = B / 1024
+};
+
+// Value an arc contributes (before adding its weight); *gathered = 1 if it
+// read a materialised row.
 __device__ __forceinline__ uint4 arc_val(const uint4* __restrict__ d4, const uint4 t, uint2 e,
-                                         uint32_t B4, uint32_t l4, const Closed& cf) {
+                                         uint32_t B4, uint32_t l4, const Closed& cf,
+                                         bool live) {
     if (e.x & kLeafBit) return leaf4(t, e.x & kIdxMask, 0u);
     if (e.x & kL1Bit) return l1_val(cf, e.x & kIdxMask, t);
+    if (!live) return make_uint4(INF, INF, INF, INF);
     return d4[(size_t)e.x * B4 + l4];
 }
 
-// One CH sweep level.  Block (x = slot in the level, y = 1024-target slab):
-// node v = nodes[slot]; its arcs (col, w) are wave-uniform (scalar loads); each
-// lane owns 4 consecutive targets.  ASCEND: upward sweep, init 0 at the lane's
-// own target else INF.  !ASCEND: downward sweep, init = current dist (the
-// upward value, or its closed form for levels 0/1).  Then acc = min(acc,
-// w + d[arc]) over the arcs, eight gathers in flight per wave.
+// One CH sweep level.  Logical block = (slot in the level, 1024-target slab),
+// slots fastest, XCD-remapped (remap != 0): node v = nodes[slot]; its arcs
+// (col, w) are wave-uniform (scalar loads); each lane owns 4 consecutive
+// targets.  ASCEND: upward sweep, init 0 at the lane's own target else INF.
+// !ASCEND: downward sweep, init = current dist (the upward value, or its closed
+// form for levels 0/1).  Then acc = min(acc, w + d[arc]) over the arcs, eight
+// gathers in flight per wave.
 template <bool ASCEND>
 __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ nodes,
                                                    const uint32_t* __restrict__ arc_off,
                                                    const uint2* __restrict__ arcs,
-                                                   uint32_t slot0,
+                                                   uint32_t slot0, uint32_t count, uint32_t remap,
                                                    uint32_t* __restrict__ dist,
                                                    const uint4* __restrict__ tgt4,
-                                                   uint32_t B4, Closed cf) {
-    const uint32_t slot = slot0 + blockIdx.x;
-    const uint32_t l4 = blockIdx.y * 256u + threadIdx.x;
+                                                   uint32_t B4, Closed cf, Live lv) {
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t slab = L / count;
+    const uint32_t slot = slot0 + (L - slab * count);
+    const uint32_t l4 = slab * 256u + threadIdx.x;
     const uint32_t vraw = nodes[slot];
     uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    const uint32_t* __restrict__ flags_in = lv.flags;  // entries of finished levels only
     const uint4 t = tgt4[l4];
     uint32_t v;
     uint4 acc;
+    uint32_t own = 0;
     if (ASCEND) {
         v = vraw;
         acc = leaf4(t, v, 0u);
@@ -111,43 +158,110 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
         acc = l1_val(cf, vraw & kIdxMask, t);
     } else {
         v = vraw;
-        acc = d4[(size_t)v * B4 + l4];
+        own = flags_in ? flags_in[(size_t)v * lv.S + slab] : 1u;
+        acc = own ? d4[(size_t)v * B4 + l4] : make_uint4(INF, INF, INF, INF);
     }
     const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
     uint32_t a = a0;
+    // only the up-sweep reads rows that may never have been stored
+    auto live_of = [&](uint2 e) -> uint32_t {
+        if (!ASCEND || !flags_in || (e.x & (kLeafBit | kL1Bit))) return 1u;
+        return flags_in[(size_t)e.x * lv.S + slab];
+    };
     for (; a + 8 <= a1; a += 8) {
         uint2 e[8];
+        uint32_t ok[8];
         uint4 x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = arc_val(d4, t, e[i], B4, l4, cf);
+        for (int i = 0; i < 8; ++i) ok[i] = live_of(e[i]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = arc_val(d4, t, e[i], B4, l4, cf, ok[i] != 0);
 #pragma unroll
         for (int i = 0; i < 8; ++i) min4(acc, x[i], e[i].y);
     }
     for (; a < a1; ++a) {
         const uint2 e = arcs[a];
-        min4(acc, arc_val(d4, t, e, B4, l4, cf), e.y);
+        min4(acc, arc_val(d4, t, e, B4, l4, cf, live_of(e) != 0), e.y);
+    }
+    if (ASCEND && lv.flags) {
+        const uint32_t lo = min(min(acc.x, acc.y), min(acc.z, acc.w));
+        const int any = __syncthreads_or(lo != INF);
+        if (threadIdx.x == 0) lv.flags[(size_t)v * lv.S + slab] = any ? 1u : 0u;
+        if (any) d4[(size_t)v * B4 + l4] = acc;
+        return;
     }
     d4[(size_t)v * B4 + l4] = acc;
+}
+
+// Row counts of one batch's sweeps for the bytes model (timing runs only),
+// thread per node slot of one sweep direction:
+//   ASCEND (slots of up-levels >= 2): stat[2 l] += rows stored (live flags of
+//     the slot's column over the active slabs), stat[2 l + 1] += rows gathered
+//     (live flags of its materialised arcs' columns);
+//   !ASCEND: stat[2 l] += own rows read (materialised slots only).
+// lvl_of[slot] = the slot's level; counts are aggregated per wave when all
+// lanes share a level (slots are level-ordered), so atomics are few.
+template <bool ASCEND>
+__global__ __launch_bounds__(256) void live_stats(const uint32_t* __restrict__ nodes,
+                                                  const uint32_t* __restrict__ arc_off,
+                                                  const uint2* __restrict__ arcs,
+                                                  const uint32_t* __restrict__ lvl_of,
+                                                  uint32_t slot0, uint32_t slot1,
+                                                  const uint32_t* __restrict__ flags, uint32_t S,
+                                                  uint32_t slabs, unsigned int* __restrict__ stat) {
+    const uint32_t slot = slot0 + blockIdx.x * 256u + threadIdx.x;
+    uint32_t own = 0, gathered = 0, lvl = 0xFFFFFFFFu;
+    if (slot < slot1) {
+        lvl = lvl_of[slot];
+        const uint32_t v = nodes[slot];
+        if (ASCEND || !(v & (kLeafBit | kL1Bit)))
+            for (uint32_t b = 0; b < slabs; ++b) own += flags[(size_t)v * S + b];
+        if (ASCEND)
+            for (uint32_t a = arc_off[slot]; a < arc_off[slot + 1]; ++a) {
+                const uint32_t c = arcs[a].x;
+                if (c & (kLeafBit | kL1Bit)) continue;
+                for (uint32_t b = 0; b < slabs; ++b) gathered += flags[(size_t)c * S + b];
+            }
+    }
+    const uint32_t l0 = __shfl(lvl, 0, 64);
+    if (__all(lvl == l0)) {
+        if (l0 == 0xFFFFFFFFu) return;
+        unsigned int o = own, g = gathered;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) {
+            o += __shfl_xor(o, d, 64);
+            g += __shfl_xor(g, d, 64);
+        }
+        if ((threadIdx.x & 63u) == 0) {
+            atomicAdd(&stat[2 * l0], o);
+            if (ASCEND) atomicAdd(&stat[2 * l0 + 1], g);
+        }
+    } else if (lvl != 0xFFFFFFFFu) {
+        atomicAdd(&stat[2 * lvl], own);
+        if (ASCEND) atomicAdd(&stat[2 * lvl + 1], gathered);
+    }
 }
 
 __device__ __forceinline__ uint32_t fm_bit(uint32_t dv, uint32_t w, uint32_t dn, uint32_t k) {
     return (sat_add(dv, w) == dn ? 1u : 0u) << k;
 }
 
+template <int FMB>
 __device__ __forceinline__ uint32_t fm_final(uint32_t c, uint32_t tc, uint32_t dn, uint32_t bits) {
-    return (c == tc || dn == INF) ? 0xFFFFu : bits;
+    return (c == tc || dn == INF) ? FmFmt<FMB>::kAll : bits;
 }
 
-// First-move sets.  Block (x = one 32-column lane segment, y = 1024-target
-// slab); thread = 4 consecutive targets (16-B dist accesses: 1 KiB per wave
-// instruction, like the sweeps).  For each column c: fm = bits k with
-// w_k + d(dst_k) == d(c), wildcard at the target and at unreachable columns;
-// the segment's 32 sets per target are one 64-B line of the target's row.
-// Edges come from the packed fixed-stride adjacency (SLOTS = 2^shift per
-// column, kNoEdge padding), so a group of G columns issues its G own-row and
-// G*SLOTS neighbour gathers back to back, with no dependent CSR lookups.
+// First-move sets.  Logical block = (one 32-column lane segment, 1024-target
+// slab), segments fastest, XCD-remapped; thread = 4 consecutive targets (16-B
+// dist accesses: 1 KiB per wave instruction, like the sweeps).  For each
+// column c: fm = bits k with w_k + d(dst_k) == d(c), wildcard at the target and
+// at unreachable columns; the segment's 32 sets per target are FMB/4 16-B
+// stores into the target's row.  Edges come from the packed fixed-stride
+// adjacency (SLOTS = 2^shift per column, kNoEdge padding), so a group of G
+// columns issues its G own-row and G*SLOTS neighbour gathers back to back,
+// with no dependent CSR lookups.
 constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
 
 template <int SLOTS, int G>
@@ -155,15 +269,20 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
                                                    const uint32_t* __restrict__ dist,
                                                    const uint32_t* __restrict__ tgt,
                                                    uint32_t B, uint32_t n, uint32_t npad,
-                                                   uint16_t* __restrict__ fm) {
-    const uint32_t l4 = blockIdx.y * 256u + threadIdx.x;
+                                                   uint32_t remap, uint32_t* __restrict__ fm) {
+    constexpr int FMB = SLOTS < 4 ? 4 : SLOTS;
+    using F = FmFmt<FMB>;
+    const uint32_t nseg = npad / kSeg;
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t slab = L / nseg;
+    const uint32_t l4 = slab * 256u + threadIdx.x;
     const uint32_t B4 = B / 4u;
-    const uint32_t c0 = blockIdx.x * kSeg;
+    const uint32_t c0 = (L - slab * nseg) * kSeg;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
-    uint32_t pk[4][16];
+    uint32_t pk[4][F::kWords];
 #pragma unroll
-    for (int p = 0; p < 16; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
+    for (int p = 0; p < F::kWords; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
     constexpr int KC = SLOTS < 4 ? SLOTS : 4;  // slots gathered per chunk
 #pragma unroll
     for (int cg = 0; cg < (int)kSeg; cg += G) {
@@ -211,19 +330,21 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
             if (c >= n) continue;  // stays the wildcard padding
             const uint32_t b0 = b[j][0], b1 = b[j][1], b2 = b[j][2], b3 = b[j][3];
             const int cc = cg + j;
-            const int sh = 16 * (cc & 1);
-            const uint32_t keep = 0xFFFF0000u >> sh;  // clear this column's half
-            pk[0][cc >> 1] = (pk[0][cc >> 1] & keep) | (fm_final(c, tc.x, dn[j].x, b0) << sh);
-            pk[1][cc >> 1] = (pk[1][cc >> 1] & keep) | (fm_final(c, tc.y, dn[j].y, b1) << sh);
-            pk[2][cc >> 1] = (pk[2][cc >> 1] & keep) | (fm_final(c, tc.z, dn[j].z, b2) << sh);
-            pk[3][cc >> 1] = (pk[3][cc >> 1] & keep) | (fm_final(c, tc.w, dn[j].w, b3) << sh);
+            const int wi = cc / F::kPer, sh = FMB * (cc % F::kPer);
+            const uint32_t keep = ~(F::kAll << sh);  // clear this column's field
+            pk[0][wi] = (pk[0][wi] & keep) | (fm_final<FMB>(c, tc.x, dn[j].x, b0) << sh);
+            pk[1][wi] = (pk[1][wi] & keep) | (fm_final<FMB>(c, tc.y, dn[j].y, b1) << sh);
+            pk[2][wi] = (pk[2][wi] & keep) | (fm_final<FMB>(c, tc.z, dn[j].z, b2) << sh);
+            pk[3][wi] = (pk[3][wi] & keep) | (fm_final<FMB>(c, tc.w, dn[j].w, b3) << sh);
         }
     }
+    const size_t row_words = npad / F::kPer;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        uint4* seg = reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * npad + c0);
+        uint4* seg = reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * row_words +
+                                              c0 / F::kPer);
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < F::kWords / 4; ++q)
             seg[q] = make_uint4(pk[i][4 * q], pk[i][4 * q + 1], pk[i][4 * q + 2], pk[i][4 * q + 3]);
     }
 }
@@ -231,13 +352,15 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
 // One lane's greedy pass over its 32 columns (warthog graph_oracle::add_row
 // [U]: keep S = AND of the current run's first-move sets; a column that would
 // empty S ends the run — word (head << 4 | lowest bit of S) — and starts a new
-// one at that column).  v holds the segment's 32 u16 sets, two per register.
-template <bool EMIT>
-__device__ __forceinline__ void seg_pass(const uint32_t (&v)[16], uint32_t c0, uint32_t& h,
-                                         uint32_t& S, uint32_t& cnt, uint32_t* stage) {
+// one at that column).  v holds the segment's 32 FMB-bit sets, 32/FMB per word.
+template <bool EMIT, int FMB>
+__device__ __forceinline__ void seg_pass(const uint32_t (&v)[FmFmt<FMB>::kWords], uint32_t c0,
+                                         uint32_t& h, uint32_t& S, uint32_t& cnt,
+                                         uint32_t* stage) {
+    using F = FmFmt<FMB>;
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-        const uint32_t f = (k & 1) ? (v[k >> 1] >> 16) : (v[k >> 1] & 0xFFFFu);
+        const uint32_t f = (v[k / F::kPer] >> (FMB * (k % F::kPer))) & F::kAll;
         const bool brk = (S & f) == 0u;
         if (EMIT) {
             if (brk) stage[cnt] = (h << 4) | (uint32_t)__builtin_ctz(S);
@@ -256,35 +379,45 @@ __device__ __forceinline__ void seg_pass(const uint32_t (&v)[16], uint32_t c0, u
 // suffice; the loop is exact for any input (at most 64 rounds).
 // COUNT: counts[row] = runs in the row.  EMIT: runs written at off[row],
 // staged per tile in LDS and stored coalesced.
-template <bool EMIT>
-__global__ __launch_bounds__(256) void rle_scan(const uint16_t* __restrict__ fm, uint32_t npad,
+template <bool EMIT, int FMB>
+__global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm, uint32_t npad,
                                                 uint32_t nrows, uint32_t* __restrict__ counts,
                                                 const uint64_t* __restrict__ off,
                                                 uint32_t* __restrict__ runs) {
+    using F = FmFmt<FMB>;
+    constexpr int Q = F::kWords / 4;  // 16-B loads per lane per tile
     __shared__ uint32_t stage_all[EMIT ? 4 * kTile : 1];
     const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     if (row >= nrows) return;
     uint32_t* stage = stage_all + (EMIT ? (threadIdx.x >> 6) * kTile : 0);
-    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(fm + (size_t)row * npad);
+    const uint4* __restrict__ src =
+        reinterpret_cast<const uint4*>(fm + (size_t)row * (npad / F::kPer)) + lane * Q;
     uint32_t* __restrict__ out = EMIT ? runs + off[row] : nullptr;
-    uint32_t carry_h = 0, carry_S = 0xFFFFu, total = 0;
+    uint32_t carry_h = 0, carry_S = F::kAll, total = 0;
     const uint32_t ntiles = npad / kTile;
-    for (uint32_t t = 0; t < ntiles; ++t) {
-        uint32_t v[16];
+    // tile t's segment of this lane, prefetched one tile ahead
+    uint4 nx[Q];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 x = src[(size_t)t * 256u + lane * 4u + q];  // 64 B per lane
-            v[4 * q] = x.x;
-            v[4 * q + 1] = x.y;
-            v[4 * q + 2] = x.z;
-            v[4 * q + 3] = x.w;
+    for (int q = 0; q < Q; ++q) nx[q] = src[q];
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        uint32_t v[F::kWords];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            v[4 * q] = nx[q].x;
+            v[4 * q + 1] = nx[q].y;
+            v[4 * q + 2] = nx[q].z;
+            v[4 * q + 3] = nx[q].w;
+        }
+        if (t + 1 < ntiles) {
+#pragma unroll
+            for (int q = 0; q < Q; ++q) nx[q] = src[(size_t)(t + 1) * (64u * Q) + q];
         }
         const uint32_t c0 = t * kTile + lane * kSeg;
         // speculative pass: a run starts at the segment (lane 0: true carry)
-        uint32_t in_h = lane == 0 ? carry_h : c0, in_S = lane == 0 ? carry_S : 0xFFFFu;
+        uint32_t in_h = lane == 0 ? carry_h : c0, in_S = lane == 0 ? carry_S : F::kAll;
         uint32_t eh = in_h, eS = in_S, cnt = 0;
-        seg_pass<false>(v, c0, eh, eS, cnt, nullptr);
+        seg_pass<false, FMB>(v, c0, eh, eS, cnt, nullptr);
         for (int round = 0; round < 64; ++round) {
             uint32_t nh = __shfl_up(eh, 1, 64), nS = __shfl_up(eS, 1, 64);
             if (lane == 0) {
@@ -299,7 +432,7 @@ __global__ __launch_bounds__(256) void rle_scan(const uint16_t* __restrict__ fm,
                 eh = nh;
                 eS = nS;
                 cnt = 0;
-                seg_pass<false>(v, c0, eh, eS, cnt, nullptr);
+                seg_pass<false, FMB>(v, c0, eh, eS, cnt, nullptr);
             }
         }
         // inclusive scan of per-lane run counts
@@ -312,7 +445,7 @@ __global__ __launch_bounds__(256) void rle_scan(const uint16_t* __restrict__ fm,
         const uint32_t tile_total = __shfl(incl, 63, 64);
         if (EMIT) {
             uint32_t h = in_h, S = in_S, k = 0;
-            seg_pass<true>(v, c0, h, S, k, stage + (incl - cnt));
+            seg_pass<true, FMB>(v, c0, h, S, k, stage + (incl - cnt));
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -531,46 +664,84 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop) {
     g_ev_stop = stop;
 }
 
+// CPD_XCD=0 turns the XCD-aware block remap off (A/B measurements).
+uint32_t xcd_remap() {
+    static const uint32_t on = [] {
+        const char* e = std::getenv("CPD_XCD");
+        return (e && *e == '0') ? 0u : 1u;
+    }();
+    return on;
+}
+
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* arcs32, uint32_t slot0, uint32_t count, uint32_t* dist,
                   const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
-                  const uint32_t* asc_off, const uint32_t* asc_arcs, hipStream_t s) {
-    dim3 grid(count, slabs);
+                  const uint32_t* asc_off, const uint32_t* asc_arcs, uint32_t* live_flags,
+                  hipStream_t s) {
+    dim3 grid(count * slabs);
     const uint4* t4 = reinterpret_cast<const uint4*>(tgt);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
     const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
+    const kern::Live lv{live_flags, B / 1024u};
     if (ascend)
-        launch(kern::sweep_level<true>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, dist, t4,
-               B / 4u, cf);
+        launch(kern::sweep_level<true>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, count,
+               xcd_remap(), dist, t4, B / 4u, cf, lv);
     else
-        launch(kern::sweep_level<false>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, dist, t4,
-               B / 4u, cf);
+        launch(kern::sweep_level<false>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, count,
+               xcd_remap(), dist, t4, B / 4u, cf, lv);
 }
+
+void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
+                       const uint32_t* arcs32, const uint32_t* lvl_of, uint32_t slot0,
+                       uint32_t slot1, const uint32_t* flags, uint32_t B, uint32_t slabs,
+                       unsigned int* stat, hipStream_t s) {
+    if (slot1 <= slot0) return;
+    const dim3 grid((slot1 - slot0 + 255u) / 256u);
+    const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
+    if (ascend)
+        launch(kern::live_stats<true>, grid, dim3(256), s, nodes, arc_off, arcs, lvl_of, slot0,
+               slot1, flags, B / 1024u, slabs, stat);
+    else
+        launch(kern::live_stats<false>, grid, dim3(256), s, nodes, arc_off, arcs, lvl_of, slot0,
+               slot1, flags, B / 1024u, slabs, stat);
+}
+
+uint32_t fm_bits(uint32_t shift) { return shift <= 2 ? 4u : (1u << shift); }
 
 void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* dist,
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
-                        uint32_t npad, uint16_t* fm, hipStream_t s) {
-    dim3 grid(npad / kern::kSeg, (rows + 1023u) / 1024u);
+                        uint32_t npad, uint32_t* fm, hipStream_t s) {
+    dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u));
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
+    const uint32_t r = xcd_remap();
     switch (shift) {  // SLOTS = 2^shift edges per column; G columns per gather group
-        case 0: launch(kern::first_moves<1, 4>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
-        case 1: launch(kern::first_moves<2, 2>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
-        case 2: launch(kern::first_moves<4, 2>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
-        case 3: launch(kern::first_moves<8, 1>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
-        default: launch(kern::first_moves<16, 1>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, fm); break;
+        case 0: launch(kern::first_moves<1, 4>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
+        case 1: launch(kern::first_moves<2, 2>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
+        case 2: launch(kern::first_moves<4, 2>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
+        case 3: launch(kern::first_moves<8, 1>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
+        default: launch(kern::first_moves<16, 1>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
     }
 }
 
-void launch_rle_count(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* counts,
-                      hipStream_t s) {
-    launch(kern::rle_scan<false>, dim3((nrows + 3u) / 4u), dim3(256), s, fm, npad, nrows, counts,
-           (const uint64_t*)nullptr, (uint32_t*)nullptr);
+template <bool EMIT>
+static void launch_rle(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
+                       uint32_t* counts, const uint64_t* off, uint32_t* runs, hipStream_t s) {
+    const dim3 grid((nrows + 3u) / 4u), block(256);
+    switch (fmb) {
+        case 4: launch(kern::rle_scan<EMIT, 4>, grid, block, s, fm, npad, nrows, counts, off, runs); break;
+        case 8: launch(kern::rle_scan<EMIT, 8>, grid, block, s, fm, npad, nrows, counts, off, runs); break;
+        default: launch(kern::rle_scan<EMIT, 16>, grid, block, s, fm, npad, nrows, counts, off, runs); break;
+    }
 }
 
-void launch_rle_emit(const uint16_t* fm, uint32_t npad, uint32_t nrows, const uint64_t* off,
-                     uint32_t* runs, hipStream_t s) {
-    launch(kern::rle_scan<true>, dim3((nrows + 3u) / 4u), dim3(256), s, fm, npad, nrows,
-           (uint32_t*)nullptr, off, runs);
+void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
+                      uint32_t* counts, hipStream_t s) {
+    launch_rle<false>(fm, fmb, npad, nrows, counts, nullptr, nullptr, s);
+}
+
+void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
+                     const uint64_t* off, uint32_t* runs, hipStream_t s) {
+    launch_rle<true>(fm, fmb, npad, nrows, nullptr, off, runs, s);
 }
 
 void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,

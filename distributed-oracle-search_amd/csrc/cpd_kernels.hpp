@@ -10,29 +10,47 @@ namespace cpd {
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 
 // One CH sweep level: `count` node slots starting at `slot0` of the
-// level-ordered node list; grid (count, slabs) x 256 threads, one slab =
-// 1024 targets of the B-wide batch row.
+// level-ordered node list; count * slabs workgroups of 256 threads, one slab =
+// 1024 targets of the B-wide batch row, XCD-remapped (CPD_XCD=0: off).
 // asc_*: the ascending sweep's arrays, read by both directions for the
 // level-1 closed forms (see kL1Bit in cpd_kernels.hip).
+// live_flags ([col][B/1024] u32, may be null): the up-sweep records which
+// (materialised row, slab) it stored; the up-sweep's gathers and the
+// down-sweep's own-row reads skip the others (their values are all INF).
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
-                  const uint32_t* arcs /* (col, w) pairs */, uint32_t slot0, uint32_t count, uint32_t* dist,
-                  const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
-                  const uint32_t* asc_off, const uint32_t* asc_arcs, hipStream_t s);
+                  const uint32_t* arcs /* (col, w) pairs */, uint32_t slot0, uint32_t count,
+                  uint32_t* dist, const uint32_t* tgt, uint32_t B, uint32_t slabs,
+                  const uint32_t* asc_nodes, const uint32_t* asc_off, const uint32_t* asc_arcs,
+                  uint32_t* live_flags, hipStream_t s);
 
-// adj: the packed fixed-stride adjacency (free-flow weights), 2^shift slots
+// Row counts behind the live flags for the bytes model (timing runs): over
+// node slots [slot0, slot1) of one sweep direction, stat[2 * lvl_of[slot]]
+// += rows stored (up) / own rows read (down), stat[2 * lvl + 1] += rows
+// gathered (up).  stat must be zeroed by the caller.
+void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
+                       const uint32_t* arcs, const uint32_t* lvl_of, uint32_t slot0,
+                       uint32_t slot1, const uint32_t* flags, uint32_t B, uint32_t slabs,
+                       unsigned int* stat, hipStream_t s);
+
+// Bits per first-move set for a packed adjacency of 2^shift slots per column:
+// max(4, 2^shift) (>= the max out-degree); sets are stored 32/bits per u32.
+uint32_t fm_bits(uint32_t shift);
+
+// adj: the packed fixed-stride adjacency (free-flow weights), 2^shift slots;
+// fm: [rows][npad] sets of fm_bits(shift) bits, npad * bits / 32 words per row.
 void launch_first_moves(const uint32_t* adj, uint32_t shift, const uint32_t* dist,
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
-                        uint32_t npad, uint16_t* fm, hipStream_t s);
+                        uint32_t npad, uint32_t* fm, hipStream_t s);
 
 // Row width of the tiled first-move rows: npad is a multiple of this.
 constexpr uint32_t kFmTile = 2048;
 
 // Greedy RLE scan, one wave per row: runs per row, then the runs themselves
-// written at off[row] (uint64 offsets into `runs`).
-void launch_rle_count(const uint16_t* fm, uint32_t npad, uint32_t nrows, uint32_t* counts,
-                      hipStream_t s);
-void launch_rle_emit(const uint16_t* fm, uint32_t npad, uint32_t nrows, const uint64_t* off,
-                     uint32_t* runs, hipStream_t s);
+// written at off[row] (uint64 offsets into `runs`).  fmb = fm_bits(shift).
+void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
+                      uint32_t* counts, hipStream_t s);
+void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
+                     const uint64_t* off, uint32_t* runs, hipStream_t s);
 
 // RLE rows -> dense 4-bit move tables, npad/8 words per row.
 void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,

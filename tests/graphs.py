@@ -37,6 +37,18 @@ def irregular_graph():
     return graph_from_edges(n, edges)
 
 
+def deg8_graph():
+    """Out-degrees 5..8 on a ring (8-bit first-move sets), weights 1..3 (ties)."""
+    rng = np.random.default_rng(8)
+    n = 400
+    edges = []
+    for a in range(n):
+        edges.append((a, (a + 1) % n, int(rng.integers(1, 4))))   # strongly connected ring
+        for _ in range(int(rng.integers(4, 8))):
+            edges.append((a, int(rng.integers(0, n)), int(rng.integers(1, 4))))
+    return graph_from_edges(n, edges)
+
+
 def tie_graph():
     """Tiny weights -> many equal-cost paths (multi-bit first-move sets)."""
     g = cpd.synth_road_graph(24, 24, seed=11)
@@ -47,5 +59,6 @@ GRAPHS = {
     "synth": lambda: cpd.synth_road_graph(40, 30, seed=7),
     "ties": tie_graph,
     "irregular": irregular_graph,
+    "deg8": deg8_graph,
     "single": lambda: graph_from_edges(1, []),
 }
