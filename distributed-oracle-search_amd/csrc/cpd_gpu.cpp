@@ -111,12 +111,19 @@ struct cpd_graph {
     uint32_t fmb = 16;  // bits per first-move set (fm_bits(adj_shift))
     DevBuf<uint32_t> dist, tgt, counts;
     DevBuf<uint32_t> fm;    // [B][npad] fmb-bit sets
-    DevBuf<uint32_t> live;  // [col][B/1024] up-sweep row-stored flags
+    DevBuf<uint32_t> live;   // [col] slab mask of the up-sweep rows stored
+    DevBuf<uint32_t> tmask;  // [col] slab mask of the batch's targets
     DevBuf<uint64_t> row_off;
     // per-level sweep counters (2 per launch: stored/own rows, gathered rows)
     DevBuf<unsigned int> stat;
     std::vector<unsigned int> stat_h;
     DevBuf<uint32_t> asc_lvl_of, dsc_lvl_of;  // slot -> level
+    // narrow upward levels (<= kNarrow nodes) run chunked: per level l,
+    // items [up_item_first[l], up_item_first[l+1]) of (slot, a0, a1, 0);
+    // up_init_cols = the columns of all their nodes (leaf-form init)
+    std::vector<uint32_t> up_item_first;
+    DevBuf<uint32_t> up_items, up_init_cols;
+    uint32_t n_init_cols = 0;
     // lane position of each caller target in the current batch (sorted by column)
     std::vector<uint32_t> pos_of, tgt_col;
     // timing
@@ -192,7 +199,8 @@ struct cpd_graph {
         B = want;
         dist.alloc((size_t)n * B);
         fm.alloc((size_t)B * (npad / (32u / fmb)));
-        live.alloc((size_t)n * (B / 1024u));
+        live.alloc(n);
+        tmask.alloc(n);
         tgt.alloc(B);
         counts.alloc(B);
     }
@@ -393,6 +401,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         }
         build_sweep(*p, true, asc_slot, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs, unused);
         g->asc_off_host = off;
+        const std::vector<uint32_t> nodes_asc_host = nodes;
         g->asc_nodes.upload(nodes.data(), nodes.size(), s);
         g->asc_off.upload(off.data(), off.size(), s);
         g->asc_arcs.upload(arcs.data(), arcs.size(), s);
@@ -413,6 +422,27 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 for (uint32_t x = first[l]; x < first[l + 1]; ++x) v[x] = (uint32_t)l;
             return v;
         };
+        {
+            constexpr uint32_t kNarrow = 1024;
+            const uint32_t C = sweep_chunk_arcs();
+            std::vector<uint32_t> items, cols;
+            g->up_item_first.assign(g->asc_lvl.size(), 0);
+            for (size_t l = 0; l + 1 < g->asc_lvl.size(); ++l) {
+                g->up_item_first[l] = (uint32_t)(items.size() / 4);
+                const uint32_t s0 = g->asc_lvl[l], s1 = g->asc_lvl[l + 1];
+                if (l < 2 || s1 - s0 > kNarrow) continue;
+                for (uint32_t x = s0; x < s1; ++x) {
+                    cols.push_back(nodes_asc_host[x]);
+                    for (uint32_t a = g->asc_off_host[x]; a < g->asc_off_host[x + 1]; a += C)
+                        items.insert(items.end(),
+                                     {x, a, std::min(a + C, g->asc_off_host[x + 1]), 0u});
+                }
+            }
+            g->up_item_first.back() = (uint32_t)(items.size() / 4);
+            g->up_items.upload(items.data(), items.size(), s);
+            g->up_init_cols.upload(cols.data(), cols.size(), s);
+            g->n_init_cols = (uint32_t)cols.size();
+        }
         std::vector<uint32_t> la = lvl_of(g->asc_lvl), ld = lvl_of(g->dsc_lvl);
         g->asc_lvl_of.upload(la.data(), n, s);
         g->dsc_lvl_of.upload(ld.data(), n, s);
@@ -424,7 +454,8 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
 int cpd_graph_set_batch(cpd_graph* g, uint32_t batch) {
     return guarded([&] {
         CPD_REQUIRE(g, CPD_E_ARG, "null graph");
-        CPD_REQUIRE(batch % 1024u == 0, CPD_E_ARG, "batch must be a multiple of 1024");
+        CPD_REQUIRE(batch % 1024u == 0 && batch <= 32768u, CPD_E_ARG,
+                    "batch must be a multiple of 1024, at most 32768");
         g->select();
         HIP_CHECK(hipStreamSynchronize(g->stream));
         g->reserve_batch(batch);
@@ -470,28 +501,43 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
     const size_t nasc = g->asc_lvl.size();
     if (stat) HIP_CHECK(hipMemsetAsync(stat, 0, g->stat.n * sizeof(unsigned int), g->stream));
     const std::vector<unsigned int>& sh = g->stat_h;  // filled by the batch's D2H copy
+    if (live) {
+        HIP_CHECK(hipMemsetAsync(g->tmask.p, 0, (size_t)n * sizeof(uint32_t), g->stream));
+        launch_target_mask(g->tgt.p, active, g->tmask.p, g->stream);
+        g->timed("sweep_up_init", 4.0 * g->n_init_cols * active, [&] {
+            launch_sweep_up_init(g->up_init_cols.p, g->n_init_cols, g->dist.p, g->tgt.p, B, slabs,
+                                 live, g->tmask.p, g->stream);
+        });
+    }
     // ascending sweep: each level reads lower levels' rows.  Levels 0 and 1
     // are never materialised (closed forms, kLeafBit / kL1Bit): not launched.
-    // Bytes per level: 4 B x target per gathered row and per stored row
-    // (1024 targets per live (row, slab) when skipping, else every row),
-    // arcs 8 B + their live flags 4 B and the node slot 12 B + flag 4 B per
-    // 1024-target slab.
+    // Dense bytes per level: gathered rows 4 B x target, row writes 4 B x
+    // target, arcs 8 B and node slot 12 B per 1024-target slab.  Sparse: 4 KiB
+    // per live (row, slab) stored and per live row gathered, arcs 8 B + their
+    // masks 4 B, node slot 12 B + masks 8 B, once per node.
     for (size_t l = 2; l + 1 < nasc; ++l) {
         uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
         if (!cnt) continue;
         double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
-        double meta = 8.0 * arcs_l * slabs + 12.0 * cnt * slabs;
-        double dense = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + meta;
+        double dense = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + 8.0 * arcs_l * slabs +
+                       12.0 * cnt * slabs;
         std::function<double()> late;
         if (live && stat)
-            late = [&sh, l, meta, arcs_l, cnt, slabs] {
-                return 4096.0 * ((double)sh[2 * l] + (double)sh[2 * l + 1]) + meta +
-                       4.0 * (arcs_l + cnt) * slabs;
+            late = [&sh, l, arcs_l, cnt] {
+                return 4096.0 * ((double)sh[2 * l] + (double)sh[2 * l + 1]) + 12.0 * arcs_l +
+                       20.0 * cnt;
             };
+        const uint32_t i0 = g->up_item_first[l], ni = g->up_item_first[l + 1] - i0;
         g->timed("sweep_up", dense, [&] {
-            launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt, g->dist.p,
-                         g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
-                         g->stream);
+            if (live && ni)
+                launch_sweep_up_chunks(g->up_items.p + 4 * (size_t)i0, ni, g->asc_nodes.p,
+                                       g->asc_arcs.p, g->dist.p, g->tgt.p, B, slabs,
+                                       g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
+                                       g->tmask.p, g->stream);
+            else
+                launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt,
+                             g->dist.p, g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p,
+                             g->asc_arcs.p, live, g->tmask.p, g->stream);
         }, std::move(late));
     }
     for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
@@ -509,17 +555,17 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
         g->timed("sweep_down", dense, [&] {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
                          g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
-                         g->stream);
+                         g->tmask.p, g->stream);
         }, std::move(late));
     }
     if (live && stat && nasc > 2) {  // row counts behind the late byte counts
         g->timed("live_stats", 0.0, [&] {
             launch_live_stats(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
-                              g->asc_lvl_of.p, g->asc_lvl[2], n, live, B, slabs, stat, g->stream);
+                              g->asc_lvl_of.p, g->asc_lvl[2], n, live, stat, g->stream);
         });
         g->timed("live_stats", 0.0, [&] {
             launch_live_stats(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p,
-                              g->dsc_lvl_of.p, 0, n, live, B, slabs, stat + 2 * nasc, g->stream);
+                              g->dsc_lvl_of.p, 0, n, live, stat + 2 * nasc, g->stream);
         });
     }
     // per row: own distance 4n + neighbour distances 4m + first-move write

@@ -11,6 +11,7 @@
 //   runs  u32 words, rows back to back at off[row] (count pass, then emit)
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 
@@ -97,37 +98,35 @@ __device__ __forceinline__ uint4 l1_val(const Closed& cf, uint32_t s, const uint
 }
 
 // Up-sweep sparsity.  d_up(x, t) is finite only for x in t's upward search
-// space, a few per cent of the (node, 1024-target slab) pairs at up-levels >= 2
-// on road graphs when a slab's targets are neighbours.  The
-// up-sweep stores a materialised row only if one of its 1024 values is finite
-// and records that in flags[col * S + slab]; readers of d_up (up-sweep
-// gathers, the down-sweep's own-row init) take INF for a row never stored.
-// flags == nullptr: every row is stored and read (no skipping).  The bytes
-// model's row counts come from live_stats (below), never from per-block
-// atomics: a level has up to ~2M blocks, and one counter word serialises them.
-struct Live {
-    uint32_t* flags;
-    uint32_t S;  // slabs per column = B / 1024
-};
+// space: a few per cent of the (node, 1024-target slab) pairs at up-levels
+// >= 2 on road graphs when a slab's targets are neighbours.
+// live[col] bit b = slab b of the column's row holds a finite value (and was
+// stored); the up-sweep computes exactly those slabs, readers of d_up (its own
+// gathers, the down-sweep's own-row init) take INF outside them.  The mask of
+// a row follows from its inputs alone — slabs holding the node as a target,
+// plus the masks of its down-arcs' rows (closed forms: the slabs holding the
+// leaf / level-1 targets) — because a finite input plus an arc weight stays
+// finite (cpd_plan_create bounds every distance below 2^32 - 1).
+// tmask[col] bit b = column col is a target of slab b (target_mask kernel).
 
-// Value an arc contributes (before adding its weight); *gathered = 1 if it
-// read a materialised row.
+// Value an arc contributes (before adding its weight); INF if !live.
 __device__ __forceinline__ uint4 arc_val(const uint4* __restrict__ d4, const uint4 t, uint2 e,
                                          uint32_t B4, uint32_t l4, const Closed& cf,
                                          bool live) {
+    if (!live) return make_uint4(INF, INF, INF, INF);
     if (e.x & kLeafBit) return leaf4(t, e.x & kIdxMask, 0u);
     if (e.x & kL1Bit) return l1_val(cf, e.x & kIdxMask, t);
-    if (!live) return make_uint4(INF, INF, INF, INF);
     return d4[(size_t)e.x * B4 + l4];
 }
 
-// One CH sweep level.  Logical block = (slot in the level, 1024-target slab),
-// slots fastest, XCD-remapped (remap != 0): node v = nodes[slot]; its arcs
-// (col, w) are wave-uniform (scalar loads); each lane owns 4 consecutive
-// targets.  ASCEND: upward sweep, init 0 at the lane's own target else INF.
-// !ASCEND: downward sweep, init = current dist (the upward value, or its closed
-// form for levels 0/1).  Then acc = min(acc, w + d[arc]) over the arcs, eight
-// gathers in flight per wave.
+// One CH sweep level, dense.  Logical block = (slot in the level, 1024-target
+// slab), slots fastest, XCD-remapped (remap != 0): node v = nodes[slot]; its
+// arcs (col, w) are wave-uniform (scalar loads); each lane owns 4 consecutive
+// targets.  ASCEND: upward sweep, init 0 at the lane's own target else INF
+// (used only when skipping is off, CPD_LIVE=0).  !ASCEND: downward sweep, init
+// = current dist (the upward value — INF outside live[v] when live != null —
+// or its closed form for levels 0/1).  Then acc = min(acc, w + d[arc]) over the
+// arcs, eight gathers in flight per wave.
 template <bool ASCEND>
 __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ nodes,
                                                    const uint32_t* __restrict__ arc_off,
@@ -135,18 +134,17 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
                                                    uint32_t slot0, uint32_t count, uint32_t remap,
                                                    uint32_t* __restrict__ dist,
                                                    const uint4* __restrict__ tgt4,
-                                                   uint32_t B4, Closed cf, Live lv) {
+                                                   uint32_t B4, Closed cf,
+                                                   const uint32_t* __restrict__ live) {
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t slab = L / count;
     const uint32_t slot = slot0 + (L - slab * count);
     const uint32_t l4 = slab * 256u + threadIdx.x;
     const uint32_t vraw = nodes[slot];
     uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
-    const uint32_t* __restrict__ flags_in = lv.flags;  // entries of finished levels only
     const uint4 t = tgt4[l4];
     uint32_t v;
     uint4 acc;
-    uint32_t own = 0;
     if (ASCEND) {
         v = vraw;
         acc = leaf4(t, v, 0u);
@@ -158,71 +156,190 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
         acc = l1_val(cf, vraw & kIdxMask, t);
     } else {
         v = vraw;
-        own = flags_in ? flags_in[(size_t)v * lv.S + slab] : 1u;
+        const bool own = !live || ((live[v] >> slab) & 1u);
         acc = own ? d4[(size_t)v * B4 + l4] : make_uint4(INF, INF, INF, INF);
     }
     const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
     uint32_t a = a0;
-    // only the up-sweep reads rows that may never have been stored
-    auto live_of = [&](uint2 e) -> uint32_t {
-        if (!ASCEND || !flags_in || (e.x & (kLeafBit | kL1Bit))) return 1u;
-        return flags_in[(size_t)e.x * lv.S + slab];
-    };
     for (; a + 8 <= a1; a += 8) {
         uint2 e[8];
-        uint32_t ok[8];
         uint4 x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) ok[i] = live_of(e[i]);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = arc_val(d4, t, e[i], B4, l4, cf, ok[i] != 0);
+        for (int i = 0; i < 8; ++i) x[i] = arc_val(d4, t, e[i], B4, l4, cf, true);
 #pragma unroll
         for (int i = 0; i < 8; ++i) min4(acc, x[i], e[i].y);
     }
     for (; a < a1; ++a) {
         const uint2 e = arcs[a];
-        min4(acc, arc_val(d4, t, e, B4, l4, cf, live_of(e) != 0), e.y);
-    }
-    if (ASCEND && lv.flags) {
-        const uint32_t lo = min(min(acc.x, acc.y), min(acc.z, acc.w));
-        const int any = __syncthreads_or(lo != INF);
-        if (threadIdx.x == 0) lv.flags[(size_t)v * lv.S + slab] = any ? 1u : 0u;
-        if (any) d4[(size_t)v * B4 + l4] = acc;
-        return;
+        min4(acc, arc_val(d4, t, e, B4, l4, cf, true), e.y);
     }
     d4[(size_t)v * B4 + l4] = acc;
 }
 
+// Slab mask of an arc's source row (see "Up-sweep sparsity").
+__device__ __forceinline__ uint32_t arc_mask(uint32_t ex, const uint32_t* __restrict__ live,
+                                             const uint32_t* __restrict__ tmask,
+                                             const Closed& cf) {
+    if (ex & kLeafBit) return tmask[ex & kIdxMask];
+    if (ex & kL1Bit) {
+        const uint32_t s = ex & kIdxMask;
+        uint32_t m = tmask[cf.nodes[s]];
+        for (uint32_t a = cf.off[s]; a < cf.off[s + 1]; ++a) m |= tmask[cf.arcs[a].x & kIdxMask];
+        return m;
+    }
+    return live[ex];
+}
+
+// Upward sweep level with row skipping.  Logical block = (slot, j), slots
+// fastest, XCD-remapped; the block computes node v's live slabs b with
+// b % nsplit == j (nsplit = 1 on wide levels: one block per node, its arcs
+// read once; > 1 on narrow top levels so they still fill the GPU).  Each
+// live slab: 256 threads x 4 targets as in sweep_level, gathers only from
+// arcs live in that slab.  live[v] = the node's mask (every split writes the
+// same value); nothing else of a dead slab is read or written.
+__global__ __launch_bounds__(256) void sweep_up_sparse(
+    const uint32_t* __restrict__ nodes, const uint32_t* __restrict__ arc_off,
+    const uint2* __restrict__ arcs, uint32_t slot0, uint32_t count, uint32_t nsplit,
+    uint32_t remap, uint32_t* __restrict__ dist, const uint4* __restrict__ tgt4, uint32_t B4,
+    Closed cf, uint32_t* __restrict__ live, const uint32_t* __restrict__ tmask,
+    uint32_t active) {
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t j = L / count;
+    const uint32_t slot = slot0 + (L - j * count);
+    const uint32_t v = nodes[slot];
+    const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
+    const uint32_t* __restrict__ live_in = live;  // rows of finished levels only
+    uint32_t m = tmask[v];
+    for (uint32_t a = a0; a < a1; ++a) m |= arc_mask(arcs[a].x, live_in, tmask, cf);
+    m &= active;
+    if (threadIdx.x == 0 && j == 0) live[v] = m;
+    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    for (uint32_t mm = m; mm; mm &= mm - 1u) {
+        const uint32_t slab = (uint32_t)__builtin_ctz(mm);
+        if (slab % nsplit != j) continue;
+        const uint32_t l4 = slab * 256u + threadIdx.x;
+        const uint4 t = tgt4[l4];
+        uint4 acc = leaf4(t, v, 0u);
+        uint32_t a = a0;
+        for (; a + 8 <= a1; a += 8) {
+            uint2 e[8];
+            uint4 x[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                x[i] = arc_val(d4, t, e[i], B4, l4, cf,
+                               (arc_mask(e[i].x, live_in, tmask, cf) >> slab) & 1u);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) min4(acc, x[i], e[i].y);
+        }
+        for (; a < a1; ++a) {
+            const uint2 e = arcs[a];
+            min4(acc, arc_val(d4, t, e, B4, l4, cf, (arc_mask(e.x, live_in, tmask, cf) >> slab) & 1u),
+                 e.y);
+        }
+        d4[(size_t)v * B4 + l4] = acc;
+    }
+}
+
+// Narrow upward levels (the top of the hierarchy: few nodes, each with up to
+// hundreds of down-arcs) are latency-bound when one block walks a node's arcs
+// eight at a time.  There, work items = (node, chunk of <= kChunk arcs) x
+// slab: every block issues its chunk's mask loads and gathers at once and
+// folds its partial minimum into the row with atomicMin; the rows start as the
+// leaf form (sweep_up_init, once per batch) and live[v] collects the chunks'
+// masks with atomicOr.
+constexpr int kChunk = 16;
+
+__global__ __launch_bounds__(256) void sweep_up_init(const uint32_t* __restrict__ cols,
+                                                     uint32_t ncols, uint32_t remap,
+                                                     uint32_t* __restrict__ dist,
+                                                     const uint4* __restrict__ tgt4, uint32_t B4,
+                                                     uint32_t* __restrict__ live,
+                                                     const uint32_t* __restrict__ tmask,
+                                                     uint32_t active) {
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t slab = L / ncols;
+    const uint32_t v = cols[L - slab * ncols];
+    const uint32_t l4 = slab * 256u + threadIdx.x;
+    reinterpret_cast<uint4*>(dist)[(size_t)v * B4 + l4] = leaf4(tgt4[l4], v, 0u);
+    if (slab == 0 && threadIdx.x == 0) live[v] = tmask[v] & active;
+}
+
+__global__ __launch_bounds__(256) void sweep_up_chunks(
+    const uint4* __restrict__ items, uint32_t nitems, uint32_t remap,
+    const uint32_t* __restrict__ nodes, const uint2* __restrict__ arcs,
+    uint32_t* __restrict__ dist, const uint4* __restrict__ tgt4, uint32_t B4, Closed cf,
+    uint32_t* __restrict__ live, const uint32_t* __restrict__ tmask, uint32_t active) {
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t slab = L / nitems;
+    const uint4 it = items[L - slab * nitems];  // (slot, first arc, end arc, -)
+    const uint32_t v = nodes[it.x];
+    const uint32_t* __restrict__ live_in = live;  // lower levels' masks only
+    uint2 e[kChunk];
+    uint32_t mk[kChunk], pm = 0;
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) e[i] = it.y + i < it.z ? arcs[it.y + i] : make_uint2(0u, 0u);
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) {
+        mk[i] = it.y + i < it.z ? arc_mask(e[i].x, live_in, tmask, cf) & active : 0u;
+        pm |= mk[i];
+    }
+    if (slab == 0 && threadIdx.x == 0 && pm) atomicOr(&live[v], pm);
+    if (!((pm >> slab) & 1u)) return;
+    const uint32_t l4 = slab * 256u + threadIdx.x;
+    const uint4 t = tgt4[l4];
+    const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
+    uint4 x[kChunk];
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) x[i] = arc_val(d4, t, e[i], B4, l4, cf, (mk[i] >> slab) & 1u);
+    uint4 acc = make_uint4(INF, INF, INF, INF);
+#pragma unroll
+    for (int i = 0; i < kChunk; ++i) min4(acc, x[i], e[i].y);
+    uint32_t* row = dist + ((size_t)v * B4 + l4) * 4u;
+    if (acc.x != INF) atomicMin(row + 0, acc.x);
+    if (acc.y != INF) atomicMin(row + 1, acc.y);
+    if (acc.z != INF) atomicMin(row + 2, acc.z);
+    if (acc.w != INF) atomicMin(row + 3, acc.w);
+}
+
+// tmask[col] |= 1 << slab for every target lane (4 per thread) of the batch;
+// the caller zeroes tmask first.
+__global__ __launch_bounds__(256) void target_mask(const uint32_t* __restrict__ tgt, uint32_t B,
+                                                   uint32_t* __restrict__ tmask) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < B) atomicOr(&tmask[tgt[i]], 1u << (i >> 10));
+}
+
 // Row counts of one batch's sweeps for the bytes model (timing runs only),
 // thread per node slot of one sweep direction:
-//   ASCEND (slots of up-levels >= 2): stat[2 l] += rows stored (live flags of
-//     the slot's column over the active slabs), stat[2 l + 1] += rows gathered
-//     (live flags of its materialised arcs' columns);
-//   !ASCEND: stat[2 l] += own rows read (materialised slots only).
+//   ASCEND (slots of up-levels >= 2): stat[2 l] += rows stored (slabs of the
+//     slot's live mask), stat[2 l + 1] += rows gathered (its materialised
+//     arcs' live slabs);
+//   !ASCEND: stat[2 l] += own rows read (live slabs of materialised slots).
 // lvl_of[slot] = the slot's level; counts are aggregated per wave when all
-// lanes share a level (slots are level-ordered), so atomics are few.
+// lanes share a level (slots are level-ordered), so atomics are few — a
+// per-block atomic on one word per level would serialise ~10^6 blocks.
 template <bool ASCEND>
 __global__ __launch_bounds__(256) void live_stats(const uint32_t* __restrict__ nodes,
                                                   const uint32_t* __restrict__ arc_off,
                                                   const uint2* __restrict__ arcs,
                                                   const uint32_t* __restrict__ lvl_of,
                                                   uint32_t slot0, uint32_t slot1,
-                                                  const uint32_t* __restrict__ flags, uint32_t S,
-                                                  uint32_t slabs, unsigned int* __restrict__ stat) {
+                                                  const uint32_t* __restrict__ live,
+                                                  unsigned int* __restrict__ stat) {
     const uint32_t slot = slot0 + blockIdx.x * 256u + threadIdx.x;
     uint32_t own = 0, gathered = 0, lvl = 0xFFFFFFFFu;
     if (slot < slot1) {
         lvl = lvl_of[slot];
         const uint32_t v = nodes[slot];
-        if (ASCEND || !(v & (kLeafBit | kL1Bit)))
-            for (uint32_t b = 0; b < slabs; ++b) own += flags[(size_t)v * S + b];
+        if (ASCEND || !(v & (kLeafBit | kL1Bit))) own = __builtin_popcount(live[v]);
         if (ASCEND)
             for (uint32_t a = arc_off[slot]; a < arc_off[slot + 1]; ++a) {
                 const uint32_t c = arcs[a].x;
-                if (c & (kLeafBit | kL1Bit)) continue;
-                for (uint32_t b = 0; b < slabs; ++b) gathered += flags[(size_t)c * S + b];
+                if (!(c & (kLeafBit | kL1Bit))) gathered += __builtin_popcount(live[c]);
             }
     }
     const uint32_t l0 = __shfl(lvl, 0, 64);
@@ -676,34 +793,67 @@ uint32_t xcd_remap() {
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* arcs32, uint32_t slot0, uint32_t count, uint32_t* dist,
                   const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
-                  const uint32_t* asc_off, const uint32_t* asc_arcs, uint32_t* live_flags,
-                  hipStream_t s) {
-    dim3 grid(count * slabs);
+                  const uint32_t* asc_off, const uint32_t* asc_arcs, uint32_t* live,
+                  const uint32_t* tmask, hipStream_t s) {
     const uint4* t4 = reinterpret_cast<const uint4*>(tgt);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
     const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
-    const kern::Live lv{live_flags, B / 1024u};
-    if (ascend)
-        launch(kern::sweep_level<true>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, count,
-               xcd_remap(), dist, t4, B / 4u, cf, lv);
-    else
-        launch(kern::sweep_level<false>, grid, dim3(256), s, nodes, arc_off, arcs, slot0, count,
-               xcd_remap(), dist, t4, B / 4u, cf, lv);
+    if (ascend && live) {
+        // one block per node on wide levels; narrow levels split the slabs
+        const uint32_t nsplit = std::max(1u, std::min(slabs, 2048u / std::max(count, 1u)));
+        const uint32_t active = slabs >= 32 ? 0xFFFFFFFFu : ((1u << slabs) - 1u);
+        launch(kern::sweep_up_sparse, dim3(count * nsplit), dim3(256), s, nodes, arc_off, arcs,
+               slot0, count, nsplit, xcd_remap(), dist, t4, B / 4u, cf, live, tmask, active);
+    } else if (ascend) {
+        launch(kern::sweep_level<true>, dim3(count * slabs), dim3(256), s, nodes, arc_off, arcs,
+               slot0, count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)nullptr);
+    } else {
+        launch(kern::sweep_level<false>, dim3(count * slabs), dim3(256), s, nodes, arc_off, arcs,
+               slot0, count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live);
+    }
+}
+
+void launch_sweep_up_init(const uint32_t* cols, uint32_t ncols, uint32_t* dist,
+                          const uint32_t* tgt, uint32_t B, uint32_t slabs, uint32_t* live,
+                          const uint32_t* tmask, hipStream_t s) {
+    if (!ncols) return;
+    const uint32_t active = slabs >= 32 ? 0xFFFFFFFFu : ((1u << slabs) - 1u);
+    launch(kern::sweep_up_init, dim3(ncols * slabs), dim3(256), s, cols, ncols, xcd_remap(), dist,
+           reinterpret_cast<const uint4*>(tgt), B / 4u, live, tmask, active);
+}
+
+void launch_sweep_up_chunks(const uint32_t* items, uint32_t nitems, const uint32_t* nodes,
+                            const uint32_t* arcs32, uint32_t* dist, const uint32_t* tgt, uint32_t B,
+                            uint32_t slabs, const uint32_t* asc_nodes, const uint32_t* asc_off,
+                            const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
+                            hipStream_t s) {
+    if (!nitems) return;
+    const uint32_t active = slabs >= 32 ? 0xFFFFFFFFu : ((1u << slabs) - 1u);
+    const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
+    launch(kern::sweep_up_chunks, dim3(nitems * slabs), dim3(256), s,
+           reinterpret_cast<const uint4*>(items), nitems, xcd_remap(), nodes,
+           reinterpret_cast<const uint2*>(arcs32), dist, reinterpret_cast<const uint4*>(tgt),
+           B / 4u, cf, live, tmask, active);
+}
+
+uint32_t sweep_chunk_arcs() { return (uint32_t)kern::kChunk; }
+
+void launch_target_mask(const uint32_t* tgt, uint32_t B, uint32_t* tmask, hipStream_t s) {
+    launch(kern::target_mask, dim3((B + 255u) / 256u), dim3(256), s, tgt, B, tmask);
 }
 
 void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                        const uint32_t* arcs32, const uint32_t* lvl_of, uint32_t slot0,
-                       uint32_t slot1, const uint32_t* flags, uint32_t B, uint32_t slabs,
-                       unsigned int* stat, hipStream_t s) {
+                       uint32_t slot1, const uint32_t* live, unsigned int* stat, hipStream_t s) {
     if (slot1 <= slot0) return;
     const dim3 grid((slot1 - slot0 + 255u) / 256u);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
     if (ascend)
         launch(kern::live_stats<true>, grid, dim3(256), s, nodes, arc_off, arcs, lvl_of, slot0,
-               slot1, flags, B / 1024u, slabs, stat);
+               slot1, live, stat);
     else
         launch(kern::live_stats<false>, grid, dim3(256), s, nodes, arc_off, arcs, lvl_of, slot0,
-               slot1, flags, B / 1024u, slabs, stat);
+               slot1, live, stat);
 }
 
 uint32_t fm_bits(uint32_t shift) { return shift <= 2 ? 4u : (1u << shift); }

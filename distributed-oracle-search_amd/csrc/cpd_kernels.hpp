@@ -14,23 +14,43 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop);
 // 1024 targets of the B-wide batch row, XCD-remapped (CPD_XCD=0: off).
 // asc_*: the ascending sweep's arrays, read by both directions for the
 // level-1 closed forms (see kL1Bit in cpd_kernels.hip).
-// live_flags ([col][B/1024] u32, may be null): the up-sweep records which
-// (materialised row, slab) it stored; the up-sweep's gathers and the
-// down-sweep's own-row reads skip the others (their values are all INF).
+// live (n u32, may be null = no skipping): bit b of live[col] = slab b of the
+// column's up-sweep row holds finite values; the up-sweep computes and writes
+// only those (sweep_up_sparse), the down-sweep's own-row reads skip the rest.
+// tmask (n u32): bit b of tmask[col] = col is a target of slab b
+// (launch_target_mask); B <= 32768 so that a mask fits in 32 bits.
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* arcs /* (col, w) pairs */, uint32_t slot0, uint32_t count,
                   uint32_t* dist, const uint32_t* tgt, uint32_t B, uint32_t slabs,
                   const uint32_t* asc_nodes, const uint32_t* asc_off, const uint32_t* asc_arcs,
-                  uint32_t* live_flags, hipStream_t s);
+                  uint32_t* live, const uint32_t* tmask, hipStream_t s);
 
-// Row counts behind the live flags for the bytes model (timing runs): over
+// Narrow upward levels, chunked: items (slot, first arc, end arc, 0) of at
+// most sweep_chunk_arcs() arcs each, nitems x slabs workgroups, partial
+// minima folded in with atomicMin.  The rows of every node handled this way
+// must first be set to their leaf form by launch_sweep_up_init (cols: their
+// columns), which also seeds live[col] = tmask[col].
+void launch_sweep_up_init(const uint32_t* cols, uint32_t ncols, uint32_t* dist,
+                          const uint32_t* tgt, uint32_t B, uint32_t slabs, uint32_t* live,
+                          const uint32_t* tmask, hipStream_t s);
+void launch_sweep_up_chunks(const uint32_t* items /* uint4 each */, uint32_t nitems,
+                            const uint32_t* nodes, const uint32_t* arcs, uint32_t* dist,
+                            const uint32_t* tgt, uint32_t B, uint32_t slabs,
+                            const uint32_t* asc_nodes, const uint32_t* asc_off,
+                            const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
+                            hipStream_t s);
+uint32_t sweep_chunk_arcs();
+
+// tmask[tgt[i]] |= 1 << (i / 1024) for i < B; tmask must be zeroed first.
+void launch_target_mask(const uint32_t* tgt, uint32_t B, uint32_t* tmask, hipStream_t s);
+
+// Row counts behind the live masks for the bytes model (timing runs): over
 // node slots [slot0, slot1) of one sweep direction, stat[2 * lvl_of[slot]]
 // += rows stored (up) / own rows read (down), stat[2 * lvl + 1] += rows
 // gathered (up).  stat must be zeroed by the caller.
 void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                        const uint32_t* arcs, const uint32_t* lvl_of, uint32_t slot0,
-                       uint32_t slot1, const uint32_t* flags, uint32_t B, uint32_t slabs,
-                       unsigned int* stat, hipStream_t s);
+                       uint32_t slot1, const uint32_t* live, unsigned int* stat, hipStream_t s);
 
 // Bits per first-move set for a packed adjacency of 2^shift slots per column:
 // max(4, 2^shift) (>= the max out-degree); sets are stored 32/bits per u32.

@@ -131,3 +131,24 @@ def test_multi_batch_and_reuse():
     off2, runs2 = rows2.export()
     np.testing.assert_array_equal(off2, ref_off[:101])
     np.testing.assert_array_equal(runs2, ref_runs[: int(ref_off[100])])
+
+
+@pytest.mark.parametrize("width,batch", [(60, 4096), (90, 8192), (200, 4096)])
+def test_multi_slab_batches(width, batch):
+    """Several 1024-target slabs per batch (slab masks, split narrow levels),
+    targets in shuffled order (the batch is sorted by column internally)."""
+    g = cpd.synth_road_graph(width, width, seed=width)
+    plan = cpd.Plan(g)
+    dev = cpd.Graph(plan, batch=batch)
+    rng = np.random.default_rng(width)
+    targets = rng.permutation(g.n).astype(np.uint32)[: min(g.n, batch + 1500)]
+    rows = dev.build_rows(targets)
+    off, runs = rows.export()
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    np.testing.assert_array_equal(off, ref_off)
+    np.testing.assert_array_equal(runs, ref_runs)
+    nd = min(len(targets), batch)
+    dist, _ = dev.debug_rows(targets[:nd], want_fm=False)
+    for i in rng.choice(nd, 5, replace=False):
+        np.testing.assert_array_equal(
+            dist[:, i], oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, targets[i]))
