@@ -111,8 +111,17 @@ struct cpd_graph {
     uint32_t fmb = 16;  // bits per first-move set (fm_bits(adj_shift))
     DevBuf<uint32_t> dist, tgt, counts;
     DevBuf<uint32_t> fm;    // [B][npad] fmb-bit sets
+    DevBuf<uint32_t> rle_st;  // [B][npad/32] RLE segment entry states (fmb == 4)
+    DevBuf<uint8_t> rle_rc;   // [B][npad/32] runs ending in each segment
     DevBuf<uint32_t> live;   // [col] slab mask of the up-sweep rows stored
     DevBuf<uint32_t> tmask;  // [col] slab mask of the batch's targets
+    // leaf first moves from the down-sweep (4-bit sets only): leafbits[col/32]
+    // bit = column is a CH leaf; fmleaf [col][B/4] u16 = its sets, 4 per lane
+    bool leaf_fm = false;
+    DevBuf<uint32_t> leafbits;
+    DevBuf<uint16_t> fmleaf;
+    double n_leaf = 0, m_leaf = 0;    // leaves, their out-edges
+    std::vector<double> dsc_lvl_leaves;
     DevBuf<uint64_t> row_off;
     // per-level sweep counters (2 per launch: stored/own rows, gathered rows)
     DevBuf<unsigned int> stat;
@@ -199,8 +208,13 @@ struct cpd_graph {
         B = want;
         dist.alloc((size_t)n * B);
         fm.alloc((size_t)B * (npad / (32u / fmb)));
+        if (fmb == 4) {
+            rle_st.alloc((size_t)B * (npad / 32u));
+            rle_rc.alloc((size_t)B * (npad / 32u));
+        }
         live.alloc(n);
         tmask.alloc(n);
+        if (leaf_fm) fmleaf.alloc((size_t)n * (B / 4u));
         tgt.alloc(B);
         counts.alloc(B);
     }
@@ -252,6 +266,14 @@ namespace {
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kL1Bit = 0x40000000u;
 
+// Optimisation switches for A/B runs: CPD_<NAME>=0 turns one off (CPD_LIVE,
+// CPD_SORT, CPD_LEAFFM here, CPD_XCD in the launchers); results are identical
+// either way.
+bool env_on(const char* name) {
+    const char* e = std::getenv(name);
+    return !(e && *e == '0');
+}
+
 void require_device() {
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);
@@ -293,6 +315,8 @@ void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& as
     const std::vector<uint32_t>& aw = ascend ? H.dn_w : H.up_w;
     const std::vector<uint32_t>& lup = H.level_up;
     CPD_REQUIRE(aoff[n] < 0xFFFFFFFFull, CPD_E_RANGE, "hierarchy has >= 2^32 arcs");
+    // (ordering a level's nodes by their lowest up-arc head instead, so that
+    // nodes gathering the same rows run side by side, measured no faster)
     std::vector<uint32_t> node_of_slot = level_order(p, level, nlev, lvl_first);
     // how a node is referenced: closed form (level 0 / 1 of the up sweep) or row
     auto ref = [&](uint32_t v) -> uint32_t {
@@ -414,6 +438,21 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
         g->ch_arcs += arcs.size() / 2;
+        // leaf first moves in the down-sweep: 4-bit sets only (<= 4 slots)
+        g->leaf_fm = g->fmb == 4 && env_on("CPD_LEAFFM");
+        {
+            std::vector<uint32_t> lb(g->npad / 32u, 0u);
+            g->dsc_lvl_leaves.assign(g->dsc_lvl.size(), 0.0);
+            for (uint32_t v = 0; v < n; ++v)
+                if (p->ch.level_up[v] == 0) {
+                    const uint32_t c = p->order[v];
+                    lb[c >> 5] |= 1u << (c & 31u);
+                    g->n_leaf += 1;
+                    g->m_leaf += p->row_ptr[v + 1] - p->row_ptr[v];
+                    g->dsc_lvl_leaves[p->ch.level_dn[v]] += 1;
+                }
+            g->leafbits.upload(lb.data(), lb.size(), s);
+        }
         g->stat.alloc(2 * (g->asc_lvl.size() + g->dsc_lvl.size()));
         g->stat_h.assign(g->stat.n, 0);
         auto lvl_of = [n](const std::vector<uint32_t>& first) {
@@ -477,10 +516,6 @@ namespace {
 
 // CPD_LIVE=0: no up-sweep row skipping; CPD_SORT=0: batches keep the caller's
 // target order (A/B measurements; results are identical either way).
-bool env_on(const char* name) {
-    const char* e = std::getenv(name);
-    return !(e && *e == '0');
-}
 bool live_on() {
     static const bool on = env_on("CPD_LIVE");
     return on;
@@ -537,7 +572,8 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
             else
                 launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt,
                              g->dist.p, g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p,
-                             g->asc_arcs.p, live, g->tmask.p, g->stream);
+                             g->asc_arcs.p, live, g->tmask.p, g->adj.p, g->adj_shift, nullptr,
+                             g->stream);
         }, std::move(late));
     }
     for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
@@ -546,6 +582,7 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
         const size_t si = 2 * (nasc + l);
         double base = (4.0 * g->dsc_lvl_arcs[l] + 4.0 * cnt) * active +
                       8.0 * g->dsc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
+        if (g->leaf_fm) base += 0.5 * g->dsc_lvl_leaves[l] * active;  // leaf sets
         double dense = base + 4.0 * g->dsc_lvl_reads[l] * active;
         std::function<double()> late;
         if (live && stat)
@@ -555,7 +592,8 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
         g->timed("sweep_down", dense, [&] {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
                          g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
-                         g->tmask.p, g->stream);
+                         g->tmask.p, g->adj.p, g->adj_shift, g->leaf_fm ? g->fmleaf.p : nullptr,
+                         g->stream);
         }, std::move(late));
     }
     if (live && stat && nasc > 2) {  // row counts behind the late byte counts
@@ -570,13 +608,18 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
     }
     // per row: own distance 4n + neighbour distances 4m + first-move write
     // npad * fmb / 8; the packed adjacency (8 B per slot) is read once per
-    // 1024-target slab
+    // 1024-target slab.  Leaf columns (leaf_fm) read 0.5 B of sets instead
+    // of their own and neighbour distances.
     const uint32_t fslabs = (k + 1023u) / 1024u;
-    double fbytes = (4.0 * n + 4.0 * g->m + g->fmb / 8.0 * g->npad) * (fslabs * 1024.0) +
-                    8.0 * (double)n * (double)(1u << g->adj_shift) * fslabs;
+    const double nl = g->leaf_fm ? g->n_leaf : 0.0, ml = g->leaf_fm ? g->m_leaf : 0.0;
+    double fbytes =
+        (4.0 * (n - nl) + 4.0 * (g->m - ml) + 0.5 * nl + g->fmb / 8.0 * g->npad) *
+            (fslabs * 1024.0) +
+        8.0 * (double)(n - nl) * (double)(1u << g->adj_shift) * fslabs + 4.0 * g->npad / 32.0;
     g->timed("first_moves", fbytes, [&] {
         launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, g->tgt.p, B, k, n, g->npad,
-                           g->fm.p, g->stream);
+                           g->fm.p, g->leaf_fm ? g->leafbits.p : nullptr,
+                           g->leaf_fm ? g->fmleaf.p : nullptr, g->stream);
     });
     if (stat)
         HIP_CHECK(hipMemcpyAsync(g->stat_h.data(), stat, g->stat.n * sizeof(unsigned int),
@@ -628,8 +671,11 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     const double t1 = now_seconds();
     const uint32_t npad = g->npad;
     const double fm_row = g->fmb / 8.0 * npad;  // first-move bytes per row
-    g->timed("rle_count", fm_row * k + 4.0 * k, [&] {
-        launch_rle_count(g->fm.p, g->fmb, npad, k, g->counts.p, g->stream);
+    // + per 32-column segment a 4-B entry state and a 1-B count (fmb == 4)
+    const double st_row = g->fmb == 4 ? 5.0 * npad / 32.0 : 0.0;
+    g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
+        launch_rle_count(g->fm.p, g->fmb, npad, k, g->counts.p, g->rle_st.p, g->rle_rc.p,
+                         g->stream);
     });
     std::vector<uint32_t> counts(k);
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
@@ -662,9 +708,10 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     }
     const double t3 = now_seconds();
     g->row_off.upload(lane_off.data(), k, g->stream);
-    double ebytes = fm_row * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
+    double ebytes = (fm_row + st_row) * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
     g->timed("rle_emit", ebytes, [&] {
-        launch_rle_emit(g->fm.p, g->fmb, npad, k, g->row_off.p, r->runs.p, g->stream);
+        launch_rle_emit(g->fm.p, g->fmb, npad, k, g->row_off.p, r->runs.p, g->rle_st.p,
+                        g->rle_rc.p, g->stream);
     });
     g->sync();
     if (trace_on())

@@ -127,6 +127,21 @@ __device__ __forceinline__ uint4 arc_val(const uint4* __restrict__ d4, const uin
 // = current dist (the upward value — INF outside live[v] when live != null —
 // or its closed form for levels 0/1).  Then acc = min(acc, w + d[arc]) over the
 // arcs, eight gathers in flight per wave.
+//
+// Leaf first moves (lf.out != null, 4-bit sets): a leaf (no down-arcs) has
+// only higher-ranked out-neighbours, all final when the down-sweep reaches
+// it, and its up-arcs ARE its out-edges.  So its block walks the out-edges in
+// file order from the packed adjacency instead: d(v) = min over them (self
+// loops excluded), and FM(v) = {k : w_k + d(v_k) == d(v)} from the same
+// gathers, stored as 4 nibbles per lane in lf.out[col][B/4] (u16) for
+// first_moves to copy — the leaf's own row and neighbour rows are not read
+// again there.
+struct LeafFm {
+    const uint2* __restrict__ adj;  // packed adjacency, 2^shift <= 4 slots
+    uint32_t shift;
+    uint16_t* __restrict__ out;
+};
+
 template <bool ASCEND>
 __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ nodes,
                                                    const uint32_t* __restrict__ arc_off,
@@ -135,11 +150,11 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ dist,
                                                    const uint4* __restrict__ tgt4,
                                                    uint32_t B4, Closed cf,
-                                                   const uint32_t* __restrict__ live) {
+                                                   const uint32_t* __restrict__ live, LeafFm lf) {
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t slab = L / count;
     const uint32_t slot = slot0 + (L - slab * count);
-    const uint32_t l4 = slab * 256u + threadIdx.x;
+    const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t vraw = nodes[slot];
     uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
     const uint4 t = tgt4[l4];
@@ -151,12 +166,46 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
     } else if (vraw & kLeafBit) {
         v = vraw & kIdxMask;
         acc = leaf4(t, v, 0u);
+        if (lf.out) {
+            const uint32_t ns = 1u << lf.shift;
+            uint2 e[4];
+            uint4 x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                e[k] = (uint32_t)k < ns ? lf.adj[((size_t)v << lf.shift) + k]
+                                        : make_uint2(0xFFFFFFFFu, 0u);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                x[k] = (e[k].x != 0xFFFFFFFFu && e[k].x != v) ? d4[(size_t)e[k].x * B4 + l4]
+                                                              : make_uint4(INF, INF, INF, INF);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (e[k].x != 0xFFFFFFFFu && e[k].x != v) min4(acc, x[k], e[k].y);
+            uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (e[k].x == 0xFFFFFFFFu) continue;
+                const uint4 dv = e[k].x == v ? acc : x[k];  // self loop: d(v) itself
+                const uint32_t w = e[k].y;
+                b0 |= (sat_add(dv.x, w) == acc.x ? 1u : 0u) << k;
+                b1 |= (sat_add(dv.y, w) == acc.y ? 1u : 0u) << k;
+                b2 |= (sat_add(dv.z, w) == acc.z ? 1u : 0u) << k;
+                b3 |= (sat_add(dv.w, w) == acc.w ? 1u : 0u) << k;
+            }
+            b0 = (t.x == v || acc.x == INF) ? 0xFu : b0;  // wildcard (target, unreachable)
+            b1 = (t.y == v || acc.y == INF) ? 0xFu : b1;
+            b2 = (t.z == v || acc.z == INF) ? 0xFu : b2;
+            b3 = (t.w == v || acc.w == INF) ? 0xFu : b3;
+            d4[(size_t)v * B4 + l4] = acc;
+            lf.out[(size_t)v * B4 + l4] = (uint16_t)(b0 | (b1 << 4) | (b2 << 8) | (b3 << 12));
+            return;
+        }
     } else if (vraw & kL1Bit) {
         v = cf.nodes[vraw & kIdxMask];
         acc = l1_val(cf, vraw & kIdxMask, t);
     } else {
         v = vraw;
-        const bool own = !live || ((live[v] >> slab) & 1u);
+        const bool own = !live || ((live[v] >> (l4 >> 8)) & 1u);  // live bits: 1024 targets
         acc = own ? d4[(size_t)v * B4 + l4] : make_uint4(INF, INF, INF, INF);
     }
     const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
@@ -386,13 +435,15 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
                                                    const uint32_t* __restrict__ dist,
                                                    const uint32_t* __restrict__ tgt,
                                                    uint32_t B, uint32_t n, uint32_t npad,
-                                                   uint32_t remap, uint32_t* __restrict__ fm) {
+                                                   uint32_t remap, uint32_t* __restrict__ fm,
+                                                   const uint32_t* __restrict__ leafbits,
+                                                   const uint16_t* __restrict__ fmleaf) {
     constexpr int FMB = SLOTS < 4 ? 4 : SLOTS;
     using F = FmFmt<FMB>;
     const uint32_t nseg = npad / kSeg;
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t slab = L / nseg;
-    const uint32_t l4 = slab * 256u + threadIdx.x;
+    const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t B4 = B / 4u;
     const uint32_t c0 = (L - slab * nseg) * kSeg;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
@@ -401,19 +452,23 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
 #pragma unroll
     for (int p = 0; p < F::kWords; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
     constexpr int KC = SLOTS < 4 ? SLOTS : 4;  // slots gathered per chunk
+    // leaf columns (bit set, 4-bit sets only): sets computed by the down-sweep
+    const uint32_t lbits = (FMB == 4 && leafbits) ? leafbits[c0 / kSeg] : 0u;
 #pragma unroll
     for (int cg = 0; cg < (int)kSeg; cg += G) {
         uint4 dn[G];
         uint2 e[G][SLOTS];  // wave-uniform: scalar registers
-        uint32_t b[G][4];
+        uint32_t b[G][4], lv[G];
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             const uint32_t c = c0 + (uint32_t)(cg + j);
             const bool ok = c < n;  // wave-uniform
+            const bool leaf = (lbits >> (cg + j)) & 1u;
 #pragma unroll
             for (int k = 0; k < SLOTS; ++k)
-                e[j][k] = ok ? adj[(size_t)c * SLOTS + k] : make_uint2(kNoEdge, 0u);
-            dn[j] = ok ? d4[(size_t)c * B4 + l4] : make_uint4(INF, INF, INF, INF);
+                e[j][k] = ok && !leaf ? adj[(size_t)c * SLOTS + k] : make_uint2(kNoEdge, 0u);
+            dn[j] = ok && !leaf ? d4[(size_t)c * B4 + l4] : make_uint4(INF, INF, INF, INF);
+            lv[j] = ok && leaf ? fmleaf[(size_t)c * B4 + l4] : 0u;
             b[j][0] = b[j][1] = b[j][2] = b[j][3] = 0;
         }
 #pragma unroll
@@ -445,14 +500,25 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
         for (int j = 0; j < G; ++j) {
             const uint32_t c = c0 + (uint32_t)(cg + j);
             if (c >= n) continue;  // stays the wildcard padding
-            const uint32_t b0 = b[j][0], b1 = b[j][1], b2 = b[j][2], b3 = b[j][3];
             const int cc = cg + j;
+            uint32_t f0, f1, f2, f3;
+            if ((lbits >> cc) & 1u) {  // 4 nibbles, wildcards included
+                f0 = lv[j] & 0xFu;
+                f1 = (lv[j] >> 4) & 0xFu;
+                f2 = (lv[j] >> 8) & 0xFu;
+                f3 = lv[j] >> 12;
+            } else {
+                f0 = fm_final<FMB>(c, tc.x, dn[j].x, b[j][0]);
+                f1 = fm_final<FMB>(c, tc.y, dn[j].y, b[j][1]);
+                f2 = fm_final<FMB>(c, tc.z, dn[j].z, b[j][2]);
+                f3 = fm_final<FMB>(c, tc.w, dn[j].w, b[j][3]);
+            }
             const int wi = cc / F::kPer, sh = FMB * (cc % F::kPer);
             const uint32_t keep = ~(F::kAll << sh);  // clear this column's field
-            pk[0][wi] = (pk[0][wi] & keep) | (fm_final<FMB>(c, tc.x, dn[j].x, b0) << sh);
-            pk[1][wi] = (pk[1][wi] & keep) | (fm_final<FMB>(c, tc.y, dn[j].y, b1) << sh);
-            pk[2][wi] = (pk[2][wi] & keep) | (fm_final<FMB>(c, tc.z, dn[j].z, b2) << sh);
-            pk[3][wi] = (pk[3][wi] & keep) | (fm_final<FMB>(c, tc.w, dn[j].w, b3) << sh);
+            pk[0][wi] = (pk[0][wi] & keep) | (f0 << sh);
+            pk[1][wi] = (pk[1][wi] & keep) | (f1 << sh);
+            pk[2][wi] = (pk[2][wi] & keep) | (f2 << sh);
+            pk[3][wi] = (pk[3][wi] & keep) | (f3 << sh);
         }
     }
     const size_t row_words = npad / F::kPer;
@@ -488,21 +554,41 @@ __device__ __forceinline__ void seg_pass(const uint32_t (&v)[FmFmt<FMB>::kWords]
     }
 }
 
+template <int FMB>
+__device__ __forceinline__ uint32_t set_at(const uint32_t (&v)[FmFmt<FMB>::kWords], int k) {
+    using F = FmFmt<FMB>;
+    return (v[k / F::kPer] >> (FMB * (k % F::kPer))) & F::kAll;
+}
+
+// Per-(row, 32-column segment) RLE entry states, written by the count pass
+// and read by the emit pass so that it needs no speculation of its own
+// (4-bit sets: the state (head, S) packs into head << 4 | S):
+//   st[row * nseg + seg] = state of the greedy scan entering the segment,
+//   rc[row * nseg + seg] = runs that end inside the segment (<= 32).
+// st == nullptr: not kept (wider sets); the emit pass then speculates too.
+struct RleState {
+    uint32_t* st;
+    uint8_t* rc;
+};
+
 // Greedy RLE, one row per wave, 2048-column tiles (lane l owns columns
 // 32l..32l+31 of the tile).  The scan is sequential by definition, so each
-// lane first speculates a fresh run at its segment start, then re-runs from
-// its predecessor's end state until no lane's input changes: with typical
-// run lengths every lane resynchronises inside its own segment and two passes
-// suffice; the loop is exact for any input (at most 64 rounds).
-// COUNT: counts[row] = runs in the row.  EMIT: runs written at off[row],
-// staged per tile in LDS and stored coalesced.
+// lane guesses the state entering its segment — the predecessor lane's last
+// 16 columns scanned from a fresh run: the greedy state forgets its past
+// within a few runs, so the guess is usually exact — runs its segment from
+// the guess, then re-runs from its predecessor's end state until no lane's
+// input changes (exact for any input: at most 64 rounds).  The count needs
+// the entry set only; the head matters once the states are kept or emitted.
+// COUNT: counts[row] = runs in the row (+ entry states if rs.st).  EMIT: runs
+// written at off[row], staged per tile in LDS and stored coalesced.
 template <bool EMIT, int FMB>
 __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm, uint32_t npad,
                                                 uint32_t nrows, uint32_t* __restrict__ counts,
                                                 const uint64_t* __restrict__ off,
-                                                uint32_t* __restrict__ runs) {
+                                                uint32_t* __restrict__ runs, RleState rs) {
     using F = FmFmt<FMB>;
     constexpr int Q = F::kWords / 4;  // 16-B loads per lane per tile
+    constexpr int LB = 16;            // lookback columns
     __shared__ uint32_t stage_all[EMIT ? 4 * kTile : 1];
     const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -511,12 +597,22 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
     const uint4* __restrict__ src =
         reinterpret_cast<const uint4*>(fm + (size_t)row * (npad / F::kPer)) + lane * Q;
     uint32_t* __restrict__ out = EMIT ? runs + off[row] : nullptr;
+    const bool keep = rs.st != nullptr;           // states kept (FMB == 4)
+    const bool use_states = EMIT && keep;         // emit from the kept states
+    const bool track_h = EMIT || keep;
+    const uint32_t nseg = npad / kSeg;
     uint32_t carry_h = 0, carry_S = F::kAll, total = 0;
     const uint32_t ntiles = npad / kTile;
-    // tile t's segment of this lane, prefetched one tile ahead
+    // tile t's segment of this lane (and its kept state), prefetched one tile ahead
     uint4 nx[Q];
+    uint32_t nst = 0, nrc = 0;
+    const size_t sbase = (size_t)row * nseg + lane;
 #pragma unroll
     for (int q = 0; q < Q; ++q) nx[q] = src[q];
+    if (use_states) {
+        nst = rs.st[sbase];
+        nrc = rs.rc[sbase];
+    }
     for (uint32_t t = 0; t < ntiles; ++t) {
         uint32_t v[F::kWords];
 #pragma unroll
@@ -526,30 +622,60 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
             v[4 * q + 2] = nx[q].z;
             v[4 * q + 3] = nx[q].w;
         }
+        const uint32_t cst = nst, crc = nrc;
         if (t + 1 < ntiles) {
 #pragma unroll
             for (int q = 0; q < Q; ++q) nx[q] = src[(size_t)(t + 1) * (64u * Q) + q];
+            if (use_states) {
+                nst = rs.st[sbase + (size_t)(t + 1) * 64u];
+                nrc = rs.rc[sbase + (size_t)(t + 1) * 64u];
+            }
         }
         const uint32_t c0 = t * kTile + lane * kSeg;
-        // speculative pass: a run starts at the segment (lane 0: true carry)
-        uint32_t in_h = lane == 0 ? carry_h : c0, in_S = lane == 0 ? carry_S : F::kAll;
-        uint32_t eh = in_h, eS = in_S, cnt = 0;
-        seg_pass<false, FMB>(v, c0, eh, eS, cnt, nullptr);
-        for (int round = 0; round < 64; ++round) {
-            uint32_t nh = __shfl_up(eh, 1, 64), nS = __shfl_up(eS, 1, 64);
-            if (lane == 0) {
-                nh = carry_h;
-                nS = carry_S;
+        uint32_t in_h, in_S, eh, eS, cnt;
+        if (use_states) {
+            in_h = cst >> 4;
+            in_S = cst & 0xFu;
+            cnt = crc;
+        } else {
+            // guess: the predecessor's last LB columns from a fresh run
+            uint32_t pv[F::kWords / 2];
+#pragma unroll
+            for (int i = 0; i < F::kWords / 2; ++i) pv[i] = __shfl_up(v[F::kWords / 2 + i], 1, 64);
+            uint32_t gh = c0 - LB, gS = F::kAll;
+#pragma unroll
+            for (int k = 0; k < LB; ++k) {
+                const uint32_t f = (pv[k / F::kPer] >> (FMB * (k % F::kPer))) & F::kAll;
+                const bool brk = (gS & f) == 0u;
+                gh = brk ? c0 - LB + (uint32_t)k : gh;
+                gS = brk ? f : (gS & f);
             }
-            const bool need = nh != in_h || nS != in_S;
-            if (!__any(need)) break;
-            if (need) {
-                in_h = nh;
-                in_S = nS;
-                eh = nh;
-                eS = nS;
-                cnt = 0;
-                seg_pass<false, FMB>(v, c0, eh, eS, cnt, nullptr);
+            in_h = lane == 0 ? carry_h : gh;
+            in_S = lane == 0 ? carry_S : gS;
+            eh = in_h;
+            eS = in_S;
+            cnt = 0;
+            seg_pass<false, FMB>(v, c0, eh, eS, cnt, nullptr);
+            for (int round = 0; round < 64; ++round) {
+                uint32_t nh = __shfl_up(eh, 1, 64), nS = __shfl_up(eS, 1, 64);
+                if (lane == 0) {
+                    nh = carry_h;
+                    nS = carry_S;
+                }
+                const bool need = nS != in_S || (track_h && nh != in_h);
+                if (!__any(need)) break;
+                if (need) {
+                    in_h = nh;
+                    in_S = nS;
+                    eh = nh;
+                    eS = nS;
+                    cnt = 0;
+                    seg_pass<false, FMB>(v, c0, eh, eS, cnt, nullptr);
+                }
+            }
+            if (!EMIT && keep) {  // coalesced: 64 lanes x 4 B + 64 x 1 B per tile
+                rs.st[sbase + (size_t)t * 64u] = (in_h << 4) | in_S;
+                rs.rc[sbase + (size_t)t * 64u] = (uint8_t)cnt;
             }
         }
         // inclusive scan of per-lane run counts
@@ -563,6 +689,8 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
         if (EMIT) {
             uint32_t h = in_h, S = in_S, k = 0;
             seg_pass<true, FMB>(v, c0, h, S, k, stage + (incl - cnt));
+            eh = h;
+            eS = S;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -790,14 +918,39 @@ uint32_t xcd_remap() {
     return on;
 }
 
+// Tuning knobs for A/B runs: waves per workgroup of the down-sweep and of
+// first_moves (CPD_DOWN_WPB, CPD_FM_WPB: 1, 2 or 4; a workgroup covers
+// 256 x wpb targets), columns per gather group of first_moves (CPD_FM_G).
+// Defaults = the fastest measured on the 1M-node bench (MI355X, 16k rows):
+// down 4 waves (1: +5 %, 2: +8 %), first_moves 2 waves (4: +11 %), G = 2
+// (1: +4 %, 4: +14 %).
+uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* e = std::getenv(name);
+    return (e && *e) ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
+}
+uint32_t down_wpb() {
+    static const uint32_t v = env_u32("CPD_DOWN_WPB", 4);
+    return v;
+}
+uint32_t fm_wpb() {
+    static const uint32_t v = env_u32("CPD_FM_WPB", 2);
+    return v;
+}
+uint32_t fm_g() {
+    static const uint32_t v = env_u32("CPD_FM_G", 2);
+    return v;
+}
+
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* arcs32, uint32_t slot0, uint32_t count, uint32_t* dist,
                   const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
                   const uint32_t* asc_off, const uint32_t* asc_arcs, uint32_t* live,
-                  const uint32_t* tmask, hipStream_t s) {
+                  const uint32_t* tmask, const uint32_t* adj, uint32_t shift, uint16_t* fmleaf,
+                  hipStream_t s) {
     const uint4* t4 = reinterpret_cast<const uint4*>(tgt);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
     const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
+    const kern::LeafFm lf{reinterpret_cast<const uint2*>(adj), shift, ascend ? nullptr : fmleaf};
     if (ascend && live) {
         // one block per node on wide levels; narrow levels split the slabs
         const uint32_t nsplit = std::max(1u, std::min(slabs, 2048u / std::max(count, 1u)));
@@ -806,10 +959,12 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                slot0, count, nsplit, xcd_remap(), dist, t4, B / 4u, cf, live, tmask, active);
     } else if (ascend) {
         launch(kern::sweep_level<true>, dim3(count * slabs), dim3(256), s, nodes, arc_off, arcs,
-               slot0, count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)nullptr);
+               slot0, count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)nullptr, lf);
     } else {
-        launch(kern::sweep_level<false>, dim3(count * slabs), dim3(256), s, nodes, arc_off, arcs,
-               slot0, count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live);
+        const uint32_t tpb = 64u * down_wpb();  // a workgroup covers 4 * tpb targets
+        launch(kern::sweep_level<false>, dim3(count * slabs * (256u / tpb)), dim3(tpb), s, nodes,
+               arc_off, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf,
+               (const uint32_t*)live, lf);
     }
 }
 
@@ -860,38 +1015,51 @@ uint32_t fm_bits(uint32_t shift) { return shift <= 2 ? 4u : (1u << shift); }
 
 void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* dist,
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
-                        uint32_t npad, uint32_t* fm, hipStream_t s) {
-    dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u));
+                        uint32_t npad, uint32_t* fm, const uint32_t* leafbits,
+                        const uint16_t* fmleaf, hipStream_t s) {
+    const uint32_t tpb = 64u * fm_wpb();  // a workgroup covers 4 * tpb targets
+    dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u) * (256u / tpb));
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     const uint32_t r = xcd_remap();
+    const dim3 blk(tpb);
     switch (shift) {  // SLOTS = 2^shift edges per column; G columns per gather group
-        case 0: launch(kern::first_moves<1, 4>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
-        case 1: launch(kern::first_moves<2, 2>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
-        case 2: launch(kern::first_moves<4, 2>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
-        case 3: launch(kern::first_moves<8, 1>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
-        default: launch(kern::first_moves<16, 1>, grid, dim3(256), s, adj, dist, tgt, B, n, npad, r, fm); break;
+        case 0: launch(kern::first_moves<1, 4>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf); break;
+        case 1: launch(kern::first_moves<2, 2>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf); break;
+        case 2:
+            if (fm_g() == 4)
+                launch(kern::first_moves<4, 4>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf);
+            else if (fm_g() == 1)
+                launch(kern::first_moves<4, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf);
+            else
+                launch(kern::first_moves<4, 2>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf);
+            break;
+        case 3: launch(kern::first_moves<8, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf); break;
+        default: launch(kern::first_moves<16, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf); break;
     }
 }
 
 template <bool EMIT>
 static void launch_rle(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                       uint32_t* counts, const uint64_t* off, uint32_t* runs, hipStream_t s) {
+                       uint32_t* counts, const uint64_t* off, uint32_t* runs, uint32_t* st,
+                       uint8_t* rc, hipStream_t s) {
     const dim3 grid((nrows + 3u) / 4u), block(256);
+    const kern::RleState rs{fmb == 4 ? st : nullptr, fmb == 4 ? rc : nullptr};
     switch (fmb) {
-        case 4: launch(kern::rle_scan<EMIT, 4>, grid, block, s, fm, npad, nrows, counts, off, runs); break;
-        case 8: launch(kern::rle_scan<EMIT, 8>, grid, block, s, fm, npad, nrows, counts, off, runs); break;
-        default: launch(kern::rle_scan<EMIT, 16>, grid, block, s, fm, npad, nrows, counts, off, runs); break;
+        case 4: launch(kern::rle_scan<EMIT, 4>, grid, block, s, fm, npad, nrows, counts, off, runs, rs); break;
+        case 8: launch(kern::rle_scan<EMIT, 8>, grid, block, s, fm, npad, nrows, counts, off, runs, rs); break;
+        default: launch(kern::rle_scan<EMIT, 16>, grid, block, s, fm, npad, nrows, counts, off, runs, rs); break;
     }
 }
 
 void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                      uint32_t* counts, hipStream_t s) {
-    launch_rle<false>(fm, fmb, npad, nrows, counts, nullptr, nullptr, s);
+                      uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s) {
+    launch_rle<false>(fm, fmb, npad, nrows, counts, nullptr, nullptr, st, rc, s);
 }
 
 void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                     const uint64_t* off, uint32_t* runs, hipStream_t s) {
-    launch_rle<true>(fm, fmb, npad, nrows, nullptr, off, runs, s);
+                     const uint64_t* off, uint32_t* runs, uint32_t* st, uint8_t* rc,
+                     hipStream_t s) {
+    launch_rle<true>(fm, fmb, npad, nrows, nullptr, off, runs, st, rc, s);
 }
 
 void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,

@@ -19,11 +19,14 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop);
 // only those (sweep_up_sparse), the down-sweep's own-row reads skip the rest.
 // tmask (n u32): bit b of tmask[col] = col is a target of slab b
 // (launch_target_mask); B <= 32768 so that a mask fits in 32 bits.
+// fmleaf (may be null; down-sweep, 4-bit sets, shift <= 2): leaf slots take
+// their out-edges from adj and also store their first-move sets there.
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* arcs /* (col, w) pairs */, uint32_t slot0, uint32_t count,
                   uint32_t* dist, const uint32_t* tgt, uint32_t B, uint32_t slabs,
                   const uint32_t* asc_nodes, const uint32_t* asc_off, const uint32_t* asc_arcs,
-                  uint32_t* live, const uint32_t* tmask, hipStream_t s);
+                  uint32_t* live, const uint32_t* tmask, const uint32_t* adj, uint32_t shift,
+                  uint16_t* fmleaf, hipStream_t s);
 
 // Narrow upward levels, chunked: items (slot, first arc, end arc, 0) of at
 // most sweep_chunk_arcs() arcs each, nitems x slabs workgroups, partial
@@ -58,19 +61,28 @@ uint32_t fm_bits(uint32_t shift);
 
 // adj: the packed fixed-stride adjacency (free-flow weights), 2^shift slots;
 // fm: [rows][npad] sets of fm_bits(shift) bits, npad * bits / 32 words per row.
+// leafbits (npad/32 words, bit = column is a CH leaf) + fmleaf ([col][B/4]
+// u16, 4 nibbles per lane, written by the down-sweep): leaf columns copy their
+// sets instead of recomputing them; both null = every column computed.  Only
+// for 4-bit sets (shift <= 2).
 void launch_first_moves(const uint32_t* adj, uint32_t shift, const uint32_t* dist,
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
-                        uint32_t npad, uint32_t* fm, hipStream_t s);
+                        uint32_t npad, uint32_t* fm, const uint32_t* leafbits,
+                        const uint16_t* fmleaf, hipStream_t s);
 
 // Row width of the tiled first-move rows: npad is a multiple of this.
 constexpr uint32_t kFmTile = 2048;
 
 // Greedy RLE scan, one wave per row: runs per row, then the runs themselves
 // written at off[row] (uint64 offsets into `runs`).  fmb = fm_bits(shift).
+// st / rc ([nrows][npad/32] u32 / u8, used when fmb == 4): the count pass
+// stores each segment's entry state and run count there, the emit pass reads
+// them instead of speculating again.
 void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                      uint32_t* counts, hipStream_t s);
+                      uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s);
 void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                     const uint64_t* off, uint32_t* runs, hipStream_t s);
+                     const uint64_t* off, uint32_t* runs, uint32_t* st, uint8_t* rc,
+                     hipStream_t s);
 
 // RLE rows -> dense 4-bit move tables, npad/8 words per row.
 void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,

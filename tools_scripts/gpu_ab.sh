@@ -12,11 +12,11 @@ tail -3 $O/gpu_tests_$TAG.log
 B="python3 -u $R/bench.py --no-pmc --no-cpu --steps 5"
 CPD_TRACE=1 timeout -k 10 300 $B > $O/bench_${TAG}_all.json 2> $O/bench_${TAG}_all.err
 echo all-done
-for v in LIVE XCD SORT; do
+for v in LIVE XCD SORT LEAFFM; do
   env CPD_$v=0 timeout -k 10 300 $B > $O/bench_${TAG}_no$v.json 2> $O/bench_${TAG}_no$v.err
   echo no$v-done
 done
-for f in all noLIVE noXCD noSORT; do
+for f in all noLIVE noXCD noSORT noLEAFFM; do
   python3 - $O/bench_${TAG}_$f.json $f <<'EOF'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
