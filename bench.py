@@ -44,7 +44,8 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=16384, help="rows per step (multiple of 1024)")
     ap.add_argument("--queries", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
-    ap.add_argument("--cpu-rows-per-thread", type=int, default=8)
+    ap.add_argument("--cpu-rows-per-thread", type=int, default=64,
+                    help="CPU baseline sample: rows per host thread (~10 s of CPU work)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--no-pmc", action="store_true",
@@ -336,6 +337,12 @@ def main():
     q_rle, q_rle_ms = time_queries("rle")
     q_totals, q_ms_max = time_queries("auto")
     index_mode = ix.mode
+    # congested leg (configs[2]): the .diff stand-in of SURVEY.md §8d — 10% of
+    # edges x U[1, 3], rounded up — sent with the batch as fifo_auto does
+    w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
+    ix.set_weights(w_cong)
+    q_cong, q_cong_ms = time_queries("auto")
+    ix.set_weights(None)
 
     # ---- CPU baseline + full-size parity sample (rank 0, N = 1) -------------
     cpu = None
@@ -362,6 +369,11 @@ def main():
         gix = cpd.Index(dev, rows=grows)
         gc, gh, gf, _ = gix.query(cs, ct)
         parity = parity and bool(np.array_equal(gc, rc) and np.array_equal(gh, rh))
+        rcc, rch, _ = oracle.table_search(g.row_ptr, g.dst, w_cong, order, sample, ref_off,
+                                          ref_runs, cs, ct, threads=threads)
+        gix.set_weights(w_cong)
+        gcc, gch, _, _ = gix.query(cs, ct)
+        parity = parity and bool(np.array_equal(gcc, rcc) and np.array_equal(gch, rch))
         cpu = {"value": round(len(sample) / cpu_s, 3), "unit": "sources/s", "cores": threads,
                "kind": "port",
                "sample": f"{len(sample)} CPD rows of the same graph and partition (reverse Dijkstra "
@@ -374,6 +386,8 @@ def main():
                        kt, cpu, parity, pinfo, traffic)
         out["query_index"] = index_mode
         out["queries_per_s_rle"] = round(q_rle[0] / (q_rle_ms / 1e3), 1) if q_rle_ms else 0.0
+        out["queries_per_s_congested"] = (round(q_cong[0] / (q_cong_ms / 1e3), 1)
+                                          if q_cong_ms else 0.0)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -6,9 +6,13 @@ import glob
 import json
 import sys
 
-NAMES = {"sweep_level<true>": "sweep_up", "sweep_level<false>": "sweep_down",
-         "first_moves": "first_moves", "rle_scan<false>": "rle_count",
-         "rle_scan<true>": "rle_emit", "table_search": "table_search"}
+# most specific first: rocprof names carry template arguments
+NAMES = [("sweep_up_sparse", "sweep_up"), ("sweep_up_chunks", "sweep_up"),
+         ("sweep_up_init", "sweep_up_init"), ("sweep_level<true>", "sweep_up"),
+         ("sweep_level<false>", "sweep_down"), ("first_moves", "first_moves"),
+         ("rle_scan<false", "rle_count"), ("rle_scan<true", "rle_emit"),
+         ("table_search_dense", "table_search_dense"), ("table_search", "table_search"),
+         ("expand_rows", "expand_rows"), ("live_stats", "live_stats")]
 
 
 def main(prof_dir, bench_json, out_md):
@@ -17,7 +21,7 @@ def main(prof_dir, bench_json, out_md):
     lines = ["| kernel | rocprof calls | rocprof avg µs | rocprof total ms | bench launches | bench avg µs |",
              "|---|---|---|---|---|---|"]
     for r in csv.DictReader(open(stats)):
-        short = next((v for k, v in NAMES.items() if k in r["Name"]), r["Name"][:40])
+        short = next((v for k, v in NAMES if k in r["Name"]), r["Name"][:40])
         b = bench.get("kernels", {}).get(short)
         bavg = f"{b['ms'] * 1e3 / b['launches']:.1f}" if b else "-"
         bl = b["launches"] if b else "-"

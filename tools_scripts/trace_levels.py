@@ -39,7 +39,7 @@ def main(d):
         for i in sorted(per):
             us = sum(x[0] for x in per[i]) / len(per[i])
             cum += us / 1e3
-            if i < 25 or i % 10 == 0 or i == len(per) - 1:
+            if i < 25 or i % 10 == 0 or i == len(per) - 1 or us > 300:
                 print(f"  {i:4d} {us:9.1f} {per[i][0][1]:10d}  {cum:8.2f}")
         print(f"  batches seen: {nb}")
 
