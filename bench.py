@@ -56,9 +56,10 @@ def parse(argv=None):
 
 
 # rocprofv3 kernel names -> the library's timing names
-KERNEL_NAMES = {"sweep_level<true>": "sweep_up", "sweep_level<false>": "sweep_down",
-                "first_moves": "first_moves", "rle_scan<false>": "rle_count",
-                "rle_scan<true>": "rle_emit", "table_search": "table_search"}
+KERNEL_NAMES = {"sweep_level<true": "sweep_up", "sweep_up_": "sweep_up",
+                "sweep_level<false": "sweep_down", "sweep_down8": "sweep_down",
+                "first_moves": "first_moves", "rle_scan<false": "rle_count",
+                "rle_scan<true": "rle_emit", "table_search": "table_search"}
 
 
 def pmc_traffic(args, plan_path):

@@ -123,6 +123,17 @@ struct cpd_graph {
     bool leaf_fm = false;
     DevBuf<uint32_t> leafbits;
     DevBuf<uint16_t> fmleaf;
+    // narrow final-distance rows (NarrowRows, cpd_kernels.hpp): on unless
+    // CPD_NARROW=0 at graph creation or a finite distance could reach the
+    // wide-row marker; group rows that do not fit are kept wide (counted)
+    bool narrow = false;
+    uint32_t ovf_h = 0;
+    DevBuf<uint16_t> d16;
+    DevBuf<uint32_t> dbase, ovf;
+    NarrowRows narrow_rows(bool on) {
+        if (!on) return NarrowRows{nullptr, nullptr, n, nullptr};
+        return NarrowRows{d16.p, dbase.p, n, ovf.p};
+    }
     double n_leaf = 0, m_leaf = 0;    // leaves, their out-edges
     std::vector<double> dsc_lvl_leaves;
     DevBuf<uint64_t> row_off;
@@ -238,8 +249,8 @@ struct cpd_graph {
         if (want == 0) {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-            // per target: dist 4n + fm + output runs (<= 4n, ~2.5n typical)
-            double per = 4.0 * n + fmb / 8.0 * npad + 4.0 * n;
+            // per target: dist 4n (+ 2n narrow) + fm + output runs (<= 4n, ~2.5n typical)
+            double per = (narrow ? 6.0 : 4.0) * n + fmb / 8.0 * npad + 4.0 * n;
             double fit = 0.4 * (double)free_b / per;
             want = (uint32_t)std::min(16384.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
         }
@@ -255,6 +266,11 @@ struct cpd_graph {
         live.alloc(n);
         tmask.alloc(n);
         if (leaf_fm) fmleaf.alloc((size_t)n * (B / 4u));
+        if (narrow) {
+            d16.alloc((size_t)n * B);
+            dbase.alloc((size_t)n * (B / 256u));
+            ovf.alloc(1);
+        }
         tgt.alloc(B);
         counts.alloc(B);
     }
@@ -480,6 +496,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->ch_arcs += arcs.size() / 2;
         // leaf first moves in the down-sweep: 4-bit sets only (<= 4 slots)
         g->leaf_fm = g->fmb == 4 && env_on("CPD_LEAFFM");
+        g->narrow = env_on("CPD_NARROW") && p->dist_bound < 0xFFFFFFFEull;
         {
             std::vector<uint32_t> lb(g->npad / 32u, 0u);
             g->dsc_lvl_leaves.assign(g->dsc_lvl.size(), 0.0);
@@ -567,8 +584,13 @@ bool sort_on() {
 
 // Distances + first-move sets for `k` targets (columns already in g->tgt,
 // padded to a multiple of 1024 with valid columns).
-void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
+void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow) {
     const uint32_t B = g->B, n = g->n;
+    const NarrowRows nr = g->narrow_rows(narrow);
+    if (narrow) HIP_CHECK(hipMemsetAsync(g->ovf.p, 0, sizeof(uint32_t), g->stream));
+    // bytes per target of a final-distance row access: 4 wide; 2 + a 4-B base
+    // per 256 targets narrow
+    const double drow = narrow ? 2.0 + 4.0 / 256.0 : 4.0;
     const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
     const uint32_t active = slabs * 1024u;
     uint32_t* live = live_on() ? g->live.p : nullptr;
@@ -614,7 +636,7 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
                 launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt,
                              g->dist.p, g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p,
                              g->asc_arcs.p, live, g->tmask.p, g->adj.p, g->adj_shift, nullptr,
-                             g->stream);
+                             g->narrow_rows(false), g->stream);
         }, std::move(late));
     }
     g->group_end();
@@ -623,7 +645,7 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
         uint32_t s0 = g->dsc_lvl[l], cnt = g->dsc_lvl[l + 1] - s0;
         if (!cnt) continue;
         const size_t si = 2 * (nasc + l);
-        double base = (4.0 * g->dsc_lvl_arcs[l] + 4.0 * cnt) * active +
+        double base = (drow * g->dsc_lvl_arcs[l] + drow * cnt) * active +
                       8.0 * g->dsc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
         if (g->leaf_fm) base += 0.5 * g->dsc_lvl_leaves[l] * active;  // leaf sets
         double dense = base + 4.0 * g->dsc_lvl_reads[l] * active;
@@ -636,10 +658,13 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
                          g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
                          g->tmask.p, g->adj.p, g->adj_shift, g->leaf_fm ? g->fmleaf.p : nullptr,
-                         g->stream);
+                         nr, g->stream);
         }, std::move(late));
     }
     g->group_end();
+    if (narrow && g->timing)
+        launch_count_wide_rows(g->dbase.p, (size_t)n * (B / 256u),
+                               reinterpret_cast<unsigned int*>(g->ovf.p), g->stream);
     if (live && stat && nasc > 2) {  // row counts behind the late byte counts
         g->timed("live_stats", 0.0, [&] {
             launch_live_stats(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
@@ -657,13 +682,13 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k) {
     const uint32_t fslabs = (k + 1023u) / 1024u;
     const double nl = g->leaf_fm ? g->n_leaf : 0.0, ml = g->leaf_fm ? g->m_leaf : 0.0;
     double fbytes =
-        (4.0 * (n - nl) + 4.0 * (g->m - ml) + 0.5 * nl + g->fmb / 8.0 * g->npad) *
+        (drow * (n - nl) + drow * (g->m - ml) + 0.5 * nl + g->fmb / 8.0 * g->npad) *
             (fslabs * 1024.0) +
         8.0 * (double)(n - nl) * (double)(1u << g->adj_shift) * fslabs + 4.0 * g->npad / 32.0;
     g->timed("first_moves", fbytes, [&] {
         launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, g->tgt.p, B, k, n, g->npad,
                            g->fm.p, g->leaf_fm ? g->leafbits.p : nullptr,
-                           g->leaf_fm ? g->fmleaf.p : nullptr, g->stream);
+                           g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream);
     });
     if (stat)
         HIP_CHECK(hipMemcpyAsync(g->stat_h.data(), stat, g->stat.n * sizeof(unsigned int),
@@ -711,12 +736,12 @@ bool trace_on() {
 void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r) {
     const double t0 = now_seconds();
     upload_targets(g, targets, k);
-    run_sweeps_and_fm(g, k);
-    const double t1 = now_seconds();
     const uint32_t npad = g->npad;
     const double fm_row = g->fmb / 8.0 * npad;  // first-move bytes per row
     // + per 32-column segment a 4-B entry state and a 1-B count (fmb == 4)
     const double st_row = g->fmb == 4 ? 5.0 * npad / 32.0 : 0.0;
+    run_sweeps_and_fm(g, k, g->narrow);
+    const double t1 = now_seconds();
     g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
         launch_rle_count(g->fm.p, g->fmb, npad, k, g->counts.p, g->rle_st.p, g->rle_rc.p,
                          g->stream);
@@ -724,7 +749,14 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     std::vector<uint32_t> counts(k);
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, g->stream));
+    if (g->narrow && g->timing)
+        HIP_CHECK(hipMemcpyAsync(&g->ovf_h, g->ovf.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                 g->stream));
     g->sync();
+    if (g->narrow && g->timing) {  // group rows kept wide / all group rows
+        g->agg["wide_rows"].launches += g->ovf_h;
+        g->agg["group_rows"].launches += (uint64_t)g->n * (g->B / 256u);
+    }
     const double t2 = now_seconds();
     // row offsets for this batch in the caller's order, appended after
     // r->total; counts[] and the emit kernel's offsets are per lane
@@ -831,13 +863,29 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
         if (!g->B) g->reserve_batch(0);
         CPD_REQUIRE(ntargets > 0 && ntargets <= g->B, CPD_E_ARG, "debug: 0 < ntargets <= batch");
         upload_targets(g, targets, ntargets);
-        run_sweeps_and_fm(g, ntargets);
+        const bool narrow = g->narrow;
+        run_sweeps_and_fm(g, ntargets, narrow);
         g->sync();
         const uint32_t n = g->n, B = g->B;
         // lane p holds the caller's target i = pos_of^-1(p)
         std::vector<uint32_t> h((size_t)n * B);
         HIP_CHECK(hipMemcpy(h.data(), g->dist.p, h.size() * sizeof(uint32_t),
                             hipMemcpyDeviceToHost));
+        if (narrow) {  // base + u16 offset (0xFFFF = unreachable), or a wide row
+            std::vector<uint16_t> q((size_t)n * B);
+            std::vector<uint32_t> b((size_t)n * (B / 256u));
+            HIP_CHECK(hipMemcpy(q.data(), g->d16.p, q.size() * sizeof(uint16_t),
+                                hipMemcpyDeviceToHost));
+            HIP_CHECK(hipMemcpy(b.data(), g->dbase.p, b.size() * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost));
+            for (uint32_t c = 0; c < n; ++c)
+                for (uint32_t p = 0; p < B; ++p) {
+                    const uint32_t base = b[(size_t)(p / 256u) * n + c];
+                    if (base == 0xFFFFFFFEu) continue;  // kept wide
+                    const uint16_t d = q[(size_t)c * B + p];
+                    h[(size_t)c * B + p] = d == 0xFFFFu ? CPD_INF : base + d;
+                }
+        }
         if (dist)
             for (uint32_t v = 0; v < n; ++v)
                 for (uint32_t i = 0; i < ntargets; ++i)

@@ -119,6 +119,52 @@ __device__ __forceinline__ uint4 arc_val(const uint4* __restrict__ d4, const uin
     return d4[(size_t)e.x * B4 + l4];
 }
 
+// Narrow final-distance rows (NarrowRows in cpd_kernels.hpp): a wave's 256
+// targets (group g = l4 / 64, wave-uniform) share one u32 base per column and
+// hold u16 offsets from it, 0xFFFF = unreachable.  A lane's 4 targets are one
+// 8-B access (512 B per wave instruction), half the wide row's bytes.  A group
+// row whose finite spread does not fit is stored wide instead, in `dist`, and
+// its base says so (kWideRow): readers branch on the (wave-uniform) base.
+constexpr uint32_t kNarrowInf = 0xFFFFu;
+constexpr uint32_t kWideRow = 0xFFFFFFFEu;  // > every finite distance (cpd_graph_create)
+
+__device__ __forceinline__ uint32_t wave_group(uint32_t l4) {
+    return __builtin_amdgcn_readfirstlane(l4 >> 6);
+}
+
+__device__ __forceinline__ uint32_t dec16(uint32_t b, uint32_t q) {
+    return q == kNarrowInf ? INF : b + q;
+}
+
+// A narrow row read in two halves, so that a kernel issues all of its
+// gathers' base and offset loads before it waits for any (nl_issue), then
+// decodes them (nl_finish): only the rare wide rows cost a second round trip.
+struct NLoad {
+    uint32_t b;
+    uint2 q;
+};
+
+__device__ __forceinline__ NLoad nl_issue(const NarrowRows& nr, uint32_t col, uint32_t grp,
+                                          uint32_t B4, uint32_t l4) {
+    return NLoad{nr.base[(size_t)grp * nr.n + col],
+                 reinterpret_cast<const uint2*>(nr.d16)[(size_t)col * B4 + l4]};
+}
+
+__device__ __forceinline__ uint4 nl_finish(const NLoad& p, const uint4* __restrict__ d4,
+                                           uint32_t col, uint32_t B4, uint32_t l4) {
+    uint4 r = make_uint4(dec16(p.b, p.q.x & 0xFFFFu), dec16(p.b, p.q.x >> 16),
+                         dec16(p.b, p.q.y & 0xFFFFu), dec16(p.b, p.q.y >> 16));
+    if (p.b == kWideRow) r = d4[(size_t)col * B4 + l4];  // wave-uniform, rare
+    return r;
+}
+
+__device__ __forceinline__ uint32_t enc16(uint32_t d, uint32_t b, bool& bad) {
+    if (d == INF) return kNarrowInf;
+    const uint32_t q = d - b;
+    bad |= q >= kNarrowInf;
+    return q;
+}
+
 // One CH sweep level, dense.  Logical block = (slot in the level, 1024-target
 // slab), slots fastest, XCD-remapped (remap != 0): node v = nodes[slot]; its
 // arcs (col, w) are wave-uniform (scalar loads); each lane owns 4 consecutive
@@ -157,6 +203,7 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
     const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t vraw = nodes[slot];
     uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+
     const uint4 t = tgt4[l4];
     uint32_t v;
     uint4 acc;
@@ -225,6 +272,189 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
         min4(acc, arc_val(d4, t, e, B4, l4, cf, true), e.y);
     }
     d4[(size_t)v * B4 + l4] = acc;
+}
+
+// Down-sweep into narrow rows, 8 targets per lane.  The narrow rows halve the
+// bytes per target, so a lane takes twice the targets of sweep_level to keep
+// 16 B per lane per access (1 KiB per wave instruction): the same number of
+// memory instructions moves the whole row in half the bytes.  Lanes 0-31 and
+// 32-63 of a wave are two 256-target groups (base per group).  Logical block =
+// (slot, 8 x blockDim targets), slots fastest, XCD-remapped; otherwise the
+// same computation as sweep_level<false> (own init, closed forms, leaf first
+// moves with lf.out).
+struct U8 {
+    uint4 a, b;
+};
+
+__device__ __forceinline__ U8 inf8() {
+    return U8{make_uint4(INF, INF, INF, INF), make_uint4(INF, INF, INF, INF)};
+}
+
+__device__ __forceinline__ void min8(U8& acc, const U8& d, uint32_t w) {
+    min4(acc.a, d.a, w);
+    min4(acc.b, d.b, w);
+}
+
+struct NLoad8 {
+    uint32_t b;
+    uint4 q;
+};
+
+__device__ __forceinline__ NLoad8 nl8_issue(const NarrowRows& nr, uint32_t col, uint32_t grp,
+                                            uint32_t B8, uint32_t l8) {
+    return NLoad8{nr.base[(size_t)grp * nr.n + col],
+                  reinterpret_cast<const uint4*>(nr.d16)[(size_t)col * B8 + l8]};
+}
+
+__device__ __forceinline__ U8 nl8_finish(const NLoad8& p, const uint4* __restrict__ d4,
+                                         uint32_t col, uint32_t B4, uint32_t l8) {
+    U8 r{make_uint4(dec16(p.b, p.q.x & 0xFFFFu), dec16(p.b, p.q.x >> 16),
+                    dec16(p.b, p.q.y & 0xFFFFu), dec16(p.b, p.q.y >> 16)),
+         make_uint4(dec16(p.b, p.q.z & 0xFFFFu), dec16(p.b, p.q.z >> 16),
+                    dec16(p.b, p.q.w & 0xFFFFu), dec16(p.b, p.q.w >> 16))};
+    if (p.b == kWideRow) {  // uniform per half-wave, rare
+        r.a = d4[(size_t)col * B4 + 2u * l8];
+        r.b = d4[(size_t)col * B4 + 2u * l8 + 1u];
+    }
+    return r;
+}
+
+__device__ __forceinline__ void narrow_store8(const NarrowRows& nr, uint4* __restrict__ d4,
+                                              uint32_t col, uint32_t grp, uint32_t B4,
+                                              uint32_t B8, uint32_t l8, const U8& acc) {
+    uint32_t b = min(min(min(acc.a.x, acc.a.y), min(acc.a.z, acc.a.w)),
+                     min(min(acc.b.x, acc.b.y), min(acc.b.z, acc.b.w)));
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) b = min(b, (uint32_t)__shfl_xor(b, o, 64));  // half-wave
+    bool bad = false;
+    const uint32_t q0 = enc16(acc.a.x, b, bad), q1 = enc16(acc.a.y, b, bad);
+    const uint32_t q2 = enc16(acc.a.z, b, bad), q3 = enc16(acc.a.w, b, bad);
+    const uint32_t q4 = enc16(acc.b.x, b, bad), q5 = enc16(acc.b.y, b, bad);
+    const uint32_t q6 = enc16(acc.b.z, b, bad), q7 = enc16(acc.b.w, b, bad);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t m = __ballot(bad);
+    const bool half_bad = ((lane < 32u ? m : (m >> 32)) & 0xFFFFFFFFull) != 0;
+    const bool head = (lane & 31u) == 0;
+    if (half_bad) {
+        d4[(size_t)col * B4 + 2u * l8] = acc.a;
+        d4[(size_t)col * B4 + 2u * l8 + 1u] = acc.b;
+        if (head) nr.base[(size_t)grp * nr.n + col] = kWideRow;
+        return;
+    }
+    reinterpret_cast<uint4*>(nr.d16)[(size_t)col * B8 + l8] =
+        make_uint4(q0 | (q1 << 16), q2 | (q3 << 16), q4 | (q5 << 16), q6 | (q7 << 16));
+    if (head) nr.base[(size_t)grp * nr.n + col] = b;
+}
+
+__device__ __forceinline__ void fm_nib(const uint4& dv, const uint4& acc, uint32_t w, int k,
+                                       uint32_t (&bits)[4]) {
+    bits[0] |= (sat_add(dv.x, w) == acc.x ? 1u : 0u) << k;
+    bits[1] |= (sat_add(dv.y, w) == acc.y ? 1u : 0u) << k;
+    bits[2] |= (sat_add(dv.z, w) == acc.z ? 1u : 0u) << k;
+    bits[3] |= (sat_add(dv.w, w) == acc.w ? 1u : 0u) << k;
+}
+
+__device__ __forceinline__ uint32_t fm_pack4(const uint4& t, const uint4& acc, uint32_t v,
+                                             const uint32_t (&bits)[4]) {
+    const uint32_t b0 = (t.x == v || acc.x == INF) ? 0xFu : bits[0];  // wildcard (target, unreachable)
+    const uint32_t b1 = (t.y == v || acc.y == INF) ? 0xFu : bits[1];
+    const uint32_t b2 = (t.z == v || acc.z == INF) ? 0xFu : bits[2];
+    const uint32_t b3 = (t.w == v || acc.w == INF) ? 0xFu : bits[3];
+    return b0 | (b1 << 4) | (b2 << 8) | (b3 << 12);
+}
+
+__global__ __launch_bounds__(256) void sweep_down8(const uint32_t* __restrict__ nodes,
+                                                   const uint32_t* __restrict__ arc_off,
+                                                   const uint2* __restrict__ arcs,
+                                                   uint32_t slot0, uint32_t count, uint32_t remap,
+                                                   uint32_t* __restrict__ dist,
+                                                   const uint4* __restrict__ tgt4, uint32_t B4,
+                                                   Closed cf, const uint32_t* __restrict__ live,
+                                                   LeafFm lf, NarrowRows nr) {
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t blk = L / count;
+    const uint32_t slot = slot0 + (L - blk * count);
+    const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
+    const uint32_t grp = l8 >> 5;                        // uniform per half-wave
+    const uint32_t B8 = B4 / 2u;
+    const uint32_t vraw = nodes[slot];
+    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    const U8 t{tgt4[2u * l8], tgt4[2u * l8 + 1u]};
+    uint32_t v;
+    U8 acc;
+    if (vraw & kLeafBit) {
+        v = vraw & kIdxMask;
+        acc = U8{leaf4(t.a, v, 0u), leaf4(t.b, v, 0u)};
+        if (lf.out) {
+            const uint32_t ns = 1u << lf.shift;
+            uint2 e[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                e[k] = (uint32_t)k < ns ? lf.adj[((size_t)v << lf.shift) + k]
+                                        : make_uint2(0xFFFFFFFFu, 0u);
+            NLoad8 pl[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (e[k].x != 0xFFFFFFFFu && e[k].x != v) pl[k] = nl8_issue(nr, e[k].x, grp, B8, l8);
+            U8 x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                x[k] = (e[k].x != 0xFFFFFFFFu && e[k].x != v) ? nl8_finish(pl[k], d4, e[k].x, B4, l8)
+                                                              : inf8();
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (e[k].x != 0xFFFFFFFFu && e[k].x != v) min8(acc, x[k], e[k].y);
+            uint32_t ba[4] = {0, 0, 0, 0}, bb[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (e[k].x == 0xFFFFFFFFu) continue;
+                const U8& dv = e[k].x == v ? acc : x[k];  // self loop: d(v) itself
+                fm_nib(dv.a, acc.a, e[k].y, k, ba);
+                fm_nib(dv.b, acc.b, e[k].y, k, bb);
+            }
+            const uint32_t sets = fm_pack4(t.a, acc.a, v, ba) | (fm_pack4(t.b, acc.b, v, bb) << 16);
+            narrow_store8(nr, d4, v, grp, B4, B8, l8, acc);
+            reinterpret_cast<uint32_t*>(lf.out)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
+            return;
+        }
+    } else if (vraw & kL1Bit) {
+        v = cf.nodes[vraw & kIdxMask];
+        acc = U8{l1_val(cf, vraw & kIdxMask, t.a), l1_val(cf, vraw & kIdxMask, t.b)};
+    } else {
+        v = vraw;
+        const bool own = !live || ((live[v] >> (l8 >> 7)) & 1u);  // live bits: 1024 targets
+        acc = own ? U8{d4[(size_t)v * B4 + 2u * l8], d4[(size_t)v * B4 + 2u * l8 + 1u]} : inf8();
+    }
+    const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
+    uint32_t a = a0;
+    for (; a + 8 <= a1; a += 8) {
+        uint2 e[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
+        NLoad8 pl[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pl[i] = nl8_issue(nr, e[i].x, grp, B8, l8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) min8(acc, nl8_finish(pl[i], d4, e[i].x, B4, l8), e[i].y);
+    }
+    for (; a < a1; ++a) {
+        const uint2 e = arcs[a];
+        min8(acc, nl8_finish(nl8_issue(nr, e.x, grp, B8, l8), d4, e.x, B4, l8), e.y);
+    }
+    narrow_store8(nr, d4, v, grp, B4, B8, l8, acc);
+}
+
+// Group rows stored wide (timing runs only): *out += #{base[i] == kWideRow}.
+__global__ __launch_bounds__(256) void count_wide_rows(const uint32_t* __restrict__ base,
+                                                       size_t total,
+                                                       unsigned int* __restrict__ out) {
+    uint32_t c = 0;
+    for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < total;
+         i += (size_t)gridDim.x * 256u)
+        c += base[i] == kWideRow ? 1u : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63u) == 0 && c) atomicAdd(out, c);
 }
 
 // Slab mask of an arc's source row (see "Up-sweep sparsity").
@@ -430,14 +660,15 @@ __device__ __forceinline__ uint32_t fm_final(uint32_t c, uint32_t tc, uint32_t d
 // with no dependent CSR lookups.
 constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
 
-template <int SLOTS, int G>
+template <int SLOTS, int G, bool NARROW>
 __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj,
                                                    const uint32_t* __restrict__ dist,
                                                    const uint32_t* __restrict__ tgt,
                                                    uint32_t B, uint32_t n, uint32_t npad,
                                                    uint32_t remap, uint32_t* __restrict__ fm,
                                                    const uint32_t* __restrict__ leafbits,
-                                                   const uint16_t* __restrict__ fmleaf) {
+                                                   const uint16_t* __restrict__ fmleaf,
+                                                   NarrowRows nr) {
     constexpr int FMB = SLOTS < 4 ? 4 : SLOTS;
     using F = FmFmt<FMB>;
     const uint32_t nseg = npad / kSeg;
@@ -448,6 +679,7 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
     const uint32_t c0 = (L - slab * nseg) * kSeg;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
+    const uint32_t grp = wave_group(l4);
     uint32_t pk[4][F::kWords];
 #pragma unroll
     for (int p = 0; p < F::kWords; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
@@ -459,6 +691,7 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
         uint4 dn[G];
         uint2 e[G][SLOTS];  // wave-uniform: scalar registers
         uint32_t b[G][4], lv[G];
+        NLoad pn[G];
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             const uint32_t c = c0 + (uint32_t)(cg + j);
@@ -467,10 +700,26 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
 #pragma unroll
             for (int k = 0; k < SLOTS; ++k)
                 e[j][k] = ok && !leaf ? adj[(size_t)c * SLOTS + k] : make_uint2(kNoEdge, 0u);
-            dn[j] = ok && !leaf ? d4[(size_t)c * B4 + l4] : make_uint4(INF, INF, INF, INF);
+            if (NARROW) {
+                if (ok && !leaf) pn[j] = nl_issue(nr, c, grp, B4, l4);
+            } else {
+                dn[j] = ok && !leaf ? d4[(size_t)c * B4 + l4] : make_uint4(INF, INF, INF, INF);
+            }
             lv[j] = ok && leaf ? fmleaf[(size_t)c * B4 + l4] : 0u;
             b[j][0] = b[j][1] = b[j][2] = b[j][3] = 0;
         }
+        // narrow: the own rows are decoded once the first neighbour loads are
+        // in flight too
+        bool dn_done = !NARROW;
+        auto finish_dn = [&] {
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const uint32_t c = c0 + (uint32_t)(cg + j);
+                dn[j] = c < n && !((lbits >> (cg + j)) & 1u) ? nl_finish(pn[j], d4, c, B4, l4)
+                                                             : make_uint4(INF, INF, INF, INF);
+            }
+            dn_done = true;
+        };
 #pragma unroll
         for (int kb = 0; kb < SLOTS; kb += KC) {
             bool any = false;  // edges are packed first: an empty chunk ends them all
@@ -478,12 +727,29 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
             for (int j = 0; j < G; ++j) any |= e[j][kb].x != kNoEdge;
             if (!any) break;
             uint4 dv[G][KC];
+            if (NARROW) {
+                NLoad pv[G][KC];
 #pragma unroll
-            for (int j = 0; j < G; ++j)
+                for (int j = 0; j < G; ++j)
 #pragma unroll
-                for (int k = 0; k < KC; ++k)
-                    if (e[j][kb + k].x != kNoEdge)
-                        dv[j][k] = d4[(size_t)e[j][kb + k].x * B4 + l4];
+                    for (int k = 0; k < KC; ++k)
+                        if (e[j][kb + k].x != kNoEdge)
+                            pv[j][k] = nl_issue(nr, e[j][kb + k].x, grp, B4, l4);
+                if (!dn_done) finish_dn();
+#pragma unroll
+                for (int j = 0; j < G; ++j)
+#pragma unroll
+                    for (int k = 0; k < KC; ++k)
+                        if (e[j][kb + k].x != kNoEdge)
+                            dv[j][k] = nl_finish(pv[j][k], d4, e[j][kb + k].x, B4, l4);
+            } else {
+#pragma unroll
+                for (int j = 0; j < G; ++j)
+#pragma unroll
+                    for (int k = 0; k < KC; ++k)
+                        if (e[j][kb + k].x != kNoEdge)
+                            dv[j][k] = d4[(size_t)e[j][kb + k].x * B4 + l4];
+            }
 #pragma unroll
             for (int j = 0; j < G; ++j)
 #pragma unroll
@@ -496,6 +762,7 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
                     b[j][3] |= fm_bit(dv[j][k].w, we, dn[j].w, kb + k);
                 }
         }
+        if (!dn_done) finish_dn();
 #pragma unroll
         for (int j = 0; j < G; ++j) {
             const uint32_t c = c0 + (uint32_t)(cg + j);
@@ -530,6 +797,124 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
         for (int q = 0; q < F::kWords / 4; ++q)
             seg[q] = make_uint4(pk[i][4 * q], pk[i][4 * q + 1], pk[i][4 * q + 2], pk[i][4 * q + 3]);
     }
+}
+
+// First-move sets from narrow rows, 4-slot adjacency (out-degree <= 4, 4-bit
+// sets): the same sets as first_moves<4, G, true>, with the latency chain
+// cut.  The segment's adjacency (32 columns x 4 slots x 8 B = 1 KiB) is ONE
+// 16-B load per lane up front — lane L holds slots 2(L&1), 2(L&1)+1 of column
+// L/2, read back with readlane — instead of a dependent scalar load per
+// column group; and the loads of group g+1 are issued before group g is
+// decoded (two groups in flight), so a wave waits about one memory round trip
+// per group instead of two.
+template <int G>
+struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR pressure)
+    NLoad own[G];
+    NLoad nb[G][4];
+    uint32_t lv[G];
+};
+
+template <int G>
+__global__ __launch_bounds__(256) void first_moves_n4(const uint2* __restrict__ adj,
+                                                      const uint32_t* __restrict__ dist,
+                                                      const uint32_t* __restrict__ tgt, uint32_t B,
+                                                      uint32_t n, uint32_t npad, uint32_t remap,
+                                                      uint32_t* __restrict__ fm,
+                                                      const uint32_t* __restrict__ leafbits,
+                                                      const uint16_t* __restrict__ fmleaf,
+                                                      NarrowRows nr) {
+    static_assert(kSeg % G == 0, "group size");
+    const uint32_t nseg = npad / kSeg;
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t slab = L / nseg;
+    const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
+    const uint32_t B4 = B / 4u;
+    const uint32_t c0 = (L - slab * nseg) * kSeg;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
+    const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
+    const uint32_t grp = wave_group(l4);
+    const uint32_t lbits = leafbits ? leafbits[c0 / kSeg] : 0u;
+    const uint4 sa = c0 + lane / 2u < n ? reinterpret_cast<const uint4*>(adj)[(size_t)c0 * 2u + lane]
+                                        : make_uint4(kNoEdge, 0u, kNoEdge, 0u);
+    auto edge = [&](int cc, int k) -> uint2 {  // wave-uniform
+        const int ln = 2 * cc + (k >> 1);
+        const uint32_t x = __builtin_amdgcn_readlane((k & 1) ? sa.z : sa.x, ln);
+        const uint32_t w = __builtin_amdgcn_readlane((k & 1) ? sa.w : sa.y, ln);
+        return make_uint2(x, w);
+    };
+    auto issue = [&](FmGroup<G>& g, int cg) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const uint32_t c = c0 + (uint32_t)(cg + j);
+            const bool ok = c < n;
+            const bool leaf = (lbits >> (cg + j)) & 1u;
+            if (ok && !leaf) {
+                g.own[j] = nl_issue(nr, c, grp, B4, l4);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint2 e = edge(cg + j, k);
+                    if (e.x != kNoEdge) g.nb[j][k] = nl_issue(nr, e.x, grp, B4, l4);
+                }
+            }
+            g.lv[j] = ok && leaf ? fmleaf[(size_t)c * B4 + l4] : 0u;
+        }
+    };
+    uint32_t pk[4][4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
+    auto finish = [&](const FmGroup<G>& g, int cg) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const uint32_t c = c0 + (uint32_t)(cg + j);
+            if (c >= n) continue;  // stays the wildcard padding
+            const int cc = cg + j;
+            uint32_t f0, f1, f2, f3;
+            if ((lbits >> cc) & 1u) {  // 4 nibbles, wildcards included
+                f0 = g.lv[j] & 0xFu;
+                f1 = (g.lv[j] >> 4) & 0xFu;
+                f2 = (g.lv[j] >> 8) & 0xFu;
+                f3 = g.lv[j] >> 12;
+            } else {
+                const uint4 dn = nl_finish(g.own[j], d4, c, B4, l4);
+                uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint2 e = edge(cc, k);
+                    if (e.x == kNoEdge) continue;
+                    const uint4 dv = nl_finish(g.nb[j][k], d4, e.x, B4, l4);
+                    const uint32_t we = e.y;
+                    b0 |= fm_bit(dv.x, we, dn.x, k);
+                    b1 |= fm_bit(dv.y, we, dn.y, k);
+                    b2 |= fm_bit(dv.z, we, dn.z, k);
+                    b3 |= fm_bit(dv.w, we, dn.w, k);
+                }
+                f0 = fm_final<4>(c, tc.x, dn.x, b0);
+                f1 = fm_final<4>(c, tc.y, dn.y, b1);
+                f2 = fm_final<4>(c, tc.z, dn.z, b2);
+                f3 = fm_final<4>(c, tc.w, dn.w, b3);
+            }
+            const int wi = cc / 8, sh = 4 * (cc % 8);
+            const uint32_t keep = ~(0xFu << sh);
+            pk[0][wi] = (pk[0][wi] & keep) | (f0 << sh);
+            pk[1][wi] = (pk[1][wi] & keep) | (f1 << sh);
+            pk[2][wi] = (pk[2][wi] & keep) | (f2 << sh);
+            pk[3][wi] = (pk[3][wi] & keep) | (f3 << sh);
+        }
+    };
+    FmGroup<G> cur, nxt;
+    issue(cur, 0);
+#pragma unroll
+    for (int cg = 0; cg < (int)kSeg; cg += G) {
+        if (cg + G < (int)kSeg) issue(nxt, cg + G);
+        finish(cur, cg);
+        cur = nxt;
+    }
+    const size_t row_words = npad / 8u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * row_words + c0 / 8u) =
+            make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
 }
 
 // One lane's greedy pass over its 32 columns (warthog graph_oracle::add_row
@@ -932,8 +1317,16 @@ uint32_t down_wpb() {
     static const uint32_t v = env_u32("CPD_DOWN_WPB", 4);
     return v;
 }
+uint32_t down8_wpb() {  // CPD_DOWN8_WPB: 1 or 2 waves per narrow down-sweep workgroup
+    static const uint32_t v = env_u32("CPD_DOWN8_WPB", 2) == 1 ? 1u : 2u;
+    return v;
+}
 uint32_t fm_wpb() {
     static const uint32_t v = env_u32("CPD_FM_WPB", 2);
+    return v;
+}
+uint32_t fm_n4() {  // CPD_FM_N4=0: narrow first moves without the pipelined kernel
+    static const uint32_t v = env_u32("CPD_FM_N4", 1);
     return v;
 }
 uint32_t fm_g() {
@@ -946,7 +1339,7 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
                   const uint32_t* asc_off, const uint32_t* asc_arcs, uint32_t* live,
                   const uint32_t* tmask, const uint32_t* adj, uint32_t shift, uint16_t* fmleaf,
-                  hipStream_t s) {
+                  NarrowRows nr, hipStream_t s) {
     const uint4* t4 = reinterpret_cast<const uint4*>(tgt);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
     const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
@@ -962,9 +1355,17 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                slot0, count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)nullptr, lf);
     } else {
         const uint32_t tpb = 64u * down_wpb();  // a workgroup covers 4 * tpb targets
-        launch(kern::sweep_level<false>, dim3(count * slabs * (256u / tpb)), dim3(tpb), s, nodes,
-               arc_off, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf,
-               (const uint32_t*)live, lf);
+        const dim3 grid(count * slabs * (256u / tpb)), blk(tpb);
+        if (nr.d16) {
+            // 8 targets per lane: a workgroup of 64 x wpb8 lanes covers 512 x wpb8
+            // targets (wpb8 = 2: one 1024-target slab)
+            const uint32_t tpb8 = 64u * down8_wpb();
+            launch(kern::sweep_down8, dim3(count * slabs * (2u / down8_wpb())), dim3(tpb8), s, nodes,
+                   arc_off, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf,
+                   (const uint32_t*)live, lf, nr);
+        } else
+            launch(kern::sweep_level<false>, grid, blk, s, nodes, arc_off, arcs, slot0, count,
+                   xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live, lf);
     }
 }
 
@@ -993,6 +1394,11 @@ void launch_sweep_up_chunks(const uint32_t* items, uint32_t nitems, const uint32
 
 uint32_t sweep_chunk_arcs() { return (uint32_t)kern::kChunk; }
 
+void launch_count_wide_rows(const uint32_t* base, size_t total, unsigned int* out,
+                            hipStream_t s) {
+    launch(kern::count_wide_rows, dim3(2048), dim3(256), s, base, total, out);
+}
+
 void launch_target_mask(const uint32_t* tgt, uint32_t B, uint32_t* tmask, hipStream_t s) {
     launch(kern::target_mask, dim3((B + 255u) / 256u), dim3(256), s, tgt, B, tmask);
 }
@@ -1013,29 +1419,45 @@ void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_o
 
 uint32_t fm_bits(uint32_t shift) { return shift <= 2 ? 4u : (1u << shift); }
 
+template <bool NARROW>
+static void launch_first_moves_t(const uint2* adj, uint32_t shift, const uint32_t* dist,
+                                 const uint32_t* tgt, uint32_t B, uint32_t n, uint32_t npad,
+                                 uint32_t* fm, const uint32_t* leafbits, const uint16_t* fmleaf,
+                                 NarrowRows nr, dim3 grid, dim3 blk, hipStream_t s) {
+    const uint32_t r = xcd_remap();
+    switch (shift) {  // SLOTS = 2^shift edges per column; G columns per gather group
+        case 0: launch(kern::first_moves<1, 4, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
+        case 1: launch(kern::first_moves<2, 2, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
+        case 2:
+            if (fm_g() == 4)
+                launch(kern::first_moves<4, 4, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
+            else if (fm_g() == 1)
+                launch(kern::first_moves<4, 1, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
+            else
+                launch(kern::first_moves<4, 2, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
+            break;
+        case 3: launch(kern::first_moves<8, 1, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
+        default: launch(kern::first_moves<16, 1, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
+    }
+}
+
 void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* dist,
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
                         uint32_t npad, uint32_t* fm, const uint32_t* leafbits,
-                        const uint16_t* fmleaf, hipStream_t s) {
+                        const uint16_t* fmleaf, NarrowRows nr, hipStream_t s) {
     const uint32_t tpb = 64u * fm_wpb();  // a workgroup covers 4 * tpb targets
-    dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u) * (256u / tpb));
+    const dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u) * (256u / tpb)), blk(tpb);
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
-    const uint32_t r = xcd_remap();
-    const dim3 blk(tpb);
-    switch (shift) {  // SLOTS = 2^shift edges per column; G columns per gather group
-        case 0: launch(kern::first_moves<1, 4>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf); break;
-        case 1: launch(kern::first_moves<2, 2>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf); break;
-        case 2:
-            if (fm_g() == 4)
-                launch(kern::first_moves<4, 4>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf);
-            else if (fm_g() == 1)
-                launch(kern::first_moves<4, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf);
-            else
-                launch(kern::first_moves<4, 2>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf);
-            break;
-        case 3: launch(kern::first_moves<8, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf); break;
-        default: launch(kern::first_moves<16, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf); break;
-    }
+    if (nr.d16 && shift == 2 && fm_n4()) {
+        const uint32_t r = xcd_remap();
+        launch(kern::first_moves_n4<2>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits,
+               fmleaf, nr);
+    } else if (nr.d16)
+        launch_first_moves_t<true>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
+                                   grid, blk, s);
+    else
+        launch_first_moves_t<false>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
+                                    grid, blk, s);
 }
 
 template <bool EMIT>

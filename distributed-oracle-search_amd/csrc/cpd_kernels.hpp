@@ -9,6 +9,22 @@ namespace cpd {
 // it); the events record the kernel's own begin/end timestamps.
 void set_launch_events(hipEvent_t start, hipEvent_t stop);
 
+// Narrow final-distance rows (the down-sweep's output, read by first_moves):
+// per 256-target group g of the batch (one wave: 64 lanes x 4 targets) and
+// column c, base[g * n + c] = the minimum of the group's finite distances
+// (0xFFFFFFFF if none) and d16[c * B + target] = distance - base as u16, with
+// 0xFFFF = unreachable.  Halves the bytes of the two dominant kernels.  A
+// group row whose finite spread reaches 0xFFFF is stored in `dist` (32-bit)
+// instead, with base 0xFFFFFFFE (counted by launch_count_wide_rows into
+// *ovf in timing runs).  Every finite distance must stay below 0xFFFFFFFE.
+// d16 == nullptr: every row in `dist`.
+struct NarrowRows {
+    uint16_t* d16;
+    uint32_t* base;
+    uint32_t n;
+    uint32_t* ovf;
+};
+
 // One CH sweep level: `count` node slots starting at `slot0` of the
 // level-ordered node list; count * slabs workgroups of 256 threads, one slab =
 // 1024 targets of the B-wide batch row, XCD-remapped (CPD_XCD=0: off).
@@ -26,7 +42,7 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   uint32_t* dist, const uint32_t* tgt, uint32_t B, uint32_t slabs,
                   const uint32_t* asc_nodes, const uint32_t* asc_off, const uint32_t* asc_arcs,
                   uint32_t* live, const uint32_t* tmask, const uint32_t* adj, uint32_t shift,
-                  uint16_t* fmleaf, hipStream_t s);
+                  uint16_t* fmleaf, NarrowRows nr, hipStream_t s);
 
 // Narrow upward levels, chunked: items (slot, first arc, end arc, 0) of at
 // most sweep_chunk_arcs() arcs each, nitems x slabs workgroups, partial
@@ -43,6 +59,10 @@ void launch_sweep_up_chunks(const uint32_t* items /* uint4 each */, uint32_t nit
                             const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
                             hipStream_t s);
 uint32_t sweep_chunk_arcs();
+
+// *out += number of the `total` narrow-row bases that mark a wide row.
+void launch_count_wide_rows(const uint32_t* base, size_t total, unsigned int* out,
+                            hipStream_t s);
 
 // tmask[tgt[i]] |= 1 << (i / 1024) for i < B; tmask must be zeroed first.
 void launch_target_mask(const uint32_t* tgt, uint32_t B, uint32_t* tmask, hipStream_t s);
@@ -68,7 +88,7 @@ uint32_t fm_bits(uint32_t shift);
 void launch_first_moves(const uint32_t* adj, uint32_t shift, const uint32_t* dist,
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
                         uint32_t npad, uint32_t* fm, const uint32_t* leafbits,
-                        const uint16_t* fmleaf, hipStream_t s);
+                        const uint16_t* fmleaf, NarrowRows nr, hipStream_t s);
 
 // Row width of the tiled first-move rows: npad is a multiple of this.
 constexpr uint32_t kFmTile = 2048;

@@ -5,6 +5,8 @@ row words, per-query costs/hops/finished flags.  Inputs are seeded synthetic
 road graphs plus hand-built edge cases (unreachable nodes, degree-15 nodes,
 self loops, parallel edges, zero weights, a single node).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -15,12 +17,29 @@ from graphs import GRAPHS
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=sorted(GRAPHS))
+def make_graph(plan, batch, narrow):
+    """Device graph with narrow (u16-offset) distance rows on or off
+    (CPD_NARROW is read when the graph is created)."""
+    old = os.environ.get("CPD_NARROW")
+    os.environ["CPD_NARROW"] = "1" if narrow else "0"
+    try:
+        return cpd.Graph(plan, batch=batch)
+    finally:
+        if old is None:
+            del os.environ["CPD_NARROW"]
+        else:
+            os.environ["CPD_NARROW"] = old
+
+
+@pytest.fixture(scope="module", params=[(name, narrow) for name in sorted(GRAPHS)
+                                        for narrow in (True, False)],
+                ids=lambda p: f"{p[0]}-{'narrow' if p[1] else 'wide'}")
 def setup(request):
-    g = GRAPHS[request.param]()
+    name, narrow = request.param
+    g = GRAPHS[name]()
     plan = cpd.Plan(g)
-    dev = cpd.Graph(plan, batch=1024)
-    return request.param, g, plan, dev
+    dev = make_graph(plan, 1024, narrow)
+    return name, g, plan, dev
 
 
 def test_distances_and_first_moves(setup):
@@ -152,3 +171,26 @@ def test_multi_slab_batches(width, batch):
     for i in rng.choice(nd, 5, replace=False):
         np.testing.assert_array_equal(
             dist[:, i], oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, targets[i]))
+
+
+def test_narrow_overflow_rows_kept_wide():
+    """Edge weights x700: a wave's 256 distances spread past 0xFFFF, so the
+    narrow rows cannot hold them; those group rows are kept 32-bit (base =
+    wide marker) and every output stays exact."""
+    g0 = cpd.synth_road_graph(40, 40, seed=12)
+    g = cpd.RoadGraph(g0.row_ptr, g0.dst, (g0.w * 700).astype(np.uint32), g0.x, g0.y)
+    plan = cpd.Plan(g)
+    dev = make_graph(plan, 1024, True)
+    rng = np.random.default_rng(12)
+    targets = rng.permutation(g.n).astype(np.uint32)[:1500]
+    rows = dev.build_rows(targets)
+    off, runs = rows.export()
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    np.testing.assert_array_equal(off, ref_off)
+    np.testing.assert_array_equal(runs, ref_runs)
+    dev2 = make_graph(plan, 1024, True)
+    dist, fm = dev2.debug_rows(targets[:300])
+    for i in range(0, 300, 37):
+        np.testing.assert_array_equal(
+            dist[:, i], oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, targets[i]))
+        np.testing.assert_array_equal(fm[i], oracle.first_moves(g.row_ptr, g.dst, g.w, targets[i]))
