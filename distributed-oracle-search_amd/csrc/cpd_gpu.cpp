@@ -102,7 +102,7 @@ struct cpd_graph {
     }
     // sweeps: level-ordered node lists, per-slot arc offsets, (col, w) arcs
     DevBuf<uint32_t> asc_nodes, asc_off, asc_arcs;
-    DevBuf<uint32_t> dsc_nodes, dsc_off, dsc_arcs;
+    DevBuf<uint32_t> dsc_nodes, dsc_off, dsc_arcs, dsc_desc;
     std::vector<uint32_t> asc_lvl, dsc_lvl;         // level -> first slot
     // bytes model: gathered arcs and own-row reads per level
     std::vector<double> asc_lvl_arcs, dsc_lvl_arcs, dsc_lvl_reads;
@@ -357,10 +357,15 @@ std::vector<uint32_t> level_order(const cpd_plan& p, const std::vector<uint32_t>
 // encodings of cpd_kernels.hip (kLeafBit: upward level 0, kL1Bit: level 1,
 // referenced by its slot in the ASCENDING list, asc_slot[node]).
 // lvl_arcs: gathered arcs per level; lvl_reads: nodes reading their own row.
+// leaf_edges (descending only): a leaf's list is its out-edges in file order
+// (self loops and parallel edges included) instead of its up-arcs — the same
+// minimum, and the list position is the move index for the leaf's first-move
+// set (the down-sweep computes leaf sets, cpd_kernels.hip sweep_down8c).
 void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& asc_slot,
                  std::vector<uint32_t>& nodes, std::vector<uint32_t>& off,
                  std::vector<uint32_t>& arcs, std::vector<uint32_t>& lvl_first,
-                 std::vector<double>& lvl_arcs, std::vector<double>& lvl_reads) {
+                 std::vector<double>& lvl_arcs, std::vector<double>& lvl_reads,
+                 bool leaf_edges = false) {
     const Hierarchy& H = p.ch;
     const uint32_t n = p.n;
     const std::vector<uint32_t>& level = ascend ? H.level_up : H.level_dn;
@@ -394,6 +399,15 @@ void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& as
     for (uint32_t s = 0; s < n; ++s) {
         uint32_t v = node_of_slot[s];
         tmp.clear();
+        if (!ascend && leaf_edges && lup[v] == 0) {
+            for (uint32_t e = p.row_ptr[v]; e < p.row_ptr[v + 1]; ++e) {
+                arcs.push_back(p.order[p.dst[e]]);
+                arcs.push_back(p.w[e]);
+                if (p.dst[e] != v) lvl_arcs[level[v]] += 1.0;
+            }
+            off[s + 1] = off[s] + (p.row_ptr[v + 1] - p.row_ptr[v]);
+            continue;
+        }
         for (uint64_t e = aoff[v]; e < aoff[v + 1]; ++e) tmp.push_back({p.order[adst[e]], aw[e]});
         std::sort(tmp.begin(), tmp.end());
         for (auto& a : tmp) {
@@ -487,15 +501,31 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->asc_arcs.upload(arcs.data(), arcs.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
         g->ch_arcs = arcs.size() / 2;
+        // leaf first moves in the down-sweep: 4-bit sets only (<= 4 slots)
+        g->leaf_fm = g->fmb == 4 && env_on("CPD_LEAFFM");
         build_sweep(*p, false, asc_slot, nodes, off, arcs, g->dsc_lvl, g->dsc_lvl_arcs,
-                    g->dsc_lvl_reads);
+                    g->dsc_lvl_reads, g->leaf_fm);
         g->dsc_nodes.upload(nodes.data(), nodes.size(), s);
         g->dsc_off.upload(off.data(), off.size(), s);
         g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
+        {
+            const uint32_t na = down_desc_arcs();
+            std::vector<uint32_t> desc((size_t)n * 16u, 0u);
+            for (uint32_t x = 0; x < n; ++x) {
+                uint32_t* d = desc.data() + (size_t)x * 16u;
+                d[0] = nodes[x];
+                d[1] = off[x];
+                d[2] = off[x + 1];
+                for (uint32_t i = 0; i < na; ++i) {
+                    const bool in = off[x] + i < off[x + 1];
+                    d[4 + 2 * i] = in ? arcs[2 * (size_t)(off[x] + i)] : 0xFFFFFFFFu;
+                    d[5 + 2 * i] = in ? arcs[2 * (size_t)(off[x] + i) + 1] : 0u;
+                }
+            }
+            g->dsc_desc.upload(desc.data(), desc.size(), s);
+        }
         HIP_CHECK(hipStreamSynchronize(s));
         g->ch_arcs += arcs.size() / 2;
-        // leaf first moves in the down-sweep: 4-bit sets only (<= 4 slots)
-        g->leaf_fm = g->fmb == 4 && env_on("CPD_LEAFFM");
         g->narrow = env_on("CPD_NARROW") && p->dist_bound < 0xFFFFFFFEull;
         {
             std::vector<uint32_t> lb(g->npad / 32u, 0u);
@@ -636,7 +666,7 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow) {
                 launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt,
                              g->dist.p, g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p,
                              g->asc_arcs.p, live, g->tmask.p, g->adj.p, g->adj_shift, nullptr,
-                             g->narrow_rows(false), g->stream);
+                             g->narrow_rows(false), nullptr, g->stream);
         }, std::move(late));
     }
     g->group_end();
@@ -658,7 +688,7 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow) {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
                          g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
                          g->tmask.p, g->adj.p, g->adj_shift, g->leaf_fm ? g->fmleaf.p : nullptr,
-                         nr, g->stream);
+                         nr, g->dsc_desc.p, g->stream);
         }, std::move(late));
     }
     g->group_end();

@@ -21,6 +21,7 @@ namespace cpd {
 namespace kern {
 
 constexpr uint32_t INF = 0xFFFFFFFFu;
+constexpr uint32_t kNoEdge = 0xFFFFFFFFu;  // packed adjacency padding past the out-degree
 
 __device__ __forceinline__ uint32_t sat_add(uint32_t d, uint32_t w) {
     uint32_t s = d + w;
@@ -286,6 +287,8 @@ struct U8 {
     uint4 a, b;
 };
 
+constexpr uint32_t kDescArcs = 6;  // arcs inline in a down-sweep slot descriptor
+
 __device__ __forceinline__ U8 inf8() {
     return U8{make_uint4(INF, INF, INF, INF), make_uint4(INF, INF, INF, INF)};
 }
@@ -363,21 +366,27 @@ __device__ __forceinline__ uint32_t fm_pack4(const uint4& t, const uint4& acc, u
     return b0 | (b1 << 4) | (b2 << 8) | (b3 << 12);
 }
 
-__global__ __launch_bounds__(256) void sweep_down8(const uint32_t* __restrict__ nodes,
-                                                   const uint32_t* __restrict__ arc_off,
+__global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ desc,
                                                    const uint2* __restrict__ arcs,
                                                    uint32_t slot0, uint32_t count, uint32_t remap,
                                                    uint32_t* __restrict__ dist,
                                                    const uint4* __restrict__ tgt4, uint32_t B4,
                                                    Closed cf, const uint32_t* __restrict__ live,
-                                                   LeafFm lf, NarrowRows nr) {
+                                                   uint16_t* __restrict__ fmleaf, NarrowRows nr) {
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t blk = L / count;
     const uint32_t slot = slot0 + (L - blk * count);
     const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
     const uint32_t grp = l8 >> 5;                        // uniform per half-wave
     const uint32_t B8 = B4 / 2u;
-    const uint32_t vraw = nodes[slot];
+    // the slot's descriptor, one 64-B scalar load: (node word, first arc, end
+    // arc, -) + its first kDescArcs arcs (a leaf's out-edges in file order)
+    const uint4* __restrict__ dp = desc + (size_t)slot * 4u;
+    const uint4 h = dp[0], i0 = dp[1], i1 = dp[2], i2 = dp[3];
+    const uint2 inl[kDescArcs] = {make_uint2(i0.x, i0.y), make_uint2(i0.z, i0.w),
+                                  make_uint2(i1.x, i1.y), make_uint2(i1.z, i1.w),
+                                  make_uint2(i2.x, i2.y), make_uint2(i2.z, i2.w)};
+    const uint32_t vraw = h.x, a0 = h.y, a1 = h.z;
     uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
     const U8 t{tgt4[2u * l8], tgt4[2u * l8 + 1u]};
     uint32_t v;
@@ -385,36 +394,31 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint32_t* __restrict__ 
     if (vraw & kLeafBit) {
         v = vraw & kIdxMask;
         acc = U8{leaf4(t.a, v, 0u), leaf4(t.b, v, 0u)};
-        if (lf.out) {
-            const uint32_t ns = 1u << lf.shift;
-            uint2 e[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                e[k] = (uint32_t)k < ns ? lf.adj[((size_t)v << lf.shift) + k]
-                                        : make_uint2(0xFFFFFFFFu, 0u);
+        if (fmleaf) {  // out-degree <= 4 (4-bit sets): all inline
+            const uint2* e = inl;
             NLoad8 pl[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (e[k].x != 0xFFFFFFFFu && e[k].x != v) pl[k] = nl8_issue(nr, e[k].x, grp, B8, l8);
+                if (e[k].x != kNoEdge && e[k].x != v) pl[k] = nl8_issue(nr, e[k].x, grp, B8, l8);
             U8 x[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                x[k] = (e[k].x != 0xFFFFFFFFu && e[k].x != v) ? nl8_finish(pl[k], d4, e[k].x, B4, l8)
-                                                              : inf8();
+                x[k] = (e[k].x != kNoEdge && e[k].x != v) ? nl8_finish(pl[k], d4, e[k].x, B4, l8)
+                                                          : inf8();
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (e[k].x != 0xFFFFFFFFu && e[k].x != v) min8(acc, x[k], e[k].y);
+                if (e[k].x != kNoEdge && e[k].x != v) min8(acc, x[k], e[k].y);
             uint32_t ba[4] = {0, 0, 0, 0}, bb[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if (e[k].x == 0xFFFFFFFFu) continue;
+                if (e[k].x == kNoEdge) continue;
                 const U8& dv = e[k].x == v ? acc : x[k];  // self loop: d(v) itself
                 fm_nib(dv.a, acc.a, e[k].y, k, ba);
                 fm_nib(dv.b, acc.b, e[k].y, k, bb);
             }
             const uint32_t sets = fm_pack4(t.a, acc.a, v, ba) | (fm_pack4(t.b, acc.b, v, bb) << 16);
             narrow_store8(nr, d4, v, grp, B4, B8, l8, acc);
-            reinterpret_cast<uint32_t*>(lf.out)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
+            reinterpret_cast<uint32_t*>(fmleaf)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
             return;
         }
     } else if (vraw & kL1Bit) {
@@ -425,8 +429,16 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint32_t* __restrict__ 
         const bool own = !live || ((live[v] >> (l8 >> 7)) & 1u);  // live bits: 1024 targets
         acc = own ? U8{d4[(size_t)v * B4 + 2u * l8], d4[(size_t)v * B4 + 2u * l8 + 1u]} : inf8();
     }
-    const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
-    uint32_t a = a0;
+    {  // the inline arcs (kNoEdge past the list), gathers in flight together
+        NLoad8 pl[kDescArcs];
+#pragma unroll
+        for (int i = 0; i < (int)kDescArcs; ++i)
+            if (inl[i].x != kNoEdge) pl[i] = nl8_issue(nr, inl[i].x, grp, B8, l8);
+#pragma unroll
+        for (int i = 0; i < (int)kDescArcs; ++i)
+            if (inl[i].x != kNoEdge) min8(acc, nl8_finish(pl[i], d4, inl[i].x, B4, l8), inl[i].y);
+    }
+    uint32_t a = a0 + kDescArcs;  // the rest of a long list
     for (; a + 8 <= a1; a += 8) {
         uint2 e[8];
 #pragma unroll
@@ -658,7 +670,6 @@ __device__ __forceinline__ uint32_t fm_final(uint32_t c, uint32_t tc, uint32_t d
 // adjacency (SLOTS = 2^shift per column, kNoEdge padding), so a group of G
 // columns issues its G own-row and G*SLOTS neighbour gathers back to back,
 // with no dependent CSR lookups.
-constexpr uint32_t kNoEdge = 0xFFFFFFFFu;
 
 template <int SLOTS, int G, bool NARROW>
 __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj,
@@ -1317,8 +1328,11 @@ uint32_t down_wpb() {
     static const uint32_t v = env_u32("CPD_DOWN_WPB", 4);
     return v;
 }
-uint32_t down8_wpb() {  // CPD_DOWN8_WPB: 1 or 2 waves per narrow down-sweep workgroup
-    static const uint32_t v = env_u32("CPD_DOWN8_WPB", 2) == 1 ? 1u : 2u;
+uint32_t down8_wpb() {  // CPD_DOWN8_WPB: 1, 2 or 4 waves per narrow down-sweep workgroup
+    static const uint32_t v = [] {
+        const uint32_t w = env_u32("CPD_DOWN8_WPB", 2);
+        return w == 1 ? 1u : (w == 4 ? 4u : 2u);
+    }();
     return v;
 }
 uint32_t fm_wpb() {
@@ -1339,7 +1353,7 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
                   const uint32_t* asc_off, const uint32_t* asc_arcs, uint32_t* live,
                   const uint32_t* tmask, const uint32_t* adj, uint32_t shift, uint16_t* fmleaf,
-                  NarrowRows nr, hipStream_t s) {
+                  NarrowRows nr, const uint32_t* desc, hipStream_t s) {
     const uint4* t4 = reinterpret_cast<const uint4*>(tgt);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
     const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
@@ -1359,10 +1373,12 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
         if (nr.d16) {
             // 8 targets per lane: a workgroup of 64 x wpb8 lanes covers 512 x wpb8
             // targets (wpb8 = 2: one 1024-target slab)
-            const uint32_t tpb8 = 64u * down8_wpb();
-            launch(kern::sweep_down8, dim3(count * slabs * (2u / down8_wpb())), dim3(tpb8), s, nodes,
-                   arc_off, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf,
-                   (const uint32_t*)live, lf, nr);
+            // (4 waves = 2048 targets: only when the slab count is even)
+            const uint32_t wpb8 = down8_wpb() == 4 && slabs % 2 ? 2u : down8_wpb();
+            const uint32_t tpb8 = 64u * wpb8;
+            launch(kern::sweep_down8, dim3(count * slabs * 2u / wpb8), dim3(tpb8), s,
+                   reinterpret_cast<const uint4*>(desc), arcs, slot0, count, xcd_remap(), dist, t4,
+                   B / 4u, cf, (const uint32_t*)live, fmleaf, nr);
         } else
             launch(kern::sweep_level<false>, grid, blk, s, nodes, arc_off, arcs, slot0, count,
                    xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live, lf);
@@ -1393,6 +1409,7 @@ void launch_sweep_up_chunks(const uint32_t* items, uint32_t nitems, const uint32
 }
 
 uint32_t sweep_chunk_arcs() { return (uint32_t)kern::kChunk; }
+uint32_t down_desc_arcs() { return kern::kDescArcs; }
 
 void launch_count_wide_rows(const uint32_t* base, size_t total, unsigned int* out,
                             hipStream_t s) {

@@ -42,7 +42,13 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   uint32_t* dist, const uint32_t* tgt, uint32_t B, uint32_t slabs,
                   const uint32_t* asc_nodes, const uint32_t* asc_off, const uint32_t* asc_arcs,
                   uint32_t* live, const uint32_t* tmask, const uint32_t* adj, uint32_t shift,
-                  uint16_t* fmleaf, NarrowRows nr, hipStream_t s);
+                  uint16_t* fmleaf, NarrowRows nr, const uint32_t* desc, hipStream_t s);
+
+// Down-sweep slot descriptors for the narrow down-sweep (desc arg of
+// launch_sweep): 16 u32 per slot = node word, first arc, end arc, 0, then the
+// slot's first down_desc_arcs() arcs as (column, weight), (kNoEdge, 0) past
+// the end of its list.
+uint32_t down_desc_arcs();
 
 // Narrow upward levels, chunked: items (slot, first arc, end arc, 0) of at
 // most sweep_chunk_arcs() arcs each, nitems x slabs workgroups, partial
