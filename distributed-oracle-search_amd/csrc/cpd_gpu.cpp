@@ -495,7 +495,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         }
         build_sweep(*p, true, asc_slot, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs, unused);
         g->asc_off_host = off;
-        const std::vector<uint32_t> nodes_asc_host = nodes;
+        const std::vector<uint32_t> nodes_asc_host = nodes, asc_arcs_host = arcs;
         g->asc_nodes.upload(nodes.data(), nodes.size(), s);
         g->asc_off.upload(off.data(), off.size(), s);
         g->asc_arcs.upload(arcs.data(), arcs.size(), s);
@@ -510,9 +510,10 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
         {
             const uint32_t na = down_desc_arcs();
-            std::vector<uint32_t> desc((size_t)n * 16u, 0u);
+            std::vector<uint32_t> desc((size_t)n * 32u, 0u);
+            const std::vector<uint32_t>& aoff = g->asc_off_host;
             for (uint32_t x = 0; x < n; ++x) {
-                uint32_t* d = desc.data() + (size_t)x * 16u;
+                uint32_t* d = desc.data() + (size_t)x * 32u;
                 d[0] = nodes[x];
                 d[1] = off[x];
                 d[2] = off[x + 1];
@@ -520,6 +521,15 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                     const bool in = off[x] + i < off[x + 1];
                     d[4 + 2 * i] = in ? arcs[2 * (size_t)(off[x] + i)] : 0xFFFFFFFFu;
                     d[5 + 2 * i] = in ? arcs[2 * (size_t)(off[x] + i) + 1] : 0u;
+                }
+                if (nodes[x] & kL1Bit) {  // level-1 closed form inputs
+                    const uint32_t s1 = nodes[x] & ~kL1Bit;
+                    d[16] = nodes_asc_host[s1];
+                    d[17] = aoff[s1 + 1] - aoff[s1];
+                    for (uint32_t i = 0; i < 4 && aoff[s1] + i < aoff[s1 + 1]; ++i) {
+                        d[18 + 2 * i] = asc_arcs_host[2 * (size_t)(aoff[s1] + i)] & ~kLeafBit;
+                        d[19 + 2 * i] = asc_arcs_host[2 * (size_t)(aoff[s1] + i) + 1];
+                    }
                 }
             }
             g->dsc_desc.upload(desc.data(), desc.size(), s);

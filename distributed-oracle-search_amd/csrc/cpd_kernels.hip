@@ -379,10 +379,12 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ des
     const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
     const uint32_t grp = l8 >> 5;                        // uniform per half-wave
     const uint32_t B8 = B4 / 2u;
-    // the slot's descriptor, one 64-B scalar load: (node word, first arc, end
-    // arc, -) + its first kDescArcs arcs (a leaf's out-edges in file order)
-    const uint4* __restrict__ dp = desc + (size_t)slot * 4u;
+    // the slot's descriptor, 128 B of scalar loads: (node word, first arc, end
+    // arc, -) + its first kDescArcs arcs (a leaf's out-edges in file order);
+    // for a level-1 node also its column and its <= 4 leaf arcs (closed form)
+    const uint4* __restrict__ dp = desc + (size_t)slot * 8u;
     const uint4 h = dp[0], i0 = dp[1], i1 = dp[2], i2 = dp[3];
+    const uint4 c0 = dp[4], c1 = dp[5], c2 = dp[6];
     const uint2 inl[kDescArcs] = {make_uint2(i0.x, i0.y), make_uint2(i0.z, i0.w),
                                   make_uint2(i1.x, i1.y), make_uint2(i1.z, i1.w),
                                   make_uint2(i2.x, i2.y), make_uint2(i2.z, i2.w)};
@@ -421,9 +423,25 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ des
             reinterpret_cast<uint32_t*>(fmleaf)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
             return;
         }
-    } else if (vraw & kL1Bit) {
-        v = cf.nodes[vraw & kIdxMask];
-        acc = U8{l1_val(cf, vraw & kIdxMask, t.a), l1_val(cf, vraw & kIdxMask, t.b)};
+    } else if (vraw & kL1Bit) {  // closed form from the descriptor
+        v = c0.x;
+        acc = U8{leaf4(t.a, v, 0u), leaf4(t.b, v, 0u)};
+        const uint2 la[4] = {make_uint2(c0.z, c0.w), make_uint2(c1.x, c1.y),
+                             make_uint2(c1.z, c1.w), make_uint2(c2.x, c2.y)};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if ((uint32_t)i < c0.y) {
+                min4(acc.a, leaf4(t.a, la[i].x, 0u), la[i].y);
+                min4(acc.b, leaf4(t.b, la[i].x, 0u), la[i].y);
+            }
+        if (c0.y > 4u) {  // more leaf arcs than fit: the ascending arrays
+            const uint32_t s1 = vraw & kIdxMask;
+            for (uint32_t a = cf.off[s1] + 4u; a < cf.off[s1 + 1]; ++a) {
+                const uint2 e = cf.arcs[a];
+                min4(acc.a, leaf4(t.a, e.x & kIdxMask, 0u), e.y);
+                min4(acc.b, leaf4(t.b, e.x & kIdxMask, 0u), e.y);
+            }
+        }
     } else {
         v = vraw;
         const bool own = !live || ((live[v] >> (l8 >> 7)) & 1u);  // live bits: 1024 targets

@@ -45,9 +45,11 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   uint16_t* fmleaf, NarrowRows nr, const uint32_t* desc, hipStream_t s);
 
 // Down-sweep slot descriptors for the narrow down-sweep (desc arg of
-// launch_sweep): 16 u32 per slot = node word, first arc, end arc, 0, then the
+// launch_sweep): 32 u32 per slot = node word, first arc, end arc, 0, then the
 // slot's first down_desc_arcs() arcs as (column, weight), (kNoEdge, 0) past
-// the end of its list.
+// the end of its list; words 16.. for a level-1 node (kL1Bit): its column,
+// its number of (leaf) down-arcs, then the first 4 of them as (column,
+// weight) — the ascending list's arcs with the leaf bit cleared.
 uint32_t down_desc_arcs();
 
 // Narrow upward levels, chunked: items (slot, first arc, end arc, 0) of at
