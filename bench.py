@@ -223,7 +223,10 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
         "parity_sample_bit_exact": parity,
         "kernels": {k: {"launches": v["launches"], "ms": round(v["ms"], 3),
                         "GBps": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1) if v["ms"] else 0}
-                    for k, v in (kt or {}).items()},
+                    for k, v in (kt or {}).items() if k not in _COUNTERS},
+        # narrow distance rows: 256-target groups kept wide (u32) / all groups
+        "narrow_rows": {"wide_groups": (kt or {}).get("wide_rows", {}).get("launches"),
+                        "groups": (kt or {}).get("group_rows", {}).get("launches")},
         "hierarchy": {"arcs": pinfo["ch_up_arcs"] + pinfo["ch_dn_arcs"],
                       "levels": [pinfo["levels_up"], pinfo["levels_dn"]],
                       "build_s": round(pinfo["ch_seconds"], 1)} if pinfo else None,
@@ -233,6 +236,10 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
                                        "write": round(v["write_bytes_per_launch"], 1)}
                                    for k, v in (traffic or {}).items()},
     }
+
+
+# libcpd reports these counters through the timing table (launches = count)
+_COUNTERS = ("wide_rows", "group_rows")
 
 
 # --------------------------------------------------------------------------
