@@ -40,7 +40,8 @@ EXPORTED = [
     "cpd_plan_create", "cpd_plan_info_get", "cpd_plan_order", "cpd_plan_export_ch",
     "cpd_plan_save", "cpd_plan_load", "cpd_plan_free", "cpd_device_count",
     "cpd_graph_create", "cpd_graph_set_batch", "cpd_graph_get_batch", "cpd_graph_free",
-    "cpd_build_rows", "cpd_rows_count", "cpd_rows_export", "cpd_rows_free",
+    "cpd_build_rows", "cpd_rows_count", "cpd_rows_export", "cpd_rows_export_range",
+    "cpd_rows_targets", "cpd_rows_free",
     "cpd_debug_rows", "cpd_index_create", "cpd_index_from_rows", "cpd_index_set_weights",
     "cpd_query_batch", "cpd_query_prepare", "cpd_query_run", "cpd_query_fetch",
     "cpd_index_free", "cpd_timing_enable", "cpd_timing_reset", "cpd_timing_get",
@@ -279,6 +280,22 @@ class Rows:
         runs = np.empty(tot, np.uint32)
         _check(lib.cpd_rows_export(self._h, _ptr(off, u64p), _ptr(runs, u32p)))
         return off, runs
+
+    def export_range(self, first: int, count: int):
+        """Rows [first, first+count): offsets relative to row `first`, runs."""
+        off = np.empty(count + 1, np.uint64)
+        _check(lib.cpd_rows_export_range(self._h, C.c_uint32(first), C.c_uint32(count),
+                                         _ptr(off, u64p), None))
+        runs = np.empty(int(off[-1]), np.uint32)
+        _check(lib.cpd_rows_export_range(self._h, C.c_uint32(first), C.c_uint32(count),
+                                         None, _ptr(runs, u32p)))
+        return off, runs
+
+    def targets(self):
+        nr, _ = self.count()
+        t = np.empty(nr, np.uint32)
+        _check(lib.cpd_rows_targets(self._h, _ptr(t, u32p)))
+        return t
 
     def __del__(self):
         if getattr(self, "_h", None):

@@ -890,6 +890,36 @@ int cpd_rows_export(const cpd_rows* r, uint64_t* offsets, uint32_t* runs) {
     });
 }
 
+int cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count, uint64_t* offsets,
+                          uint32_t* runs) {
+    return guarded([&] {
+        CPD_REQUIRE(r, CPD_E_ARG, "null rows");
+        CPD_REQUIRE(first <= r->nrows && count <= r->nrows - first, CPD_E_ARG,
+                    "export range: rows out of range");
+        const uint64_t base = r->offsets[first], end = r->offsets[first + count];
+        if (offsets)
+            for (uint32_t i = 0; i <= count; ++i) offsets[i] = r->offsets[first + i] - base;
+        if (!runs || end == base) return;
+        HIP_CHECK(hipSetDevice(r->device));
+        // one non-blocking stream per (host thread, device), kept for the
+        // thread's lifetime: exports never queue behind a build's stream
+        thread_local std::vector<hipStream_t> streams;
+        if (streams.size() <= (size_t)r->device) streams.resize(r->device + 1, nullptr);
+        hipStream_t& st = streams[r->device];
+        if (!st) HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIP_CHECK(hipMemcpyAsync(runs, r->runs.p + base, (end - base) * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    });
+}
+
+int cpd_rows_targets(const cpd_rows* r, uint32_t* targets) {
+    return guarded([&] {
+        CPD_REQUIRE(r && targets, CPD_E_ARG, "null argument");
+        std::memcpy(targets, r->targets.data(), r->nrows * sizeof(uint32_t));
+    });
+}
+
 void cpd_rows_free(cpd_rows* r) {
     if (r) (void)hipSetDevice(r->device);
     delete r;

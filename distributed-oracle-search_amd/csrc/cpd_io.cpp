@@ -1,6 +1,7 @@
 // File formats on the drop-in boundary — see cpd_io.hpp.
 #include "cpd_io.hpp"
 
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -284,6 +285,60 @@ void write_bucket(const std::string& path, const CpdBucket& b) {
         if (!f) throw Error(CPD_E_IO, "write failed: " + tmp);
     }
     if (std::rename(tmp.c_str(), path.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path);
+}
+
+// bucket layout: magic 8 | n nrows bid method key maxworker (6 x u32) |
+// total u64 | fingerprint u64 | targets u32[nrows] | offsets u64[nrows+1] |
+// runs u32[total]
+static constexpr uint64_t kBucketHeader = 8 + 24 + 8 + 8;
+
+BucketFile::BucketFile(const std::string& path, const CpdBucket& b)
+    : path_(path), tmp_(path + ".tmp"), nrows_((uint32_t)b.targets.size()) {
+    fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd_ < 0) throw Error(CPD_E_IO, "cannot write " + tmp_);
+    char h[kBucketHeader] = {};
+    std::memcpy(h, kBucketMagic, 8);
+    const uint32_t h32[6] = {b.n, nrows_, b.bid, b.method, b.key, b.maxworker};
+    std::memcpy(h + 8, h32, sizeof h32);
+    std::memcpy(h + 40, &b.fingerprint, 8);  // total (h + 32) is written by close()
+    pwrite_all(h, sizeof h, 0);
+    pwrite_all(b.targets.data(), nrows_ * 4ull, kBucketHeader);
+}
+
+BucketFile::~BucketFile() {
+    if (fd_ >= 0) {
+        ::close(fd_);
+        ::unlink(tmp_.c_str());
+    }
+}
+
+void BucketFile::pwrite_all(const void* p, size_t bytes, uint64_t pos) {
+    const char* c = static_cast<const char*>(p);
+    while (bytes > 0) {
+        const ssize_t k = ::pwrite(fd_, c, std::min<size_t>(bytes, size_t(1) << 30), (off_t)pos);
+        if (k <= 0) throw Error(CPD_E_IO, "write failed: " + tmp_);
+        c += k;
+        pos += (uint64_t)k;
+        bytes -= (size_t)k;
+    }
+}
+
+void BucketFile::write_offsets(uint32_t first_row, const uint64_t* off, uint32_t count) {
+    if (first_row > nrows_ + 1u || count > nrows_ + 1u - first_row)
+        throw Error(CPD_E_ARG, "bucket offsets out of range: " + tmp_);
+    pwrite_all(off, count * 8ull, kBucketHeader + 4ull * nrows_ + 8ull * first_row);
+}
+
+void BucketFile::write_runs(uint64_t first_run, const uint32_t* runs, uint64_t count) {
+    pwrite_all(runs, count * 4ull, kBucketHeader + 4ull * nrows_ + 8ull * (nrows_ + 1ull) + 4ull * first_run);
+}
+
+void BucketFile::close(uint64_t total) {
+    pwrite_all(&total, 8, 32);
+    const int fd = fd_;
+    fd_ = -1;
+    if (::close(fd) != 0) throw Error(CPD_E_IO, "close failed: " + tmp_);
+    if (std::rename(tmp_.c_str(), path_.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path_);
 }
 
 CpdBucket read_bucket(const std::string& path) {

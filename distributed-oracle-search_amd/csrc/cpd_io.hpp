@@ -56,6 +56,31 @@ std::string bucket_path(const std::string& outdir, const std::string& xy_path,
 std::string order_path(const std::string& outdir, const std::string& xy_path);
 
 void write_bucket(const std::string& path, const CpdBucket& b);
+
+// A bucket file written in pieces, from several threads and in any order:
+// header fields and targets at open, offsets and runs by positional writes
+// into the layout write_bucket produces, the total at close (then the .tmp is
+// renamed).  The finished file is byte-identical to write_bucket's.
+class BucketFile {
+public:
+    // `b` supplies the header fields and targets (its offsets/runs are unused)
+    BucketFile(const std::string& path, const CpdBucket& b);
+    ~BucketFile();  // without close(): the .tmp is removed
+    BucketFile(const BucketFile&) = delete;
+    BucketFile& operator=(const BucketFile&) = delete;
+    uint32_t nrows() const { return nrows_; }
+    // offsets of rows [first_row, first_row + count), bucket-relative
+    void write_offsets(uint32_t first_row, const uint64_t* off, uint32_t count);
+    // runs [first_run, first_run + count) of the bucket
+    void write_runs(uint64_t first_run, const uint32_t* runs, uint64_t count);
+    void close(uint64_t total);
+
+private:
+    void pwrite_all(const void* p, size_t bytes, uint64_t pos);
+    std::string path_, tmp_;
+    int fd_ = -1;
+    uint32_t nrows_ = 0;
+};
 CpdBucket read_bucket(const std::string& path);
 void write_order(const std::string& path, uint64_t fingerprint, const std::vector<uint32_t>& order);
 std::vector<uint32_t> read_order(const std::string& path, uint64_t fingerprint);

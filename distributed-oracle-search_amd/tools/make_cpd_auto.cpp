@@ -8,6 +8,8 @@
 //                 [--batch B]          rows per GPU sweep (multiple of 1024)
 //                 [--threads T]        host threads for the hierarchy build
 //                 [--plan P | --no-plan-cache]
+//                 [--write-threads T]  host threads copying + writing rows (8)
+//                 [--no-pipeline]      build, then export, then write, per group
 //
 // Builds the CPD rows of every target this worker owns under the
 // distribution_controller partition, on the GPU, and writes one file per
@@ -18,8 +20,16 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cli.hpp"
@@ -37,6 +47,162 @@ static std::string dir_of(const std::string& p) {
     return s == std::string::npos ? "." : p.substr(0, s);
 }
 
+static void ok(int rc, const char* what) {
+    if (rc != CPD_OK)
+        throw std::runtime_error(std::string(what) + " failed (" + std::to_string(rc) + "): " + cpd_last_error());
+}
+
+// Overlapped bucket writer ("overlap D2H of RLE rows with
+// the next batch's SSSP, plus parallel bucket-file writes").  Rows are built
+// one sweep batch (B rows) per block, in bucket order, alternating between two
+// cpd_rows.  While the GPU builds block k+1, a pool of host threads copies
+// block k out of HBM in pieces (cpd_rows_export_range: each thread on its own
+// stream) and writes each piece straight to its final position in its bucket
+// file (BucketFile), so no bucket is ever held whole in host memory.  A
+// bucket's .tmp is renamed once its last block is written.  The files are
+// byte-identical to the sequential path (--no-pipeline).
+class Pipeline {
+public:
+    Pipeline(cpd_graph* g, uint32_t B, int threads) : g_(g), B_(B) {
+        for (int i = 0; i < std::max(1, threads); ++i) pool_.emplace_back([this] { worker(); });
+    }
+    ~Pipeline() {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : pool_) t.join();
+        for (cpd_rows* r : rows_)
+            if (r) cpd_rows_free(r);
+    }
+
+    void run(const std::vector<uint32_t>& targets, const std::vector<uint64_t>& first,
+             const std::vector<CpdBucket>& heads, const std::vector<std::string>& paths) {
+        using cpd::io::BucketFile;
+        const size_t N = targets.size(), nb = heads.size();
+        std::vector<std::unique_ptr<BucketFile>> files(nb);
+        std::vector<uint64_t> bruns(nb, 0);  // runs of the bucket's rows scheduled so far
+        std::vector<size_t> to_close;        // buckets finished by the block in flight
+        for (size_t k = 0; k < nb; ++k)
+            if (first[k] == first[k + 1]) {  // empty bucket: header + one offset
+                BucketFile f(paths[k], heads[k]);
+                const uint64_t zero = 0;
+                f.write_offsets(0, &zero, 1);
+                f.close(0);
+            }
+        size_t kb = 0;
+        for (size_t b0 = 0, blk = 0; b0 < N; b0 += B_, ++blk) {
+            const uint32_t cnt = (uint32_t)std::min<size_t>(B_, N - b0);
+            cpd_rows*& r = rows_[blk & 1];
+            const double tb = now();
+            ok(cpd_build_rows(g_, targets.data() + b0, cnt, r, &r), "build");
+            t_build += now() - tb;
+            auto offs = std::make_shared<std::vector<uint64_t>>(cnt + 1);
+            ok(cpd_rows_export_range(r, 0, cnt, offs->data(), nullptr), "export offsets");
+            // block k-1 written (it read the other cpd_rows): close what it finished
+            const double tw = now();
+            drain();
+            t_wait += now() - tw;
+            for (size_t k : to_close) {
+                files[k]->close(bruns[k]);
+                files[k].reset();
+            }
+            to_close.clear();
+            cpd_rows* rr = r;
+            for (size_t i = b0; i < b0 + cnt;) {
+                while (first[kb + 1] <= i) ++kb;
+                if (!files[kb]) files[kb] = std::make_unique<BucketFile>(paths[kb], heads[kb]);
+                BucketFile* f = files[kb].get();
+                const size_t seg_end = std::min<size_t>(first[kb + 1], b0 + cnt);
+                const uint32_t r0 = (uint32_t)(i - b0), r1 = (uint32_t)(seg_end - b0);
+                const uint32_t brow0 = (uint32_t)(i - first[kb]);
+                const uint64_t base = bruns[kb];
+                const bool last = seg_end == first[kb + 1];
+                submit([=] {  // bucket-relative offsets; the end offset with the last rows
+                    std::vector<uint64_t> o;
+                    for (uint32_t u = r0; u < r1 + (last ? 1u : 0u); ++u)
+                        o.push_back(base + (*offs)[u] - (*offs)[r0]);
+                    f->write_offsets(brow0, o.data(), (uint32_t)o.size());
+                });
+                for (uint32_t p0 = r0; p0 < r1;) {
+                    uint32_t p1 = p0 + 1;
+                    while (p1 < r1 && (*offs)[p1 + 1] - (*offs)[p0] <= kPieceRuns) ++p1;
+                    const uint64_t run0 = base + (*offs)[p0] - (*offs)[r0];
+                    submit([=] {
+                        thread_local std::vector<uint32_t> buf;
+                        const uint64_t nr = (*offs)[p1] - (*offs)[p0];
+                        buf.resize(nr);
+                        ok(cpd_rows_export_range(rr, p0, p1 - p0, nullptr, buf.data()), "export");
+                        f->write_runs(run0, buf.data(), nr);
+                    });
+                    p0 = p1;
+                }
+                bruns[kb] += (*offs)[r1] - (*offs)[r0];
+                if (last) to_close.push_back(kb);
+                i = seg_end;
+            }
+            runs += offs->back();
+        }
+        const double tw = now();
+        drain();
+        t_wait += now() - tw;
+        for (size_t k : to_close) files[k]->close(bruns[k]);
+    }
+
+    double t_build = 0, t_wait = 0;
+    uint64_t runs = 0;
+
+private:
+    static constexpr uint64_t kPieceRuns = 64ull << 20;  // 256 MB of runs per copy+write
+
+    void submit(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            q_.push_back(std::move(f));
+            ++pending_;
+        }
+        cv_.notify_one();
+    }
+    void drain() {  // wait for every submitted job; rethrow the first failure
+        std::unique_lock<std::mutex> l(mu_);
+        done_.wait(l, [this] { return pending_ == 0; });
+        if (err_) std::rethrow_exception(err_);
+    }
+    void worker() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                cv_.wait(l, [this] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            std::exception_ptr e;
+            try {
+                f();
+            } catch (...) {
+                e = std::current_exception();
+            }
+            std::lock_guard<std::mutex> l(mu_);
+            if (e && !err_) err_ = e;
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+
+    cpd_graph* g_;
+    uint32_t B_;
+    cpd_rows* rows_[2] = {nullptr, nullptr};
+    std::vector<std::thread> pool_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::deque<std::function<void()>> q_;
+    size_t pending_ = 0;
+    bool stop_ = false;
+    std::exception_ptr err_;
+};
+
 int main(int argc, char** argv) {
     cli::Args a(argc, argv);
     std::string input = a.str("input");
@@ -46,7 +212,8 @@ int main(int argc, char** argv) {
         std::fprintf(stderr,
                      "usage: make_cpd_auto --input X.xy --partmethod {div|mod} --partkey K "
                      "--workerid I --maxworker W [--outdir D] [--device G] [--batch B] "
-                     "[--threads T] [--plan P | --no-plan-cache]\n");
+                     "[--threads T] [--plan P | --no-plan-cache] [--write-threads T] "
+                     "[--no-pipeline]\n");
         return 2;
     }
     int mcode = cli::method_code(method);
@@ -117,46 +284,75 @@ int main(int argc, char** argv) {
         double t_build = 0, t_io = 0;
         uint64_t rows_done = 0, runs_done = 0;
         cpd_rows* rows = nullptr;
-        size_t i = 0;
-        while (i < owned.size()) {
-            // gather buckets until at least 4 sweeps' worth of rows
-            std::vector<uint32_t> group, targets;
-            std::vector<size_t> first;
-            while (i < owned.size() && targets.size() < 4ull * B) {
-                auto v = bucket_nodes(owned[i]);
-                group.push_back(owned[i]);
+        if (a.has("no-pipeline")) {
+            size_t i = 0;
+            while (i < owned.size()) {
+                // gather buckets until at least 4 sweeps' worth of rows
+                std::vector<uint32_t> group, targets;
+                std::vector<size_t> first;
+                while (i < owned.size() && targets.size() < 4ull * B) {
+                    auto v = bucket_nodes(owned[i]);
+                    group.push_back(owned[i]);
+                    first.push_back(targets.size());
+                    targets.insert(targets.end(), v.begin(), v.end());
+                    ++i;
+                }
                 first.push_back(targets.size());
-                targets.insert(targets.end(), v.begin(), v.end());
-                ++i;
+                double tb = now();
+                cli::check(cpd_build_rows(dg, targets.data(), (uint32_t)targets.size(), rows, &rows), "build");
+                uint32_t nr = 0;
+                uint64_t tot = 0;
+                cli::check(cpd_rows_count(rows, &nr, &tot), "rows");
+                std::vector<uint64_t> off(nr + 1);
+                std::vector<uint32_t> runs(tot);
+                cli::check(cpd_rows_export(rows, off.data(), runs.data()), "export");
+                t_build += now() - tb;
+                double ti = now();
+                for (size_t k = 0; k < group.size(); ++k) {
+                    CpdBucket b;
+                    b.n = g.n;
+                    b.bid = group[k];
+                    b.method = (uint32_t)mcode;
+                    b.key = (uint32_t)key;
+                    b.maxworker = (uint32_t)W;
+                    b.fingerprint = fp;
+                    b.targets.assign(targets.begin() + first[k], targets.begin() + first[k + 1]);
+                    uint64_t base = off[first[k]];
+                    for (size_t r = first[k]; r <= first[k + 1]; ++r) b.offsets.push_back(off[r] - base);
+                    b.runs.assign(runs.begin() + base, runs.begin() + off[first[k + 1]]);
+                    cpd::io::write_bucket(cpd::io::bucket_path(outdir, input, method, (uint32_t)key, group[k]), b);
+                }
+                t_io += now() - ti;
+                rows_done += nr;
+                runs_done += tot;
             }
-            first.push_back(targets.size());
-            double tb = now();
-            cli::check(cpd_build_rows(dg, targets.data(), (uint32_t)targets.size(), rows, &rows), "build");
-            uint32_t nr = 0;
-            uint64_t tot = 0;
-            cli::check(cpd_rows_count(rows, &nr, &tot), "rows");
-            std::vector<uint64_t> off(nr + 1);
-            std::vector<uint32_t> runs(tot);
-            cli::check(cpd_rows_export(rows, off.data(), runs.data()), "export");
-            t_build += now() - tb;
-            double ti = now();
-            for (size_t k = 0; k < group.size(); ++k) {
-                CpdBucket b;
+        } else {
+            Pipeline pl(dg, B, (int)a.num("write-threads", 8));
+            std::vector<uint32_t> targets;
+            std::vector<CpdBucket> heads(owned.size());
+            std::vector<uint64_t> first(owned.size() + 1, 0);
+            for (size_t k = 0; k < owned.size(); ++k) {
+                CpdBucket& b = heads[k];
                 b.n = g.n;
-                b.bid = group[k];
+                b.bid = owned[k];
                 b.method = (uint32_t)mcode;
                 b.key = (uint32_t)key;
                 b.maxworker = (uint32_t)W;
                 b.fingerprint = fp;
-                b.targets.assign(targets.begin() + first[k], targets.begin() + first[k + 1]);
-                uint64_t base = off[first[k]];
-                for (size_t r = first[k]; r <= first[k + 1]; ++r) b.offsets.push_back(off[r] - base);
-                b.runs.assign(runs.begin() + base, runs.begin() + off[first[k + 1]]);
-                cpd::io::write_bucket(cpd::io::bucket_path(outdir, input, method, (uint32_t)key, group[k]), b);
+                b.targets = bucket_nodes(owned[k]);
+                first[k] = targets.size();
+                targets.insert(targets.end(), b.targets.begin(), b.targets.end());
+                b.targets.shrink_to_fit();
             }
-            t_io += now() - ti;
-            rows_done += nr;
-            runs_done += tot;
+            first[owned.size()] = targets.size();
+            std::vector<std::string> paths(owned.size());
+            for (size_t k = 0; k < owned.size(); ++k)
+                paths[k] = cpd::io::bucket_path(outdir, input, method, (uint32_t)key, owned[k]);
+            pl.run(targets, first, heads, paths);
+            t_build = pl.t_build;
+            t_io = pl.t_wait;
+            rows_done = targets.size();
+            runs_done = pl.runs;
         }
         if (rows) cpd_rows_free(rows);
         cpd_graph_free(dg);
@@ -165,11 +361,12 @@ int main(int argc, char** argv) {
         std::printf(
             "make_cpd_auto: worker %lld/%lld device %d: %llu rows in %zu buckets, %llu runs "
             "(%.1f per row); read %.3fs plan %.3fs (hierarchy %llu arcs, %u+%u levels) "
-            "build %.3fs = %.1f rows/s, %.3f GTEPS; write %.3fs; total %.3fs\n",
+            "build %.3fs = %.1f rows/s, %.3f GTEPS; write %.3fs%s; total %.3fs\n",
             wid, W, device, (unsigned long long)rows_done, owned.size(),
             (unsigned long long)runs_done, rows_done ? (double)runs_done / rows_done : 0.0, t_read,
             t_plan, (unsigned long long)(info.ch_up_arcs + info.ch_dn_arcs), info.levels_up,
-            info.levels_dn, t_build, rate, rate * g.m / 1e9, t_io, now() - t_start);
+            info.levels_dn, t_build, rate, rate * g.m / 1e9, t_io,
+            a.has("no-pipeline") ? "" : " (not hidden behind the build)", now() - t_start);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "make_cpd_auto: %s\n", e.what());
         return 1;

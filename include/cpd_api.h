@@ -165,6 +165,14 @@ int  cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
 int  cpd_rows_count(const cpd_rows* r, uint32_t* nrows, uint64_t* total_runs);
 int  cpd_rows_export(const cpd_rows* r, uint64_t* offsets /* nrows+1 */,
                      uint32_t* runs /* total_runs */);
+/* Rows [first, first + count) of r: offsets relative to row `first`
+ * (count + 1 values, offsets[0] = 0) and their runs.  Copies on a stream of
+ * the calling thread's own, so exports from several host threads, and a
+ * cpd_build_rows into ANOTHER cpd_rows on the same device, run concurrently
+ * (the overlapped writer of bin/make_cpd_auto).  Either output may be NULL. */
+int  cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count,
+                           uint64_t* offsets /* count+1 */, uint32_t* runs);
+int  cpd_rows_targets(const cpd_rows* r, uint32_t* targets /* nrows */);
 void cpd_rows_free(cpd_rows* r);
 
 /* [gpu] Inspection (tests): distances d(n,t) in NODE order, n-major

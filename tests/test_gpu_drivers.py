@@ -119,3 +119,56 @@ def test_drivers_end_to_end(tmp_path, method, key):
             fifo = f"/tmp/worker{wid}.fifo"
             if os.path.exists(fifo):
                 os.remove(fifo)
+
+
+def _read_bucket(path):
+    """The bucket layout of csrc/cpd_io.cpp (write_bucket / BucketFile)."""
+    raw = open(path, "rb").read()
+    assert raw[:8] == b"DOSCPD01"
+    n, nrows, bid, method, key, maxworker = np.frombuffer(raw, np.uint32, 6, 8)
+    total = int(np.frombuffer(raw, np.uint64, 1, 32)[0])
+    p = 48
+    targets = np.frombuffer(raw, np.uint32, nrows, p)
+    p += 4 * int(nrows)
+    off = np.frombuffer(raw, np.uint64, nrows + 1, p)
+    p += 8 * (int(nrows) + 1)
+    runs = np.frombuffer(raw, np.uint32, total, p)
+    assert p + 4 * total == len(raw)
+    return targets, off, runs
+
+
+@pytest.mark.parametrize("method,key", [("mod", 5), ("div", 7)])
+def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key):
+    """The overlapped writer (build block k+1 while a pool copies block k out
+    of HBM and writes it in place) gives byte-identical bucket files to the
+    sequential path; with --batch 1024 the blocks straddle bucket boundaries
+    and --write-threads 3 interleaves pieces of several buckets."""
+    prefix = str(tmp_path / "g")
+    subprocess.run([os.path.join(BIN, "gen_synth"), "--width", "64", "--height", "48", "--seed",
+                    "5", "--out", prefix, "--queries", "10"], check=True, capture_output=True)
+    xy = prefix + ".xy"
+    dirs = {}
+    for mode, extra in [("seq", ["--no-pipeline"]), ("pipe", ["--write-threads", "3"])]:
+        out = str(tmp_path / mode)
+        p = subprocess.run([os.path.join(BIN, "make_cpd_auto"), "--input", xy, "--partmethod",
+                            method, "--partkey", str(key), "--workerid", "1", "--maxworker", "2",
+                            "--outdir", out, "--device", "0", "--batch", "1024",
+                            "--plan", str(tmp_path / "g.plan")] + extra,
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr
+        dirs[mode] = out
+    seq = sorted(f for f in os.listdir(dirs["seq"]) if f.endswith(".cpd"))
+    pipe = sorted(f for f in os.listdir(dirs["pipe"]) if f.endswith(".cpd"))
+    assert seq == pipe and len(seq) == key // 2
+    assert not [f for f in os.listdir(dirs["pipe"]) if f.endswith(".tmp")]
+    for f in seq:
+        a = open(os.path.join(dirs["seq"], f), "rb").read()
+        b = open(os.path.join(dirs["pipe"], f), "rb").read()
+        assert a == b, f
+    # one bucket against the CPU oracle
+    g = cpd.synth_road_graph(64, 48, seed=5)
+    order = oracle.dfs_preorder(g.row_ptr, g.dst)
+    targets, off, runs = _read_bucket(os.path.join(dirs["pipe"], pipe[0]))
+    o_off, o_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, np.array(targets))
+    np.testing.assert_array_equal(off, o_off)
+    np.testing.assert_array_equal(runs, o_runs)
