@@ -41,7 +41,8 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--partmethod", default="div")
     ap.add_argument("--partkey", type=int, default=8)
-    ap.add_argument("--batch", type=int, default=16384, help="rows per step (multiple of 1024)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="rows per step (multiple of 1024); 0 = what fits in HBM, <= 16384")
     ap.add_argument("--queries", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--cpu-rows-per-thread", type=int, default=64,

@@ -127,6 +127,12 @@ struct cpd_graph {
     // CPD_NARROW=0 at graph creation or a finite distance could reach the
     // wide-row marker; group rows that do not fit are kept wide (counted)
     bool narrow = false;
+    // the first kNarrowProbe full batches count their wide group rows; if
+    // most are wide (long edges: the spread of 256 distances passes 0xFFFF),
+    // narrow rows only add a base load per gather and are switched off for
+    // the graph's lifetime — the results are identical either way
+    static constexpr uint32_t kNarrowProbe = 2;
+    uint32_t narrow_probe = kNarrowProbe;
     uint32_t ovf_h = 0;
     DevBuf<uint16_t> d16;
     DevBuf<uint32_t> dbase, ovf;
@@ -184,11 +190,16 @@ struct cpd_graph {
     // (per-packet profiling signals cost ~7 us per launch, ~3 % of a batch's
     // ~580 sweep launches; the group interval also counts the inter-kernel
     // gaps, so its per-launch average is a slight over-estimate).
+    // Every launch is checked: hipGetLastError() is cleared first, so an
+    // error left behind by an unrelated earlier runtime call on this thread
+    // (it is sticky until read) is not blamed on the launch.
     template <class F>
     void timed(const char* name, double bytes, F&& launch,
                std::function<double()> late_bytes = nullptr) {
+        (void)hipGetLastError();
         if (!timing) {
             launch();
+            HIP_CHECK(hipGetLastError());
             return;
         }
         if (group_open && std::strcmp(group.name, name) == 0) {
@@ -249,9 +260,13 @@ struct cpd_graph {
         if (want == 0) {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-            // per target: dist 4n (+ 2n narrow) + fm + output runs (<= 4n, ~2.5n typical)
-            double per = (narrow ? 6.0 : 4.0) * n + fmb / 8.0 * npad + 4.0 * n;
-            double fit = 0.4 * (double)free_b / per;
+            // per target: dist 4n (+ 2n narrow) + fm + leaf sets + RLE segment
+            // states + one row of output runs at its worst case (4n; ~2.5n on
+            // road graphs), leaving a quarter of free HBM for the rest
+            const double per = (narrow ? 6.0 : 4.0) * n + fmb / 8.0 * npad +
+                               (leaf_fm ? 0.5 * n : 0.0) + (fmb == 4 ? 5.0 / 32.0 * npad : 0.0) +
+                               4.0 * n;
+            const double fit = 0.75 * (double)free_b / per;
             want = (uint32_t)std::min(16384.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
         }
         want = (want + 1023u) / 1024u * 1024u;
@@ -421,6 +436,7 @@ void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& as
         if (!ascend && !(nodes[s] & (kLeafBit | kL1Bit))) lvl_reads[level[v]] += 1.0;
     }
 }
+
 
 }  // namespace
 
@@ -624,6 +640,22 @@ bool sort_on() {
 
 // Distances + first-move sets for `k` targets (columns already in g->tgt,
 // padded to a multiple of 1024 with valid columns).
+bool trace_on();
+
+// After a full narrow batch (g->ovf_h = its wide group rows): switch narrow
+// rows off for good when most group rows had to be kept wide.
+void narrow_decide(cpd_graph* g) {
+    const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
+    if (2ull * g->ovf_h <= groups) return;
+    g->narrow = false;
+    g->narrow_probe = 0;
+    g->d16.release();
+    g->dbase.release();
+    if (trace_on())
+        std::fprintf(stderr, "[cpd] narrow rows off: %u of %llu group rows wide\n", g->ovf_h,
+                     (unsigned long long)groups);
+}
+
 void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow) {
     const uint32_t B = g->B, n = g->n;
     const NarrowRows nr = g->narrow_rows(narrow);
@@ -702,7 +734,7 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow) {
         }, std::move(late));
     }
     g->group_end();
-    if (narrow && g->timing)
+    if (narrow && (g->timing || g->narrow_probe))
         launch_count_wide_rows(g->dbase.p, (size_t)n * (B / 256u),
                                reinterpret_cast<unsigned int*>(g->ovf.p), g->stream);
     if (live && stat && nasc > 2) {  // row counts behind the late byte counts
@@ -789,13 +821,19 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     std::vector<uint32_t> counts(k);
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, g->stream));
-    if (g->narrow && g->timing)
+    const bool probe = g->narrow && g->narrow_probe && k == g->B;
+    if (g->narrow && (g->timing || probe))
         HIP_CHECK(hipMemcpyAsync(&g->ovf_h, g->ovf.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                  g->stream));
     g->sync();
+    const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
     if (g->narrow && g->timing) {  // group rows kept wide / all group rows
         g->agg["wide_rows"].launches += g->ovf_h;
-        g->agg["group_rows"].launches += (uint64_t)g->n * (g->B / 256u);
+        g->agg["group_rows"].launches += groups;
+    }
+    if (probe) {
+        --g->narrow_probe;
+        narrow_decide(g);
     }
     const double t2 = now_seconds();
     // row offsets for this batch in the caller's order, appended after

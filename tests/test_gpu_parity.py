@@ -176,7 +176,8 @@ def test_multi_slab_batches(width, batch):
 def test_narrow_overflow_rows_kept_wide():
     """Edge weights x700: a wave's 256 distances spread past 0xFFFF, so the
     narrow rows cannot hold them; those group rows are kept 32-bit (base =
-    wide marker) and every output stays exact."""
+    wide marker) and every output stays exact.  The first full batch finds
+    most group rows wide and switches narrow rows off for the second."""
     g0 = cpd.synth_road_graph(40, 40, seed=12)
     g = cpd.RoadGraph(g0.row_ptr, g0.dst, (g0.w * 700).astype(np.uint32), g0.x, g0.y)
     plan = cpd.Plan(g)
@@ -194,3 +195,26 @@ def test_narrow_overflow_rows_kept_wide():
         np.testing.assert_array_equal(
             dist[:, i], oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, targets[i]))
         np.testing.assert_array_equal(fm[i], oracle.first_moves(g.row_ptr, g.dst, g.w, targets[i]))
+
+
+@pytest.mark.parametrize("scale,narrow_kept", [(1, True), (700, False)])
+def test_narrow_rows_switched_off_when_mostly_wide(scale, narrow_kept):
+    """The first full batches count their wide group rows; when most are
+    wide, narrow rows are switched off for the graph's lifetime (later builds
+    record no narrow batch in the timing counters).  Rows stay bit-exact
+    before, across and after the switch."""
+    g0 = cpd.synth_road_graph(70, 70, seed=13)
+    g = cpd.RoadGraph(g0.row_ptr, g0.dst, (g0.w * scale).astype(np.uint32), g0.x, g0.y)
+    plan = cpd.Plan(g)
+    dev = make_graph(plan, 1024, True)
+    dev.timing(True)
+    rng = np.random.default_rng(13)
+    targets = rng.permutation(g.n).astype(np.uint32)[:1500]
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    for rep in range(2):
+        dev.timing_reset()
+        off, runs = dev.build_rows(targets).export()
+        np.testing.assert_array_equal(off, ref_off)
+        np.testing.assert_array_equal(runs, ref_runs)
+        if rep == 1:
+            assert ("group_rows" in dev.timing_get()) == narrow_kept
