@@ -301,6 +301,11 @@ def main():
         f"{pinfo['levels_up']}+{pinfo['levels_dn']})")
 
     dev = cpd.Graph(plan, device=gpu, batch=args.batch)
+    # every rank builds the same number of rows per step (weak scaling): the
+    # smallest batch any rank's free HBM allows
+    (bmin,) = comm.reduce([float(dev.batch)], "MIN")
+    if int(bmin) != dev.batch:
+        dev.set_batch(int(bmin))
     B = dev.batch
     owned = shard_targets(g.n, world, args.partmethod, args.partkey, rank)
     if len(owned) == 0:

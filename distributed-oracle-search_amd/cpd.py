@@ -319,6 +319,10 @@ class Graph:
         _check(lib.cpd_graph_get_batch(self._h, C.byref(b)))
         return b.value
 
+    def set_batch(self, batch: int) -> None:
+        """Rows per sweep (multiple of 1024; 0 = what fits in free HBM)."""
+        _check(lib.cpd_graph_set_batch(self._h, C.c_uint32(batch)))
+
     def build_rows(self, targets, reuse: Rows | None = None) -> Rows:
         t = _u32(targets)
         h = C.c_void_p()
