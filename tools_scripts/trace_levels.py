@@ -22,7 +22,7 @@ def main(d):
     for k, (c, us) in sorted(tot.items(), key=lambda kv: -kv[1][1]):
         print(f"{k[:40]:40s} {c:6d} {us / 1e3:10.2f} {us / c:8.1f}")
     # per level: sweeps between two first_moves launches form one batch
-    for kind in ("sweep_up_sparse", "sweep_level<false>", "sweep_level<true>"):
+    for kind in ("sweep_up_sparse", "sweep_up_chunks", "sweep_down8", "sweep_level<false>", "sweep_level<true>"):
         per = defaultdict(list)
         idx = 0
         for r in rows:
