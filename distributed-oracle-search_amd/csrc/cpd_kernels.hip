@@ -34,6 +34,9 @@ __device__ __forceinline__ uint32_t sat_add(uint32_t d, uint32_t w) {
 // same way.  The wildcard is all FMB bits: every real set lies inside them
 // (FMB >= out-degree), so S & wildcard == S and lowest-bit(wildcard) == 0 as
 // with the u16 0xFFFF of the oracle — the scan's output is unchanged.
+#ifndef CPD_RLE_LOOKBACK
+#define CPD_RLE_LOOKBACK 16  // RLE guess: columns of the predecessor's segment rescanned
+#endif
 constexpr uint32_t kSeg = 32;          // columns per lane
 constexpr uint32_t kTile = 64 * kSeg;  // columns per wave tile (npad % kTile == 0)
 
@@ -1002,7 +1005,7 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
                                                 uint32_t* __restrict__ runs, RleState rs) {
     using F = FmFmt<FMB>;
     constexpr int Q = F::kWords / 4;  // 16-B loads per lane per tile
-    constexpr int LB = 16;            // lookback columns
+    constexpr int LB = CPD_RLE_LOOKBACK;  // lookback columns
     __shared__ uint32_t stage_all[EMIT ? 4 * kTile : 1];
     const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -1053,9 +1056,11 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
             cnt = crc;
         } else {
             // guess: the predecessor's last LB columns from a fresh run
-            uint32_t pv[F::kWords / 2];
+            constexpr int PW = LB / F::kPer;  // words holding those columns
+            static_assert(LB % F::kPer == 0 && PW <= F::kWords, "lookback: whole words");
+            uint32_t pv[PW];
 #pragma unroll
-            for (int i = 0; i < F::kWords / 2; ++i) pv[i] = __shfl_up(v[F::kWords / 2 + i], 1, 64);
+            for (int i = 0; i < PW; ++i) pv[i] = __shfl_up(v[F::kWords - PW + i], 1, 64);
             uint32_t gh = c0 - LB, gS = F::kAll;
 #pragma unroll
             for (int k = 0; k < LB; ++k) {
