@@ -285,6 +285,8 @@ def main():
     # GPU 0 and the harness collectives go over gloo.  Never used for numbers.
     share = os.environ.get("CPD_BENCH_SHARE_GPU") == "1"
     gpu = 0 if share else local
+    if share and args.batch == 0:  # ranks sized from one card's free HBM would overcommit it
+        args.batch = 4096
     if world > 1:
         if share:
             dist.init_process_group("gloo")
