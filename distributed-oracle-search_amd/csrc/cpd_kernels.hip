@@ -846,7 +846,12 @@ struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR press
     uint32_t lv[G];
 };
 
-template <int G>
+// S = 32-column segments per workgroup: with S = 2 a lane stores 32 contiguous
+// bytes of each of its 4 rows (two 16-B stores back to back) instead of 16,
+// so fewer partial-sector writes reach HBM (PMC writes 14.2 -> 10.1 GB per
+// 16384-row launch) — but the kernel is slower (16.0 -> 17.7 ms at 101 VGPRs,
+// 18.9 ms capped to 96 with spills): S = 1 is the default (CPD_FM_SEGS=2 to try).
+template <int G, int S>
 __global__ __launch_bounds__(256) void first_moves_n4(const uint2* __restrict__ adj,
                                                       const uint32_t* __restrict__ dist,
                                                       const uint32_t* __restrict__ tgt, uint32_t B,
@@ -856,31 +861,44 @@ __global__ __launch_bounds__(256) void first_moves_n4(const uint2* __restrict__ 
                                                       const uint16_t* __restrict__ fmleaf,
                                                       NarrowRows nr) {
     static_assert(kSeg % G == 0, "group size");
-    const uint32_t nseg = npad / kSeg;
+    const uint32_t nblk = npad / (kSeg * S);
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t slab = L / nseg;
+    const uint32_t slab = L / nblk;
     const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t B4 = B / 4u;
-    const uint32_t c0 = (L - slab * nseg) * kSeg;
+    const uint32_t cb = (L - slab * nblk) * (kSeg * S);
     const uint32_t lane = threadIdx.x & 63u;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
     const uint32_t grp = wave_group(l4);
-    const uint32_t lbits = leafbits ? leafbits[c0 / kSeg] : 0u;
-    const uint4 sa = c0 + lane / 2u < n ? reinterpret_cast<const uint4*>(adj)[(size_t)c0 * 2u + lane]
-                                        : make_uint4(kNoEdge, 0u, kNoEdge, 0u);
-    auto edge = [&](int cc, int k) -> uint2 {  // wave-uniform
-        const int ln = 2 * cc + (k >> 1);
-        const uint32_t x = __builtin_amdgcn_readlane((k & 1) ? sa.z : sa.x, ln);
-        const uint32_t w = __builtin_amdgcn_readlane((k & 1) ? sa.w : sa.y, ln);
+    uint32_t pk[4][4 * S];
+#pragma unroll
+    for (int p = 0; p < 4 * S; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
+    // the block's adjacency (S x 1 KiB) and leaf bits up front; the group
+    // pipeline then runs over all S x 32 columns without a bubble
+    uint4 sa[S];
+    uint32_t lb[S];
+#pragma unroll
+    for (int sg = 0; sg < S; ++sg) {
+        const uint32_t c0 = cb + (uint32_t)sg * kSeg;
+        lb[sg] = leafbits ? leafbits[c0 / kSeg] : 0u;
+        sa[sg] = c0 + lane / 2u < n ? reinterpret_cast<const uint4*>(adj)[(size_t)c0 * 2u + lane]
+                                    : make_uint4(kNoEdge, 0u, kNoEdge, 0u);
+    }
+    auto edge = [&](int cc, int k) -> uint2 {  // wave-uniform; cc in [0, S x 32)
+        const uint4& q = sa[cc / (int)kSeg];
+        const int ln = 2 * (cc % (int)kSeg) + (k >> 1);
+        const uint32_t x = __builtin_amdgcn_readlane((k & 1) ? q.z : q.x, ln);
+        const uint32_t w = __builtin_amdgcn_readlane((k & 1) ? q.w : q.y, ln);
         return make_uint2(x, w);
     };
+    auto is_leaf = [&](int cc) -> bool { return (lb[cc / (int)kSeg] >> (cc % (int)kSeg)) & 1u; };
     auto issue = [&](FmGroup<G>& g, int cg) {
 #pragma unroll
         for (int j = 0; j < G; ++j) {
-            const uint32_t c = c0 + (uint32_t)(cg + j);
+            const uint32_t c = cb + (uint32_t)(cg + j);
             const bool ok = c < n;
-            const bool leaf = (lbits >> (cg + j)) & 1u;
+            const bool leaf = is_leaf(cg + j);
             if (ok && !leaf) {
                 g.own[j] = nl_issue(nr, c, grp, B4, l4);
 #pragma unroll
@@ -892,17 +910,14 @@ __global__ __launch_bounds__(256) void first_moves_n4(const uint2* __restrict__ 
             g.lv[j] = ok && leaf ? fmleaf[(size_t)c * B4 + l4] : 0u;
         }
     };
-    uint32_t pk[4][4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
     auto finish = [&](const FmGroup<G>& g, int cg) {
 #pragma unroll
         for (int j = 0; j < G; ++j) {
-            const uint32_t c = c0 + (uint32_t)(cg + j);
+            const uint32_t c = cb + (uint32_t)(cg + j);
             if (c >= n) continue;  // stays the wildcard padding
             const int cc = cg + j;
             uint32_t f0, f1, f2, f3;
-            if ((lbits >> cc) & 1u) {  // 4 nibbles, wildcards included
+            if (is_leaf(cc)) {  // 4 nibbles, wildcards included
                 f0 = g.lv[j] & 0xFu;
                 f1 = (g.lv[j] >> 4) & 0xFu;
                 f2 = (g.lv[j] >> 8) & 0xFu;
@@ -934,19 +949,24 @@ __global__ __launch_bounds__(256) void first_moves_n4(const uint2* __restrict__ 
             pk[3][wi] = (pk[3][wi] & keep) | (f3 << sh);
         }
     };
+    constexpr int NC = S * (int)kSeg;
     FmGroup<G> cur, nxt;
     issue(cur, 0);
 #pragma unroll
-    for (int cg = 0; cg < (int)kSeg; cg += G) {
-        if (cg + G < (int)kSeg) issue(nxt, cg + G);
+    for (int cg = 0; cg < NC; cg += G) {
+        if (cg + G < NC) issue(nxt, cg + G);
         finish(cur, cg);
         cur = nxt;
     }
     const size_t row_words = npad / 8u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * row_words + c0 / 8u) =
-            make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
+    for (int i = 0; i < 4; ++i) {
+        uint4* __restrict__ o =
+            reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * row_words + cb / 8u);
+#pragma unroll
+        for (int sg = 0; sg < S; ++sg)
+            o[sg] = make_uint4(pk[i][4 * sg], pk[i][4 * sg + 1], pk[i][4 * sg + 2], pk[i][4 * sg + 3]);
+    }
 }
 
 // One lane's greedy pass over its 32 columns (warthog graph_oracle::add_row
@@ -1366,6 +1386,10 @@ uint32_t fm_n4() {  // CPD_FM_N4=0: narrow first moves without the pipelined ker
     static const uint32_t v = env_u32("CPD_FM_N4", 1);
     return v;
 }
+uint32_t fm_segs() {  // CPD_FM_SEGS: 32-column segments per pipelined first-moves workgroup
+    static const uint32_t v = env_u32("CPD_FM_SEGS", 1);
+    return v;
+}
 uint32_t fm_g() {
     static const uint32_t v = env_u32("CPD_FM_G", 2);
     return v;
@@ -1490,8 +1514,12 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     if (nr.d16 && shift == 2 && fm_n4()) {
         const uint32_t r = xcd_remap();
-        launch(kern::first_moves_n4<2>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits,
-               fmleaf, nr);
+        if (fm_segs() == 2)
+            launch(kern::first_moves_n4<2, 2>, dim3(grid.x / 2u), blk, s, adj, dist, tgt, B, n, npad,
+                   r, fm, leafbits, fmleaf, nr);
+        else
+            launch(kern::first_moves_n4<2, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm,
+                   leafbits, fmleaf, nr);
     } else if (nr.d16)
         launch_first_moves_t<true>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
                                    grid, blk, s);
