@@ -45,7 +45,8 @@ EXPORTED = [
     "cpd_debug_rows", "cpd_index_create", "cpd_index_from_rows", "cpd_index_set_weights",
     "cpd_query_batch", "cpd_query_prepare", "cpd_query_run", "cpd_query_fetch",
     "cpd_index_free", "cpd_timing_enable", "cpd_timing_reset", "cpd_timing_get",
-    "cpd_index_set_mode", "cpd_index_get_mode",
+    "cpd_index_set_mode", "cpd_index_get_mode", "cpd_plan_cache", "cpd_index_create_empty",
+    "cpd_index_append_rows", "cpd_index_append_built_rows", "cpd_index_info",
 ]
 INDEX_MODES = {"auto": 0, "rle": 1, "dense": 2}
 
@@ -219,6 +220,19 @@ class Plan:
         _check(lib.cpd_plan_load(path.encode(), C.byref(h)))
         return cls(_handle=h)
 
+    @classmethod
+    def cache(cls, path: str, g: RoadGraph, threads: int = 0, hierarchy: bool = True):
+        """(plan, status): the plan cached at `path` for this graph, built and
+        saved under an flock if absent (status 0 loaded, 1 built and saved,
+        2 built but not saved) — cpd_plan_cache."""
+        h = C.c_void_p()
+        st = C.c_int()
+        opts = PlanOpts(threads, 0, 0, int(not hierarchy))
+        _check(lib.cpd_plan_cache(path.encode(), _ptr(g.row_ptr, u32p), _ptr(g.dst, u32p),
+                                  _ptr(g.w, u32p), C.c_uint32(g.n), C.c_uint32(g.m),
+                                  C.byref(opts), C.byref(h), C.byref(st)))
+        return cls(_handle=h), st.value
+
     def save(self, path: str) -> None:
         _check(lib.cpd_plan_save(self._h, path.encode()))
 
@@ -362,16 +376,45 @@ class Graph:
 
 class Index:
     def __init__(self, graph: Graph, rows: Rows | None = None, row_targets=None,
-                 offsets=None, runs=None):
+                 offsets=None, runs=None, _handle=None):
         self.graph = graph
         self._h = C.c_void_p()
-        if rows is not None:
+        if _handle is not None:
+            self._h = _handle
+        elif rows is not None:
             _check(lib.cpd_index_from_rows(graph._h, rows._h, C.byref(self._h)))
         else:
             rt, off = _u32(row_targets), np.ascontiguousarray(offsets, np.uint64)
             rn = _u32(runs)
             _check(lib.cpd_index_create(graph._h, _ptr(rt, u32p), C.c_uint32(len(rt)),
                                         _ptr(off, u64p), _ptr(rn, u32p), C.byref(self._h)))
+
+    @classmethod
+    def streamed(cls, graph: Graph, row_targets, total_runs: int, mode: str = "auto") -> "Index":
+        """Empty index of len(row_targets) rows filled by append()/append_rows()
+        in order (cpd_index_create_empty)."""
+        rt = _u32(row_targets)
+        h = C.c_void_p()
+        _check(lib.cpd_index_create_empty(graph._h, _ptr(rt, u32p), C.c_uint32(len(rt)),
+                                          C.c_int(INDEX_MODES[mode]), C.c_uint64(total_runs),
+                                          C.byref(h)))
+        return cls(graph, _handle=h)
+
+    def append(self, offsets, runs) -> None:
+        """Host rows: offsets relative to the chunk (count + 1 values)."""
+        off = np.ascontiguousarray(offsets, np.uint64)
+        rn = _u32(runs)
+        _check(lib.cpd_index_append_rows(self._h, C.c_uint32(len(off) - 1), _ptr(off, u64p),
+                                         _ptr(rn, u32p)))
+
+    def append_rows(self, rows: Rows) -> None:
+        _check(lib.cpd_index_append_built_rows(self._h, rows._h))
+
+    def info(self) -> dict:
+        nr, ad, rr, db = C.c_uint32(), C.c_uint32(), C.c_uint64(), C.c_uint64()
+        _check(lib.cpd_index_info(self._h, C.byref(nr), C.byref(ad), C.byref(rr), C.byref(db)))
+        return {"nrows": nr.value, "added": ad.value, "runs_resident": rr.value,
+                "dense_bytes": db.value}
 
     def set_mode(self, mode: str) -> None:
         """'auto' (default), 'rle' or 'dense' — see cpd_index_set_mode."""

@@ -301,31 +301,50 @@ struct cpd_rows {
     DevBuf<uint64_t> off;
 };
 
+// A table-search index: nrows rows (row i = target row_targets[i]) that arrive
+// in append order — all at once (cpd_index_create / _from_rows) or streamed
+// (cpd_index_create_empty + cpd_index_append_*).  Two HBM forms:
+//   keep_rle      the RLE runs stay resident (offsets + runs); dense tables,
+//                 if asked for, are expanded from them on first use;
+//   stream_dense  each appended chunk is expanded into the 4-bit move tables
+//                 straight away and its runs are dropped, so a worker whose
+//                 runs outgrow HBM (1M nodes div 8: ~312 GB of runs, 62.5 GB
+//                 of tables) is still served.
 struct cpd_index {
     cpd_graph* g = nullptr;
-    uint32_t nrows = 0;
-    uint64_t total = 0;
+    uint32_t nrows = 0;   // rows when complete
+    uint32_t added = 0;   // rows appended so far
+    uint64_t total = 0;   // runs resident so far (keep_rle)
+    uint64_t cap = 0;     // run capacity of `runs` (keep_rle)
+    uint64_t declared = 0;  // total runs of all rows (from the caller or the rows)
     std::vector<uint32_t> row_of_col;   // host copy
-    std::vector<uint64_t> offsets;      // host copy
+    std::vector<uint64_t> offsets;      // host copy, added + 1 (keep_rle)
     DevBuf<uint32_t> d_row_of_col, runs, adj_sel;  // adj_sel: packed adjacency, custom weights
     DevBuf<uint64_t> off;
     bool custom_w = false;
     // CPD_INDEX_AUTO / _RLE / _DENSE; dense = 4-bit move tables expanded from
-    // the RLE rows (built on first use)
+    // the RLE rows (built on first use, or as rows stream in)
     int mode = CPD_INDEX_AUTO;
+    bool keep_rle = true;
+    bool stream_dense = false;
     DevBuf<uint32_t> dense;
     bool dense_ready = false;
+    // staging of host-appended chunks (stream_dense), format flag
+    DevBuf<uint32_t> stage;
+    DevBuf<uint64_t> stage_off;
+    DevBuf<uint32_t> flag;
 
     bool use_dense() const {
+        if (stream_dense) return true;
         if (mode == CPD_INDEX_DENSE) return true;
         if (mode == CPD_INDEX_RLE) return false;
         // auto: the table whose bytes are fewer (4 B per run vs n/2 B per row)
-        return nrows > 0 && 4.0 * (double)total > (double)g->npad / 2.0 * nrows;
+        return nrows > 0 && 4.0 * (double)declared > (double)g->npad / 2.0 * nrows;
     }
     // query workspace; queries run sorted by target row (perm[i] = caller index)
     uint32_t nq = 0;
     std::vector<uint32_t> perm;
-    DevBuf<uint32_t> qs, qt, hops;
+    DevBuf<uint32_t> qs, qt, qrow, hops;
     DevBuf<uint64_t> cost;
     DevBuf<uint8_t> fin;
     DevBuf<unsigned long long> agg;
@@ -1022,37 +1041,172 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
 // ---------------------------------------------------------------------------
 // Index + queries
 
+}  // extern "C"
+
+namespace {
+
+// Runs staged per host chunk of a streamed dense index (a row larger than
+// this is staged alone).
+constexpr uint64_t kStageRuns = 1ull << 28;  // 1 GiB
+
+std::unique_ptr<cpd_index> index_init(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows) {
+    CPD_REQUIRE(nrows == 0 || row_targets, CPD_E_ARG, "index: null row targets");
+    auto ix = std::make_unique<cpd_index>();
+    ix->g = g;
+    ix->nrows = nrows;
+    ix->row_of_col.assign(g->n, CPD_INF);
+    for (uint32_t i = 0; i < nrows; ++i) {
+        CPD_REQUIRE(row_targets[i] < g->n, CPD_E_ARG, "index: row target out of range");
+        ix->row_of_col[g->order[row_targets[i]]] = i;
+    }
+    ix->offsets.assign(1, 0);
+    ix->d_row_of_col.upload(ix->row_of_col.data(), g->n, g->stream);
+    ix->agg.alloc(3);
+    ix->flag.alloc(1);
+    return ix;
+}
+
+void index_keep_rle(cpd_index* ix, uint64_t cap) {
+    ix->keep_rle = true;
+    ix->stream_dense = false;
+    ix->cap = cap;
+    ix->runs.alloc(cap);
+    ix->off.alloc((size_t)ix->nrows + 1);
+    HIP_CHECK(hipMemsetAsync(ix->off.p, 0, sizeof(uint64_t), ix->g->stream));
+}
+
+void index_stream_dense(cpd_index* ix) {
+    cpd_graph* g = ix->g;
+    CPD_REQUIRE(g->npad / kFmTile < 65536u, CPD_E_RANGE, "graph too large for dense tables");
+    ix->keep_rle = false;
+    ix->stream_dense = true;
+    ix->mode = CPD_INDEX_DENSE;
+    ix->dense.alloc((size_t)ix->nrows * (g->npad / 8u));
+    ix->dense_ready = true;
+}
+
+// Host-side checks of a chunk's offsets (relative, offsets[0] == 0).
+void check_chunk_offsets(const uint64_t* offsets, uint32_t count) {
+    CPD_REQUIRE(offsets[0] == 0, CPD_E_ARG, "index: offsets[0] must be 0");
+    for (uint32_t i = 0; i < count; ++i)
+        CPD_REQUIRE(offsets[i + 1] > offsets[i], CPD_E_ARG, "index: empty or unsorted row");
+}
+
+// Format check of `count` device rows (validate_rows); throws on a bad row.
+void validate_device_rows(cpd_index* ix, const uint64_t* d_off, const uint32_t* d_runs,
+                          uint32_t count) {
+    cpd_graph* g = ix->g;
+    HIP_CHECK(hipMemsetAsync(ix->flag.p, 0, sizeof(uint32_t), g->stream));
+    g->timed("validate_rows", 0.0, [&] {
+        launch_validate_rows(d_off, d_runs, count, g->n, ix->flag.p, g->stream);
+    });
+    uint32_t bad = 0;
+    HIP_CHECK(hipMemcpyAsync(&bad, ix->flag.p, sizeof bad, hipMemcpyDeviceToHost, g->stream));
+    g->sync();
+    CPD_REQUIRE(!bad, CPD_E_ARG,
+                "index: malformed row (must start at column 0, run columns strictly increasing "
+                "and < n)");
+}
+
+// Expand `count` rows (device offsets into d_runs) into dense rows starting
+// at index row `first`.
+void expand_into(cpd_index* ix, const uint64_t* d_off, const uint32_t* d_runs, uint32_t count,
+                 uint64_t runs_in_chunk, uint32_t first) {
+    cpd_graph* g = ix->g;
+    const size_t wpr = g->npad / 8u;
+    g->timed("expand_rows", 4.0 * (double)runs_in_chunk + 4.0 * (double)wpr * count + 16.0 * count,
+             [&] {
+                 launch_expand_rows(d_off, d_runs, count, g->npad, ix->dense.p + first * wpr,
+                                    g->stream);
+             });
+}
+
+// Append `count` host rows (offsets relative, count + 1 values).
+void append_host(cpd_index* ix, uint32_t count, const uint64_t* offsets, const uint32_t* runs) {
+    cpd_graph* g = ix->g;
+    CPD_REQUIRE(offsets, CPD_E_ARG, "index: null offsets");
+    CPD_REQUIRE(count <= ix->nrows - ix->added, CPD_E_ARG, "index: more rows than declared");
+    if (!count) return;
+    check_chunk_offsets(offsets, count);
+    const uint64_t nr = offsets[count];
+    CPD_REQUIRE(runs, CPD_E_ARG, "index: null runs");
+    hipStream_t s = g->stream;
+    if (ix->keep_rle) {
+        CPD_REQUIRE(ix->total + nr <= ix->cap, CPD_E_ARG,
+                    "index: more runs than the index was created for");
+        std::vector<uint64_t> o(count + 1);
+        for (uint32_t i = 0; i <= count; ++i) o[i] = ix->total + offsets[i];
+        HIP_CHECK(hipMemcpyAsync(ix->runs.p + ix->total, runs, nr * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(ix->off.p + ix->added, o.data(), o.size() * sizeof(uint64_t),
+                                 hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        validate_device_rows(ix, ix->off.p + ix->added, ix->runs.p, count);
+        ix->offsets.insert(ix->offsets.end(), o.begin() + 1, o.end());
+        ix->total += nr;
+        ix->added += count;
+        return;
+    }
+    // stream_dense: stage pieces of <= kStageRuns runs (a longer row alone)
+    for (uint32_t r0 = 0; r0 < count;) {
+        uint32_t r1 = r0 + 1;
+        while (r1 < count && offsets[r1 + 1] - offsets[r0] <= kStageRuns) ++r1;
+        const uint64_t base = offsets[r0], pr = offsets[r1] - base;
+        std::vector<uint64_t> o(r1 - r0 + 1);
+        for (uint32_t i = r0; i <= r1; ++i) o[i - r0] = offsets[i] - base;
+        ix->stage.alloc(std::max<uint64_t>(pr, std::min<uint64_t>(nr, kStageRuns)));
+        ix->stage_off.alloc(std::max<size_t>(o.size(), std::min<size_t>(count + 1, 1u << 20)));
+        HIP_CHECK(hipMemcpyAsync(ix->stage.p, runs + base, pr * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipMemcpyAsync(ix->stage_off.p, o.data(), o.size() * sizeof(uint64_t),
+                                 hipMemcpyHostToDevice, s));
+        validate_device_rows(ix, ix->stage_off.p, ix->stage.p, r1 - r0);
+        expand_into(ix, ix->stage_off.p, ix->stage.p, r1 - r0, pr, ix->added);
+        g->sync();  // the stage is reused by the next piece
+        ix->added += r1 - r0;
+        r0 = r1;
+    }
+}
+
+// Append every row of a device-built cpd_rows (no host round trip).
+void append_built(cpd_index* ix, const cpd_rows* r) {
+    cpd_graph* g = ix->g;
+    CPD_REQUIRE(r->device == g->device, CPD_E_ARG, "index: rows live on another device");
+    CPD_REQUIRE(r->nrows <= ix->nrows - ix->added, CPD_E_ARG, "index: more rows than declared");
+    if (!r->nrows) return;
+    if (ix->keep_rle) {
+        CPD_REQUIRE(ix->total + r->total <= ix->cap, CPD_E_ARG,
+                    "index: more runs than the index was created for");
+        std::vector<uint64_t> o(r->nrows + 1);
+        for (uint32_t i = 0; i <= r->nrows; ++i) o[i] = ix->total + r->offsets[i];
+        HIP_CHECK(hipMemcpyAsync(ix->runs.p + ix->total, r->runs.p, r->total * sizeof(uint32_t),
+                                 hipMemcpyDeviceToDevice, g->stream));
+        HIP_CHECK(hipMemcpyAsync(ix->off.p + ix->added, o.data(), o.size() * sizeof(uint64_t),
+                                 hipMemcpyHostToDevice, g->stream));
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        ix->offsets.insert(ix->offsets.end(), o.begin() + 1, o.end());
+        ix->total += r->total;
+    } else {
+        expand_into(ix, r->off.p, r->runs.p, r->nrows, r->total, ix->added);
+        g->sync();
+    }
+    ix->added += r->nrows;
+}
+
+}  // namespace
+
+extern "C" {
+
 int cpd_index_create(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows,
                      const uint64_t* offsets, const uint32_t* runs, cpd_index** out) {
     return guarded([&] {
         CPD_REQUIRE(g && out && row_targets && offsets, CPD_E_ARG, "index: null argument");
         *out = nullptr;
         g->select();
-        auto ix = std::make_unique<cpd_index>();
-        ix->g = g;
-        ix->nrows = nrows;
-        ix->row_of_col.assign(g->n, CPD_INF);
-        CPD_REQUIRE(offsets[0] == 0, CPD_E_ARG, "index: offsets[0] must be 0");
-        for (uint32_t i = 0; i < nrows; ++i) {
-            CPD_REQUIRE(row_targets[i] < g->n, CPD_E_ARG, "index: row target out of range");
-            CPD_REQUIRE(offsets[i + 1] > offsets[i], CPD_E_ARG, "index: empty or unsorted row");
-            ix->row_of_col[g->order[row_targets[i]]] = i;
-        }
-        ix->total = offsets[nrows];
-        CPD_REQUIRE(ix->total == 0 || runs, CPD_E_ARG, "index: null runs");
-        // every run must name a legal column; a row must start at column 0
-        for (uint32_t i = 0; i < nrows; ++i) {
-            CPD_REQUIRE((runs[offsets[i]] >> 4) == 0, CPD_E_ARG, "index: row does not start at column 0");
-            for (uint64_t e = offsets[i] + 1; e < offsets[i + 1]; ++e)
-                CPD_REQUIRE((runs[e] >> 4) > (runs[e - 1] >> 4) && (runs[e] >> 4) < g->n,
-                            CPD_E_ARG, "index: run columns must increase and be < n");
-        }
-        ix->offsets.assign(offsets, offsets + nrows + 1);
-        ix->d_row_of_col.upload(ix->row_of_col.data(), g->n, g->stream);
-        ix->off.upload(offsets, (size_t)nrows + 1, g->stream);
-        ix->runs.upload(runs, ix->total, g->stream);
-        ix->agg.alloc(3);
-        HIP_CHECK(hipStreamSynchronize(g->stream));
+        auto ix = index_init(g, row_targets, nrows);
+        ix->declared = offsets[nrows];
+        index_keep_rle(ix.get(), ix->declared);
+        append_host(ix.get(), nrows, offsets, runs);
         *out = ix.release();
     });
 }
@@ -1060,25 +1214,59 @@ int cpd_index_create(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows,
 int cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out) {
     return guarded([&] {
         CPD_REQUIRE(g && r && out, CPD_E_ARG, "index: null argument");
-        CPD_REQUIRE(r->device == g->device, CPD_E_ARG, "index: rows live on another device");
         *out = nullptr;
         g->select();
-        auto ix = std::make_unique<cpd_index>();
-        ix->g = g;
-        ix->nrows = r->nrows;
-        ix->total = r->total;
-        ix->row_of_col.assign(g->n, CPD_INF);
-        for (uint32_t i = 0; i < r->nrows; ++i) ix->row_of_col[g->order[r->targets[i]]] = i;
-        ix->offsets = r->offsets;
-        ix->d_row_of_col.upload(ix->row_of_col.data(), g->n, g->stream);
-        ix->off.upload(r->offsets.data(), r->offsets.size(), g->stream);
-        ix->runs.alloc(r->total);
-        if (r->total)
-            HIP_CHECK(hipMemcpyAsync(ix->runs.p, r->runs.p, r->total * sizeof(uint32_t),
-                                     hipMemcpyDeviceToDevice, g->stream));
-        ix->agg.alloc(3);
+        auto ix = index_init(g, r->targets.data(), r->nrows);
+        ix->declared = r->total;
+        index_keep_rle(ix.get(), r->total);
+        append_built(ix.get(), r);
+        *out = ix.release();
+    });
+}
+
+int cpd_index_create_empty(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows, int mode,
+                           uint64_t total_runs, cpd_index** out) {
+    return guarded([&] {
+        CPD_REQUIRE(g && out, CPD_E_ARG, "index: null argument");
+        CPD_REQUIRE(mode == CPD_INDEX_AUTO || mode == CPD_INDEX_RLE || mode == CPD_INDEX_DENSE,
+                    CPD_E_ARG, "index mode must be CPD_INDEX_AUTO, _RLE or _DENSE");
+        *out = nullptr;
+        g->select();
+        auto ix = index_init(g, row_targets, nrows);
+        ix->declared = total_runs;
+        ix->mode = mode;
+        if (ix->use_dense()) index_stream_dense(ix.get());
+        else index_keep_rle(ix.get(), total_runs);
         HIP_CHECK(hipStreamSynchronize(g->stream));
         *out = ix.release();
+    });
+}
+
+int cpd_index_append_rows(cpd_index* ix, uint32_t count, const uint64_t* offsets,
+                          const uint32_t* runs) {
+    return guarded([&] {
+        CPD_REQUIRE(ix, CPD_E_ARG, "index: null argument");
+        ix->g->select();
+        append_host(ix, count, offsets, runs);
+    });
+}
+
+int cpd_index_append_built_rows(cpd_index* ix, const cpd_rows* r) {
+    return guarded([&] {
+        CPD_REQUIRE(ix && r, CPD_E_ARG, "index: null argument");
+        ix->g->select();
+        append_built(ix, r);
+    });
+}
+
+int cpd_index_info(const cpd_index* ix, uint32_t* nrows, uint32_t* added, uint64_t* runs_resident,
+                   uint64_t* dense_bytes) {
+    return guarded([&] {
+        CPD_REQUIRE(ix, CPD_E_ARG, "index: null argument");
+        if (nrows) *nrows = ix->nrows;
+        if (added) *added = ix->added;
+        if (runs_resident) *runs_resident = ix->keep_rle ? ix->total : 0;
+        if (dense_bytes) *dense_bytes = ix->dense_ready ? ix->dense.n * sizeof(uint32_t) : 0;
     });
 }
 
@@ -1103,6 +1291,9 @@ int cpd_index_set_weights(cpd_index* ix, const uint32_t* w) {
 int cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint32_t nq) {
     return guarded([&] {
         CPD_REQUIRE(ix && (nq == 0 || (s && t)), CPD_E_ARG, "query: null argument");
+        CPD_REQUIRE(ix->added == ix->nrows, CPD_E_ARG,
+                    "query: index incomplete (" + std::to_string(ix->added) + " of " +
+                        std::to_string(ix->nrows) + " rows appended)");
         cpd_graph* g = ix->g;
         g->select();
         // counting sort by target row: a wave's lanes then walk the same row
@@ -1117,16 +1308,19 @@ int cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint3
         }
         for (uint32_t r = 0; r < ix->nrows; ++r) bucket[r + 1] += bucket[r];
         ix->perm.resize(nq);
-        std::vector<uint32_t> sc(nq), tc(nq);
+        std::vector<uint32_t> sc(nq), tc(nq), rq(nq);
         for (uint32_t q = 0; q < nq; ++q) {
             uint32_t tcol = g->order[t[q]];
-            uint32_t i = bucket[ix->row_of_col[tcol]]++;
+            const uint32_t row = ix->row_of_col[tcol];
+            uint32_t i = bucket[row]++;
             ix->perm[i] = q;
             tc[i] = tcol;
             sc[i] = g->order[s[q]];
+            rq[i] = row;
         }
         ix->qs.upload(sc.data(), nq, g->stream);
         ix->qt.upload(tc.data(), nq, g->stream);
+        ix->qrow.upload(rq.data(), nq, g->stream);
         ix->cost.alloc(nq);
         ix->hops.alloc(nq);
         ix->fin.alloc(nq);
@@ -1139,18 +1333,12 @@ int cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint3
 
 namespace {
 
-// Expand the index's RLE rows into dense move tables (once per index).
+// Expand the resident RLE rows into dense move tables (once per index).
 void ensure_dense(cpd_index* ix) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(g->npad / kFmTile < 65536u, CPD_E_RANGE, "graph too large for dense tables");
-    const size_t words = (size_t)ix->nrows * (g->npad / 8u);
-    ix->dense.alloc(words);
-    if (ix->nrows)
-        g->timed("expand_rows", 4.0 * (double)ix->total + 4.0 * (double)words + 16.0 * ix->nrows,
-                 [&] {
-                     launch_expand_rows(ix->off.p, ix->runs.p, ix->nrows, g->npad, ix->dense.p,
-                                        g->stream);
-                 });
+    ix->dense.alloc((size_t)ix->nrows * (g->npad / 8u));
+    if (ix->nrows) expand_into(ix, ix->off.p, ix->runs.p, ix->nrows, ix->total, 0);
     g->sync();
     ix->dense_ready = true;
 }
@@ -1164,7 +1352,9 @@ int cpd_index_set_mode(cpd_index* ix, int mode) {
         CPD_REQUIRE(ix, CPD_E_ARG, "null index");
         CPD_REQUIRE(mode == CPD_INDEX_AUTO || mode == CPD_INDEX_RLE || mode == CPD_INDEX_DENSE,
                     CPD_E_ARG, "index mode must be CPD_INDEX_AUTO, _RLE or _DENSE");
-        ix->mode = mode;
+        CPD_REQUIRE(!(ix->stream_dense && mode == CPD_INDEX_RLE), CPD_E_ARG,
+                    "index was streamed into dense tables: its runs were not kept");
+        if (!ix->stream_dense) ix->mode = mode;
     });
 }
 
@@ -1187,14 +1377,16 @@ int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
         hipEvent_t a = g->get_event(), b = g->get_event();
         HIP_CHECK(hipEventRecord(a, g->stream));
         const uint32_t* adj = ix->custom_w ? ix->adj_sel.p : g->adj.p;
+        (void)hipGetLastError();
         if (nq && dense)
             launch_table_search_dense(adj, g->adj_shift, ix->d_row_of_col.p, ix->dense.p, g->npad,
-                                      ix->qs.p, ix->qt.p, nq, k_moves, g->n, ix->cost.p,
-                                      ix->hops.p, ix->fin.p, ix->agg.p, g->stream);
+                                      ix->qs.p, ix->qt.p, ix->qrow.p, nq, k_moves, g->n,
+                                      ix->cost.p, ix->hops.p, ix->fin.p, ix->agg.p, g->stream);
         else if (nq)
             launch_table_search(adj, g->adj_shift, ix->d_row_of_col.p, ix->off.p, ix->runs.p,
-                                ix->qs.p, ix->qt.p, nq, k_moves, g->n, ix->cost.p, ix->hops.p,
-                                ix->fin.p, ix->agg.p, g->stream);
+                                ix->qs.p, ix->qt.p, ix->qrow.p, nq, k_moves, g->n, ix->cost.p,
+                                ix->hops.p, ix->fin.p, ix->agg.p, g->stream);
+        HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipEventRecord(b, g->stream));
         unsigned long long hagg[3] = {0, 0, 0};
         HIP_CHECK(hipMemcpyAsync(hagg, ix->agg.p, sizeof hagg, hipMemcpyDeviceToHost, g->stream));

@@ -341,6 +341,60 @@ void BucketFile::close(uint64_t total) {
     if (std::rename(tmp_.c_str(), path_.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path_);
 }
 
+CpdBucket read_bucket_head(const std::string& path) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f) throw Error(CPD_E_IO, "cannot open " + path);
+    const uint64_t size = (uint64_t)f.tellg();
+    f.seekg(0);
+    char magic[8];
+    f.read(magic, 8);
+    if (!f || std::memcmp(magic, kBucketMagic, 8) != 0) throw Error(CPD_E_IO, path + ": not a CPD bucket file");
+    CpdBucket b;
+    uint32_t h32[6];
+    uint64_t total = 0;
+    f.read(reinterpret_cast<char*>(h32), sizeof h32);
+    f.read(reinterpret_cast<char*>(&total), 8);
+    f.read(reinterpret_cast<char*>(&b.fingerprint), 8);
+    if (!f) throw Error(CPD_E_IO, path + ": truncated header");
+    b.n = h32[0];
+    const uint32_t nrows = h32[1];
+    b.bid = h32[2];
+    b.method = h32[3];
+    b.key = h32[4];
+    b.maxworker = h32[5];
+    if (size != kBucketHeader + 4ull * nrows + 8ull * (nrows + 1ull) + 4ull * total)
+        throw Error(CPD_E_IO, path + ": size does not match its header");
+    b.targets.resize(nrows);
+    b.offsets.resize((size_t)nrows + 1);
+    f.read(reinterpret_cast<char*>(b.targets.data()), nrows * 4ull);
+    f.read(reinterpret_cast<char*>(b.offsets.data()), (nrows + 1) * 8ull);
+    if (!f) throw Error(CPD_E_IO, path + ": truncated body");
+    if (b.offsets[0] != 0 || b.offsets[nrows] != total) throw Error(CPD_E_IO, path + ": bad offsets");
+    return b;
+}
+
+void read_bucket_runs(const std::string& path, const CpdBucket& head, uint64_t first,
+                      uint64_t count, uint32_t* out) {
+    const uint64_t nrows = head.targets.size();
+    if (first + count > head.offsets.back()) throw Error(CPD_E_ARG, path + ": runs out of range");
+    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) throw Error(CPD_E_IO, "cannot open " + path);
+    uint64_t pos = kBucketHeader + 4ull * nrows + 8ull * (nrows + 1ull) + 4ull * first;
+    char* c = reinterpret_cast<char*>(out);
+    uint64_t left = 4ull * count;
+    while (left) {
+        const ssize_t k = ::pread(fd, c, std::min<uint64_t>(left, 1ull << 30), (off_t)pos);
+        if (k <= 0) {
+            ::close(fd);
+            throw Error(CPD_E_IO, path + ": truncated runs");
+        }
+        c += k;
+        pos += (uint64_t)k;
+        left -= (uint64_t)k;
+    }
+    ::close(fd);
+}
+
 CpdBucket read_bucket(const std::string& path) {
     std::ifstream f(path, std::ios::binary);
     if (!f) throw Error(CPD_E_IO, "cannot open " + path);

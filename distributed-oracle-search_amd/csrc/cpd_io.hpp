@@ -82,6 +82,12 @@ private:
     uint32_t nrows_ = 0;
 };
 CpdBucket read_bucket(const std::string& path);
+// Header, targets and offsets only (runs left empty; total = offsets.back()),
+// the file size checked against the header; then runs [first, first+count)
+// read by position, so a bucket of any size streams through a small buffer.
+CpdBucket read_bucket_head(const std::string& path);
+void read_bucket_runs(const std::string& path, const CpdBucket& head, uint64_t first,
+                      uint64_t count, uint32_t* out);
 void write_order(const std::string& path, uint64_t fingerprint, const std::vector<uint32_t>& order);
 std::vector<uint32_t> read_order(const std::string& path, uint64_t fingerprint);
 

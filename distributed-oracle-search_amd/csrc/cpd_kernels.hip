@@ -1209,6 +1209,7 @@ __global__ __launch_bounds__(256) void table_search(
             }
             pos = lo;
             const uint32_t mv = rr[lo] & 0xFu;
+            if (mv >> shift) break;  // names no slot of cur: malformed row
             const uint2 e = adj[((size_t)cur << shift) + mv];
             if (e.x == kNoEdge) break;  // move past the out-degree: malformed row
             cost += e.y;
@@ -1274,6 +1275,31 @@ __global__ __launch_bounds__(64) void expand_rows(const uint64_t* __restrict__ o
     *out = make_uint4(words[0], words[1], words[2], words[3]);
 }
 
+// Row format check for rows loaded from outside the library (bucket files,
+// host arrays): one wave per row; *bad |= 1 when a row does not start at
+// column 0, its run columns do not strictly increase, or a column is >= n.
+// expand_rows and the binary searches rely on exactly these properties (a
+// run's move is checked by the walk itself: a move naming no edge of its
+// column stops the walk, so it is not checked here — a run that starts on a
+// wildcard column may legally carry a move that column does not have).
+__global__ __launch_bounds__(256) void validate_rows(const uint64_t* __restrict__ offsets,
+                                                     const uint32_t* __restrict__ runs,
+                                                     uint32_t nrows, uint32_t n,
+                                                     uint32_t* __restrict__ bad) {
+    const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (row >= nrows) return;
+    const uint64_t o0 = offsets[row], o1 = offsets[row + 1];
+    bool b = o1 <= o0;
+    for (uint64_t i = o0 + lane; i < o1; i += 64u) {
+        const uint32_t c = runs[i] >> 4;
+        b |= c >= n;
+        if (i == o0) b |= c != 0u;
+        else b |= c <= (runs[i - 1] >> 4);
+    }
+    if (__any(b) && lane == 0) atomicOr(bad, 1u);
+}
+
 // Table-search over dense move tables: one nibble load + one packed edge load
 // per move.  Same walk, same results as table_search.
 __global__ __launch_bounds__(256) void table_search_dense(
@@ -1293,6 +1319,7 @@ __global__ __launch_bounds__(256) void table_search_dense(
         const uint32_t limit = kmoves >= 0 ? (uint32_t)kmoves : n;
         while (cur != t && hops < limit && hops < n) {
             const uint32_t mv = (row[cur >> 3] >> (4u * (cur & 7u))) & 0xFu;
+            if (mv >> shift) break;  // names no slot of cur: malformed row
             const uint2 e = adj[((size_t)cur << shift) + mv];
             if (e.x == kNoEdge) break;
             cost += e.y;
@@ -1305,6 +1332,280 @@ __global__ __launch_bounds__(256) void table_search_dense(
         fin_out[q] = (uint8_t)fin;
     }
     wave_stats(cost, hops, fin, agg);
+}
+
+// ---------------------------------------------------------------------------
+// Table-search v2: the same walk, the same results, restructured for latency.
+//
+// (1) Adjacency co-fetch.  A hop's two loads — the move of column cur and the
+//     packed edge (cur, move) — both depend only on cur, so for <= 4 slots per
+//     column the whole adjacency row of cur (<= 32 B: one or two 16-B loads)
+//     is fetched beside the move word and the edge is picked in registers: one
+//     memory round trip per hop instead of two.  (Wider adjacency: the edge
+//     load still follows the move.)
+// (2) Lane refill.  Path lengths differ by several x inside a wave (s is
+//     uniform over the graph), so a lane per query leaves most lanes idle
+//     while the wave waits for its longest walk.  Here a wave owns `chunk`
+//     consecutive queries of the target-sorted batch; a lane whose walk ends
+//     stores its result and takes the next unstarted query of the chunk (rank
+//     among the wave's finishing lanes by mbcnt, a wave-uniform cursor in an
+//     SGPR), so lanes stay busy until the chunk runs dry.
+// (3) ILP walks per lane, issued together: more loads in flight per wave.
+// qrow[q] = the row of query q's target (host-computed with the sort).
+constexpr uint32_t kIdleQ = 0xFFFFFFFFu;
+
+struct DenseRows {
+    const uint32_t* __restrict__ dense;
+    uint32_t wpr;  // words per row
+};
+
+struct RleRows {
+    const uint64_t* __restrict__ off;
+    const uint32_t* __restrict__ runs;
+};
+
+struct WalkState {
+    uint32_t q, cur, t, hops, pos, R;
+    uint64_t cost;
+    const uint32_t* row;  // dense words / RLE runs of the query's row
+    bool bad;             // a move past the out-degree (malformed row): stop
+};
+
+__device__ __forceinline__ void walk_begin(WalkState& w, uint32_t q, const uint32_t* __restrict__ qs,
+                                           const uint32_t* __restrict__ qt,
+                                           const uint32_t* __restrict__ qrow, const DenseRows& d) {
+    w.q = q;
+    w.cur = qs[q];
+    w.t = qt[q];
+    w.row = d.dense + (size_t)qrow[q] * d.wpr;
+    w.hops = 0;
+    w.cost = 0;
+    w.bad = false;
+}
+
+__device__ __forceinline__ void walk_begin(WalkState& w, uint32_t q, const uint32_t* __restrict__ qs,
+                                           const uint32_t* __restrict__ qt,
+                                           const uint32_t* __restrict__ qrow, const RleRows& r) {
+    w.q = q;
+    w.cur = qs[q];
+    w.t = qt[q];
+    const uint32_t row = qrow[q];
+    const uint64_t o0 = r.off[row], o1 = r.off[row + 1];
+    w.row = r.runs + o0;
+    w.R = (uint32_t)(o1 - o0);
+    w.pos = 0;
+    w.hops = 0;
+    w.cost = 0;
+    w.bad = false;
+}
+
+__device__ __forceinline__ const uint32_t* rows_base(const DenseRows& d) { return d.dense; }
+__device__ __forceinline__ const uint32_t* rows_base(const RleRows& r) { return r.runs; }
+
+__device__ __forceinline__ uint32_t walk_move(WalkState& w, const DenseRows&) {
+    return (w.row[w.cur >> 3] >> (4u * (w.cur & 7u))) & 0xFu;
+}
+
+// The last run with start <= cur, galloping from the previous hop's run.
+__device__ __forceinline__ uint32_t walk_move(WalkState& w, const RleRows&) {
+    const uint32_t* __restrict__ rr = w.row;
+    const uint32_t cur = w.cur, R = w.R, pos = w.pos;
+    uint32_t lo, hi;  // invariant: start(lo) <= cur < start(hi) (hi == R: +inf)
+    if ((rr[pos] >> 4) <= cur) {
+        lo = pos;
+        uint32_t step = 1;
+        hi = pos + 1;
+        while (hi < R && (rr[hi] >> 4) <= cur) {
+            lo = hi;
+            step <<= 1;
+            hi = lo + step;
+        }
+        if (hi > R) hi = R;
+    } else {
+        hi = pos;
+        uint32_t step = 1;
+        lo = pos >= 1 ? pos - 1 : 0;
+        while (lo > 0 && (rr[lo] >> 4) > cur) {
+            hi = lo;
+            step <<= 1;
+            lo = hi > step ? hi - step : 0;
+        }
+    }
+    while (lo + 1 < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if ((rr[mid] >> 4) > cur) hi = mid;
+        else lo = mid;
+    }
+    w.pos = lo;
+    return rr[lo] & 0xFu;
+}
+
+// One hop of a walking lane.  SHIFT <= 2: the adjacency row of cur is loaded
+// before the move is known (co-fetch); otherwise the edge load follows it.
+template <int SHIFT, class Rows>
+__device__ __forceinline__ void walk_hop(WalkState& w, const uint2* __restrict__ adj,
+                                         const Rows& rows) {
+    uint32_t ex, ew;
+    if (SHIFT == 2) {
+        const uint4* a4 = reinterpret_cast<const uint4*>(adj) + 2u * (size_t)w.cur;
+        const uint4 p0 = a4[0], p1 = a4[1];
+        const uint32_t mv = walk_move(w, rows);
+        const uint4 p = (mv & 2u) ? p1 : p0;
+        ex = (mv & 1u) ? p.z : p.x;
+        ew = (mv & 1u) ? p.w : p.y;
+        if (mv > 3u) ex = kNoEdge;
+    } else if (SHIFT == 1) {
+        const uint4 p = reinterpret_cast<const uint4*>(adj)[w.cur];
+        const uint32_t mv = walk_move(w, rows);
+        ex = (mv & 1u) ? p.z : p.x;
+        ew = (mv & 1u) ? p.w : p.y;
+        if (mv > 1u) ex = kNoEdge;
+    } else if (SHIFT == 0) {
+        const uint2 p = adj[w.cur];
+        const uint32_t mv = walk_move(w, rows);
+        ex = mv == 0u ? p.x : kNoEdge;
+        ew = p.y;
+    } else {  // wide adjacency: the edge load follows the move
+        const uint32_t mv = walk_move(w, rows);
+        if (mv >> SHIFT) {  // names no slot of cur: malformed row
+            w.bad = true;
+            return;
+        }
+        const uint2 e = adj[((size_t)w.cur << SHIFT) + mv];
+        ex = e.x;
+        ew = e.y;
+    }
+    if (ex == kNoEdge) {
+        w.bad = true;
+        return;
+    }
+    w.cost += ew;
+    w.cur = ex;
+    ++w.hops;
+}
+
+// Dense rows, all ILP walks of a lane at once: every slot's move word and
+// adjacency row are loaded unconditionally (an idle slot keeps a valid column
+// and row pointer), then the walking slots step — the loads of the ILP walks
+// are in flight together instead of one branch region after another.
+template <int SHIFT, int ILP>
+__device__ __forceinline__ void walk_hops(WalkState (&w)[ILP], const uint2* __restrict__ adj,
+                                          const DenseRows&) {
+    constexpr int NQ = SHIFT == 2 ? 2 : 1;  // 16-B pieces of an adjacency row
+    uint32_t word[ILP];
+    uint4 p[ILP][NQ];
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+        word[i] = w[i].row[w[i].cur >> 3];
+        if (SHIFT <= 2) {
+            if (SHIFT == 0) {
+                const uint2 e = adj[w[i].cur];
+                p[i][0] = make_uint4(e.x, e.y, kNoEdge, 0u);
+            } else {
+                const uint4* a4 = reinterpret_cast<const uint4*>(adj) + (size_t)w[i].cur * NQ;
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) p[i][k] = a4[k];
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+        if (w[i].q == kIdleQ || w[i].cur == w[i].t) continue;
+        const uint32_t mv = (word[i] >> (4u * (w[i].cur & 7u))) & 0xFu;
+        uint32_t ex, ew;
+        if (SHIFT <= 2) {
+            const uint4 q = (NQ == 2 && (mv & 2u)) ? p[i][NQ - 1] : p[i][0];
+            ex = (mv & 1u) ? q.z : q.x;
+            ew = (mv & 1u) ? q.w : q.y;
+            if (mv >> SHIFT) ex = kNoEdge;
+        } else {
+            if (mv >> SHIFT) {
+                w[i].bad = true;
+                continue;
+            }
+            const uint2 e = adj[((size_t)w[i].cur << SHIFT) + mv];
+            ex = e.x;
+            ew = e.y;
+        }
+        if (ex == kNoEdge) {
+            w[i].bad = true;
+            continue;
+        }
+        w[i].cost += ew;
+        w[i].cur = ex;
+        ++w[i].hops;
+    }
+}
+
+template <int SHIFT, int ILP>
+__device__ __forceinline__ void walk_hops(WalkState (&w)[ILP], const uint2* __restrict__ adj,
+                                          const RleRows& rows) {
+#pragma unroll
+    for (int i = 0; i < ILP; ++i)
+        if (w[i].q != kIdleQ && w[i].cur != w[i].t) walk_hop<SHIFT>(w[i], adj, rows);
+}
+
+template <int SHIFT, int ILP, class Rows>
+__global__ __launch_bounds__(256) void table_walk(
+    const uint2* __restrict__ adj, Rows rows, const uint32_t* __restrict__ qs,
+    const uint32_t* __restrict__ qt, const uint32_t* __restrict__ qrow, uint32_t nq,
+    uint32_t chunk, uint32_t limit, uint64_t* __restrict__ cost_out,
+    uint32_t* __restrict__ hops_out, uint8_t* __restrict__ fin_out,
+    unsigned long long* __restrict__ agg) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t q0l = wave * chunk;
+    const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
+    const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
+    uint64_t sum_cost = 0;
+    uint32_t sum_hops = 0, sum_fin = 0;
+    WalkState w[ILP];
+    uint32_t next = q0;  // wave-uniform: first query of the chunk not yet started
+#pragma unroll
+    for (int i = 0; i < ILP; ++i) {
+        const uint32_t q = next + (uint32_t)i * 64u + lane;
+        w[i].q = kIdleQ;  // idle: column 0 of row 0 stays loadable
+        w[i].cur = 0;
+        w[i].t = 0;
+        w[i].hops = 0;
+        w[i].bad = false;
+        w[i].cost = 0;
+        w[i].pos = 0;
+        w[i].R = 0;
+        w[i].row = rows_base(rows);
+        if (q < q1) walk_begin(w[i], q, qs, qt, qrow, rows);
+    }
+    next = min(q1, next + 64u * ILP);
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    for (;;) {
+        // retire finished walks; their lanes take the next queries of the chunk
+        bool live = false;
+#pragma unroll
+        for (int i = 0; i < ILP; ++i) {
+            const bool idle = w[i].q == kIdleQ;
+            const bool done = !idle && (w[i].cur == w[i].t || w[i].hops >= limit || w[i].bad);
+            const uint64_t m = __ballot(done);
+            if (m) {
+                if (done) {
+                    const uint32_t fin = w[i].cur == w[i].t ? 1u : 0u;
+                    cost_out[w[i].q] = w[i].cost;
+                    hops_out[w[i].q] = w[i].hops;
+                    fin_out[w[i].q] = (uint8_t)fin;
+                    sum_cost += w[i].cost;
+                    sum_hops += w[i].hops;
+                    sum_fin += fin;
+                    const uint32_t nqi = next + (uint32_t)__builtin_popcountll(m & lt_mask);
+                    if (nqi < q1) walk_begin(w[i], nqi, qs, qt, qrow, rows);
+                    else w[i].q = kIdleQ;
+                }
+                next = min(q1, next + (uint32_t)__builtin_popcountll(m));
+            }
+            live |= w[i].q != kIdleQ;
+        }
+        if (!__any(live)) break;
+        walk_hops<SHIFT, ILP>(w, adj, rows);  // one hop of every walking slot
+    }
+    wave_stats(sum_cost, sum_hops, sum_fin, agg);
 }
 
 __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
@@ -1552,30 +1853,102 @@ void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t n
     launch_rle<true>(fm, fmb, npad, nrows, nullptr, off, runs, st, rc, s);
 }
 
+void launch_validate_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,
+                          uint32_t n, uint32_t* bad, hipStream_t s) {
+    if (!nrows) return;
+    launch(kern::validate_rows, dim3((nrows + 3u) / 4u), dim3(256), s, offsets, runs, nrows, n,
+           bad);
+}
+
 void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,
                         uint32_t npad, uint32_t* dense, hipStream_t s) {
     launch(kern::expand_rows, dim3(nrows, npad / kern::kTile), dim3(64), s, offsets, runs,
            npad / 8u, dense);
 }
 
+// Table-search knobs (A/B runs; results are identical under every setting):
+// CPD_TS_V1=1 runs the lane-per-query kernels without co-fetch or refill;
+// CPD_TS_ILP (1 or 2) walks per lane; CPD_TS_WAVES = waves the batch is cut
+// into (chunk = nq / waves rounded up to 64 x ILP, at least that).
+uint32_t ts_v1() {
+    static const uint32_t v = env_u32("CPD_TS_V1", 0);
+    return v;
+}
+uint32_t ts_ilp() {
+    static const uint32_t v = env_u32("CPD_TS_ILP", 2) >= 2 ? 2u : 1u;
+    return v;
+}
+uint32_t ts_waves() {
+    static const uint32_t v = std::max(1u, env_u32("CPD_TS_WAVES", 8192));
+    return v;
+}
+
+template <class Rows>
+static void launch_walk(const uint2* adj, uint32_t shift, const Rows& rows, const uint32_t* qs,
+                        const uint32_t* qt, const uint32_t* qrow, uint32_t nq, uint32_t limit,
+                        uint64_t* cost, uint32_t* hops, uint8_t* fin, unsigned long long* agg,
+                        hipStream_t s) {
+    const uint32_t ilp = ts_ilp(), unit = 64u * ilp;
+    uint64_t chunk = ((uint64_t)nq + ts_waves() - 1u) / ts_waves();
+    chunk = std::max<uint64_t>(unit, (chunk + unit - 1u) / unit * unit);
+    const uint64_t waves = ((uint64_t)nq + chunk - 1u) / chunk;
+    const dim3 grid((uint32_t)std::max<uint64_t>(1u, (waves + 3u) / 4u)), blk(256);
+    const uint32_t c = (uint32_t)chunk;
+#define CPD_WALK(SH, IL)                                                                       \
+    launch(kern::table_walk<SH, IL, Rows>, grid, blk, s, adj, rows, qs, qt, qrow, nq, c, limit, \
+           cost, hops, fin, agg)
+    if (ilp == 2) {
+        switch (shift) {
+            case 0: CPD_WALK(0, 2); break;
+            case 1: CPD_WALK(1, 2); break;
+            case 2: CPD_WALK(2, 2); break;
+            case 3: CPD_WALK(3, 2); break;
+            default: CPD_WALK(4, 2); break;
+        }
+    } else {
+        switch (shift) {
+            case 0: CPD_WALK(0, 1); break;
+            case 1: CPD_WALK(1, 1); break;
+            case 2: CPD_WALK(2, 1); break;
+            case 3: CPD_WALK(3, 1); break;
+            default: CPD_WALK(4, 1); break;
+        }
+    }
+#undef CPD_WALK
+}
+
+static uint32_t walk_limit(int32_t kmoves, uint32_t n) {
+    return kmoves >= 0 ? std::min((uint32_t)kmoves, n) : n;
+}
+
 void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
                                const uint32_t* dense, uint32_t npad, const uint32_t* qs,
-                               const uint32_t* qt, uint32_t nq, int32_t kmoves, uint32_t n,
-                               uint64_t* cost, uint32_t* hops, uint8_t* fin,
-                               unsigned long long* agg, hipStream_t s) {
-    launch(kern::table_search_dense, dim3((nq + 255u) / 256u), dim3(256), s,
-           reinterpret_cast<const uint2*>(adj), shift, row_of_col, dense, npad / 8u, qs, qt, nq,
-           kmoves, n, cost, hops, fin, agg);
+                               const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
+                               int32_t kmoves, uint32_t n, uint64_t* cost, uint32_t* hops,
+                               uint8_t* fin, unsigned long long* agg, hipStream_t s) {
+    if (ts_v1()) {
+        launch(kern::table_search_dense, dim3((nq + 255u) / 256u), dim3(256), s,
+               reinterpret_cast<const uint2*>(adj), shift, row_of_col, dense, npad / 8u, qs, qt,
+               nq, kmoves, n, cost, hops, fin, agg);
+        return;
+    }
+    launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::DenseRows{dense, npad / 8u}, qs,
+                qt, qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, s);
 }
 
 void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
                          const uint64_t* offsets, const uint32_t* runs, const uint32_t* qs,
-                         const uint32_t* qt, uint32_t nq, int32_t kmoves, uint32_t n,
-                         uint64_t* cost, uint32_t* hops, uint8_t* fin, unsigned long long* agg,
-                         hipStream_t s) {
-    launch(kern::table_search, dim3((nq + 255u) / 256u), dim3(256), s,
-           reinterpret_cast<const uint2*>(adj), shift, row_of_col, offsets, runs, qs, qt, nq, kmoves,
-           n, cost, hops, fin, agg);
+                         const uint32_t* qt, const uint32_t* qrow, uint32_t nq, int32_t kmoves,
+                         uint32_t n, uint64_t* cost, uint32_t* hops, uint8_t* fin,
+                         unsigned long long* agg, hipStream_t s) {
+    if (ts_v1()) {
+        launch(kern::table_search, dim3((nq + 255u) / 256u), dim3(256), s,
+               reinterpret_cast<const uint2*>(adj), shift, row_of_col, offsets, runs, qs, qt, nq,
+               kmoves, n, cost, hops, fin, agg);
+        return;
+    }
+    launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::RleRows{offsets, runs}, qs, qt,
+                qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, s);
 }
 
 }  // namespace cpd

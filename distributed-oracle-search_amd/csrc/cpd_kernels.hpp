@@ -112,22 +112,30 @@ void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t n
                      const uint64_t* off, uint32_t* runs, uint32_t* st, uint8_t* rc,
                      hipStream_t s);
 
+// *bad |= 1 if some row [0, nrows) of (offsets, runs) does not start at column
+// 0, has non-increasing run columns, a column >= n, or is empty.  Rows from
+// outside the library pass this before expand_rows / the walks touch them.
+void launch_validate_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,
+                          uint32_t n, uint32_t* bad, hipStream_t s);
+
 // RLE rows -> dense 4-bit move tables, npad/8 words per row.
 void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,
                         uint32_t npad, uint32_t* dense, hipStream_t s);
-// table-search over dense move tables
+// table-search over dense move tables.  qs / qt: query columns, sorted by
+// target row; qrow[q]: the row of query q's target (row_of_col is only read
+// by the CPD_TS_V1=1 kernels).
 void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
                                const uint32_t* dense, uint32_t npad, const uint32_t* qs,
-                               const uint32_t* qt, uint32_t nq, int32_t kmoves, uint32_t n,
-                               uint64_t* cost, uint32_t* hops, uint8_t* fin,
-                               unsigned long long* agg, hipStream_t s);
+                               const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
+                               int32_t kmoves, uint32_t n, uint64_t* cost, uint32_t* hops,
+                               uint8_t* fin, unsigned long long* agg, hipStream_t s);
 
 // adj: packed fixed-stride adjacency, (dst column, weight) pairs, 2^shift
 // slots per column, dst = 0xFFFFFFFF past the out-degree.
 void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
                          const uint64_t* offsets, const uint32_t* runs, const uint32_t* qs,
-                         const uint32_t* qt, uint32_t nq, int32_t kmoves, uint32_t n,
-                         uint64_t* cost, uint32_t* hops, uint8_t* fin, unsigned long long* agg,
-                         hipStream_t s);
+                         const uint32_t* qt, const uint32_t* qrow, uint32_t nq, int32_t kmoves,
+                         uint32_t n, uint64_t* cost, uint32_t* hops, uint8_t* fin,
+                         unsigned long long* agg, hipStream_t s);
 
 }  // namespace cpd

@@ -1,4 +1,11 @@
 // cpd_plan: the once-per-graph host preprocessing (column order + hierarchy).
+#include <errno.h>
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -10,6 +17,37 @@ using namespace cpd;
 namespace {
 
 const char kPlanMagic[8] = {'D', 'O', 'S', 'P', 'L', 'A', 'N', '1'};
+
+// A loaded hierarchy must be self-consistent before anything indexes by it:
+// empty (a query-only plan) or rank / levels of n entries, up / down CSR with
+// n + 1 monotone offsets ending at their arc counts, heads < n, levels below
+// their level counts.
+void check_hierarchy(const cpd_plan& p) {
+    const Hierarchy& H = p.ch;
+    const size_t n = p.n;
+    if (H.rank.empty()) {
+        CPD_REQUIRE(H.up_off.empty() && H.dn_off.empty() && H.level_up.empty() &&
+                        H.level_dn.empty(),
+                    CPD_E_IO, "plan file: partial hierarchy");
+        return;
+    }
+    CPD_REQUIRE(H.rank.size() == n && H.level_up.size() == n && H.level_dn.size() == n,
+                CPD_E_IO, "plan file: hierarchy arrays of the wrong size");
+    auto csr = [&](const std::vector<uint64_t>& off, const std::vector<uint32_t>& to,
+                   const std::vector<uint32_t>& wt) {
+        CPD_REQUIRE(off.size() == n + 1 && off[0] == 0 && off[n] == to.size() &&
+                        to.size() == wt.size(),
+                    CPD_E_IO, "plan file: hierarchy arcs inconsistent");
+        for (size_t v = 0; v < n; ++v)
+            CPD_REQUIRE(off[v] <= off[v + 1], CPD_E_IO, "plan file: arc offsets not monotone");
+        for (uint32_t x : to) CPD_REQUIRE(x < n, CPD_E_IO, "plan file: arc head out of range");
+    };
+    csr(H.up_off, H.up_dst, H.up_w);
+    csr(H.dn_off, H.dn_dst, H.dn_w);
+    for (size_t v = 0; v < n; ++v)
+        CPD_REQUIRE(H.level_up[v] < H.nlev_up && H.level_dn[v] < H.nlev_dn, CPD_E_IO,
+                    "plan file: level out of range");
+}
 
 template <class T>
 void put_vec(std::ofstream& f, const std::vector<T>& v) {
@@ -113,7 +151,18 @@ int cpd_plan_export_ch(const cpd_plan* p, uint32_t* rank, uint64_t* up_off,
 int cpd_plan_save(const cpd_plan* p, const char* path) {
     return guarded([&] {
         CPD_REQUIRE(p && path, CPD_E_ARG, "plan save: null argument");
-        std::string tmp = std::string(path) + ".tmp";
+        // a name of this process and call alone: concurrent savers (workers
+        // started together, make_cpds.py:58-60) never truncate each other
+        static std::atomic<unsigned> seq{0};
+        std::string tmp = std::string(path) + ".tmp." + std::to_string(::getpid()) + "." +
+                          std::to_string(seq++);
+        struct Unlink {  // the temporary never outlives a failed save
+            const std::string& f;
+            bool armed = true;
+            ~Unlink() {
+                if (armed) ::unlink(f.c_str());
+            }
+        } cleanup{tmp};
         {
             std::ofstream f(tmp, std::ios::binary);
             CPD_REQUIRE(f, CPD_E_IO, std::string("cannot write ") + tmp);
@@ -136,9 +185,11 @@ int cpd_plan_save(const cpd_plan* p, const char* path) {
             put_vec(f, H.dn_w);
             put_vec(f, H.level_up);
             put_vec(f, H.level_dn);
+            f.flush();
             CPD_REQUIRE(f, CPD_E_IO, "plan write failed");
         }
         CPD_REQUIRE(std::rename(tmp.c_str(), path) == 0, CPD_E_IO, "plan rename failed");
+        cleanup.armed = false;
     });
 }
 
@@ -176,12 +227,61 @@ int cpd_plan_load(const char* path, cpd_plan** out) {
         get_vec(f, H.level_up);
         get_vec(f, H.level_dn);
         CPD_REQUIRE(p->row_ptr.size() == (size_t)p->n + 1 && p->order.size() == p->n &&
-                        (H.level_dn.size() == p->n || H.level_dn.empty()),
+                        p->dst.size() == p->m && p->w.size() == p->m,
                     CPD_E_IO, "plan file inconsistent");
         check_csr(p->n, p->m, p->row_ptr.data(), p->dst.data(), p->w.data());
-        p->inv.resize(p->n);
-        for (uint32_t v = 0; v < p->n; ++v) p->inv[p->order[v]] = v;
+        // the column order must be a permutation (inv[] and every GPU array
+        // are indexed by it)
+        p->inv.assign(p->n, 0xFFFFFFFFu);
+        for (uint32_t v = 0; v < p->n; ++v) {
+            CPD_REQUIRE(p->order[v] < p->n && p->inv[p->order[v]] == 0xFFFFFFFFu, CPD_E_IO,
+                        "plan file: column order is not a permutation");
+            p->inv[p->order[v]] = v;
+        }
+        check_hierarchy(*p);
         *out = p.release();
+    });
+}
+
+int cpd_plan_cache(const char* path, const uint32_t* row_ptr, const uint32_t* dst,
+                   const uint32_t* w, uint32_t n, uint32_t m, const cpd_plan_opts* opts,
+                   cpd_plan** out, int* status) {
+    return guarded([&] {
+        CPD_REQUIRE(path && out, CPD_E_ARG, "plan cache: null argument");
+        *out = nullptr;
+        check_csr(n, m, row_ptr, dst, w);
+        // one builder per cache file: the others block here until it has
+        // saved, then load its plan
+        const std::string lock = std::string(path) + ".lock";
+        const int fd = ::open(lock.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+        if (fd >= 0)
+            while (::flock(fd, LOCK_EX) != 0 && errno == EINTR) {
+            }
+        struct Unlock {
+            int fd;
+            ~Unlock() {
+                if (fd >= 0) ::close(fd);  // releases the flock
+            }
+        } unlock{fd};
+        cpd_plan* p = nullptr;
+        if (cpd_plan_load(path, &p) == CPD_OK) {
+            const bool same = p->n == n && p->m == m &&
+                              std::equal(p->row_ptr.begin(), p->row_ptr.end(), row_ptr) &&
+                              std::equal(p->dst.begin(), p->dst.end(), dst) &&
+                              std::equal(p->w.begin(), p->w.end(), w) &&
+                              (p->ch.rank.empty() == (opts && opts->no_hierarchy));
+            if (same) {
+                *out = p;
+                if (status) *status = 0;
+                return;
+            }
+            cpd_plan_free(p);  // built for another graph: rebuild over it
+        }
+        int rc = cpd_plan_create(row_ptr, dst, w, n, m, opts, &p);
+        if (rc != CPD_OK) throw Error(rc, cpd_last_error());
+        rc = cpd_plan_save(p, path);
+        if (status) *status = rc == CPD_OK ? 1 : 2;
+        *out = p;
     });
 }
 

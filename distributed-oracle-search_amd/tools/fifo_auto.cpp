@@ -4,8 +4,11 @@
 //   fifo_auto --input X.xy DIFF --partmethod {div|mod} --partkey K
 //             --workerid I --maxworker W --outdir D --alg table-search
 //             [--partition M] [--device G] [--fifo PATH] [--once]
+//             [--index auto|rle|dense]
 //
-// Loads the CPD buckets this worker owns onto its GPU, then serves requests on
+// Creates its request FIFO, streams the CPD buckets this worker owns onto its
+// GPU (as 4-bit move tables when they are smaller than the runs, the runs
+// then never held whole in HBM or host memory), then serves requests on
 // /tmp/worker{I}.fifo (process_query.py:86).  A request is what
 // process_query.send_remote pipes in (process_query.py:66-79,89):
 //     {worker JSON config}\n<query file> <answer fifo> <diff file>\n
@@ -130,6 +133,23 @@ int main(int argc, char** argv) {
     signal(SIGTERM, on_signal);
     signal(SIGPIPE, SIG_IGN);
 
+    // The request FIFO exists before the (possibly long) index load: a request
+    // sent meanwhile blocks in its writer's open() until the loop below reads
+    // it, instead of `cat <<CONF > fifo` creating a regular file there.  A
+    // non-FIFO left at the path (such a file from an earlier run) is replaced.
+    {
+        struct stat st;
+        if (::lstat(fifo.c_str(), &st) == 0 && !S_ISFIFO(st.st_mode)) ::unlink(fifo.c_str());
+        if (::mkfifo(fifo.c_str(), 0666) != 0 && errno != EEXIST) {
+            std::fprintf(stderr, "fifo_auto: mkfifo %s: %s\n", fifo.c_str(), std::strerror(errno));
+            return 1;
+        }
+        if (::lstat(fifo.c_str(), &st) != 0 || !S_ISFIFO(st.st_mode)) {
+            std::fprintf(stderr, "fifo_auto: %s is not a FIFO\n", fifo.c_str());
+            return 1;
+        }
+    }
+
     cpd_index* ix = nullptr;
     cpd_graph* dg = nullptr;
     cpd_plan* plan = nullptr;
@@ -149,42 +169,65 @@ int main(int argc, char** argv) {
         cli::check(cpd_plan_order(plan, order.data()), "order");
         std::vector<uint32_t> stored = cpd::io::read_order(cpd::io::order_path(outdir, xy), fp);
         if (stored != order) throw std::runtime_error("stored column order differs from this build's");
-        // this worker's buckets, concatenated
+        // this worker's buckets: headers first (targets, offsets, run totals)
         uint32_t nb = 0;
         cli::check(cpd_partition_nbuckets(g.n, mcode, (uint32_t)key, &nb), "buckets");
-        std::vector<uint32_t> targets, runs;
-        std::vector<uint64_t> offsets{0};
+        std::vector<std::string> paths;
+        std::vector<cpd::io::CpdBucket> heads;
+        std::vector<uint32_t> targets;
+        uint64_t total_runs = 0;
         for (uint32_t b = 0; b < nb; ++b) {
             if (b % (uint32_t)W != (uint32_t)wid) continue;
-            auto bk = cpd::io::read_bucket(cpd::io::bucket_path(outdir, xy, method, (uint32_t)key, b));
+            paths.push_back(cpd::io::bucket_path(outdir, xy, method, (uint32_t)key, b));
+            heads.push_back(cpd::io::read_bucket_head(paths.back()));
+            const auto& bk = heads.back();
             if (bk.fingerprint != fp || bk.key != (uint32_t)key || bk.method != (uint32_t)mcode)
                 throw std::runtime_error("bucket " + std::to_string(b) + " was built for another graph/partition");
-            uint64_t base = runs.size();
             targets.insert(targets.end(), bk.targets.begin(), bk.targets.end());
-            for (size_t r = 1; r < bk.offsets.size(); ++r) offsets.push_back(base + bk.offsets[r]);
-            runs.insert(runs.end(), bk.runs.begin(), bk.runs.end());
+            total_runs += bk.offsets.back();
         }
         int ndev = 0;
         cli::check(cpd_device_count(&ndev), "device count");
         if (ndev == 0) throw std::runtime_error("no GPU visible (this build has no CPU path)");
         int device = (int)a.num("device", wid % ndev);
         cli::check(cpd_graph_create(plan, device, &dg), "graph upload");
-        cli::check(cpd_index_create(dg, targets.data(), (uint32_t)targets.size(), offsets.data(),
-                                    runs.data(), &ix),
+        // then the runs, streamed in pieces of <= kPieceRuns (a longer row
+        // alone): a dense index never holds the worker's runs in HBM or RAM
+        const std::string im = a.str("index", "auto");
+        const int imode = im == "rle" ? CPD_INDEX_RLE : im == "dense" ? CPD_INDEX_DENSE : CPD_INDEX_AUTO;
+        cli::check(cpd_index_create_empty(dg, targets.data(), (uint32_t)targets.size(), imode,
+                                          total_runs, &ix),
                    "index");
-        std::printf("fifo_auto: worker %lld: %zu rows, %zu runs on device %d, ready in %.3fs; "
-                    "listening on %s\n",
-                    wid, targets.size(), runs.size(), device, now() - t0, fifo.c_str());
+        constexpr uint64_t kPieceRuns = 64ull << 20;  // 256 MB
+        std::vector<uint32_t> buf;
+        std::vector<uint64_t> rel;
+        for (size_t k = 0; k < heads.size(); ++k) {
+            const auto& off = heads[k].offsets;
+            const uint32_t nr = (uint32_t)heads[k].targets.size();
+            for (uint32_t r0 = 0; r0 < nr;) {
+                uint32_t r1 = r0 + 1;
+                while (r1 < nr && off[r1 + 1] - off[r0] <= kPieceRuns) ++r1;
+                buf.resize(off[r1] - off[r0]);
+                cpd::io::read_bucket_runs(paths[k], heads[k], off[r0], buf.size(), buf.data());
+                rel.resize(r1 - r0 + 1);
+                for (uint32_t i = r0; i <= r1; ++i) rel[i - r0] = off[i] - off[r0];
+                cli::check(cpd_index_append_rows(ix, r1 - r0, rel.data(), buf.data()), "index rows");
+                r0 = r1;
+            }
+        }
+        int mode = 0;
+        cli::check(cpd_index_get_mode(ix, &mode), "index mode");
+        std::printf("fifo_auto: worker %lld: %zu rows, %llu runs (%s index) on device %d, ready in "
+                    "%.3fs; listening on %s\n",
+                    wid, targets.size(), (unsigned long long)total_runs,
+                    mode == CPD_INDEX_DENSE ? "dense" : "rle", device, now() - t0, fifo.c_str());
         std::fflush(stdout);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "fifo_auto: %s\n", e.what());
+        ::unlink(fifo.c_str());
         return 1;
     }
 
-    if (::mkfifo(fifo.c_str(), 0666) != 0 && errno != EEXIST) {
-        std::fprintf(stderr, "fifo_auto: mkfifo %s: %s\n", fifo.c_str(), std::strerror(errno));
-        return 1;
-    }
     while (!g_stop) {
         std::string msg = read_all(fifo);
         if (g_stop) break;

@@ -10,6 +10,10 @@
 //                 [--plan P | --no-plan-cache]
 //                 [--write-threads T]  host threads copying + writing rows (8)
 //                 [--no-pipeline]      build, then export, then write, per group
+//                 [--plan-only]        build / load the cached plan and exit
+//
+// The plan (column order + hierarchy) is cached in D per graph; workers that
+// start together share it through cpd_plan_cache (one builds, the rest wait).
 //
 // Builds the CPD rows of every target this worker owns under the
 // distribution_controller partition, on the GPU, and writes one file per
@@ -232,17 +236,29 @@ int main(int argc, char** argv) {
         bool use_cache = !a.has("no-plan-cache");
         cpd_plan* plan = nullptr;
         double t0 = now();
-        if (use_cache && cpd_plan_load(plan_path.c_str(), &plan) == CPD_OK) {
-            std::printf("make_cpd_auto: loaded plan %s\n", plan_path.c_str());
+        cpd_plan_opts o{};
+        o.threads = (int)a.num("threads", 0);
+        o.verbose = a.has("verbose");
+        if (use_cache) {
+            // workers started together (make_cpds.py:58-60) share one cache:
+            // one builds, the others wait for it and load its plan
+            int status = 0;
+            cli::check(cpd_plan_cache(plan_path.c_str(), g.row_ptr.data(), g.dst.data(), g.w.data(),
+                                      g.n, g.m, &o, &plan, &status),
+                       "plan");
+            std::printf("make_cpd_auto: %s plan %s\n",
+                        status == 0 ? "loaded" : status == 1 ? "built and cached" : "built (cache not written)",
+                        plan_path.c_str());
         } else {
-            cpd_plan_opts o{};
-            o.threads = (int)a.num("threads", 0);
-            o.verbose = a.has("verbose");
             cli::check(cpd_plan_create(g.row_ptr.data(), g.dst.data(), g.w.data(), g.n, g.m, &o, &plan),
                        "plan");
-            if (use_cache) cli::check(cpd_plan_save(plan, plan_path.c_str()), "plan save");
         }
         double t_plan = now() - t0;
+        if (a.has("plan-only")) {  // warm the cache (host only, no GPU needed)
+            std::printf("make_cpd_auto: plan ready in %.3fs\n", t_plan);
+            cpd_plan_free(plan);
+            return 0;
+        }
         cpd_plan_info info{};
         cli::check(cpd_plan_info_get(plan, &info), "plan info");
         std::vector<uint32_t> order(g.n);

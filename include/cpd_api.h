@@ -136,8 +136,22 @@ int  cpd_plan_export_ch(const cpd_plan* p, uint32_t* rank,
                         uint64_t* up_off, uint32_t* up_dst, uint32_t* up_w,
                         uint64_t* dn_off, uint32_t* dn_dst, uint32_t* dn_w,
                         uint32_t* level_up, uint32_t* level_dn);
+/* save writes `path`.tmp.<pid>.<n> and renames it into place (atomic for
+ * concurrent readers; concurrent savers of the same plan do not collide).
+ * load checks the file's consistency: the column order is a permutation and
+ * the hierarchy's arrays agree in size and range.                           */
 int  cpd_plan_save(const cpd_plan* p, const char* path);
 int  cpd_plan_load(const char* path, cpd_plan** out);
+/* Load the plan cached at `path` if it was built from this very graph, else
+ * build it and save it there.  make_cpds.py:58-60 starts every worker at once
+ * (tmux -d) on one --outdir, so several processes may reach a cold cache
+ * together: an exclusive flock(2) on `path`.lock lets one of them build while
+ * the others wait and then load what it saved.  *status = 0 loaded, 1 built
+ * and saved, 2 built but the cache could not be written (the plan is still
+ * returned: a cache failure never fails the build).                         */
+int  cpd_plan_cache(const char* path, const uint32_t* row_ptr, const uint32_t* dst,
+                    const uint32_t* w, uint32_t n, uint32_t m, const cpd_plan_opts* opts,
+                    cpd_plan** out, int* status);
 void cpd_plan_free(cpd_plan* p);
 
 /* ------------------------------------------------------------------------ */
@@ -189,6 +203,27 @@ int  cpd_index_create(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows,
                       cpd_index** out);
 /* Same, straight from device-resident rows (no host round trip). */
 int  cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out);
+
+/* Streamed index — the load of fifo_auto (make_fifos.py:21 loads every CPD
+ * the worker owns; README.md:110).  Declare the rows (row i = target
+ * row_targets[i]) and their total run count, then append the rows in order,
+ * in chunks, from host arrays (a bucket file read piece by piece) or from a
+ * device-built cpd_rows; queries need every row appended.  The mode is fixed
+ * at creation: DENSE (or AUTO resolving to it: 4 * total_runs > n/2 * nrows)
+ * expands each chunk into the 4-bit move tables as it arrives and keeps no
+ * runs, so HBM holds nrows * n/2 bytes however large the runs are; RLE keeps
+ * the runs (total_runs of capacity).  Appended host rows are format-checked
+ * on the GPU (first run at column 0, columns increasing and < n), CPD_E_ARG
+ * otherwise.                                                                 */
+int  cpd_index_create_empty(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows,
+                            int mode, uint64_t total_runs, cpd_index** out);
+/* offsets: count + 1 values relative to the chunk (offsets[0] = 0). */
+int  cpd_index_append_rows(cpd_index* ix, uint32_t count, const uint64_t* offsets,
+                           const uint32_t* runs);
+int  cpd_index_append_built_rows(cpd_index* ix, const cpd_rows* r);
+/* Rows declared / appended, runs resident in HBM, bytes of dense tables.     */
+int  cpd_index_info(const cpd_index* ix, uint32_t* nrows, uint32_t* added,
+                    uint64_t* runs_resident, uint64_t* dense_bytes);
 
 /* In-HBM representation the extraction walks.  RLE: binary search in the run
  * rows (galloping from the previous move's run).  DENSE: the rows expanded on
