@@ -47,7 +47,12 @@ EXPORTED = [
     "cpd_index_free", "cpd_timing_enable", "cpd_timing_reset", "cpd_timing_get",
     "cpd_index_set_mode", "cpd_index_get_mode", "cpd_plan_cache", "cpd_index_create_empty",
     "cpd_index_append_rows", "cpd_index_append_built_rows", "cpd_index_info",
+    "cpd_synth_road_graph_ex",
 ]
+# generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
+# graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
+# SURVEY.md §8(d) as written (row-major ids, bidirectional, E/N/W/S order)
+SYNTH_STYLES = {"shuffled": 7, "spec": 0}
 INDEX_MODES = {"auto": 0, "rle": 1, "dense": 2}
 
 
@@ -175,18 +180,22 @@ class RoadGraph:
         return len(self.dst)
 
 
-def synth_road_graph(width: int, height: int, seed: int, mean_outdeg: float = 2.5) -> RoadGraph:
+def synth_road_graph(width: int, height: int, seed: int, mean_outdeg: float = 2.5,
+                     style: str = "shuffled") -> RoadGraph:
+    flags = SYNTH_STYLES[style]
     n, m = C.c_uint32(), C.c_uint32()
-    _check(lib.cpd_synth_road_graph(width, height, C.c_double(mean_outdeg), C.c_uint64(seed),
-                                    C.byref(n), C.byref(m), None, None, None, None, None))
+    _check(lib.cpd_synth_road_graph_ex(width, height, C.c_double(mean_outdeg), C.c_uint64(seed),
+                                       C.c_uint32(flags), C.byref(n), C.byref(m), None, None,
+                                       None, None, None))
     rp = np.empty(n.value + 1, np.uint32)
     dst = np.empty(m.value, np.uint32)
     w = np.empty(m.value, np.uint32)
     x = np.empty(n.value, np.int32)
     y = np.empty(n.value, np.int32)
-    _check(lib.cpd_synth_road_graph(width, height, C.c_double(mean_outdeg), C.c_uint64(seed),
-                                    C.byref(n), C.byref(m), _ptr(rp, u32p), _ptr(dst, u32p),
-                                    _ptr(w, u32p), _ptr(x, i32p), _ptr(y, i32p)))
+    _check(lib.cpd_synth_road_graph_ex(width, height, C.c_double(mean_outdeg), C.c_uint64(seed),
+                                       C.c_uint32(flags), C.byref(n), C.byref(m), _ptr(rp, u32p),
+                                       _ptr(dst, u32p), _ptr(w, u32p), _ptr(x, i32p),
+                                       _ptr(y, i32p)))
     return RoadGraph(rp, dst, w, x, y)
 
 

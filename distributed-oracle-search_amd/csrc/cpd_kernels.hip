@@ -1868,28 +1868,38 @@ void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t 
 
 // Table-search knobs (A/B runs; results are identical under every setting):
 // CPD_TS_V1=1 runs the lane-per-query kernels without co-fetch or refill;
-// CPD_TS_ILP (1 or 2) walks per lane; CPD_TS_WAVES = waves the batch is cut
-// into (chunk = nq / waves rounded up to 64 x ILP, at least that).
+// CPD_TS_ILP (1 or 2) walks per lane; the batch is cut into chunks of
+// ceil(nq / waves) queries (a multiple of 64 x ILP, at most CPD_TS_CHUNK_MAX
+// for dense rows).  Measured on the 1M-node bench (1M queries, MI355X,
+// tools_scripts/query_ab.py): dense walks want few waves that each refill
+// their lanes ~16 times (waves 1024: 88M q/s; 8192 waves, i.e. no refill:
+// 60M; lane per query: 43.7M), RLE walks — a chain of dependent loads per hop
+// — want every wave slot filled (8192); ILP 2 was slower in both.
 uint32_t ts_v1() {
     static const uint32_t v = env_u32("CPD_TS_V1", 0);
     return v;
 }
 uint32_t ts_ilp() {
-    static const uint32_t v = env_u32("CPD_TS_ILP", 2) >= 2 ? 2u : 1u;
+    static const uint32_t v = env_u32("CPD_TS_ILP", 1) >= 2 ? 2u : 1u;
     return v;
 }
-uint32_t ts_waves() {
-    static const uint32_t v = std::max(1u, env_u32("CPD_TS_WAVES", 8192));
-    return v;
+uint32_t ts_waves(uint32_t dflt) {
+    static const uint32_t v = env_u32("CPD_TS_WAVES", 0);
+    return v ? v : dflt;
+}
+uint32_t ts_chunk_max(uint32_t dflt) {
+    static const uint32_t v = env_u32("CPD_TS_CHUNK_MAX", 0);
+    return v ? v : dflt;
 }
 
 template <class Rows>
 static void launch_walk(const uint2* adj, uint32_t shift, const Rows& rows, const uint32_t* qs,
                         const uint32_t* qt, const uint32_t* qrow, uint32_t nq, uint32_t limit,
                         uint64_t* cost, uint32_t* hops, uint8_t* fin, unsigned long long* agg,
-                        hipStream_t s) {
+                        uint32_t waves_target, uint32_t chunk_max, hipStream_t s) {
     const uint32_t ilp = ts_ilp(), unit = 64u * ilp;
-    uint64_t chunk = ((uint64_t)nq + ts_waves() - 1u) / ts_waves();
+    uint64_t chunk = ((uint64_t)nq + waves_target - 1u) / waves_target;
+    chunk = std::min<uint64_t>(chunk, std::max(unit, chunk_max));
     chunk = std::max<uint64_t>(unit, (chunk + unit - 1u) / unit * unit);
     const uint64_t waves = ((uint64_t)nq + chunk - 1u) / chunk;
     const dim3 grid((uint32_t)std::max<uint64_t>(1u, (waves + 3u) / 4u)), blk(256);
@@ -1933,7 +1943,8 @@ void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32
         return;
     }
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::DenseRows{dense, npad / 8u}, qs,
-                qt, qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, s);
+                qt, qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(1024),
+                ts_chunk_max(1024), s);
 }
 
 void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
@@ -1948,7 +1959,8 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
         return;
     }
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::RleRows{offsets, runs}, qs, qt,
-                qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, s);
+                qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(8192),
+                ts_chunk_max(1u << 30), s);
 }
 
 }  // namespace cpd

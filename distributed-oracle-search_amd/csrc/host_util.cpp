@@ -162,19 +162,28 @@ static uint32_t uf_find(std::vector<uint32_t>& p, uint32_t a) {
     return a;
 }
 
-static SynthGraph synth(uint32_t W, uint32_t H, double mean_outdeg, uint64_t seed) {
+// flags (CPD_SYNTH_*): SHUFFLE_IDS permutes node ids (else id = row-major
+// lattice cell), ONE_WAY makes a fifth of the extra lattice edges one-way
+// (else every edge is bidirectional), SHUFFLE_EDGES shuffles each node's
+// out-edge order (else east, north, west, south).  The RNG stream is the same
+// for every flag set, so the lattice, tree, extras and weights do not depend
+// on the flags beyond what they switch.
+static SynthGraph synth(uint32_t W, uint32_t H, double mean_outdeg, uint64_t seed,
+                        uint32_t flags = CPD_SYNTH_SHUFFLED) {
     CPD_REQUIRE(W >= 2 && H >= 2, CPD_E_ARG, "lattice must be at least 2x2");
     CPD_REQUIRE((uint64_t)W * H < (1u << 28), CPD_E_RANGE, "lattice too large");
     CPD_REQUIRE(mean_outdeg >= 2.0 && mean_outdeg <= 4.0, CPD_E_ARG,
                 "mean out-degree must be in [2, 4]");
+    CPD_REQUIRE((flags & ~CPD_SYNTH_SHUFFLED) == 0, CPD_E_ARG, "unknown synth flags");
     Rng rng(seed);
     const uint32_t n = W * H;
     SynthGraph g;
     g.n = n;
-    // random node ids
+    // node ids: random permutation, or the lattice cell itself
     std::vector<uint32_t> id(n);
     std::iota(id.begin(), id.end(), 0u);
-    shuffle(id, rng);
+    shuffle(id, rng);  // drawn either way (same RNG stream for every flag set)
+    if (!(flags & CPD_SYNTH_SHUFFLE_IDS)) std::iota(id.begin(), id.end(), 0u);
     std::vector<int32_t> gx(n), gy(n);
     for (uint32_t j = 0; j < H; ++j)
         for (uint32_t i = 0; i < W; ++i) {
@@ -224,16 +233,28 @@ static SynthGraph synth(uint32_t W, uint32_t H, double mean_outdeg, uint64_t see
         if (in_tree[k]) continue;
         double speed = 0.6 + 0.8 * rng.uniform();
         uint32_t a = lat[k].first, b = lat[k].second;
-        if (rng.uniform() < 0.2) {  // one-way street, random direction
-            if (rng.uniform() < 0.5) std::swap(a, b);
+        const bool one_way = rng.uniform() < 0.2;
+        const bool flip = one_way && rng.uniform() < 0.5;  // drawn under every flag set
+        if (one_way && (flags & CPD_SYNTH_ONE_WAY)) {  // one-way street, random direction
+            if (flip) std::swap(a, b);
             arcs.push_back({a, b, weight(a, b, speed)});
         } else {
             arcs.push_back({a, b, weight(a, b, speed)});
             arcs.push_back({b, a, weight(b, a, speed)});
         }
     }
-    // CSR in node-id space with shuffled per-node out-edge order
+    // CSR in node-id space; per-node out-edge order shuffled or by direction
     const uint32_t m = (uint32_t)arcs.size();
+    if (!(flags & CPD_SYNTH_SHUFFLE_EDGES)) {
+        // east, north, west, south (cell space): the k-th out-edge of every
+        // node points the same way wherever that way has an edge
+        auto dir = [W](const Arc& a) {
+            return a.b == a.a + 1 ? 0 : a.b == a.a + W ? 1 : a.b + 1 == a.a ? 2 : 3;
+        };
+        std::stable_sort(arcs.begin(), arcs.end(), [&](const Arc& x, const Arc& y) {
+            return x.a != y.a ? x.a < y.a : dir(x) < dir(y);
+        });
+    }
     g.row_ptr.assign(n + 1, 0);
     for (auto& a : arcs) g.row_ptr[id[a.a] + 1]++;
     for (uint32_t v = 0; v < n; ++v) g.row_ptr[v + 1] += g.row_ptr[v];
@@ -249,6 +270,7 @@ static SynthGraph synth(uint32_t W, uint32_t H, double mean_outdeg, uint64_t see
         uint32_t b = g.row_ptr[v], e = g.row_ptr[v + 1];
         for (uint32_t i = e - b; i > 1; --i) {
             uint32_t j = rng.below(i);
+            if (!(flags & CPD_SYNTH_SHUFFLE_EDGES)) continue;  // drawn, not applied
             std::swap(g.dst[b + i - 1], g.dst[b + j]);
             std::swap(g.w[b + i - 1], g.w[b + j]);
         }
@@ -323,9 +345,17 @@ int cpd_synth_road_graph(uint32_t width, uint32_t height, double mean_outdeg,
                          uint64_t seed, uint32_t* n, uint32_t* m,
                          uint32_t* row_ptr, uint32_t* dst, uint32_t* w,
                          int32_t* x, int32_t* y) {
+    return cpd_synth_road_graph_ex(width, height, mean_outdeg, seed, CPD_SYNTH_SHUFFLED, n, m,
+                                   row_ptr, dst, w, x, y);
+}
+
+int cpd_synth_road_graph_ex(uint32_t width, uint32_t height, double mean_outdeg,
+                            uint64_t seed, uint32_t flags, uint32_t* n, uint32_t* m,
+                            uint32_t* row_ptr, uint32_t* dst, uint32_t* w,
+                            int32_t* x, int32_t* y) {
     return guarded([&] {
         CPD_REQUIRE(n && m, CPD_E_ARG, "synth: n/m outputs required");
-        SynthGraph g = synth(width, height, mean_outdeg, seed);
+        SynthGraph g = synth(width, height, mean_outdeg, seed, flags);
         uint32_t gm = (uint32_t)g.dst.size();
         if (!row_ptr) {
             *n = g.n;

@@ -33,14 +33,22 @@ int main(int argc, char** argv) {
     long long W = a.num("width", -1), H = a.num("height", W);
     std::string out = a.str("out");
     if (W < 2 || H < 2 || out.empty()) {
-        std::fprintf(stderr, "usage: gen_synth --width W [--height H] --seed S --out PREFIX ...\n");
+        std::fprintf(stderr, "usage: gen_synth --width W [--height H] --seed S --out PREFIX [--style shuffled|spec] ...\n");
         return 2;
     }
     uint64_t seed = (uint64_t)a.num("seed", 1);
     double outdeg = std::atof(a.str("outdeg", "2.5").c_str());
+    // --style shuffled (default; round-1 graphs) | spec (SURVEY.md §8d as
+    // written: row-major ids, bidirectional edges, E/N/W/S out-edge order)
+    const std::string style = a.str("style", "shuffled");
+    if (style != "shuffled" && style != "spec") {
+        std::fprintf(stderr, "gen_synth: --style must be shuffled or spec\n");
+        return 2;
+    }
+    const uint32_t flags = style == "spec" ? 0u : CPD_SYNTH_SHUFFLED;
     uint32_t n = 0, m = 0;
-    cli::check(cpd_synth_road_graph((uint32_t)W, (uint32_t)H, outdeg, seed, &n, &m, nullptr, nullptr,
-                                    nullptr, nullptr, nullptr),
+    cli::check(cpd_synth_road_graph_ex((uint32_t)W, (uint32_t)H, outdeg, seed, flags, &n, &m, nullptr,
+                                       nullptr, nullptr, nullptr, nullptr),
                "synth");
     cpd::io::XYGraph g;
     g.n = n;
@@ -50,8 +58,9 @@ int main(int argc, char** argv) {
     g.w.resize(m);
     g.x.resize(n);
     g.y.resize(n);
-    cli::check(cpd_synth_road_graph((uint32_t)W, (uint32_t)H, outdeg, seed, &n, &m, g.row_ptr.data(),
-                                    g.dst.data(), g.w.data(), g.x.data(), g.y.data()),
+    cli::check(cpd_synth_road_graph_ex((uint32_t)W, (uint32_t)H, outdeg, seed, flags, &n, &m,
+                                       g.row_ptr.data(), g.dst.data(), g.w.data(), g.x.data(),
+                                       g.y.data()),
                "synth");
     try {
         cpd::io::write_xy(out + ".xy", n, g.row_ptr.data(), g.dst.data(), g.w.data(), g.x.data(),

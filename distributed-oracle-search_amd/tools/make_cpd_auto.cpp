@@ -11,6 +11,7 @@
 //                 [--write-threads T]  host threads copying + writing rows (8)
 //                 [--no-pipeline]      build, then export, then write, per group
 //                 [--plan-only]        build / load the cached plan and exit
+//                 [--targets-from S]   only rows of targets of scenario S (q s t)
 //
 // The plan (column order + hierarchy) is cached in D per graph; workers that
 // start together share it through cpd_plan_cache (one builds, the rest wait).
@@ -217,7 +218,7 @@ int main(int argc, char** argv) {
                      "usage: make_cpd_auto --input X.xy --partmethod {div|mod} --partkey K "
                      "--workerid I --maxworker W [--outdir D] [--device G] [--batch B] "
                      "[--threads T] [--plan P | --no-plan-cache] [--write-threads T] "
-                     "[--no-pipeline]\n");
+                     "[--no-pipeline] [--plan-only] [--targets-from SCEN]\n");
         return 2;
     }
     int mcode = cli::method_code(method);
@@ -271,13 +272,27 @@ int main(int argc, char** argv) {
         for (uint32_t b = 0; b < nb; ++b)
             if (b % (uint32_t)W == (uint32_t)wid) owned.push_back(b);
         uint32_t chunk = (uint32_t)(((uint64_t)g.n + key - 1) / key);
+        // --targets-from SCEN: only the rows some query of the scenario needs
+        // (its "q s t" targets; process_query.py:56-57 routes by t), so a
+        // partial CPD for a known workload stays small on disk
+        std::vector<char> wanted;
+        if (a.has("targets-from")) {
+            wanted.assign(g.n, 0);
+            for (const auto& q : cpd::io::read_scen(a.str("targets-from"))) {
+                if (q.second >= g.n) throw std::runtime_error("scenario target out of range");
+                wanted[q.second] = 1;
+            }
+        }
         auto bucket_nodes = [&](uint32_t b) {
             std::vector<uint32_t> v;
+            auto keep = [&](uint64_t x) {
+                if (wanted.empty() || wanted[x]) v.push_back((uint32_t)x);
+            };
             if (mcode == CPD_PART_MOD) {
-                for (uint64_t x = b; x < g.n; x += (uint64_t)key) v.push_back((uint32_t)x);
+                for (uint64_t x = b; x < g.n; x += (uint64_t)key) keep(x);
             } else {
                 for (uint64_t x = (uint64_t)b * chunk; x < std::min<uint64_t>(g.n, (uint64_t)(b + 1) * chunk); ++x)
-                    v.push_back((uint32_t)x);
+                    keep(x);
             }
             return v;
         };

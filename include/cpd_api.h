@@ -96,6 +96,22 @@ int cpd_synth_road_graph(uint32_t width, uint32_t height, double mean_outdeg,
                          uint64_t seed, uint32_t* n, uint32_t* m,
                          uint32_t* row_ptr, uint32_t* dst, uint32_t* w,
                          int32_t* x, int32_t* y);
+/* The same generator with its departures from SURVEY.md §8(d) switchable:
+ * flags = 0 is the §8(d) recipe as written (node id = row-major lattice cell,
+ * every edge bidirectional, out-edges ordered east, north, west, south);
+ * CPD_SYNTH_SHUFFLED (= what cpd_synth_road_graph builds) permutes node ids,
+ * makes a fifth of the extra edges one-way and shuffles each out-edge list.
+ * The shuffled edge order makes a reverse-CPD column's move (the column's own
+ * out-edge index) uncorrelated with its neighbours', so rows compress
+ * poorly; the direction order lets neighbouring columns share moves.        */
+#define CPD_SYNTH_SHUFFLE_IDS   1u
+#define CPD_SYNTH_SHUFFLE_EDGES 2u
+#define CPD_SYNTH_ONE_WAY       4u
+#define CPD_SYNTH_SHUFFLED      7u
+int cpd_synth_road_graph_ex(uint32_t width, uint32_t height, double mean_outdeg,
+                            uint64_t seed, uint32_t flags, uint32_t* n, uint32_t* m,
+                            uint32_t* row_ptr, uint32_t* dst, uint32_t* w,
+                            int32_t* x, int32_t* y);
 /* [host] Congested weights (the `.diff` stand-in): a share
  * `frac` of the edges get w * U[lo, hi] rounded up; others unchanged.        */
 int cpd_synth_congestion(uint32_t m, const uint32_t* w, double frac, double lo,

@@ -1,0 +1,52 @@
+"""Shared set-up of the at-size GPU tests (BASELINE.json configs): the graphs,
+a per-session plan cache, and the sampled-target definition of configs[4]."""
+import os
+
+import numpy as np
+
+import cpd
+
+CACHE = os.environ.get("CPD_TEST_CACHE", "/tmp/cpd-test-cache")
+
+
+def plan_for(g, tag):
+    """The graph's plan, built once and cached on local disk for the session
+    (and later sessions on the same box)."""
+    os.makedirs(CACHE, exist_ok=True)
+    plan, _ = cpd.Plan.cache(os.path.join(CACHE, f"{tag}.plan"), g)
+    return plan
+
+
+def sample_targets(n, k, seed):
+    """configs[4]: k targets sampled without replacement."""
+    return np.sort(np.random.default_rng(seed).choice(n, size=k, replace=False)).astype(np.uint32)
+
+
+def owned(nodes, maxworker, method, key, wid, n):
+    """The members of `nodes` that worker `wid` owns (distribution_controller)."""
+    nodes = np.asarray(nodes, np.int64)
+    if method == "mod":
+        bid = nodes % key
+    else:
+        bid = nodes // (-(-n // key))
+    return nodes[(bid % maxworker) == wid].astype(np.uint32)
+
+
+def spread(a, k):
+    """k entries of a, evenly spaced (first and last included)."""
+    idx = np.unique(np.linspace(0, len(a) - 1, k).round().astype(np.int64))
+    return np.asarray(a)[idx]
+
+
+def check_row_format(off, runs, n):
+    """Every row starts at column 0, its run columns strictly increase and are
+    < n; moves are 4-bit (checked by construction)."""
+    off = np.asarray(off, np.int64)
+    cols = (np.asarray(runs) >> 4).astype(np.int64)
+    starts = off[:-1]
+    assert np.all(np.diff(off) > 0)
+    assert np.all(cols[starts] == 0)
+    inc = np.diff(cols) > 0
+    inc[starts[1:] - 1] = True  # row boundaries
+    assert np.all(inc)
+    assert cols.max() < n

@@ -1,0 +1,113 @@
+"""GPU parity at BASELINE.json configs[3]: the synthetic 1M-node / 2.5M-edge
+road graph (1000 x 1000 lattice, seed 1), partition div 8, worker 0's targets
+at the full default batch (16384 rows) — the bench's own workload.
+
+  - 128 rows spread over the worker's targets: bit-exact against the oracle;
+  - one full 16384-row batch: every row well formed, 8 rows (first / last /
+    interior lanes and slabs) bit-exact, then streamed into a dense index and
+    walked: free-flow cost == Dijkstra distance for every query of 16 targets;
+  - congested (.diff stand-in, SURVEY.md §8d: 10% of edges x U[1, 3], seed 3)
+    and free-flow queries over the oracle's 128 rows, dense and RLE: cost,
+    moves and finished flags bit-exact.
+"""
+import gc
+
+import numpy as np
+import pytest
+
+import cpd
+import oracle
+from scale_common import check_row_format, owned, plan_for, spread
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def w1m():
+    g = cpd.synth_road_graph(1000, 1000, seed=1)
+    plan = plan_for(g, "synth1000-s1")
+    dev = cpd.Graph(plan, device=0, batch=16384)  # the bench's default batch at 1M nodes
+    mine = owned(np.arange(g.n), 8, "div", 8, 0, g.n)
+    yield g, plan, dev, mine
+    del dev, plan
+    gc.collect()
+
+
+@pytest.fixture(scope="module")
+def rows128(w1m):
+    g, plan, dev, mine = w1m
+    targets = spread(mine, 128)
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    return targets, ref_off, ref_runs
+
+
+def test_1m_rows_bit_exact(w1m, rows128):
+    g, plan, dev, mine = w1m
+    targets, ref_off, ref_runs = rows128
+    off, runs = dev.build_rows(targets).export()
+    np.testing.assert_array_equal(off, ref_off)
+    np.testing.assert_array_equal(runs, ref_runs)
+
+
+def test_1m_full_batch(w1m):
+    g, plan, dev, mine = w1m
+    B = dev.batch
+    assert B == 16384
+    targets = mine[:B]
+    rows = dev.build_rows(targets)
+    nrows, total = rows.count()
+    assert nrows == B
+    lanes = np.unique(np.concatenate([[0, 1, 1023, 1024, 8191, 8192, B - 2, B - 1],
+                                      np.arange(0, B, 997)]))
+    sample = [0, 1023, 1024, 5000, 8192, 12345, B - 2, B - 1]
+    for i in lanes:
+        off, runs = rows.export_range(int(i), 1)
+        check_row_format(off, runs, g.n)
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets[sample])
+    for k, i in enumerate(sample):
+        off, runs = rows.export_range(i, 1)
+        np.testing.assert_array_equal(runs, ref_runs[int(ref_off[k]):int(ref_off[k + 1])],
+                                      err_msg=f"row {i} (target {targets[i]})")
+    # the whole batch as a streamed dense index (what fifo_auto holds), walked
+    ix = cpd.Index.streamed(dev, targets, total, mode="dense")
+    ix.append_rows(rows)
+    del rows  # the dense index alone stays in HBM
+    gc.collect()
+    rng = np.random.default_rng(7)
+    probe = rng.choice(targets, 16, replace=False)
+    nq = 200_000
+    s = rng.integers(0, g.n, nq).astype(np.uint32)
+    t = np.where(np.arange(nq) % 4 == 0, probe[rng.integers(0, 16, nq)],
+                 targets[rng.integers(0, B, nq)]).astype(np.uint32)
+    cost, hops, fin, st = ix.query(s, t)
+    assert fin.all(), "the graph is strongly connected: every walk must reach t"
+    assert st["finished"] == nq and st["hops"] == int(hops.sum())
+    for tt in probe:
+        d = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, tt)
+        sel = t == tt
+        np.testing.assert_array_equal(cost[sel], d[s[sel]].astype(np.uint64))
+
+
+@pytest.mark.parametrize("mode", ["dense", "rle"])
+def test_1m_congested_and_free_flow_vs_oracle(w1m, rows128, mode):
+    g, plan, dev, mine = w1m
+    targets, ref_off, ref_runs = rows128
+    # load the oracle's rows the way fifo_auto loads bucket files: in chunks
+    ix = cpd.Index.streamed(dev, targets, int(ref_off[-1]), mode=mode)
+    for a in range(0, 128, 40):
+        b = min(128, a + 40)
+        ix.append(ref_off[a:b + 1] - ref_off[a], ref_runs[int(ref_off[a]):int(ref_off[b])])
+    rng = np.random.default_rng(8)
+    nq = 50_000
+    s = rng.integers(0, g.n, nq).astype(np.uint32)
+    t = targets[rng.integers(0, len(targets), nq)]
+    w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
+    order = plan.order()
+    for w_sel in (g.w, w_cong, g.w):
+        ix.set_weights(None if w_sel is g.w else w_sel)
+        rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, w_sel, order, targets, ref_off,
+                                         ref_runs, s, t)
+        cost, hops, fin, _ = ix.query(s, t)
+        np.testing.assert_array_equal(cost, rc)
+        np.testing.assert_array_equal(hops, rh)
+        np.testing.assert_array_equal(fin, rf)
