@@ -1,21 +1,33 @@
 #!/usr/bin/env python3
 """bench.py — MI355X CPD build (sources/s, GTEPS) and table-search (queries/s).
 
-Workload (BASELINE.json configs[3]; melb-both.xy is a missing blob, so the
-1M-node synthetic road graph the north star names is the headline graph):
-  synthetic grid-perturbed road graph, 1000 x 1000 lattice (1M nodes, 2.5M
-  edges), seed 1; partition `div 8` over the ranks (distribution_controller
-  semantics), one rank per GPU.  A step = one batch of `--batch` CPD rows built
-  from the rank's own targets: two CH sweeps, first-move sets and the RLE rows,
-  all resident in HBM (weak scaling: every rank builds the same number of rows
-  per step; no collective on the data path).  After the timed steps each rank
-  runs `--queries` table-search queries against its last batch of rows.
+Workloads (--workload; melb-both.xy is a missing blob, so every graph is the
+seeded synthetic road graph of SURVEY.md §8d):
+  synth1m (default, BASELINE.json configs[3]): 1000 x 1000 lattice (1M nodes,
+    2.5M edges), seed 1, partition `div 8` over the ranks.  A step = one batch
+    of --batch CPD rows built from the rank's own targets: two CH sweeps,
+    first-move sets and the RLE rows, all resident in HBM (weak scaling: every
+    rank builds the same number of rows per step; no collective on the data
+    path).  Then 1M table-search queries against the rank's last batch.
+  synth1m-spec: the same lattice with SURVEY.md §8d's recipe as written (node
+    id = lattice cell, every edge bidirectional, out-edges E/N/W/S) instead
+    of the shuffled ids / one-way streets / shuffled out-edge order.
+  synth4m (configs[4]): 2000 x 2000, seed 4; 256k targets sampled (seed 5),
+    `div 8`: rank r is worker r of 8 (one worker's ~32k rows per GPU, weak
+    scaling).  Steps build batches of the worker's rows; then ALL its rows are
+    streamed into a dense index and it serves its share of the 10M-query
+    batch (t uniform over the sample, seed 6: ~1.25M routed to each worker).
+  melb300k (configs[0]-[2] stand-in): 548 x 548 spec-style graph, seed 1,
+    `mod 3`; query leg with the .diff stand-in as for synth1m.
 
 One JSON line on rank 0: value = rows/s over all ranks; roofline for the
-dominant kernel from HIP events; cpu_baseline = the C oracle (OpenMP) on a
-bounded sample of the same workload, rank 0 at N = 1 only.
+dominant build kernel from HIP events, query_roofline for the walk kernel;
+cpu_baseline = the C oracle (OpenMP, all host threads of this job) on a
+bounded sample of the same workload, plus the configs[0] partitioned run
+(300k stand-in, mod 3: three workers one after another with every thread,
+then at once with a third each), rank 0 at N = 1 only.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
   (N > 1 is launched by torch.distributed.run; RANK/LOCAL_RANK/WORLD_SIZE)
 """
 import argparse
@@ -31,48 +43,86 @@ METRIC = "CPD build sources/sec + GTEPS; table-search queries/sec; % HBM rooflin
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PLAN_TAG = "ch823"      # bump when the hierarchy builder changes (cache key)
 
+WORKLOADS = {
+    "synth1m": dict(width=1000, seed=1, style="shuffled", method="div", key=8, sample=None,
+                    queries=1_000_000, config="configs[3]"),
+    "synth1m-spec": dict(width=1000, seed=1, style="spec", method="div", key=8, sample=None,
+                         queries=1_000_000, config="configs[3], SURVEY 8d recipe as written"),
+    "synth4m": dict(width=2000, seed=4, style="shuffled", method="div", key=8,
+                    sample=(262144, 5), queries=10_000_000, config="configs[4]"),
+    "melb300k": dict(width=548, seed=1, style="spec", method="mod", key=3, sample=None,
+                     queries=1_000_000, config="configs[0]-[2] stand-in"),
+}
+
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=1000, help="lattice side (nodes = width^2)")
-    ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--partmethod", default="div")
-    ap.add_argument("--partkey", type=int, default=8)
+    ap.add_argument("--workload", default="synth1m", choices=sorted(WORKLOADS))
+    ap.add_argument("--width", type=int, default=0, help="override the lattice side")
+    ap.add_argument("--seed", type=int, default=0, help="override the graph seed")
+    ap.add_argument("--partmethod", default="")
+    ap.add_argument("--partkey", type=int, default=0)
     ap.add_argument("--batch", type=int, default=0,
                     help="rows per step (multiple of 1024); 0 = what fits in HBM, <= 16384")
-    ap.add_argument("--queries", type=int, default=1_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--queries", type=int, default=0, help="0 = the workload's")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every host thread this job may use (OMP_NUM_THREADS or affinity)")
     ap.add_argument("--cpu-rows-per-thread", type=int, default=64,
                     help="CPU baseline sample: rows per host thread (~10 s of CPU work)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu-partitioned", action="store_true",
+                    help="skip the configs[0] mod-3 partitioned CPU run")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-worker", default="", help=argparse.SUPPRESS)
     ap.add_argument("--cache", default=os.environ.get("CPD_BENCH_CACHE", "/tmp/cpd-bench-cache"))
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    wl = WORKLOADS[a.workload]
+    a.width = a.width or wl["width"]
+    a.seed = a.seed or wl["seed"]
+    a.style = wl["style"]
+    a.partmethod = a.partmethod or wl["method"]
+    a.partkey = a.partkey or wl["key"]
+    a.sample = wl["sample"]
+    a.queries = a.queries or wl["queries"]
+    return a
+
+
+def plan_path(args):
+    style = "" if args.style == "shuffled" else f"-{args.style}"
+    return os.path.join(args.cache, f"synth{args.width}-s{args.seed}{style}-{PLAN_TAG}.plan")
 
 
 # rocprofv3 kernel names -> the library's timing names
 KERNEL_NAMES = {"sweep_level<true": "sweep_up", "sweep_up_": "sweep_up",
                 "sweep_level<false": "sweep_down", "sweep_down8": "sweep_down",
                 "first_moves": "first_moves", "rle_scan<false": "rle_count",
-                "rle_scan<true": "rle_emit", "table_search": "table_search"}
+                "rle_scan<true": "rle_emit", "DenseRows": "table_search_dense",
+                "RleRows": "table_search", "table_search_dense": "table_search_dense",
+                "table_search(": "table_search", "expand_rows": "expand_rows"}
 
 
-def pmc_traffic(args, plan_path):
+def kernel_key(name):
+    return next((v for k, v in KERNEL_NAMES.items() if k in name), None)
+
+
+def pmc_traffic(args):
     """HBM traffic per launch from rocprofv3 PMC counters.
 
     One child run per counter (MI355X_MICROARCH.md: FETCH_SIZE costs 3 and
     WRITE_SIZE 2 of the 4 TCC slots, so they cannot share a pass), each a
-    one-step build of the same workload.  Both counters are in KiB; on gfx950
-    FETCH_SIZE reports half the bytes of a 16-B/lane streaming read, so it is
-    doubled (our kernels' loads are 16 B per lane); WRITE_SIZE is exact for
-    16-B stores.  Started before this process touches the GPU.  Returns
-    {name: {"launches", "FETCH_SIZE", "WRITE_SIZE", "bytes_per_launch"}} or None.
+    one-step build plus one dense query launch of the same workload.  Both
+    counters are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a
+    16-B/lane streaming read, so it is doubled (the build kernels' loads are 16
+    B per lane; the walk's 4-B and 16-B gathers are uncalibrated — the walk's
+    read figure is reported raw x 2 as well, as an upper estimate); WRITE_SIZE
+    is exact for 16-B stores.  Started before this process touches the GPU.
+    Returns {name: {"launches", "read/write/bytes_per_launch"}} or None.
     """
     import csv
     import glob
@@ -86,9 +136,9 @@ def pmc_traffic(args, plan_path):
         d = os.path.join(base, counter)
         cmd = ["rocprofv3", "--pmc", counter, "-d", d, "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "1",
-               "--warmup", "0", "--width", str(args.width), "--seed", str(args.seed),
-               "--partmethod", args.partmethod, "--partkey", str(args.partkey),
-               "--batch", str(args.batch), "--cache", args.cache]
+               "--warmup", "0", "--workload", args.workload, "--width", str(args.width),
+               "--seed", str(args.seed), "--partmethod", args.partmethod, "--partkey",
+               str(args.partkey), "--batch", str(args.batch), "--cache", args.cache]
         try:
             p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
                                timeout=240, cwd=base)
@@ -100,7 +150,7 @@ def pmc_traffic(args, plan_path):
             log(f"pmc pass {counter} failed: {p.stderr[-400:]}")
             return None
         for row in csv.DictReader(open(files[0])):
-            name = next((v for k, v in KERNEL_NAMES.items() if k in row["Kernel_Name"]), None)
+            name = kernel_key(row["Kernel_Name"])
             if name is None:
                 continue
             e = out.setdefault(name, {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0, "n_FETCH_SIZE": 0,
@@ -118,14 +168,24 @@ def pmc_traffic(args, plan_path):
 
 
 def pmc_child(args):
-    """One build step under the profiler (no torch: nothing else on the GPU)."""
+    """One build step and one dense query launch under the profiler (no torch:
+    nothing else on the GPU)."""
     sys.path.insert(0, PKG)
+    import numpy as np
     import cpd
-    plan = cpd.Plan.load(os.path.join(args.cache, f"synth{args.width}-s{args.seed}-{PLAN_TAG}.plan"))
+    plan = cpd.Plan.load(plan_path(args))
     n = plan.info()["n"]
     dev = cpd.Graph(plan, device=0, batch=args.batch)
-    owned = shard_targets(n, 1, args.partmethod, args.partkey, 0)
-    dev.build_rows(batch_of(owned, dev.batch, 0))
+    owned = rank_targets(args, n, 1, 0)
+    targets = batch_of(owned, dev.batch, 0)
+    rows = dev.build_rows(targets)
+    ix = cpd.Index.streamed(dev, targets, rows.count()[1], mode="dense")
+    ix.append_rows(rows)
+    del rows
+    rng = np.random.default_rng(100)
+    nq = min(args.queries, 1_000_000)
+    ix.prepare(rng.integers(0, n, nq).astype(np.uint32), targets[rng.integers(0, len(targets), nq)])
+    ix.run()
 
 
 def log(*a):
@@ -167,6 +227,24 @@ def shard_targets(nodenum, world, method, key, rank):
     return cpd.owned_nodes(nodenum, world, method, key, rank)
 
 
+def sample_nodes(n, k, seed):
+    """configs[4]'s sampled targets (without replacement), sorted."""
+    import numpy as np
+    return np.sort(np.random.default_rng(seed).choice(n, size=k, replace=False)).astype(np.uint32)
+
+
+def rank_targets(args, n, world, rank):
+    """synth1m / melb300k: the partition over `world` workers (rank = worker).
+    synth4m: worker `rank` of the configuration's 8 over the sampled targets
+    (one worker per GPU at any N: weak scaling)."""
+    import numpy as np
+    if args.sample is None:
+        return shard_targets(n, world, args.partmethod, args.partkey, rank)
+    s = sample_nodes(n, *args.sample).astype(np.int64)
+    bid = s % args.partkey if args.partmethod == "mod" else s // (-(-n // args.partkey))
+    return s[(bid % 8) == rank].astype(np.uint32)
+
+
 def batch_of(owned, B, i):
     """Step i's targets: the next B of the rank's own, wrapping around."""
     import numpy as np
@@ -185,7 +263,8 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
     value = total_rows / elapsed_max
     roof = None
     if kt:
-        name, k = max(kt.items(), key=lambda kv: kv[1]["ms"])
+        name, k = max(((a, b) for a, b in kt.items() if a not in _COUNTERS),
+                      key=lambda kv: kv[1]["ms"])
         achieved = k["bytes"] / (k["ms"] / 1e3) / 1e9 if k["ms"] > 0 else 0.0
         t = (traffic or {}).get(name)
         roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
@@ -196,6 +275,7 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
                 "avg_launch_us": round(k["ms"] * 1e3 / max(1, k["launches"]), 3),
                 "bytes_per_launch": round(k["bytes"] / max(1, k["launches"]), 1)}
     qps = q_totals[0] / (q_ms_max / 1e3) if q_ms_max > 0 else 0.0
+    wl = WORKLOADS[getattr(args, "workload", "synth1m")]
     return {
         "metric": METRIC,
         "value": round(value, 2),
@@ -211,7 +291,9 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
         "data": "synthetic (seeded grid-perturbed road graph; melb-both.xy blob is missing)",
         "config": {"workload": f"synthetic-{n // 1000}k-road cpd-build {args.partmethod} "
                                f"{args.partkey} + table-search",
-                   "graph": f"grid-perturbed {args.width}x{args.width} seed {args.seed}",
+                   "baseline_config": wl["config"],
+                   "graph": f"grid-perturbed {args.width}x{args.width} seed {args.seed} "
+                            f"({getattr(args, 'style', 'shuffled')})",
                    "nodes": n, "edges": m, "rows_per_step_per_gpu": B,
                    "partition": f"{args.partmethod} {args.partkey}",
                    "parallelism": f"target-partition x{world} (no collective)"},
@@ -244,9 +326,105 @@ _COUNTERS = ("wide_rows", "group_rows")
 
 
 # --------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the C oracle on host threads
+
+def host_threads(args):
+    """Every thread this job may use: OMP_NUM_THREADS when the box sets it
+    (the GPU box's share is 16 of a much larger host), else the affinity."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def host_info(threads):
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "threads": threads,
+            "cpu_model": model, "omp_proc_bind": os.environ.get("OMP_PROC_BIND", ""),
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS", "")}
+
+
+def cpu_worker(spec):
+    """One configs[0] worker on the CPU (a child process): its sample of rows
+    (reverse Dijkstra + first moves + RLE) and its queries, on `threads`."""
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import cpd
+    import oracle
+    sp = json.loads(spec)
+    g = cpd.synth_road_graph(sp["width"], sp["width"], seed=sp["seed"], style=sp["style"])
+    order = oracle.dfs_preorder(g.row_ptr, g.dst)
+    mine = cpd.owned_nodes(g.n, 3, "mod", 3, sp["wid"])
+    rng = np.random.default_rng(10 + sp["wid"])
+    targets = np.sort(rng.choice(mine, sp["rows"], replace=False)).astype(np.uint32)
+    s = rng.integers(0, g.n, sp["queries"]).astype(np.uint32)
+    t = targets[rng.integers(0, len(targets), sp["queries"])]
+    t0 = time.perf_counter()
+    off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, targets, threads=sp["threads"])
+    t1 = time.perf_counter()
+    _, hops, _ = oracle.table_search(g.row_ptr, g.dst, g.w, order, targets, off, runs, s, t,
+                                     threads=sp["threads"])
+    t2 = time.perf_counter()
+    print(json.dumps({"rows_s": t1 - t0, "queries_s": t2 - t1, "rows": len(targets),
+                      "queries": len(s), "runs": int(off[-1]), "hops": int(hops.sum()),
+                      "n": g.n, "m": g.m}), flush=True)
+
+
+def cpu_partitioned(threads, rows_per_worker=384, queries=20000):
+    """configs[0] on the 300k stand-in (mod 3): three workers one after another
+    with every thread, then all three at once with a third each."""
+    env = dict(os.environ, OMP_PROC_BIND="close")
+    spec = lambda wid, th: json.dumps({"width": 548, "seed": 1, "style": "spec", "wid": wid,
+                                       "threads": th, "rows": rows_per_worker,
+                                       "queries": queries})
+    cmd = lambda wid, th: [sys.executable, os.path.abspath(__file__), "--cpu-worker",
+                           spec(wid, th)]
+    seq = []
+    for wid in range(3):
+        p = subprocess.run(cmd(wid, threads), capture_output=True, text=True, env=env,
+                           timeout=600, check=True)
+        seq.append(json.loads(p.stdout.strip().splitlines()[-1]))
+    per = max(1, threads // 3)
+    procs = [subprocess.Popen(cmd(wid, per), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True, env=env) for wid in range(3)]
+    con = []
+    for p in procs:
+        o, e = p.communicate(timeout=900)
+        if p.returncode:
+            raise RuntimeError(e[-400:])
+        con.append(json.loads(o.strip().splitlines()[-1]))
+    rows = sum(r["rows"] for r in seq)
+    q = sum(r["queries"] for r in seq)
+    return {
+        "graph": "melb stand-in: 548x548 spec-style synthetic (300,304 nodes), seed 1, mod 3",
+        "rows_per_worker": rows_per_worker, "queries_per_worker": queries,
+        "mean_runs_per_row": round(sum(r["runs"] for r in seq) / rows, 1),
+        "sequential": {"threads_per_worker": threads,
+                       "rows_per_s": round(rows / sum(r["rows_s"] for r in seq), 2),
+                       "queries_per_s": round(q / sum(r["queries_s"] for r in seq), 1)},
+        "concurrent": {"threads_per_worker": per,
+                       "rows_per_s": round(rows / max(r["rows_s"] for r in con), 2),
+                       "queries_per_s": round(q / max(r["queries_s"] for r in con), 1)},
+    }
+
+
+# --------------------------------------------------------------------------
 
 def main():
     args = parse()
+    if args.cpu_worker:
+        cpu_worker(args.cpu_worker)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world == 1:
         # not under torch.distributed.run: launch ourselves that way (a child,
@@ -260,6 +438,7 @@ def main():
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("OMP_PROC_BIND", "close")  # before any OpenMP runtime starts
 
     import numpy as np
     import torch  # first: libcpd then binds to the same HIP runtime
@@ -270,16 +449,16 @@ def main():
 
     # ---- graph + host preprocessing (cached, built once per node; host only)
     t0 = time.time()
-    g = cpd.synth_road_graph(args.width, args.width, seed=args.seed)
+    g = cpd.synth_road_graph(args.width, args.width, seed=args.seed, style=args.style)
     os.makedirs(args.cache, exist_ok=True)
-    plan_path = os.path.join(args.cache, f"synth{args.width}-s{args.seed}-{PLAN_TAG}.plan")
-    if local == 0 and not os.path.exists(plan_path):
+    ppath = plan_path(args)
+    if local == 0 and not os.path.exists(ppath):
         log(f"building hierarchy for {g.n} nodes / {g.m} edges ...")
-        cpd.Plan(g).save(plan_path)
+        cpd.Plan(g).save(ppath)
     # PMC passes: children, before this process initialises the GPU
     traffic = None
     if world == 1 and not args.no_pmc:
-        traffic = pmc_traffic(args, plan_path)
+        traffic = pmc_traffic(args)
 
     # CPD_BENCH_SHARE_GPU=1 (rehearsal on a 1-GPU box only): every rank uses
     # GPU 0 and the harness collectives go over gloo.  Never used for numbers.
@@ -295,7 +474,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     comm = Comm(world, rank, local, device=None if share else f"cuda:{local}")
     comm.barrier()
-    plan = cpd.Plan.load(plan_path)
+    while not os.path.exists(ppath):  # another local rank is still saving it
+        time.sleep(0.5)
+    plan = cpd.Plan.load(ppath)
     pinfo = plan.info()
     assert pinfo["n"] == g.n and pinfo["m"] == g.m
     log(f"rank {rank}: plan ready in {time.time() - t0:.1f}s (hierarchy build "
@@ -309,7 +490,7 @@ def main():
     if int(bmin) != dev.batch:
         dev.set_batch(int(bmin))
     B = dev.batch
-    owned = shard_targets(g.n, world, args.partmethod, args.partkey, rank)
+    owned = rank_targets(args, g.n, world, rank)
     if len(owned) == 0:
         raise SystemExit(f"rank {rank} owns no targets")
 
@@ -330,12 +511,38 @@ def main():
     nrows, nruns = rows.count()
     last_targets = batch_of(owned, B, args.warmup + args.steps - 1)
 
-    # ---- table-search on the last batch's rows ------------------------------
-    ix = cpd.Index(dev, rows=rows)
+    # ---- table-search ------------------------------------------------------
     rng = np.random.default_rng(100 + rank)
-    nq = args.queries
-    qs = rng.integers(0, g.n, nq).astype(np.uint32)
-    qt = last_targets[rng.integers(0, len(last_targets), nq)]
+    extra = {}
+    w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
+    if args.sample is None:
+        # the rank's last batch of rows, kept as RLE too (both forms timed)
+        ix = cpd.Index(dev, rows=rows)
+        nq = args.queries
+        qs = rng.integers(0, g.n, nq).astype(np.uint32)
+        qt = last_targets[rng.integers(0, len(last_targets), nq)]
+        index_rows = len(last_targets)
+    else:
+        # every row the worker owns, streamed batch by batch into dense tables
+        ti = time.perf_counter()
+        ix = cpd.Index.streamed(dev, owned, 1 << 62, mode="dense")
+        for a in range(0, len(owned), B):
+            rows = dev.build_rows(owned[a:a + B], reuse=rows)
+            ix.append_rows(rows)
+        comm.barrier()
+        extra["worker_index_build_s"] = round(time.perf_counter() - ti, 3)
+        del rows
+        rows = None
+        index_rows = len(owned)
+        # the 10M-query batch: t uniform over the sample (seed 6), s uniform;
+        # this worker's share is what the head routes to it
+        qrng = np.random.default_rng(6)
+        allt = sample_nodes(g.n, *args.sample)[qrng.integers(0, args.sample[0], args.queries)]
+        alls = qrng.integers(0, g.n, args.queries).astype(np.uint32)
+        mine = np.isin(allt, owned)
+        qs, qt = alls[mine], allt[mine]
+        nq = len(qs)
+        extra["worker_queries"] = nq
     ix.prepare(qs, qt)
 
     def time_queries(mode, reps=3):
@@ -350,15 +557,29 @@ def main():
         (ms_max,) = comm.reduce([ms], "MAX")
         return tot, ms_max
 
-    q_rle, q_rle_ms = time_queries("rle")
+    q_rle = q_rle_ms = None
+    if args.sample is None:
+        q_rle, q_rle_ms = time_queries("rle")
     q_totals, q_ms_max = time_queries("auto")
     index_mode = ix.mode
     # congested leg (configs[2]): the .diff stand-in of SURVEY.md §8d — 10% of
     # edges x U[1, 3], rounded up — sent with the batch as fifo_auto does
-    w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
     ix.set_weights(w_cong)
     q_cong, q_cong_ms = time_queries("auto")
     ix.set_weights(None)
+    # walk kernel vs its roofline: per query 8 (s, t) + 4 (row) + 13 (cost,
+    # moves, flag) bytes, per move the 4-B word holding the move + the 8-B edge
+    qbytes = 25.0 * q_totals[0] + 12.0 * q_totals[2]
+    qach = qbytes / (q_totals[1] / 1e3) / 1e9 if q_totals[1] else 0.0
+    qkey = "table_search_dense" if index_mode == "dense" else "table_search"
+    qt_pmc = (traffic or {}).get(qkey)
+    query_roof = {"bound": "hbm", "kernel": qkey, "achieved": round(qach, 1),
+                  "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(qach / HBM_PEAK_GBPS, 4),
+                  "traffic": round(qt_pmc["bytes_per_launch"], 1) if qt_pmc else None,
+                  "traffic_unit": "bytes/launch (PMC, 1M-query launch of the pmc child)",
+                  "bytes_per_launch": round(qbytes / max(1, q_totals[0]) * nq, 1),
+                  "avg_launch_ms": round(q_totals[1] / max(1.0, q_totals[0] / max(1, nq)), 3),
+                  "note": "latency/request-bound dependent walk; HBM bytes are not its limit"}
 
     # ---- CPU baseline + full-size parity sample (rank 0, N = 1) -------------
     cpu = None
@@ -366,8 +587,11 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        sample = batch_of(owned, B, 0)[: threads * args.cpu_rows_per_thread]
+        threads = host_threads(args)
+        # ~10 s of CPU work: the per-row Dijkstra grows with n (64 rows per
+        # thread at 1M nodes)
+        per_thread = max(4, round(args.cpu_rows_per_thread * 1e6 / g.n))
+        sample = batch_of(owned, B, 0)[: threads * per_thread]
         order = plan.order()
         tc = time.perf_counter()
         ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, sample, threads=threads)
@@ -383,27 +607,39 @@ def main():
                                          cs, ct, threads=threads)
         cpu_q_s = time.perf_counter() - tq
         gix = cpd.Index(dev, rows=grows)
-        gc, gh, gf, _ = gix.query(cs, ct)
-        parity = parity and bool(np.array_equal(gc, rc) and np.array_equal(gh, rh))
+        gc_, gh, gf, _ = gix.query(cs, ct)
+        parity = parity and bool(np.array_equal(gc_, rc) and np.array_equal(gh, rh))
         rcc, rch, _ = oracle.table_search(g.row_ptr, g.dst, w_cong, order, sample, ref_off,
                                           ref_runs, cs, ct, threads=threads)
         gix.set_weights(w_cong)
         gcc, gch, _, _ = gix.query(cs, ct)
         parity = parity and bool(np.array_equal(gcc, rcc) and np.array_equal(gch, rch))
+        del gix, grows
         cpu = {"value": round(len(sample) / cpu_s, 3), "unit": "sources/s", "cores": threads,
                "kind": "port",
                "sample": f"{len(sample)} CPD rows of the same graph and partition (reverse Dijkstra "
-                         f"+ first moves + RLE, C oracle, OpenMP {threads} threads, {cpu_s:.1f}s); "
-                         f"table-search {cq} queries in {cpu_q_s:.2f}s",
-               "queries_per_s": round(cq / cpu_q_s, 1)}
+                         f"+ first moves + RLE, C oracle, OpenMP {threads} threads, "
+                         f"OMP_PROC_BIND=close, {cpu_s:.1f}s); table-search {cq} queries in "
+                         f"{cpu_q_s:.2f}s",
+               "queries_per_s": round(cq / cpu_q_s, 1),
+               "host": host_info(threads)}
+        if not args.no_cpu_partitioned:
+            try:
+                cpu["partitioned_configs0"] = cpu_partitioned(threads)
+            except Exception as e:  # reported, never fatal to the GPU numbers
+                cpu["partitioned_configs0"] = {"error": str(e)[-300:]}
 
     if rank == 0:
         out = assemble(args, world, (g.n, g.m), B, elapsed_max, q_totals, q_ms_max, nrows, nruns,
                        kt, cpu, parity, pinfo, traffic)
         out["query_index"] = index_mode
-        out["queries_per_s_rle"] = round(q_rle[0] / (q_rle_ms / 1e3), 1) if q_rle_ms else 0.0
+        out["query_index_rows_per_gpu"] = index_rows
+        out["query_roofline"] = query_roof
+        if q_rle_ms:
+            out["queries_per_s_rle"] = round(q_rle[0] / (q_rle_ms / 1e3), 1)
         out["queries_per_s_congested"] = (round(q_cong[0] / (q_cong_ms / 1e3), 1)
                                           if q_cong_ms else 0.0)
+        out.update(extra)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
