@@ -7,7 +7,8 @@ import json
 import sys
 
 # most specific first: rocprof names carry template arguments
-NAMES = [("sweep_down8", "sweep_down"), ("first_moves_n4", "first_moves"),
+NAMES = [("DenseRows", "table_search_dense"), ("RleRows", "table_search"),
+         ("validate_rows", "validate_rows"), ("sweep_down8", "sweep_down"), ("first_moves_n4", "first_moves"),
          ("count_wide_rows", "wide_rows_count"), ("target_mask", "target_mask"),
          ("sweep_up_sparse", "sweep_up"), ("sweep_up_chunks", "sweep_up"),
          ("sweep_up_init", "sweep_up_init"), ("sweep_level<true>", "sweep_up"),
