@@ -349,13 +349,28 @@ def host_info(threads):
     except OSError:
         pass
     return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "threads": threads,
-            "cpu_model": model, "omp_proc_bind": os.environ.get("OMP_PROC_BIND", ""),
+            "cpu_model": model, "omp_proc_bind": "unset (see _child_env)",
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS", "")}
 
 
+def _child_env(threads):
+    """A clean OpenMP environment for a CPU leg: its own process (torch's and
+    libcpd's OpenMP runtimes in the bench process may have pinned the main
+    thread), `threads` threads, no binding.  OMP_PROC_BIND=close was measured
+    harmful here: the job's CPU share is a quota over all host CPUs (affinity
+    = every CPU), so bound workers all start at CPU 0 and stack on the same
+    cores (r02: the concurrent mod-3 run at a third of the sequential rate)."""
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    env.pop("OMP_PROC_BIND", None)
+    env.pop("OMP_PLACES", None)
+    return env
+
+
 def cpu_worker(spec):
-    """One configs[0] worker on the CPU (a child process): its sample of rows
-    (reverse Dijkstra + first moves + RLE) and its queries, on `threads`."""
+    """One timed CPU leg in a child process: CPD rows (reverse Dijkstra +
+    first moves + RLE) for its targets, then table-search over them, with the
+    C oracle on `threads`.  Targets: worker `wid` of `mod 3` (a sample of
+    `rows`), or the list in `targets_npy`."""
     sys.path.insert(0, PKG)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -364,9 +379,12 @@ def cpu_worker(spec):
     sp = json.loads(spec)
     g = cpd.synth_road_graph(sp["width"], sp["width"], seed=sp["seed"], style=sp["style"])
     order = oracle.dfs_preorder(g.row_ptr, g.dst)
-    mine = cpd.owned_nodes(g.n, 3, "mod", 3, sp["wid"])
-    rng = np.random.default_rng(10 + sp["wid"])
-    targets = np.sort(rng.choice(mine, sp["rows"], replace=False)).astype(np.uint32)
+    rng = np.random.default_rng(sp.get("qseed", 10 + sp.get("wid", 0)))
+    if sp.get("targets_npy"):
+        targets = np.load(sp["targets_npy"]).astype(np.uint32)
+    else:
+        mine = cpd.owned_nodes(g.n, 3, "mod", 3, sp["wid"])
+        targets = np.sort(rng.choice(mine, sp["rows"], replace=False)).astype(np.uint32)
     s = rng.integers(0, g.n, sp["queries"]).astype(np.uint32)
     t = targets[rng.integers(0, len(targets), sp["queries"])]
     t0 = time.perf_counter()
@@ -380,29 +398,29 @@ def cpu_worker(spec):
                       "n": g.n, "m": g.m}), flush=True)
 
 
+def run_cpu_worker(spec, threads, timeout=900):
+    p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker",
+                          json.dumps(dict(spec, threads=threads))], stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True, env=_child_env(threads))
+    return p
+
+
+def collect(p, timeout=900):
+    o, e = p.communicate(timeout=timeout)
+    if p.returncode:
+        raise RuntimeError(e[-400:])
+    return json.loads(o.strip().splitlines()[-1])
+
+
 def cpu_partitioned(threads, rows_per_worker=384, queries=20000):
     """configs[0] on the 300k stand-in (mod 3): three workers one after another
     with every thread, then all three at once with a third each."""
-    env = dict(os.environ, OMP_PROC_BIND="close")
-    spec = lambda wid, th: json.dumps({"width": 548, "seed": 1, "style": "spec", "wid": wid,
-                                       "threads": th, "rows": rows_per_worker,
-                                       "queries": queries})
-    cmd = lambda wid, th: [sys.executable, os.path.abspath(__file__), "--cpu-worker",
-                           spec(wid, th)]
-    seq = []
-    for wid in range(3):
-        p = subprocess.run(cmd(wid, threads), capture_output=True, text=True, env=env,
-                           timeout=600, check=True)
-        seq.append(json.loads(p.stdout.strip().splitlines()[-1]))
+    spec = lambda wid: {"width": 548, "seed": 1, "style": "spec", "wid": wid,
+                        "rows": rows_per_worker, "queries": queries}
+    seq = [collect(run_cpu_worker(spec(wid), threads)) for wid in range(3)]
     per = max(1, threads // 3)
-    procs = [subprocess.Popen(cmd(wid, per), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                              text=True, env=env) for wid in range(3)]
-    con = []
-    for p in procs:
-        o, e = p.communicate(timeout=900)
-        if p.returncode:
-            raise RuntimeError(e[-400:])
-        con.append(json.loads(o.strip().splitlines()[-1]))
+    procs = [run_cpu_worker(spec(wid), per) for wid in range(3)]
+    con = [collect(p) for p in procs]
     rows = sum(r["rows"] for r in seq)
     q = sum(r["queries"] for r in seq)
     return {
@@ -438,7 +456,6 @@ def main():
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    os.environ.setdefault("OMP_PROC_BIND", "close")  # before any OpenMP runtime starts
 
     import numpy as np
     import torch  # first: libcpd then binds to the same HIP runtime
@@ -592,36 +609,38 @@ def main():
         # thread at 1M nodes)
         per_thread = max(4, round(args.cpu_rows_per_thread * 1e6 / g.n))
         sample = batch_of(owned, B, 0)[: threads * per_thread]
+        tnpy = os.path.join(args.cache, f"cpu-targets-{os.getpid()}.npy")
+        np.save(tnpy, sample)
+        cq = 20000
+        leg = collect(run_cpu_worker({"width": args.width, "seed": args.seed, "style": args.style,
+                                      "targets_npy": tnpy, "queries": cq, "qseed": 200},
+                                     threads))
+        os.remove(tnpy)
+        # parity at full size (untimed): 128 of the sample's rows and 20k
+        # queries over them, free-flow and congested, GPU against the oracle
         order = plan.order()
-        tc = time.perf_counter()
-        ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, sample, threads=threads)
-        cpu_s = time.perf_counter() - tc
-        grows = dev.build_rows(sample)
+        psamp = sample[:: max(1, len(sample) // 128)][:128]
+        ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, psamp, threads=threads)
+        grows = dev.build_rows(psamp)
         goff, gruns = grows.export()
         parity = bool(np.array_equal(goff, ref_off) and np.array_equal(gruns, ref_runs))
-        cq = 20000
         cs = rng.integers(0, g.n, cq).astype(np.uint32)
-        ct = sample[rng.integers(0, len(sample), cq)]
-        tq = time.perf_counter()
-        rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, order, sample, ref_off, ref_runs,
-                                         cs, ct, threads=threads)
-        cpu_q_s = time.perf_counter() - tq
+        ct = psamp[rng.integers(0, len(psamp), cq)]
         gix = cpd.Index(dev, rows=grows)
-        gc_, gh, gf, _ = gix.query(cs, ct)
-        parity = parity and bool(np.array_equal(gc_, rc) and np.array_equal(gh, rh))
-        rcc, rch, _ = oracle.table_search(g.row_ptr, g.dst, w_cong, order, sample, ref_off,
-                                          ref_runs, cs, ct, threads=threads)
-        gix.set_weights(w_cong)
-        gcc, gch, _, _ = gix.query(cs, ct)
-        parity = parity and bool(np.array_equal(gcc, rcc) and np.array_equal(gch, rch))
+        for w_sel in (g.w, w_cong):
+            rc, rh, _ = oracle.table_search(g.row_ptr, g.dst, w_sel, order, psamp, ref_off,
+                                            ref_runs, cs, ct, threads=threads)
+            gix.set_weights(None if w_sel is g.w else w_sel)
+            gc_, gh, _, _ = gix.query(cs, ct)
+            parity = parity and bool(np.array_equal(gc_, rc) and np.array_equal(gh, rh))
         del gix, grows
-        cpu = {"value": round(len(sample) / cpu_s, 3), "unit": "sources/s", "cores": threads,
-               "kind": "port",
-               "sample": f"{len(sample)} CPD rows of the same graph and partition (reverse Dijkstra "
-                         f"+ first moves + RLE, C oracle, OpenMP {threads} threads, "
-                         f"OMP_PROC_BIND=close, {cpu_s:.1f}s); table-search {cq} queries in "
-                         f"{cpu_q_s:.2f}s",
-               "queries_per_s": round(cq / cpu_q_s, 1),
+        cpu = {"value": round(leg["rows"] / leg["rows_s"], 3), "unit": "sources/s",
+               "cores": threads, "kind": "port",
+               "sample": f"{leg['rows']} CPD rows of the same graph and partition (reverse "
+                         f"Dijkstra + first moves + RLE, C oracle, OpenMP {threads} threads in a "
+                         f"child process, {leg['rows_s']:.1f}s); table-search {cq} queries over "
+                         f"them in {leg['queries_s']:.2f}s",
+               "queries_per_s": round(leg["queries"] / leg["queries_s"], 1),
                "host": host_info(threads)}
         if not args.no_cpu_partitioned:
             try:
