@@ -150,7 +150,7 @@ struct NLoad {
 
 __device__ __forceinline__ NLoad nl_issue(const NarrowRows& nr, uint32_t col, uint32_t grp,
                                           uint32_t B4, uint32_t l4) {
-    return NLoad{nr.base[(size_t)grp * nr.n + col],
+    return NLoad{nr.base[(size_t)col * nr.ng + grp],
                  reinterpret_cast<const uint2*>(nr.d16)[(size_t)col * B4 + l4]};
 }
 
@@ -308,7 +308,7 @@ struct NLoad8 {
 
 __device__ __forceinline__ NLoad8 nl8_issue(const NarrowRows& nr, uint32_t col, uint32_t grp,
                                             uint32_t B8, uint32_t l8) {
-    return NLoad8{nr.base[(size_t)grp * nr.n + col],
+    return NLoad8{nr.base[(size_t)col * nr.ng + grp],
                   reinterpret_cast<const uint4*>(nr.d16)[(size_t)col * B8 + l8]};
 }
 
@@ -344,12 +344,12 @@ __device__ __forceinline__ void narrow_store8(const NarrowRows& nr, uint4* __res
     if (half_bad) {
         d4[(size_t)col * B4 + 2u * l8] = acc.a;
         d4[(size_t)col * B4 + 2u * l8 + 1u] = acc.b;
-        if (head) nr.base[(size_t)grp * nr.n + col] = kWideRow;
+        if (head) nr.base[(size_t)col * nr.ng + grp] = kWideRow;
         return;
     }
     reinterpret_cast<uint4*>(nr.d16)[(size_t)col * B8 + l8] =
         make_uint4(q0 | (q1 << 16), q2 | (q3 << 16), q4 | (q5 << 16), q6 | (q7 << 16));
-    if (head) nr.base[(size_t)grp * nr.n + col] = b;
+    if (head) nr.base[(size_t)col * nr.ng + grp] = b;
 }
 
 __device__ __forceinline__ void fm_nib(const uint4& dv, const uint4& acc, uint32_t w, int k,
@@ -369,31 +369,37 @@ __device__ __forceinline__ uint32_t fm_pack4(const uint4& t, const uint4& acc, u
     return b0 | (b1 << 4) | (b2 << 8) | (b3 << 12);
 }
 
-__global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ desc,
-                                                   const uint2* __restrict__ arcs,
-                                                   uint32_t slot0, uint32_t count, uint32_t remap,
-                                                   uint32_t* __restrict__ dist,
-                                                   const uint4* __restrict__ tgt4, uint32_t B4,
-                                                   Closed cf, const uint32_t* __restrict__ live,
-                                                   uint16_t* __restrict__ fmleaf, NarrowRows nr) {
-    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t blk = L / count;
-    const uint32_t slot = slot0 + (L - blk * count);
-    const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
-    const uint32_t grp = l8 >> 5;                        // uniform per half-wave
-    const uint32_t B8 = B4 / 2u;
-    // the slot's descriptor, 128 B of scalar loads: (node word, first arc, end
-    // arc, -) + its first kDescArcs arcs (a leaf's out-edges in file order);
-    // for a level-1 node also its column and its <= 4 leaf arcs (closed form)
+// A down-sweep slot's descriptor (see down_desc_arcs): the 64-B head (node
+// word, arc range, first kDescArcs arcs) and, for a level-1 node, the
+// closed-form part (c0..c2).  LAZY: the closed-form part is loaded inside the
+// level-1 branch (only those slots pay for it) instead of with the head.
+struct Desc8 {
+    uint4 h, i0, i1, i2, c0, c1, c2;
+};
+
+template <bool LAZY>
+__device__ __forceinline__ Desc8 load_desc8(const uint4* __restrict__ desc, uint32_t slot) {
     const uint4* __restrict__ dp = desc + (size_t)slot * 8u;
-    const uint4 h = dp[0], i0 = dp[1], i1 = dp[2], i2 = dp[3];
-    const uint4 c0 = dp[4], c1 = dp[5], c2 = dp[6];
+    if (LAZY) return Desc8{dp[0], dp[1], dp[2], dp[3], {}, {}, {}};
+    return Desc8{dp[0], dp[1], dp[2], dp[3], dp[4], dp[5], dp[6]};
+}
+
+// One slot of the narrow down-sweep for the lane's 8 targets t.
+template <bool LAZY>
+__device__ __forceinline__ void down8_slot(const Desc8& D, const uint4* __restrict__ desc,
+                                           uint32_t slot, const U8& t, uint32_t l8, uint32_t grp,
+                                           uint32_t B4, uint32_t B8, uint4* __restrict__ d4,
+                                           const uint2* __restrict__ arcs, const Closed& cf,
+                                           const uint32_t* __restrict__ live,
+                                           uint16_t* __restrict__ fmleaf, const NarrowRows& nr) {
+    // (node word, first arc, end arc, -) + its first kDescArcs arcs (a leaf's
+    // out-edges in file order); for a level-1 node also its column and its
+    // <= 4 leaf arcs (closed form)
+    const uint4 i0 = D.i0, i1 = D.i1, i2 = D.i2;
     const uint2 inl[kDescArcs] = {make_uint2(i0.x, i0.y), make_uint2(i0.z, i0.w),
                                   make_uint2(i1.x, i1.y), make_uint2(i1.z, i1.w),
                                   make_uint2(i2.x, i2.y), make_uint2(i2.z, i2.w)};
-    const uint32_t vraw = h.x, a0 = h.y, a1 = h.z;
-    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
-    const U8 t{tgt4[2u * l8], tgt4[2u * l8 + 1u]};
+    const uint32_t vraw = D.h.x, a0 = D.h.y, a1 = D.h.z;
     uint32_t v;
     U8 acc;
     if (vraw & kLeafBit) {
@@ -427,6 +433,8 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ des
             return;
         }
     } else if (vraw & kL1Bit) {  // closed form from the descriptor
+        const uint4* __restrict__ dp = desc + (size_t)slot * 8u;
+        const uint4 c0 = LAZY ? dp[4] : D.c0, c1 = LAZY ? dp[5] : D.c1, c2 = LAZY ? dp[6] : D.c2;
         v = c0.x;
         acc = U8{leaf4(t.a, v, 0u), leaf4(t.b, v, 0u)};
         const uint2 la[4] = {make_uint2(c0.z, c0.w), make_uint2(c1.x, c1.y),
@@ -475,6 +483,46 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ des
         min8(acc, nl8_finish(nl8_issue(nr, e.x, grp, B8, l8), d4, e.x, B4, l8), e.y);
     }
     narrow_store8(nr, d4, v, grp, B4, B8, l8, acc);
+}
+
+
+// Narrow down-sweep launch: logical block = (group of K consecutive slots,
+// 8 x blockDim targets), slot groups fastest, XCD-remapped.  A wave walks its
+// K slots for the same targets (loaded once) and loads the next slot's
+// descriptor while the current slot's gathers are in flight, so the scalar
+// descriptor fetch leaves the critical path after the first slot.  K = 1 is
+// one slot per block.
+template <int K>
+__global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ desc,
+                                                   const uint2* __restrict__ arcs,
+                                                   uint32_t slot0, uint32_t count, uint32_t remap,
+                                                   uint32_t* __restrict__ dist,
+                                                   const uint4* __restrict__ tgt4, uint32_t B4,
+                                                   Closed cf, const uint32_t* __restrict__ live,
+                                                   uint16_t* __restrict__ fmleaf, NarrowRows nr) {
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t ngrp = (count + K - 1) / K;
+    const uint32_t blk = L / ngrp;
+    const uint32_t s0 = slot0 + (L - blk * ngrp) * K;
+    const uint32_t s1 = min(s0 + K, slot0 + count);
+    const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
+    const uint32_t grp = l8 >> 5;                        // uniform per half-wave
+    const uint32_t B8 = B4 / 2u;
+    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    const U8 t{tgt4[2u * l8], tgt4[2u * l8 + 1u]};
+    if (K == 1) {
+        down8_slot<false>(load_desc8<false>(desc, s0), desc, s0, t, l8, grp, B4, B8, d4, arcs,
+                          cf, live, fmleaf, nr);
+        return;
+    }
+    Desc8 cur = load_desc8<true>(desc, s0);
+#pragma unroll 1
+    for (uint32_t s = s0; s < s1; ++s) {
+        Desc8 nxt = cur;
+        if (s + 1 < s1) nxt = load_desc8<true>(desc, s + 1);
+        down8_slot<true>(cur, desc, s, t, l8, grp, B4, B8, d4, arcs, cf, live, fmleaf, nr);
+        cur = nxt;
+    }
 }
 
 // Group rows stored wide (timing runs only): *out += #{base[i] == kWideRow}.
@@ -1679,6 +1727,13 @@ uint32_t down8_wpb() {  // CPD_DOWN8_WPB: 1, 2 or 4 waves per narrow down-sweep 
     }();
     return v;
 }
+uint32_t down8_k() {  // CPD_DOWN8_K: slots per wave in the narrow down-sweep (1, 2, 4, 8)
+    static const uint32_t v = [] {
+        const uint32_t k = env_u32("CPD_DOWN8_K", 1);
+        return k >= 8 ? 8u : k >= 4 ? 4u : k >= 2 ? 2u : 1u;
+    }();
+    return v;
+}
 uint32_t fm_wpb() {
     static const uint32_t v = env_u32("CPD_FM_WPB", 2);
     return v;
@@ -1724,9 +1779,17 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
             // (4 waves = 2048 targets: only when the slab count is even)
             const uint32_t wpb8 = down8_wpb() == 4 && slabs % 2 ? 2u : down8_wpb();
             const uint32_t tpb8 = 64u * wpb8;
-            launch(kern::sweep_down8, dim3(count * slabs * 2u / wpb8), dim3(tpb8), s,
-                   reinterpret_cast<const uint4*>(desc), arcs, slot0, count, xcd_remap(), dist, t4,
-                   B / 4u, cf, (const uint32_t*)live, fmleaf, nr);
+            const uint32_t K = down8_k();
+            const uint32_t ngrp = (count + K - 1u) / K;
+            const dim3 g8(ngrp * slabs * 2u / wpb8), b8(tpb8);
+            const uint4* d = reinterpret_cast<const uint4*>(desc);
+            const uint32_t* lv = live;
+            switch (K) {
+                case 1: launch(kern::sweep_down8<1>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                case 2: launch(kern::sweep_down8<2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                case 4: launch(kern::sweep_down8<4>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                default: launch(kern::sweep_down8<8>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+            }
         } else
             launch(kern::sweep_level<false>, grid, blk, s, nodes, arc_off, arcs, slot0, count,
                    xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live, lf);
