@@ -137,8 +137,8 @@ struct cpd_graph {
     DevBuf<uint16_t> d16;
     DevBuf<uint32_t> dbase, ovf;
     NarrowRows narrow_rows(bool on) {
-        if (!on) return NarrowRows{nullptr, nullptr, B / 256u, nullptr};
-        return NarrowRows{d16.p, dbase.p, B / 256u, ovf.p};
+        if (!on) return NarrowRows{nullptr, nullptr, n, nullptr};
+        return NarrowRows{d16.p, dbase.p, n, ovf.p};
     }
     double n_leaf = 0, m_leaf = 0;    // leaves, their out-edges
     std::vector<double> dsc_lvl_leaves;
@@ -1007,7 +1007,7 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
                                 hipMemcpyDeviceToHost));
             for (uint32_t c = 0; c < n; ++c)
                 for (uint32_t p = 0; p < B; ++p) {
-                    const uint32_t base = b[(size_t)c * (B / 256u) + p / 256u];
+                    const uint32_t base = b[(size_t)(p / 256u) * n + c];
                     if (base == 0xFFFFFFFEu) continue;  // kept wide
                     const uint16_t d = q[(size_t)c * B + p];
                     h[(size_t)c * B + p] = d == 0xFFFFu ? CPD_INF : base + d;

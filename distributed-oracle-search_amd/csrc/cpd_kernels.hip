@@ -150,7 +150,7 @@ struct NLoad {
 
 __device__ __forceinline__ NLoad nl_issue(const NarrowRows& nr, uint32_t col, uint32_t grp,
                                           uint32_t B4, uint32_t l4) {
-    return NLoad{nr.base[(size_t)col * nr.ng + grp],
+    return NLoad{nr.base[(size_t)grp * nr.n + col],
                  reinterpret_cast<const uint2*>(nr.d16)[(size_t)col * B4 + l4]};
 }
 
@@ -308,7 +308,7 @@ struct NLoad8 {
 
 __device__ __forceinline__ NLoad8 nl8_issue(const NarrowRows& nr, uint32_t col, uint32_t grp,
                                             uint32_t B8, uint32_t l8) {
-    return NLoad8{nr.base[(size_t)col * nr.ng + grp],
+    return NLoad8{nr.base[(size_t)grp * nr.n + col],
                   reinterpret_cast<const uint4*>(nr.d16)[(size_t)col * B8 + l8]};
 }
 
@@ -344,12 +344,12 @@ __device__ __forceinline__ void narrow_store8(const NarrowRows& nr, uint4* __res
     if (half_bad) {
         d4[(size_t)col * B4 + 2u * l8] = acc.a;
         d4[(size_t)col * B4 + 2u * l8 + 1u] = acc.b;
-        if (head) nr.base[(size_t)col * nr.ng + grp] = kWideRow;
+        if (head) nr.base[(size_t)grp * nr.n + col] = kWideRow;
         return;
     }
     reinterpret_cast<uint4*>(nr.d16)[(size_t)col * B8 + l8] =
         make_uint4(q0 | (q1 << 16), q2 | (q3 << 16), q4 | (q5 << 16), q6 | (q7 << 16));
-    if (head) nr.base[(size_t)col * nr.ng + grp] = b;
+    if (head) nr.base[(size_t)grp * nr.n + col] = b;
 }
 
 __device__ __forceinline__ void fm_nib(const uint4& dv, const uint4& acc, uint32_t w, int k,
@@ -899,8 +899,14 @@ struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR press
 // so fewer partial-sector writes reach HBM (PMC writes 14.2 -> 10.1 GB per
 // 16384-row launch) — but the kernel is slower (16.0 -> 17.7 ms at 101 VGPRs,
 // 18.9 ms capped to 96 with spills): S = 1 is the default (CPD_FM_SEGS=2 to try).
-template <int G, int S>
-__global__ __launch_bounds__(256) void first_moves_n4(const uint2* __restrict__ adj,
+//
+// X = segments exchanged per workgroup (S = 1): the workgroup holds X wave
+// groups of TPS threads, group j computing segment j of X consecutive ones for
+// the same TPS x 4 targets; the groups swap their 16-B pieces through LDS so
+// that each lane stores 16 X contiguous bytes of a row (one row in X of the
+// lane's 4) — whole 64-B sectors at X = 4 instead of 16-B partial ones.
+template <int G, int S, int X = 1>
+__global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ adj,
                                                       const uint32_t* __restrict__ dist,
                                                       const uint32_t* __restrict__ tgt, uint32_t B,
                                                       uint32_t n, uint32_t npad, uint32_t remap,
@@ -909,12 +915,18 @@ __global__ __launch_bounds__(256) void first_moves_n4(const uint2* __restrict__ 
                                                       const uint16_t* __restrict__ fmleaf,
                                                       NarrowRows nr) {
     static_assert(kSeg % G == 0, "group size");
-    const uint32_t nblk = npad / (kSeg * S);
+    static_assert(X == 1 || S == 1, "exchange or wide segments, not both");
+    constexpr uint32_t TPS = 128;  // threads per segment group when X > 1
+    const uint32_t tps = X > 1 ? TPS : blockDim.x;
+    const uint32_t sgi = X > 1 ? threadIdx.x / TPS : 0u;   // this group's segment
+    const uint32_t tl = X > 1 ? threadIdx.x % TPS : threadIdx.x;
+    const uint32_t nblk = npad / (kSeg * S * X);
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t slab = L / nblk;
-    const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
+    const uint32_t l4 = slab * tps + tl;  // slab = tps x 4 targets
     const uint32_t B4 = B / 4u;
-    const uint32_t cb = (L - slab * nblk) * (kSeg * S);
+    const uint32_t cb0 = (L - slab * nblk) * (kSeg * S * X);
+    const uint32_t cb = cb0 + sgi * kSeg;
     const uint32_t lane = threadIdx.x & 63u;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
@@ -1007,6 +1019,22 @@ __global__ __launch_bounds__(256) void first_moves_n4(const uint2* __restrict__ 
         cur = nxt;
     }
     const size_t row_words = npad / 8u;
+    if (X > 1) {
+        // xch[segment][row of 4][thread]: conflict-free 16-B LDS accesses
+        __shared__ uint4 xch[X > 1 ? X : 1][4][TPS];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xch[sgi][i][tl] = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if ((uint32_t)i % X != sgi) continue;  // group j stores rows i == j (mod X)
+            uint4* __restrict__ o =
+                reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * row_words + cb0 / 8u);
+#pragma unroll
+            for (int sg = 0; sg < X; ++sg) o[sg] = xch[sg][i][tl];
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         uint4* __restrict__ o =
@@ -1746,6 +1774,13 @@ uint32_t fm_segs() {  // CPD_FM_SEGS: 32-column segments per pipelined first-mov
     static const uint32_t v = env_u32("CPD_FM_SEGS", 1);
     return v;
 }
+uint32_t fm_x() {  // CPD_FM_X: segments exchanged per first-moves workgroup (1, 2, 4)
+    static const uint32_t v = [] {
+        const uint32_t x = env_u32("CPD_FM_X", 1);
+        return x >= 4 ? 4u : x >= 2 ? 2u : 1u;
+    }();
+    return v;
+}
 uint32_t fm_g() {
     static const uint32_t v = env_u32("CPD_FM_G", 2);
     return v;
@@ -1878,7 +1913,16 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     if (nr.d16 && shift == 2 && fm_n4()) {
         const uint32_t r = xcd_remap();
-        if (fm_segs() == 2)
+        const uint32_t X = fm_x();
+        if (X > 1) {  // X groups of 128 threads, each 512 targets x one segment
+            const dim3 gx((npad / (kern::kSeg * X)) * ((rows + 1023u) / 1024u) * 2u), bx(128u * X);
+            if (X == 2)
+                launch(kern::first_moves_n4<2, 1, 2>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm,
+                       leafbits, fmleaf, nr);
+            else
+                launch(kern::first_moves_n4<2, 1, 4>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm,
+                       leafbits, fmleaf, nr);
+        } else if (fm_segs() == 2)
             launch(kern::first_moves_n4<2, 2>, dim3(grid.x / 2u), blk, s, adj, dist, tgt, B, n, npad,
                    r, fm, leafbits, fmleaf, nr);
         else
