@@ -1781,6 +1781,10 @@ uint32_t fm_x() {  // CPD_FM_X: segments exchanged per first-moves workgroup (1,
     }();
     return v;
 }
+uint32_t fm_xg() {  // CPD_FM_XG: columns per gather group in the exchange kernel (1 or 2)
+    static const uint32_t v = env_u32("CPD_FM_XG", 1) >= 2 ? 2u : 1u;
+    return v;
+}
 uint32_t fm_g() {
     static const uint32_t v = env_u32("CPD_FM_G", 2);
     return v;
@@ -1916,12 +1920,16 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
         const uint32_t X = fm_x();
         if (X > 1) {  // X groups of 128 threads, each 512 targets x one segment
             const dim3 gx((npad / (kern::kSeg * X)) * ((rows + 1023u) / 1024u) * 2u), bx(128u * X);
-            if (X == 2)
-                launch(kern::first_moves_n4<2, 1, 2>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm,
-                       leafbits, fmleaf, nr);
+            // gather groups of 1 column keep the exchange kernel at 90 VGPRs (5
+            // waves/SIMD); 2 columns take it to 124 (4 waves)
+            if (X == 2 && fm_xg() == 2)
+                launch(kern::first_moves_n4<2, 1, 2>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
+            else if (X == 2)
+                launch(kern::first_moves_n4<1, 1, 2>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
+            else if (fm_xg() == 2)
+                launch(kern::first_moves_n4<2, 1, 4>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
             else
-                launch(kern::first_moves_n4<2, 1, 4>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm,
-                       leafbits, fmleaf, nr);
+                launch(kern::first_moves_n4<1, 1, 4>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
         } else if (fm_segs() == 2)
             launch(kern::first_moves_n4<2, 2>, dim3(grid.x / 2u), blk, s, adj, dist, tgt, B, n, npad,
                    r, fm, leafbits, fmleaf, nr);
