@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Per-level down-sweep table: rocprofv3 kernel-trace durations and per-
+dispatch PMC bytes (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH §HBM) of one
+bench build step, matched by dispatch order (the trace and the two PMC passes
+run the same deterministic single-step child).
+
+  level_pmc.py TRACE_DIR FETCH_DIR WRITE_DIR OUT.txt
+"""
+import csv
+import glob
+import sys
+
+
+def rows(d, pat):
+    f = glob.glob(f"{d}/**/{pat}", recursive=True)[0]
+    return list(csv.DictReader(open(f)))
+
+
+def seq(rs, key):  # sweep_down8 dispatches in order, with a value per dispatch
+    out = []
+    for r in sorted(rs, key=lambda r: int(r["Dispatch_Id"])):
+        if "sweep_down8" in r["Kernel_Name"]:
+            out.append(key(r))
+    return out
+
+
+def main(trace, fetch, write, out):
+    t = seq(rows(trace, "*kernel_trace.csv"),
+            lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                       int(r["Grid_Size_X"])))
+    pf, pw = {}, {}
+    for r in rows(fetch, "*counter_collection.csv"):
+        if "sweep_down8" in r["Kernel_Name"]:
+            pf[int(r["Dispatch_Id"])] = pf.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+    for r in rows(write, "*counter_collection.csv"):
+        if "sweep_down8" in r["Kernel_Name"]:
+            pw[int(r["Dispatch_Id"])] = pw.get(int(r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
+    f = [pf[k] for k in sorted(pf)]
+    w = [pw[k] for k in sorted(pw)]
+    n = min(len(t), len(f), len(w))
+    lines = ["level  time_us  grid_threads  read_MB  write_MB  PMC_GB/s"]
+    tot_t = tot_b = 0.0
+    wide_t = wide_b = 0.0
+    order = sorted(range(n), key=lambda i: -t[i][0])[:20]
+    for i in range(n):
+        us = t[i][0] / 1e3
+        rd = 2.0 * f[i] * 1024 / 1e6
+        wr = w[i] * 1024 / 1e6
+        tot_t += us
+        tot_b += rd + wr
+        if i in order:
+            wide_t += us
+            wide_b += rd + wr
+        lines.append(f"{i:5d} {us:8.1f} {t[i][1]:12d} {rd:8.1f} {wr:8.1f} {(rd + wr) / us * 1e-3 * 1e3:8.0f}")
+    lines.append(f"all {n} levels: {tot_t / 1e3:.2f} ms, {tot_b / 1e3:.1f} GB PMC, "
+                 f"{tot_b / tot_t:.0f} GB/s")
+    lines.append(f"20 longest levels: {wide_t / 1e3:.2f} ms, {wide_b / 1e3:.1f} GB PMC, "
+                 f"{wide_b / wide_t:.0f} GB/s")
+    open(out, "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines[-2:]))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:5])
