@@ -47,7 +47,7 @@ EXPORTED = [
     "cpd_index_free", "cpd_timing_enable", "cpd_timing_reset", "cpd_timing_get",
     "cpd_index_set_mode", "cpd_index_get_mode", "cpd_plan_cache", "cpd_index_create_empty",
     "cpd_index_append_rows", "cpd_index_append_built_rows", "cpd_index_info",
-    "cpd_synth_road_graph_ex",
+    "cpd_synth_road_graph_ex", "cpd_query_search", "cpd_query_search_counters",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
@@ -77,6 +77,17 @@ class PlanInfo(C.Structure):
 class QueryStats(C.Structure):
     _fields_ = [("queries", C.c_uint64), ("finished", C.c_uint64), ("hops", C.c_uint64),
                 ("cost", C.c_uint64), ("kernel_ms", C.c_double)]
+
+
+class SearchOpts(C.Structure):
+    _fields_ = [("hscale", C.c_double), ("fscale", C.c_double), ("k_moves", C.c_int32),
+                ("itrs", C.c_int64), ("time_ns", C.c_uint64), ("capacity", C.c_uint32)]
+
+
+class SearchStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("queries", "finished", "expanded", "inserted",
+                                          "touched", "updated", "surplus", "plen", "overflow")] + \
+               [("kernel_ms", C.c_double), ("tables_ms", C.c_double)]
 
 
 class KernelTime(C.Structure):
@@ -462,6 +473,25 @@ class Index:
         st = QueryStats()
         _check(lib.cpd_query_run(self._h, C.c_int32(k_moves), C.byref(st)))
         return {k: getattr(st, k) for k, _ in QueryStats._fields_}
+
+    def search(self, s, t, hscale=1.0, fscale=0.0, k_moves=-1, itrs=-1, time_ns=0,
+               capacity=0):
+        """CPD-heuristic search (cpd_query_search) for queries (s, t):
+        (cost, plen, finished, counters[nq, 5], stats)."""
+        self.prepare(s, t)
+        o = SearchOpts(float(hscale), float(fscale), int(k_moves), int(itrs), int(time_ns),
+                       int(capacity))
+        st = SearchStats()
+        _check(lib.cpd_query_search(self._h, C.byref(o), C.byref(st)))
+        nq = len(s)
+        cost = np.empty(nq, np.uint64)
+        plen = np.empty(nq, np.uint32)
+        fin = np.empty(nq, np.uint8)
+        _check(lib.cpd_query_fetch(self._h, _ptr(cost, u64p), _ptr(plen, u32p), _ptr(fin, u8p)))
+        cnt = np.empty((nq, 5), np.uint32)
+        if nq:
+            _check(lib.cpd_query_search_counters(self._h, _ptr(cnt, u32p)))
+        return cost, plen, fin, cnt, {k: getattr(st, k) for k, _ in SearchStats._fields_}
 
     def __del__(self):
         if getattr(self, "_h", None):

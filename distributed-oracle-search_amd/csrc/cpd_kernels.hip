@@ -1701,6 +1701,378 @@ __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
     }
 }
 
+// ---------------------------------------------------------------------------
+// CPD-heuristic search (semantics restated in
+// oracle/cpd_oracle.c ora_cpd_search, [U]).
+//
+// Per index row r (target t), three tables over the columns, computed from
+// the dense move table by pointer jumping over the CPD's next-hop tree — the
+// CPD walk from every column at once, in log2(n) + 1 doubling rounds:
+//   hrow[r][c] = free-flow cost of the CPD path c -> t (the heuristic),
+//   crow[r][c] = its cost under the selected weights (the incumbent bound),
+//   lrow[r][c] = its moves;  INF (hrow, crow) when the walk never reaches t.
+// Jump state per (row, column): next column (kJumpBad = no path), cf, cw,
+// lw; t points to itself with zero cost (absorbing).
+constexpr uint32_t kJumpBad = 0xFFFFFFFFu;
+constexpr uint64_t kInf64 = 0xFFFFFFFFFFFFFFFFull;
+
+struct JumpState {
+    uint32_t* next;
+    uint64_t* cf;
+    uint64_t* cw;
+    uint32_t* lw;
+};
+
+__global__ __launch_bounds__(256) void jump_init(const uint32_t* __restrict__ dense,
+                                                 uint32_t wpr, const uint2* __restrict__ adj_f,
+                                                 const uint2* __restrict__ adj_w, uint32_t shift,
+                                                 const uint32_t* __restrict__ tcol, uint32_t rows,
+                                                 uint32_t n, JumpState js) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (j >= (uint64_t)rows * n) return;
+    const uint32_t r = (uint32_t)(j / n), c = (uint32_t)(j - (uint64_t)r * n);
+    uint32_t nx = kJumpBad, l = 0;
+    uint64_t f = 0, w = 0;
+    if (c == tcol[r]) {
+        nx = c;
+    } else {
+        const uint32_t mv = (dense[(size_t)r * wpr + (c >> 3)] >> (4u * (c & 7u))) & 0xFu;
+        if (!(mv >> shift)) {
+            const size_t e = ((size_t)c << shift) + mv;
+            const uint2 ef = adj_f[e];
+            if (ef.x != kNoEdge) {
+                nx = ef.x;
+                f = ef.y;
+                w = adj_w[e].y;
+                l = 1;
+            }
+        }
+    }
+    js.next[j] = nx;
+    js.cf[j] = f;
+    js.cw[j] = w;
+    js.lw[j] = l;
+}
+
+// One doubling round a -> b: b(c) = a(c) followed by a(next(c)).
+__global__ __launch_bounds__(256) void jump_round(JumpState a, JumpState b,
+                                                  const uint32_t* __restrict__ tcol, uint32_t rows,
+                                                  uint32_t n) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (j >= (uint64_t)rows * n) return;
+    const uint32_t r = (uint32_t)(j / n);
+    const uint32_t nx = a.next[j];
+    uint32_t o = nx;
+    uint64_t f = a.cf[j], w = a.cw[j];
+    uint32_t l = a.lw[j];
+    if (nx != kJumpBad && nx != tcol[r]) {
+        const uint64_t k = (uint64_t)r * n + nx;
+        o = a.next[k];
+        if (o != kJumpBad) {
+            f += a.cf[k];
+            w += a.cw[k];
+            l += a.lw[k];
+        }
+    }
+    b.next[j] = o;
+    b.cf[j] = f;
+    b.cw[j] = w;
+    b.lw[j] = l;
+}
+
+__global__ __launch_bounds__(256) void jump_final(JumpState a, const uint32_t* __restrict__ tcol,
+                                                  uint32_t rows, uint32_t n,
+                                                  uint64_t* __restrict__ hrow,
+                                                  uint64_t* __restrict__ crow,
+                                                  uint32_t* __restrict__ lrow, int write_h) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (j >= (uint64_t)rows * n) return;
+    const uint32_t r = (uint32_t)(j / n);
+    const bool ok = a.next[j] == tcol[r];
+    if (write_h) hrow[j] = ok ? a.cf[j] : kInf64;
+    crow[j] = ok ? a.cw[j] : kInf64;
+    lrow[j] = ok ? a.lw[j] : 0u;
+}
+
+// The search, one lane per query, lanes refilled from the wave's chunk of the
+// target-sorted batch (as table_walk).  Each lane slot owns a workspace in
+// HBM: an open-addressing hash of the columns seen (tag = query + 1, column,
+// g, depth) with 2C slots, and a binary heap of C entries keyed (f, column, g)
+// — the oracle's order.  A lane advances its query by one pop per loop
+// iteration, so lanes of a wave with searches of different lengths stay busy.
+// A query whose search needs more than C nodes or heap entries stops
+// unfinished and is counted in agg[7] (overflow) — never silently wrong.
+struct SearchWs {
+    uint4* hk;      // [slots][2C] tag, column, g lo, g hi
+    uint32_t* hd;   // [slots][2C] depth
+    uint4* he;      // [slots][C] f lo, f hi, g lo, g hi
+    uint32_t* hc;   // [slots][C] column
+    uint32_t cap;   // C (power of 2)
+};
+
+struct SearchOpt {
+    double hscale, fscale;
+    int32_t kmoves;
+    int64_t itrs;
+    uint64_t time_ticks;  // 0 = none; else limit in 100-MHz s_memrealtime ticks
+};
+
+__device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) {
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ bool hkey_less(uint64_t f1, uint32_t c1, uint64_t g1, uint64_t f2,
+                                          uint32_t c2, uint64_t g2) {
+    if (f1 != f2) return f1 < f2;
+    if (c1 != c2) return c1 < c2;
+    return g1 < g2;
+}
+
+struct Lane {
+    uint32_t q, s, t, row, hsize, best_len, tag;
+    uint64_t ub, t0;
+    uint32_t expanded, inserted, touched, updated, surplus;
+    bool done, overflow;
+};
+
+// Hash probe: slot index of column c (found = true) or of the free slot to
+// insert it in; 2C slots at most 50% full (inserts beyond C overflow).
+__device__ __forceinline__ uint32_t hprobe(const uint4* __restrict__ hk, uint32_t mask,
+                                           uint32_t tag, uint32_t c, bool& found, uint4& ent) {
+    uint32_t i = (c * 0x9E3779B1u) & mask;
+    for (;;) {
+        ent = hk[i];
+        if (ent.x != tag) {
+            found = false;
+            return i;
+        }
+        if (ent.y == c) {
+            found = true;
+            return i;
+        }
+        i = (i + 1u) & mask;
+    }
+}
+
+__device__ __forceinline__ void heap_push(uint4* __restrict__ he, uint32_t* __restrict__ hc,
+                                          uint32_t& size, uint64_t f, uint32_t c, uint64_t g) {
+    uint32_t i = size++;
+    while (i) {
+        const uint32_t p = (i - 1u) >> 1;
+        const uint4 pe = he[p];
+        const uint32_t pc = hc[p];
+        if (!hkey_less(f, c, g, u64of(pe.x, pe.y), pc, u64of(pe.z, pe.w))) break;
+        he[i] = pe;
+        hc[i] = pc;
+        i = p;
+    }
+    he[i] = make_uint4((uint32_t)f, (uint32_t)(f >> 32), (uint32_t)g, (uint32_t)(g >> 32));
+    hc[i] = c;
+}
+
+__device__ __forceinline__ void heap_pop(uint4* __restrict__ he, uint32_t* __restrict__ hc,
+                                         uint32_t& size, uint64_t& f, uint32_t& c, uint64_t& g) {
+    const uint4 top = he[0];
+    f = u64of(top.x, top.y);
+    g = u64of(top.z, top.w);
+    c = hc[0];
+    --size;
+    if (!size) return;
+    const uint4 le = he[size];
+    const uint32_t lc = hc[size];
+    const uint64_t lf = u64of(le.x, le.y), lg = u64of(le.z, le.w);
+    uint32_t i = 0;
+    for (;;) {
+        uint32_t k = 2u * i + 1u;
+        if (k >= size) break;
+        uint4 ke = he[k];
+        uint32_t kc = hc[k];
+        if (k + 1u < size) {
+            const uint4 k2 = he[k + 1u];
+            const uint32_t c2 = hc[k + 1u];
+            if (hkey_less(u64of(k2.x, k2.y), c2, u64of(k2.z, k2.w), u64of(ke.x, ke.y), kc,
+                          u64of(ke.z, ke.w))) {
+                ++k;
+                ke = k2;
+                kc = c2;
+            }
+        }
+        if (!hkey_less(u64of(ke.x, ke.y), kc, u64of(ke.z, ke.w), lf, lc, lg)) break;
+        he[i] = ke;
+        hc[i] = kc;
+        i = k;
+    }
+    he[i] = le;
+    hc[i] = lc;
+}
+
+template <int SHIFT>
+__global__ __launch_bounds__(256) void cpd_search(
+    const uint2* __restrict__ adj, const uint64_t* __restrict__ hrow,
+    const uint64_t* __restrict__ crow, const uint32_t* __restrict__ lrow, uint32_t n,
+    const uint32_t* __restrict__ qs, const uint32_t* __restrict__ qt,
+    const uint32_t* __restrict__ qrow, uint32_t nq, uint32_t chunk, SearchOpt opt,
+    SearchWs ws, uint64_t* __restrict__ cost_out, uint32_t* __restrict__ plen_out,
+    uint8_t* __restrict__ fin_out, uint32_t* __restrict__ qstats,
+    unsigned long long* __restrict__ agg) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t slot = wave * 64u + lane;  // this lane's workspace
+    const uint64_t q0l = wave * chunk;
+    const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
+    const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
+    const uint32_t C = ws.cap, mask = 2u * C - 1u;
+    uint4* __restrict__ hk = ws.hk + slot * 2u * C;
+    uint32_t* __restrict__ hd = ws.hd + slot * 2u * C;
+    uint4* __restrict__ he = ws.he + slot * C;
+    uint32_t* __restrict__ hc = ws.hc + slot * C;
+    unsigned long long s_exp = 0, s_ins = 0, s_tou = 0, s_upd = 0, s_sur = 0, s_len = 0,
+                       s_fin = 0, s_ovf = 0;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    // the tag of a hash slot is the query index + 1 of the search that wrote
+    // it; slots are cleared once per launch so stale tags never match
+    for (uint32_t i = 0; i < 2u * C; ++i) hk[i] = make_uint4(0u, 0u, 0u, 0u);
+
+    Lane L;
+    L.q = kIdleQ;
+    L.done = false;
+    auto begin = [&](uint32_t q) {
+        L.q = q;
+        L.s = qs[q];
+        L.t = qt[q];
+        L.row = qrow[q];
+        L.tag = q + 1u;
+        L.hsize = 0;
+        L.ub = kInf64;
+        L.best_len = 0;
+        L.expanded = L.inserted = L.touched = L.updated = L.surplus = 0;
+        L.done = false;
+        L.overflow = false;
+        L.t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t* hr = hrow + (size_t)L.row * n;
+        const uint64_t hs = hr[L.s];
+        if (hs != kInf64) {
+            bool found;
+            uint4 ent;
+            const uint32_t i = hprobe(hk, mask, L.tag, L.s, found, ent);
+            hk[i] = make_uint4(L.tag, L.s, 0u, 0u);
+            hd[i] = 0u;
+            L.inserted = 1;
+            heap_push(he, hc, L.hsize, (uint64_t)(opt.hscale * (double)hs), L.s, 0ull);
+        }
+    };
+    uint32_t next = q0;
+    if (q0 + lane < q1) begin(q0 + lane);
+    next = min(q1, q0 + 64u);
+    for (;;) {
+        // retire finished searches, refill from the chunk
+        const bool fin_now = L.q != kIdleQ && (L.done || L.hsize == 0);
+        const uint64_t m = __ballot(fin_now);
+        if (m) {
+            if (fin_now) {
+                const bool found = L.ub != kInf64 && !L.overflow;
+                cost_out[L.q] = found ? L.ub : 0ull;
+                plen_out[L.q] = found ? L.best_len : 0u;
+                fin_out[L.q] = (uint8_t)found;
+                uint32_t* st = qstats + 5ull * L.q;
+                st[0] = L.expanded;
+                st[1] = L.inserted;
+                st[2] = L.touched;
+                st[3] = L.updated;
+                st[4] = L.surplus;
+                s_exp += L.expanded;
+                s_ins += L.inserted;
+                s_tou += L.touched;
+                s_upd += L.updated;
+                s_sur += L.surplus;
+                s_len += found ? L.best_len : 0u;
+                s_fin += found ? 1u : 0u;
+                s_ovf += L.overflow ? 1u : 0u;
+                const uint32_t nqi = next + (uint32_t)__builtin_popcountll(m & lt_mask);
+                if (nqi < q1) begin(nqi);
+                else L.q = kIdleQ;
+            }
+            next = min(q1, next + (uint32_t)__builtin_popcountll(m));
+        }
+        if (!__any(L.q != kIdleQ)) break;
+        if (L.q == kIdleQ || L.done || L.hsize == 0) continue;
+        // one pop of this lane's search
+        uint64_t f, g;
+        uint32_t v;
+        heap_pop(he, hc, L.hsize, f, v, g);
+        bool found;
+        uint4 ent;
+        const uint32_t hi = hprobe(hk, mask, L.tag, v, found, ent);
+        if (g > u64of(ent.z, ent.w)) {  // stale entry
+            ++L.surplus;
+            continue;
+        }
+        if ((double)f * (1.0 + opt.fscale) >= (double)L.ub ||
+            (opt.itrs >= 0 && (int64_t)L.expanded >= opt.itrs) ||
+            (opt.time_ticks && __builtin_amdgcn_s_memrealtime() - L.t0 > opt.time_ticks)) {
+            L.done = true;
+            continue;
+        }
+        ++L.expanded;
+        const size_t rb = (size_t)L.row * n;
+        const uint32_t dv = hd[hi];
+        const uint64_t cw = crow[rb + v];
+        const uint32_t lw = lrow[rb + v];
+        if (cw != kInf64 && (opt.kmoves < 0 || lw <= (uint32_t)opt.kmoves)) {
+            const uint64_t cand = g + cw;
+            if (cand < L.ub) {
+                L.ub = cand;
+                L.best_len = dv + lw;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < (1 << SHIFT); ++k) {
+            const uint2 e = adj[((size_t)v << SHIFT) + k];
+            if (e.x == kNoEdge) break;  // edges are packed first
+            ++L.touched;
+            const uint32_t u = e.x;
+            const uint64_t ng = g + e.y;
+            bool fu;
+            uint4 eu;
+            const uint32_t ui = hprobe(hk, mask, L.tag, u, fu, eu);
+            if (!fu) {
+                const uint64_t hu = hrow[rb + u];
+                if (hu == kInf64) continue;
+                if (L.inserted >= C || L.hsize >= C) {
+                    L.overflow = true;
+                    L.done = true;
+                    break;
+                }
+                hk[ui] = make_uint4(L.tag, u, (uint32_t)ng, (uint32_t)(ng >> 32));
+                hd[ui] = dv + 1u;
+                ++L.inserted;
+                heap_push(he, hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
+            } else if (ng < u64of(eu.z, eu.w)) {
+                if (L.hsize >= C) {
+                    L.overflow = true;
+                    L.done = true;
+                    break;
+                }
+                hk[ui] = make_uint4(L.tag, u, (uint32_t)ng, (uint32_t)(ng >> 32));
+                hd[ui] = dv + 1u;
+                ++L.updated;
+                heap_push(he, hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hrow[rb + u]), u,
+                          ng);
+            }
+        }
+    }
+    // wave sums, one atomic per wave per counter
+    unsigned long long v8[8] = {s_exp, s_ins, s_tou, s_upd, s_sur, s_len, s_fin, s_ovf};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v8[i] += __shfl_xor(v8[i], o, 64);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) atomicAdd(&agg[i], v8[i]);
+}
+
 }  // namespace kern
 
 // ---------------------------------------------------------------------------
@@ -2076,6 +2448,75 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::RleRows{offsets, runs}, qs, qt,
                 qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(8192),
                 ts_chunk_max(1u << 30), s);
+}
+
+// CPD-search tables for `rows` index rows starting at `first`: pointer
+// jumping in chunks of rows (scratch: 2 jump states of 24 B per column per
+// row of the chunk).
+void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* adj_f,
+                          const uint32_t* adj_w, uint32_t shift, const uint32_t* tcol,
+                          uint32_t rows, uint32_t n, void* scratch, uint32_t chunk_rows,
+                          uint64_t* hrow, uint64_t* crow, uint32_t* lrow, int write_h,
+                          hipStream_t s) {
+    uint32_t rounds = 1;
+    while ((1ull << (rounds - 1)) < (uint64_t)n + 1ull) ++rounds;  // 2^(rounds-1) > n hops
+    const size_t per = (size_t)chunk_rows * n;
+    char* base = static_cast<char*>(scratch);
+    auto state = [&](int k) {
+        char* p = base + (size_t)k * per * 24u;
+        return kern::JumpState{reinterpret_cast<uint32_t*>(p),
+                               reinterpret_cast<uint64_t*>(p + per * 4u),
+                               reinterpret_cast<uint64_t*>(p + per * 12u),
+                               reinterpret_cast<uint32_t*>(p + per * 20u)};
+    };
+    const kern::JumpState A = state(0), Bs = state(1);
+    const uint2* af = reinterpret_cast<const uint2*>(adj_f);
+    const uint2* aw = reinterpret_cast<const uint2*>(adj_w);
+    for (uint32_t r0 = 0; r0 < rows; r0 += chunk_rows) {
+        const uint32_t R = std::min(chunk_rows, rows - r0);
+        const uint64_t items = (uint64_t)R * n;
+        const dim3 grid((uint32_t)((items + 255u) / 256u)), blk(256);
+        launch(kern::jump_init, grid, blk, s, dense + (size_t)r0 * (npad / 8u), npad / 8u, af, aw,
+               shift, tcol + r0, R, n, A);
+        kern::JumpState a = A, b = Bs;
+        for (uint32_t k = 0; k < rounds; ++k) {
+            launch(kern::jump_round, grid, blk, s, a, b, tcol + r0, R, n);
+            std::swap(a, b);
+        }
+        launch(kern::jump_final, grid, blk, s, a, tcol + r0, R, n, hrow + (size_t)r0 * n,
+               crow + (size_t)r0 * n, lrow + (size_t)r0 * n, write_h);
+    }
+}
+
+uint32_t search_slots(uint32_t nq) {  // lanes with a workspace: whole blocks of 4 waves
+    static const uint32_t waves = std::max(4u, env_u32("CPD_SEARCH_WAVES", 256));
+    const uint32_t want = (nq + 63u) / 64u;
+    const uint32_t w = std::max(1u, std::min(waves, want));
+    return 64u * ((w + 3u) / 4u * 4u);
+}
+
+void launch_cpd_search(const uint32_t* adj, uint32_t shift, const uint64_t* hrow,
+                       const uint64_t* crow, const uint32_t* lrow, uint32_t n, const uint32_t* qs,
+                       const uint32_t* qt, const uint32_t* qrow, uint32_t nq, double hscale,
+                       double fscale, int32_t kmoves, int64_t itrs, uint64_t time_ns,
+                       void* ws, uint32_t cap, uint32_t slots, uint64_t* cost, uint32_t* plen,
+                       uint8_t* fin, uint32_t* qstats, unsigned long long* agg, hipStream_t s) {
+    const uint32_t waves = slots / 64u;  // a multiple of 4 (search_slots)
+    char* p = static_cast<char*>(ws);
+    const size_t hs = (size_t)slots * 2u * cap, hp = (size_t)slots * cap;
+    kern::SearchWs w{reinterpret_cast<uint4*>(p), reinterpret_cast<uint32_t*>(p + hs * 16u),
+                     reinterpret_cast<uint4*>(p + hs * 20u),
+                     reinterpret_cast<uint32_t*>(p + hs * 20u + hp * 16u), cap};
+    const kern::SearchOpt o{hscale, fscale, kmoves, itrs, time_ns ? std::max<uint64_t>(1u, time_ns / 10u) : 0u};
+    const dim3 grid(waves / 4u), blk(256);  // every wave has a workspace slot
+    const uint32_t c2 = (uint32_t)(((uint64_t)nq + waves - 1u) / waves);
+    switch (shift) {
+        case 0: launch(kern::cpd_search<0>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
+        case 1: launch(kern::cpd_search<1>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
+        case 2: launch(kern::cpd_search<2>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
+        case 3: launch(kern::cpd_search<3>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
+        default: launch(kern::cpd_search<4>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
+    }
 }
 
 }  // namespace cpd

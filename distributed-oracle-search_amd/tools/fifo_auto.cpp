@@ -2,7 +2,7 @@
 // `--alg table-search` (make_fifos.py:20-21, README.md:107-111):
 //
 //   fifo_auto --input X.xy DIFF --partmethod {div|mod} --partkey K
-//             --workerid I --maxworker W --outdir D --alg table-search
+//             --workerid I --maxworker W --outdir D --alg {table-search|cpd-search}
 //             [--partition M] [--device G] [--fifo PATH] [--once]
 //             [--index auto|rle|dense]
 //
@@ -19,7 +19,10 @@
 //     t_receive,t_astar,t_search
 // For table-search: n_expanded = plen = moves walked, finished = queries that
 // reached t, t_receive = read + upload ns, t_search = extraction kernel ns,
-// the A*-only fields are 0.  With "debug": true in the config, per-query
+// the A*-only fields are 0.  For --alg cpd-search (cpd_query_search, driven
+// by the request's hscale / fscale / time / itrs / k_moves): the five search
+// counters, plen of the paths found, finished, t_astar = search (+ table
+// rebuild after a weight change) ns, t_search = t_receive + t_astar.  With "debug": true in the config, per-query
 // results are written to <query file>.res ("s t cost moves finished").
 #include <errno.h>
 #include <fcntl.h>
@@ -116,11 +119,14 @@ int main(int argc, char** argv) {
     if (inputs.empty() || method.empty() || key <= 0 || wid < 0 || W <= 0 || wid >= W) {
         std::fprintf(stderr,
                      "usage: fifo_auto --input X.xy [DIFF] --partmethod {div|mod} --partkey K "
-                     "--workerid I --maxworker W --outdir D --alg table-search\n");
+                     "--workerid I --maxworker W --outdir D --alg table-search|cpd-search\n");
         return 2;
     }
-    if (alg != "table-search") {
-        std::fprintf(stderr, "fifo_auto: only --alg table-search is implemented (got '%s')\n",
+    // table-search (make_fifos.py:20) or the CPD-heuristic search
+    // (cpd_query_search; args.py:29-57)
+    const bool search = alg == "cpd-search" || alg == "cpd_search";
+    if (alg != "table-search" && !search) {
+        std::fprintf(stderr, "fifo_auto: --alg must be table-search or cpd-search (got '%s')\n",
                      alg.c_str());
         return 2;
     }
@@ -247,6 +253,16 @@ int main(int argc, char** argv) {
         std::string km = json_field(conf, "k_moves");
         if (!km.empty()) k_moves = std::atoi(km.c_str());
         bool debug = json_field(conf, "debug") == "true";
+        // cpd-search knobs (process_query.py:149-160): hscale, fscale, time
+        // (ns; args.get_time_ns may send a float), itrs
+        cpd_search_opts so{1.0, 0.0, k_moves, -1, 0, 0};
+        if (!json_field(conf, "hscale").empty()) so.hscale = std::atof(json_field(conf, "hscale").c_str());
+        if (!json_field(conf, "fscale").empty()) so.fscale = std::atof(json_field(conf, "fscale").c_str());
+        if (!json_field(conf, "itrs").empty()) so.itrs = std::atoll(json_field(conf, "itrs").c_str());
+        if (!json_field(conf, "time").empty()) {
+            const double tn = std::atof(json_field(conf, "time").c_str());
+            so.time_ns = tn > 0 ? (uint64_t)tn : 0;
+        }
         std::string line = "0,0,0,0,0,0,0,0,0,0";
         try {
             double t0 = now();
@@ -271,8 +287,17 @@ int main(int argc, char** argv) {
             if (rc != CPD_OK) throw std::runtime_error(cpd_last_error());
             double t_receive = now() - t0;
             cpd_query_stats st{};
-            rc = cpd_query_run(ix, k_moves, &st);
-            if (rc != CPD_OK) throw std::runtime_error(cpd_last_error());
+            cpd_search_stats ss{};
+            if (search) {
+                rc = cpd_query_search(ix, &so, &ss);
+                if (rc != CPD_OK) throw std::runtime_error(cpd_last_error());
+                if (ss.overflow)
+                    std::fprintf(stderr, "fifo_auto: %llu searches exceeded the workspace and stopped unfinished\n",
+                                 (unsigned long long)ss.overflow);
+            } else {
+                rc = cpd_query_run(ix, k_moves, &st);
+                if (rc != CPD_OK) throw std::runtime_error(cpd_last_error());
+            }
             if (debug) {
                 std::vector<uint64_t> cost(q.size());
                 std::vector<uint32_t> hops(q.size());
@@ -287,10 +312,19 @@ int main(int argc, char** argv) {
                 }
             }
             char buf[512];
-            std::snprintf(buf, sizeof buf, "%llu,0,0,0,0,%llu,%llu,%lld,0,%lld",
-                          (unsigned long long)st.hops, (unsigned long long)st.hops,
-                          (unsigned long long)st.finished, (long long)(t_receive * 1e9),
-                          (long long)(st.kernel_ms * 1e6));
+            if (search)  // t_astar = the search kernel, t_search = receive + search
+                std::snprintf(buf, sizeof buf, "%llu,%llu,%llu,%llu,%llu,%llu,%llu,%lld,%lld,%lld",
+                              (unsigned long long)ss.expanded, (unsigned long long)ss.inserted,
+                              (unsigned long long)ss.touched, (unsigned long long)ss.updated,
+                              (unsigned long long)ss.surplus, (unsigned long long)ss.plen,
+                              (unsigned long long)ss.finished, (long long)(t_receive * 1e9),
+                              (long long)((ss.kernel_ms + ss.tables_ms) * 1e6),
+                              (long long)(t_receive * 1e9 + (ss.kernel_ms + ss.tables_ms) * 1e6));
+            else
+                std::snprintf(buf, sizeof buf, "%llu,0,0,0,0,%llu,%llu,%lld,0,%lld",
+                              (unsigned long long)st.hops, (unsigned long long)st.hops,
+                              (unsigned long long)st.finished, (long long)(t_receive * 1e9),
+                              (long long)(st.kernel_ms * 1e6));
             line = buf;
         } catch (const std::exception& e) {
             std::fprintf(stderr, "fifo_auto: request failed: %s\n", e.what());

@@ -284,6 +284,40 @@ int  cpd_query_fetch(cpd_index* ix, uint64_t* cost, uint32_t* hops,
                      uint8_t* finished);
 void cpd_index_free(cpd_index* ix);
 
+/* [gpu] CPD-heuristic search — fifo_auto's other algorithm family
+ * (args.py:29-57 --h-scale / --f-scale / -k / time
+ * limits, worker JSON keys hscale, fscale, time, itrs, k_moves,
+ * process_query.py:149-160).  warthog's cpd_search is absent: the semantics
+ * are restated in oracle/cpd_oracle.c (ora_cpd_search) [U].  A* from s under
+ * the index's current weights (cpd_index_set_weights), heuristic hscale x the
+ * free-flow cost of the CPD path to t, incumbent from the CPD path's cost
+ * under the current weights (only paths of <= k_moves moves when k_moves >=
+ * 0); stops when f_min x (1 + fscale) >= incumbent, after itrs expansions,
+ * or after time_ns.  Runs on the queries of the last cpd_query_prepare; per
+ * query results (cost, plen as hops, finished) via cpd_query_fetch.  Needs
+ * 20 B per column per index row for its tables (CPD_E_OOM if they do not
+ * fit) and a workspace of `capacity` nodes per concurrent search; a search
+ * that needs more stops unfinished and is counted in `overflow`.          */
+typedef struct cpd_search_opts {
+    double   hscale;       /* 1.0 */
+    double   fscale;       /* 0.0 */
+    int32_t  k_moves;      /* -1: whole CPD paths */
+    int64_t  itrs;         /* -1: no expansion limit */
+    uint64_t time_ns;      /* 0: no time limit (per query) */
+    uint32_t capacity;     /* nodes per search, power of 2 (0 = 32768) */
+} cpd_search_opts;
+
+typedef struct cpd_search_stats {
+    uint64_t queries, finished, expanded, inserted, touched, updated, surplus, plen, overflow;
+    double   kernel_ms;    /* device time of the search kernel              */
+    double   tables_ms;    /* device time spent (re)building its tables     */
+} cpd_search_stats;
+
+int  cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st);
+/* Per-query counters of the last search: counters[5 q + k] = expanded,
+ * inserted, touched, updated, surplus of query q (caller order).            */
+int  cpd_query_search_counters(cpd_index* ix, uint32_t* counters);
+
 /* ------------------------------------------------------------------------ */
 /* [gpu] Per-kernel device timing (HIP events on the library's stream).      */
 typedef struct cpd_kernel_time {

@@ -1,0 +1,110 @@
+"""GPU: the CPD-heuristic search (cpd_query_search; SURVEY.md §8f item 4,
+args.py:29-57) against the oracle's restatement (oracle/cpd_oracle.c
+ora_cpd_search) — per query cost, plen, finished and the five search
+counters, bit-exact — over hscale / fscale / k_moves / itrs, free-flow and
+congested weights, dense and RLE-loaded indexes, plus the properties that
+pin the restatement: optimal (== congested Dijkstra) at hscale 1, fscale 0;
+within (1 + fscale) of it otherwise."""
+import numpy as np
+import pytest
+from scipy.sparse import csr_matrix
+from scipy.sparse.csgraph import dijkstra
+
+import cpd
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    g = cpd.synth_road_graph(64, 48, seed=31)
+    plan = cpd.Plan(g)
+    dev = cpd.Graph(plan, batch=1024)
+    rng = np.random.default_rng(31)
+    targets = rng.choice(g.n, size=60, replace=False).astype(np.uint32)
+    off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    nq = 3000
+    s = rng.integers(0, g.n, nq).astype(np.uint32)
+    t = targets[rng.integers(0, len(targets), nq)]
+    wc = cpd.synth_congestion(g.w, frac=0.2, lo=1.0, hi=3.0, seed=4)
+    return g, plan, dev, targets, off, runs, s, t, wc
+
+
+def _oracle(env_, w_sel, **kw):
+    g, plan, dev, targets, off, runs, s, t, wc = env_
+    return oracle.cpd_search(g.row_ptr, g.dst, g.w, w_sel, plan.order(), targets, off, runs, s,
+                             t, **kw)
+
+
+def _index(env_, mode):
+    g, plan, dev, targets, off, runs = env_[:6]
+    ix = cpd.Index.streamed(dev, targets, int(off[-1]), mode=mode)
+    ix.append(off, runs)
+    return ix
+
+
+@pytest.mark.parametrize("mode", ["dense", "rle"])
+@pytest.mark.parametrize("opts", [dict(), dict(hscale=1.5), dict(fscale=0.25),
+                                  dict(hscale=0.5, fscale=0.1), dict(k_moves=40),
+                                  dict(itrs=7), dict(k_moves=0, itrs=200)],
+                         ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()) or "default")
+def test_search_matches_oracle(env, mode, opts):
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, mode)
+    for w_sel in (wc, g.w):
+        ix.set_weights(None if w_sel is g.w else w_sel)
+        rc, rp, rf, rs = _oracle(env, w_sel, **opts)
+        cost, plen, fin, cnt, st = ix.search(s, t, **opts)
+        assert st["overflow"] == 0
+        np.testing.assert_array_equal(cost, rc)
+        np.testing.assert_array_equal(plen, rp)
+        np.testing.assert_array_equal(fin, rf)
+        np.testing.assert_array_equal(cnt.astype(np.uint64), rs)
+        assert st["expanded"] == int(rs[:, 0].sum()) and st["finished"] == int(rf.sum())
+        assert st["plen"] == int(rp[rf == 1].sum())
+
+
+def test_search_optimal_and_bounded(env):
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    src = np.repeat(np.arange(g.n), np.diff(g.row_ptr))
+    D = dijkstra(csr_matrix((wc.astype(float), (src, g.dst)), shape=(g.n, g.n)),
+                 indices=np.unique(s))
+    row = {v: i for i, v in enumerate(np.unique(s))}
+    opt = np.array([D[row[a], b] for a, b in zip(s, t)])
+    cost, plen, fin, cnt, st = ix.search(s, t)
+    assert fin.all()
+    np.testing.assert_array_equal(cost.astype(float), opt)
+    # table-search under the same weights is never better than the search
+    tc, _, _, _ = ix.query(s, t)
+    assert np.all(cost <= tc)
+    for fs in (0.1, 0.5):
+        c2, _, f2, cnt2, _ = ix.search(s, t, fscale=fs)
+        assert f2.all() and np.all(c2 <= (1 + fs) * opt + 1e-9)
+        assert cnt2[:, 0].sum() <= cnt[:, 0].sum()
+    # free-flow weights: the CPD path is optimal, the search stops at once
+    ix.set_weights(None)
+    c3, _, _, cnt3, _ = ix.search(s, t)
+    np.testing.assert_array_equal(c3, ix.query(s, t)[0])
+    assert np.all(cnt3[:, 0] == 1)
+
+
+def test_search_overflow_is_counted(env):
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    rc, rp, rf, rs = _oracle(env, wc)
+    need = rs[:, 1].max()  # most nodes any query inserts
+    cap = 64
+    assert need > cap
+    cost, plen, fin, cnt, st = ix.search(s, t, capacity=cap)
+    assert st["overflow"] >= 1
+    # pushes = inserted + updated bound a search's nodes and heap entries:
+    # searches below the capacity are exact, those above it stop unfinished
+    small = rs[:, 1] + rs[:, 3] < cap
+    assert small.sum() > 100
+    np.testing.assert_array_equal(cost[small], rc[small])
+    np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small])
+    assert not fin[rs[:, 1] > cap].any()
