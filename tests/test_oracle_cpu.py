@@ -135,3 +135,70 @@ def test_missing_row_raises():
     off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, [3])
     with pytest.raises(KeyError):
         oracle.table_search(g.row_ptr, g.dst, g.w, order, [3], off, runs, [0], [4])
+
+
+# ---------------------------------------------------------------------------
+# CPD-heuristic search restatement (ora_cpd_search):
+# warthog's cpd_search source is absent, so the oracle is pinned by the
+# properties the published algorithm guarantees.
+
+def _search_case(w=36, seed=5, frac=0.25):
+    import cpd
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import dijkstra
+    g = cpd.synth_road_graph(w, w, seed=seed)
+    order = oracle.dfs_preorder(g.row_ptr, g.dst)
+    rng = np.random.default_rng(seed)
+    T = rng.choice(g.n, 12, replace=False).astype(np.uint32)
+    off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, T)
+    s = rng.integers(0, g.n, 600).astype(np.uint32)
+    t = T[rng.integers(0, len(T), 600)]
+    wc = cpd.synth_congestion(g.w, frac, 1.0, 3.0, seed)
+    src = np.repeat(np.arange(g.n), np.diff(g.row_ptr))
+    us = np.unique(s)
+    D = dijkstra(csr_matrix((wc.astype(float), (src, g.dst)), shape=(g.n, g.n)), indices=us)
+    row = {v: i for i, v in enumerate(us)}
+    opt = np.array([D[row[a], b] for a, b in zip(s, t)])
+    return g, order, T, off, runs, s, t, wc, opt
+
+
+def test_search_optimal_at_default_scales():
+    g, order, T, off, runs, s, t, wc, opt = _search_case()
+    c, pl, f, st = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t)
+    assert f.all()
+    np.testing.assert_array_equal(c.astype(float), opt)      # == congested Dijkstra
+    tc, th, tf = oracle.table_search(g.row_ptr, g.dst, wc, order, T, off, runs, s, t)
+    assert np.all(c <= tc)                                    # never worse than the CPD path
+    assert np.all(st[:, 0] >= 1) and np.all(st[:, 1] >= st[:, 0] - st[:, 3])
+
+
+@pytest.mark.parametrize("fs", [0.05, 0.3, 1.0])
+def test_search_bounded_suboptimal(fs):
+    g, order, T, off, runs, s, t, wc, opt = _search_case()
+    c, _, f, st = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t,
+                                    fscale=fs)
+    assert f.all() and np.all(c <= (1 + fs) * opt + 1e-9)
+    c0, _, _, st0 = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t)
+    assert st[:, 0].sum() <= st0[:, 0].sum()
+
+
+def test_search_free_flow_is_one_expansion_and_plen_is_the_walk():
+    g, order, T, off, runs, s, t, wc, opt = _search_case()
+    c, pl, f, st = oracle.cpd_search(g.row_ptr, g.dst, g.w, g.w, order, T, off, runs, s, t)
+    tc, th, tf = oracle.table_search(g.row_ptr, g.dst, g.w, order, T, off, runs, s, t)
+    np.testing.assert_array_equal(c, tc)
+    np.testing.assert_array_equal(pl, th)
+    assert np.all(st[:, 0] == 1)
+
+
+def test_search_limits():
+    g, order, T, off, runs, s, t, wc, opt = _search_case()
+    c, pl, f, st = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t,
+                                     itrs=3)
+    assert np.all(st[:, 0] <= 3)
+    assert f.all()  # the first expansion already has the CPD path as incumbent
+    c0, _, f0, st0 = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t,
+                                       k_moves=0)
+    # k_moves = 0: only t itself yields an incumbent, so the search ends at t
+    np.testing.assert_array_equal(c0.astype(float), opt)
+    assert np.all(st0[:, 0] >= 1)
