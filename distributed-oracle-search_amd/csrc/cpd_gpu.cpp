@@ -1523,8 +1523,18 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             tables_ms = ms;
             ix->h_ready = ix->c_ready = true;
         }
-        // workspace: 60 B per node of capacity per lane slot
-        const uint32_t slots = nq ? search_slots(nq) : 0u;
+        // workspace: 60 B per node of capacity per lane slot; as many slots
+        // (whole blocks of 4 waves) as a quarter of free HBM holds
+        uint32_t slots = nq ? search_slots(nq) : 0u;
+        if (nq) {
+            size_t free_b = 0, total_b = 0;
+            HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            const size_t per_block = 256ull * o.capacity * 60u;
+            const size_t fit = std::max<size_t>(1, (free_b / 4 + ix->sws.n) / per_block);
+            CPD_REQUIRE((free_b + ix->sws.n) / 2 >= per_block, CPD_E_OOM,
+                        "search workspace of 256 lanes x capacity does not fit in HBM");
+            slots = (uint32_t)std::min<size_t>(slots, fit * 256u);
+        }
         const size_t ws_bytes = (size_t)slots * o.capacity * 60u;
         if (nq) ix->sws.alloc(ws_bytes);
         ix->qstats.alloc(5ull * std::max(1u, nq));
