@@ -75,6 +75,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-cpu-partitioned", action="store_true",
                     help="skip the configs[0] mod-3 partitioned CPU run")
+    ap.add_argument("--no-search", action="store_true", help="skip the cpd-search leg")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
@@ -584,6 +585,32 @@ def main():
     ix.set_weights(w_cong)
     q_cong, q_cong_ms = time_queries("auto")
     ix.set_weights(None)
+    # CPD-heuristic search leg: 256 rows of the index, the
+    # .diff stand-in weights, hscale 1 / fscale 0.1 (10%-bounded: at fscale 0
+    # a 1M-node search inserts up to ~235k nodes, a lane-serial search's
+    # worst case), 20k queries
+    search = None
+    if args.sample is None and not args.no_search:
+        srows = last_targets[:256]
+        sr = dev.build_rows(srows)
+        six = cpd.Index.streamed(dev, srows, sr.count()[1], mode="dense")
+        six.append_rows(sr)
+        del sr
+        six.set_weights(w_cong)
+        sq = 20000
+        ss = rng.integers(0, g.n, sq).astype(np.uint32)
+        st_ = srows[rng.integers(0, len(srows), sq)]
+        wst = six.search(ss[:256], st_[:256], fscale=0.1)[4]  # warm: tables built here
+        _, _, sfin, scnt, sst = six.search(ss, st_, fscale=0.1)
+        tot = comm.reduce([float(sq), sst["kernel_ms"]], "SUM")
+        (smax,) = comm.reduce([sst["kernel_ms"]], "MAX")
+        search = {"queries_per_s": round(tot[0] / (smax / 1e3), 1) if smax else 0.0,
+                  "config": "256-row dense index, .diff stand-in weights, hscale 1, fscale 0.1",
+                  "mean_expanded": round(float(scnt[:, 0].mean()), 1),
+                  "finished": int(sfin.sum()), "overflow": int(sst["overflow"]),
+                  "kernel_ms": round(sst["kernel_ms"], 3),
+                  "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
+        search_sample = (six, ss[:2000], st_[:2000], srows)
     # walk kernel vs its roofline: per query 8 (s, t) + 4 (row) + 13 (cost,
     # moves, flag) bytes, per move the 4-B word holding the move + the 8-B edge
     qbytes = 25.0 * q_totals[0] + 12.0 * q_totals[2]
@@ -634,6 +661,17 @@ def main():
             gc_, gh, _, _ = gix.query(cs, ct)
             parity = parity and bool(np.array_equal(gc_, rc) and np.array_equal(gh, rh))
         del gix, grows
+        if search:
+            six, ss2, st2, srows = search_sample
+            sref = oracle.build_rows(g.row_ptr, g.dst, g.w, order, srows, threads=threads)
+            rc, rp, rf, rs = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, order, srows,
+                                               sref[0], sref[1], ss2, st2, fscale=0.1,
+                                               threads=threads)
+            gcs, gps, gfs, gcnt, _ = six.search(ss2, st2, fscale=0.1)
+            search["parity_2000_bit_exact"] = bool(
+                np.array_equal(gcs, rc) and np.array_equal(gps, rp) and np.array_equal(gfs, rf)
+                and np.array_equal(gcnt.astype(np.uint64), rs))
+            parity = parity and search["parity_2000_bit_exact"]
         cpu = {"value": round(leg["rows"] / leg["rows_s"], 3), "unit": "sources/s",
                "cores": threads, "kind": "port",
                "sample": f"{leg['rows']} CPD rows of the same graph and partition (reverse "
@@ -654,6 +692,7 @@ def main():
         out["query_index"] = index_mode
         out["query_index_rows_per_gpu"] = index_rows
         out["query_roofline"] = query_roof
+        out["cpd_search"] = search
         if q_rle_ms:
             out["queries_per_s_rle"] = round(q_rle[0] / (q_rle_ms / 1e3), 1)
         out["queries_per_s_congested"] = (round(q_cong[0] / (q_cong_ms / 1e3), 1)
