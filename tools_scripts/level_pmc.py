@@ -38,7 +38,7 @@ def main(trace, fetch, write, out):
     f = [pf[k] for k in sorted(pf)]
     w = [pw[k] for k in sorted(pw)]
     n = min(len(t), len(f), len(w))
-    lines = ["level  time_us  grid_threads  read_MB  write_MB  PMC_GB/s"]
+    lines = ["level  time_us  grid_threads  read_MB  write_MB  PMC_TB/s"]
     tot_t = tot_b = 0.0
     wide_t = wide_b = 0.0
     order = sorted(range(n), key=lambda i: -t[i][0])[:20]
@@ -51,11 +51,11 @@ def main(trace, fetch, write, out):
         if i in order:
             wide_t += us
             wide_b += rd + wr
-        lines.append(f"{i:5d} {us:8.1f} {t[i][1]:12d} {rd:8.1f} {wr:8.1f} {(rd + wr) / us * 1e-3 * 1e3:8.0f}")
+        lines.append(f"{i:5d} {us:8.1f} {t[i][1]:12d} {rd:8.1f} {wr:8.1f} {(rd + wr) / us:8.2f}")
     lines.append(f"all {n} levels: {tot_t / 1e3:.2f} ms, {tot_b / 1e3:.1f} GB PMC, "
-                 f"{tot_b / tot_t:.0f} GB/s")
+                 f"{tot_b / tot_t:.2f} TB/s")
     lines.append(f"20 longest levels: {wide_t / 1e3:.2f} ms, {wide_b / 1e3:.1f} GB PMC, "
-                 f"{wide_b / wide_t:.0f} GB/s")
+                 f"{wide_b / wide_t:.2f} TB/s")
     open(out, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines[-2:]))
 
