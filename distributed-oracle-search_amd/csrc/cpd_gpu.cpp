@@ -70,6 +70,8 @@ struct Agg {
     double ms = 0.0, bytes = 0.0;
 };
 
+bool async_on();  // CPD_ASYNC (defined with the other switches)
+
 }  // namespace
 
 struct cpd_graph {
@@ -113,9 +115,36 @@ struct cpd_graph {
     uint32_t B = 0;
     uint32_t fmb = 16;  // bits per first-move set (fm_bits(adj_shift))
     DevBuf<uint32_t> dist, tgt, counts;
-    DevBuf<uint32_t> fm;    // [B][npad] fmb-bit sets
-    DevBuf<uint32_t> rle_st;  // [B][npad/32] RLE segment entry states (fmb == 4)
-    DevBuf<uint8_t> rle_rc;   // [B][npad/32] runs ending in each segment
+    // Emit overlap (CPD_ASYNC, default on): a batch's rle_emit runs on
+    // `estream` while the next batch's sweeps start on `stream` — the sweeps'
+    // narrow, latency-bound levels overlap the bandwidth-bound emit.  The
+    // buffers emit reads (first-move rows, RLE states, lane offsets) are
+    // doubled: set x serves every other batch and is reused only after the
+    // emit that read it (ev_emit[x]) has finished.
+    hipStream_t estream = nullptr;
+    bool async = false;
+    uint32_t cur = 0;
+    hipEvent_t ev_emit[2] = {nullptr, nullptr};
+    bool emit_pending[2] = {false, false};
+    DevBuf<uint32_t> fmx[2];      // [B][npad] fmb-bit sets
+    DevBuf<uint32_t> rle_stx[2];  // [B][npad/32] RLE segment entry states (fmb == 4)
+    DevBuf<uint8_t> rle_rcx[2];   // [B][npad/32] runs ending in each segment
+    DevBuf<uint64_t> row_offx[2];
+    std::vector<uint64_t> lane_off_h[2];  // host source of row_offx[x] (kept alive)
+    // the buffer set the next batch uses, once the emit that last read it is done
+    uint32_t acquire_set() {
+        const uint32_t x = async ? cur : 0u;
+        if (async) cur ^= 1u;
+        if (emit_pending[x]) {
+            HIP_CHECK(hipStreamWaitEvent(stream, ev_emit[x], 0));
+            emit_pending[x] = false;
+        }
+        return x;
+    }
+    void drain_emits() {
+        if (estream) HIP_CHECK(hipStreamSynchronize(estream));
+        emit_pending[0] = emit_pending[1] = false;
+    }
     DevBuf<uint32_t> live;   // [col] slab mask of the up-sweep rows stored
     DevBuf<uint32_t> tmask;  // [col] slab mask of the batch's targets
     // leaf first moves from the down-sweep (4-bit sets only): leafbits[col/32]
@@ -142,7 +171,6 @@ struct cpd_graph {
     }
     double n_leaf = 0, m_leaf = 0;    // leaves, their out-edges
     std::vector<double> dsc_lvl_leaves;
-    DevBuf<uint64_t> row_off;
     // per-level sweep counters (2 per launch: stored/own rows, gathered rows)
     DevBuf<unsigned int> stat;
     std::vector<unsigned int> stat_h;
@@ -163,6 +191,10 @@ struct cpd_graph {
 
     ~cpd_graph() {
         if (hipSetDevice(device) == hipSuccess) {
+            if (estream) (void)hipStreamSynchronize(estream);
+            for (auto e : ev_emit)
+                if (e) (void)hipEventDestroy(e);
+            if (estream) (void)hipStreamDestroy(estream);
             if (stream) (void)hipStreamSynchronize(stream);
             for (auto& p : pending) {
                 (void)hipEventDestroy(p.a);
@@ -239,9 +271,18 @@ struct cpd_graph {
         }
         group = Pending{};
     }
-    void sync() {
+    // Wait for `stream` (all = also the emit stream), then fold the timed
+    // intervals that have completed into agg; intervals of an emit still
+    // running on estream stay pending until a later sync.
+    void sync(bool all = false) {
         HIP_CHECK(hipStreamSynchronize(stream));
+        if (all) drain_emits();
+        std::vector<Pending> keep;
         for (auto& p : pending) {
+            if (hipEventQuery(p.b) != hipSuccess) {
+                keep.push_back(std::move(p));
+                continue;
+            }
             float ms = 0.f;
             HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
             Agg& g = agg[p.name];
@@ -252,7 +293,7 @@ struct cpd_graph {
             ev_pool.push_back(p.a);
             ev_pool.push_back(p.b);
         }
-        pending.clear();
+        pending.swap(keep);
     }
     void select() const { HIP_CHECK(hipSetDevice(device)); }
 
@@ -271,13 +312,32 @@ struct cpd_graph {
         }
         want = (want + 1023u) / 1024u * 1024u;
         if (want == B && dist.p) return;
+        drain_emits();
         B = want;
         dist.alloc((size_t)n * B);
-        fm.alloc((size_t)B * (npad / (32u / fmb)));
-        if (fmb == 4) {
-            rle_st.alloc((size_t)B * (npad / 32u));
-            rle_rc.alloc((size_t)B * (npad / 32u));
+        // the second buffer set when a quarter of free HBM still holds it
+        // after the batch's own buffers (else one set: emits do not overlap)
+        const size_t set_bytes = (size_t)B * (npad / (32u / fmb)) * 4u +
+                                 (fmb == 4 ? (size_t)B * (npad / 32u) * 5u : 0u) + 8u * B;
+        for (int x = 0; x < 2; ++x) {
+            if (x == 1) {
+                size_t free_b = 0, total_b = 0;
+                HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+                async = async_on() && set_bytes * 8 < free_b;
+                if (!async) {
+                    fmx[1].release();
+                    rle_stx[1].release();
+                    rle_rcx[1].release();
+                    break;
+                }
+            }
+            fmx[x].alloc((size_t)B * (npad / (32u / fmb)));
+            if (fmb == 4) {
+                rle_stx[x].alloc((size_t)B * (npad / 32u));
+                rle_rcx[x].alloc((size_t)B * (npad / 32u));
+            }
         }
+        cur = 0;
         live.alloc(n);
         tmask.alloc(n);
         if (leaf_fm) fmleaf.alloc((size_t)n * (B / 4u));
@@ -295,6 +355,16 @@ struct cpd_rows {
     int device = 0;
     uint32_t nrows = 0;
     uint64_t total = 0;
+    hipEvent_t done = nullptr;  // after the last emit into `runs` (emit overlap)
+    void wait() const {
+        if (done) HIP_CHECK(hipEventSynchronize(done));
+    }
+    ~cpd_rows() {
+        if (done) {
+            (void)hipEventSynchronize(done);
+            (void)hipEventDestroy(done);
+        }
+    }
     std::vector<uint32_t> targets;   // node ids, row order
     std::vector<uint64_t> offsets;   // host copy, nrows+1
     DevBuf<uint32_t> runs;
@@ -485,6 +555,9 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->device = device;
         g->select();
         HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+        // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step)
+        HIP_CHECK(hipStreamCreateWithFlags(&g->estream, hipStreamNonBlocking));
+        for (auto& e : g->ev_emit) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         const uint32_t n = p->n, m = p->m;
         g->n = n;
         g->m = m;
@@ -663,6 +736,10 @@ bool sort_on() {
     static const bool on = env_on("CPD_SORT");
     return on;
 }
+bool async_on() {  // CPD_ASYNC=0: every emit finishes before its batch returns
+    static const bool on = env_on("CPD_ASYNC");
+    return on;
+}
 
 // Distances + first-move sets for `k` targets (columns already in g->tgt,
 // padded to a multiple of 1024 with valid columns).
@@ -682,7 +759,7 @@ void narrow_decide(cpd_graph* g) {
                      (unsigned long long)groups);
 }
 
-void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow) {
+void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm) {
     const uint32_t B = g->B, n = g->n;
     const NarrowRows nr = g->narrow_rows(narrow);
     if (narrow) HIP_CHECK(hipMemsetAsync(g->ovf.p, 0, sizeof(uint32_t), g->stream));
@@ -785,7 +862,7 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow) {
         8.0 * (double)(n - nl) * (double)(1u << g->adj_shift) * fslabs + 4.0 * g->npad / 32.0;
     g->timed("first_moves", fbytes, [&] {
         launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, g->tgt.p, B, k, n, g->npad,
-                           g->fm.p, g->leaf_fm ? g->leafbits.p : nullptr,
+                           fm, g->leaf_fm ? g->leafbits.p : nullptr,
                            g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream);
     });
     if (stat)
@@ -833,16 +910,19 @@ bool trace_on() {
 // Build rows for one batch of k <= B targets; append to r (device).
 void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r) {
     const double t0 = now_seconds();
+    const uint32_t x = g->acquire_set();
+    uint32_t* fm = g->fmx[x].p;
+    uint32_t* rst = g->rle_stx[x].p;
+    uint8_t* rrc = g->rle_rcx[x].p;
     upload_targets(g, targets, k);
     const uint32_t npad = g->npad;
     const double fm_row = g->fmb / 8.0 * npad;  // first-move bytes per row
     // + per 32-column segment a 4-B entry state and a 1-B count (fmb == 4)
     const double st_row = g->fmb == 4 ? 5.0 * npad / 32.0 : 0.0;
-    run_sweeps_and_fm(g, k, g->narrow);
+    run_sweeps_and_fm(g, k, g->narrow, fm);
     const double t1 = now_seconds();
     g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
-        launch_rle_count(g->fm.p, g->fmb, npad, k, g->counts.p, g->rle_st.p, g->rle_rc.p,
-                         g->stream);
+        launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);
     });
     std::vector<uint32_t> counts(k);
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
@@ -873,6 +953,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     }
     uint64_t new_total = off[k];
     if (new_total > r->runs.n) {  // grow, preserving the rows already built
+        g->drain_emits();  // an earlier batch's emit may still write the old buffer
         // 25% headroom: batches differ by a few runs, and re-allocating tens of
         // GB costs ~1 s, so a reused buffer must not grow again per batch
         size_t want = std::max<size_t>(new_total + new_total / 4, r->runs.n + r->runs.n / 2);
@@ -887,12 +968,22 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
         r->runs.n = want;
     }
     const double t3 = now_seconds();
-    g->row_off.upload(lane_off.data(), k, g->stream);
+    // the emit: on estream (the next batch's sweeps start meanwhile on
+    // stream), or in line when overlap is off; everything it reads came from
+    // `stream`, which the count sync above has drained
+    hipStream_t es = g->async ? g->estream : g->stream;
+    g->lane_off_h[x].swap(lane_off);
+    g->row_offx[x].upload(g->lane_off_h[x].data(), k, es);
     double ebytes = (fm_row + st_row) * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
     g->timed("rle_emit", ebytes, [&] {
-        launch_rle_emit(g->fm.p, g->fmb, npad, k, g->row_off.p, r->runs.p, g->rle_st.p,
-                        g->rle_rc.p, g->stream);
+        launch_rle_emit(fm, g->fmb, npad, k, g->row_offx[x].p, r->runs.p, rst, rrc, es);
     });
+    if (!r->done) HIP_CHECK(hipEventCreateWithFlags(&r->done, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(r->done, es));
+    if (g->async) {
+        HIP_CHECK(hipEventRecord(g->ev_emit[x], es));
+        g->emit_pending[x] = true;
+    }
     g->sync();
     if (trace_on())
         std::fprintf(stderr,
@@ -948,6 +1039,7 @@ int cpd_rows_export(const cpd_rows* r, uint64_t* offsets, uint32_t* runs) {
     return guarded([&] {
         CPD_REQUIRE(r, CPD_E_ARG, "null rows");
         HIP_CHECK(hipSetDevice(r->device));
+        r->wait();
         if (offsets) std::memcpy(offsets, r->offsets.data(), (r->nrows + 1) * sizeof(uint64_t));
         if (runs && r->total)
             HIP_CHECK(hipMemcpy(runs, r->runs.p, r->total * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -965,6 +1057,7 @@ int cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count, uin
             for (uint32_t i = 0; i <= count; ++i) offsets[i] = r->offsets[first + i] - base;
         if (!runs || end == base) return;
         HIP_CHECK(hipSetDevice(r->device));
+        r->wait();
         // one non-blocking stream per (host thread, device), kept for the
         // thread's lifetime: exports never queue behind a build's stream
         thread_local std::vector<hipStream_t> streams;
@@ -996,9 +1089,10 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
         g->select();
         if (!g->B) g->reserve_batch(0);
         CPD_REQUIRE(ntargets > 0 && ntargets <= g->B, CPD_E_ARG, "debug: 0 < ntargets <= batch");
+        const uint32_t x = g->acquire_set();
         upload_targets(g, targets, ntargets);
         const bool narrow = g->narrow;
-        run_sweeps_and_fm(g, ntargets, narrow);
+        run_sweeps_and_fm(g, ntargets, narrow, g->fmx[x].p);
         g->sync();
         const uint32_t n = g->n, B = g->B;
         // lane p holds the caller's target i = pos_of^-1(p)
@@ -1030,7 +1124,7 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
             const uint32_t per = 32u / g->fmb, all = (1u << g->fmb) - 1u;
             const size_t row_words = g->npad / per;
             std::vector<uint32_t> w((size_t)B * row_words);
-            HIP_CHECK(hipMemcpy(w.data(), g->fm.p, w.size() * sizeof(uint32_t),
+            HIP_CHECK(hipMemcpy(w.data(), g->fmx[x].p, w.size() * sizeof(uint32_t),
                                 hipMemcpyDeviceToHost));
             for (uint32_t i = 0; i < ntargets; ++i) {
                 const uint32_t p = g->pos_of[i];
@@ -1179,6 +1273,7 @@ void append_host(cpd_index* ix, uint32_t count, const uint64_t* offsets, const u
 void append_built(cpd_index* ix, const cpd_rows* r) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(r->device == g->device, CPD_E_ARG, "index: rows live on another device");
+    r->wait();
     CPD_REQUIRE(r->nrows <= ix->nrows - ix->added, CPD_E_ARG, "index: more rows than declared");
     if (!r->nrows) return;
     if (ix->keep_rle) {
@@ -1606,6 +1701,8 @@ int cpd_timing_enable(cpd_graph* g, int enable) {
 int cpd_timing_reset(cpd_graph* g) {
     return guarded([&] {
         CPD_REQUIRE(g, CPD_E_ARG, "null graph");
+        g->select();
+        g->sync(true);
         g->agg.clear();
     });
 }
@@ -1613,6 +1710,10 @@ int cpd_timing_reset(cpd_graph* g) {
 int cpd_timing_get(const cpd_graph* g, cpd_kernel_time* out, int max, int* count) {
     return guarded([&] {
         CPD_REQUIRE(g && count, CPD_E_ARG, "null argument");
+        // emits may still run on the emit stream: fold them in first
+        auto* gm = const_cast<cpd_graph*>(g);
+        gm->select();
+        gm->sync(true);
         int k = 0;
         for (auto& kv : g->agg) {
             if (out && k < max) {
