@@ -850,14 +850,15 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm) {
                               g->dsc_lvl_of.p, 0, n, live, stat + 2 * nasc, g->stream);
         });
     }
-    // per row: own distance 4n + neighbour distances 4m + first-move write
-    // npad * fmb / 8; the packed adjacency (8 B per slot) is read once per
-    // 1024-target slab.  Leaf columns (leaf_fm) read 0.5 B of sets instead
-    // of their own and neighbour distances.
+    // per row: own distance 4n (kernels that read it) + neighbour distances
+    // 4m + first-move write npad * fmb / 8; the packed adjacency (8 B per
+    // slot) is read once per 1024-target slab.  Leaf columns (leaf_fm) read
+    // 0.5 B of sets instead of their own and neighbour distances.
     const uint32_t fslabs = (k + 1023u) / 1024u;
     const double nl = g->leaf_fm ? g->n_leaf : 0.0, ml = g->leaf_fm ? g->m_leaf : 0.0;
+    const double own = first_moves_reads_own(g->adj_shift, narrow) ? drow * (n - nl) : 0.0;
     double fbytes =
-        (drow * (n - nl) + drow * (g->m - ml) + 0.5 * nl + g->fmb / 8.0 * g->npad) *
+        (own + drow * (g->m - ml) + 0.5 * nl + g->fmb / 8.0 * g->npad) *
             (fslabs * 1024.0) +
         8.0 * (double)(n - nl) * (double)(1u << g->adj_shift) * fslabs + 4.0 * g->npad / 32.0;
     g->timed("first_moves", fbytes, [&] {

@@ -525,6 +525,155 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ des
     }
 }
 
+// The same slot computation split into issue (descriptor, own row or closed
+// form, the inline gathers) and finish (decode, minimum, leaf sets, the rest
+// of a long list, store), so that a wave keeps the gathers of P slots in
+// flight at once (sweep_down8p).  A down-sweep wave is latency-bound: it
+// lives for one descriptor load plus one gather round trip, and moves ~4 KiB
+// in that time; P slots per wave put P times the bytes behind one wait.
+struct Slot8 {
+    uint32_t vraw, v, a0, a1;
+    uint2 inl[kDescArcs];
+    U8 acc;
+    NLoad8 pl[kDescArcs];
+};
+
+__device__ __forceinline__ void down8_issue(Slot8& S, const uint4* __restrict__ desc,
+                                            uint32_t slot, const U8& t, uint32_t l8,
+                                            uint32_t grp, uint32_t B4, uint32_t B8,
+                                            const uint4* __restrict__ d4, const Closed& cf,
+                                            const uint32_t* __restrict__ live,
+                                            const NarrowRows& nr) {
+    const uint4* __restrict__ dp = desc + (size_t)slot * 8u;
+    const uint4 h = dp[0], i0 = dp[1], i1 = dp[2], i2 = dp[3];
+    S.inl[0] = make_uint2(i0.x, i0.y);
+    S.inl[1] = make_uint2(i0.z, i0.w);
+    S.inl[2] = make_uint2(i1.x, i1.y);
+    S.inl[3] = make_uint2(i1.z, i1.w);
+    S.inl[4] = make_uint2(i2.x, i2.y);
+    S.inl[5] = make_uint2(i2.z, i2.w);
+    S.vraw = h.x;
+    S.a0 = h.y;
+    S.a1 = h.z;
+    if (S.vraw & kLeafBit) {
+        S.v = S.vraw & kIdxMask;
+        S.acc = U8{leaf4(t.a, S.v, 0u), leaf4(t.b, S.v, 0u)};
+    } else if (S.vraw & kL1Bit) {  // closed form from the descriptor
+        const uint4 c0 = dp[4], c1 = dp[5], c2 = dp[6];
+        S.v = c0.x;
+        U8 acc{leaf4(t.a, S.v, 0u), leaf4(t.b, S.v, 0u)};
+        const uint2 la[4] = {make_uint2(c0.z, c0.w), make_uint2(c1.x, c1.y),
+                             make_uint2(c1.z, c1.w), make_uint2(c2.x, c2.y)};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if ((uint32_t)i < c0.y) {
+                min4(acc.a, leaf4(t.a, la[i].x, 0u), la[i].y);
+                min4(acc.b, leaf4(t.b, la[i].x, 0u), la[i].y);
+            }
+        if (c0.y > 4u) {  // more leaf arcs than fit: the ascending arrays
+            const uint32_t s1 = S.vraw & kIdxMask;
+            for (uint32_t a = cf.off[s1] + 4u; a < cf.off[s1 + 1]; ++a) {
+                const uint2 e = cf.arcs[a];
+                min4(acc.a, leaf4(t.a, e.x & kIdxMask, 0u), e.y);
+                min4(acc.b, leaf4(t.b, e.x & kIdxMask, 0u), e.y);
+            }
+        }
+        S.acc = acc;
+    } else {
+        S.v = S.vraw;
+        const bool own = !live || ((live[S.v] >> (l8 >> 7)) & 1u);  // live bits: 1024 targets
+        S.acc = own ? U8{d4[(size_t)S.v * B4 + 2u * l8], d4[(size_t)S.v * B4 + 2u * l8 + 1u]}
+                    : inf8();
+    }
+#pragma unroll
+    for (int i = 0; i < (int)kDescArcs; ++i)  // a leaf's self loop is not gathered
+        if (S.inl[i].x != kNoEdge && S.inl[i].x != S.v)
+            S.pl[i] = nl8_issue(nr, S.inl[i].x, grp, B8, l8);
+}
+
+__device__ __forceinline__ void down8_finish(Slot8& S, const U8& t, uint32_t l8, uint32_t grp,
+                                             uint32_t B4, uint32_t B8, uint4* __restrict__ d4,
+                                             const uint2* __restrict__ arcs,
+                                             uint16_t* __restrict__ fmleaf,
+                                             const NarrowRows& nr) {
+    const uint32_t v = S.v;
+    if ((S.vraw & kLeafBit) && fmleaf) {  // out-degree <= 4 (4-bit sets): all inline
+        U8 x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            x[k] = (S.inl[k].x != kNoEdge && S.inl[k].x != v)
+                       ? nl8_finish(S.pl[k], d4, S.inl[k].x, B4, l8)
+                       : inf8();
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (S.inl[k].x != kNoEdge && S.inl[k].x != v) min8(S.acc, x[k], S.inl[k].y);
+        uint32_t ba[4] = {0, 0, 0, 0}, bb[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (S.inl[k].x == kNoEdge) continue;
+            const U8& dv = S.inl[k].x == v ? S.acc : x[k];  // self loop: d(v) itself
+            fm_nib(dv.a, S.acc.a, S.inl[k].y, k, ba);
+            fm_nib(dv.b, S.acc.b, S.inl[k].y, k, bb);
+        }
+        const uint32_t sets =
+            fm_pack4(t.a, S.acc.a, v, ba) | (fm_pack4(t.b, S.acc.b, v, bb) << 16);
+        narrow_store8(nr, d4, v, grp, B4, B8, l8, S.acc);
+        reinterpret_cast<uint32_t*>(fmleaf)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < (int)kDescArcs; ++i)
+        if (S.inl[i].x != kNoEdge && S.inl[i].x != v)
+            min8(S.acc, nl8_finish(S.pl[i], d4, S.inl[i].x, B4, l8), S.inl[i].y);
+    uint32_t a = S.a0 + kDescArcs;  // the rest of a long list
+    for (; a + 8 <= S.a1; a += 8) {
+        uint2 e[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
+        NLoad8 pl[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pl[i] = nl8_issue(nr, e[i].x, grp, B8, l8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) min8(S.acc, nl8_finish(pl[i], d4, e[i].x, B4, l8), e[i].y);
+    }
+    for (; a < S.a1; ++a) {
+        const uint2 e = arcs[a];
+        min8(S.acc, nl8_finish(nl8_issue(nr, e.x, grp, B8, l8), d4, e.x, B4, l8), e.y);
+    }
+    narrow_store8(nr, d4, v, grp, B4, B8, l8, S.acc);
+}
+
+// Narrow down-sweep with P slots in flight per wave: logical block = (group
+// of P consecutive slots, 8 x blockDim targets), slot groups fastest,
+// XCD-remapped; every slot's descriptor and gathers are issued before the
+// first is finished.
+template <int P>
+__global__ __launch_bounds__(256) void sweep_down8p(const uint4* __restrict__ desc,
+                                                    const uint2* __restrict__ arcs,
+                                                    uint32_t slot0, uint32_t count, uint32_t remap,
+                                                    uint32_t* __restrict__ dist,
+                                                    const uint4* __restrict__ tgt4, uint32_t B4,
+                                                    Closed cf, const uint32_t* __restrict__ live,
+                                                    uint16_t* __restrict__ fmleaf, NarrowRows nr) {
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t ngrp = (count + P - 1) / P;
+    const uint32_t blk = L / ngrp;
+    const uint32_t s0 = slot0 + (L - blk * ngrp) * P;
+    const uint32_t np = min((uint32_t)P, slot0 + count - s0);  // wave-uniform
+    const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
+    const uint32_t grp = l8 >> 5;                        // uniform per half-wave
+    const uint32_t B8 = B4 / 2u;
+    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    const U8 t{tgt4[2u * l8], tgt4[2u * l8 + 1u]};
+    Slot8 S[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+        if ((uint32_t)p < np) down8_issue(S[p], desc, s0 + p, t, l8, grp, B4, B8, d4, cf, live, nr);
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+        if ((uint32_t)p < np) down8_finish(S[p], t, l8, grp, B4, B8, d4, arcs, fmleaf, nr);
+}
+
 // Group rows stored wide (timing runs only): *out += #{base[i] == kWideRow}.
 __global__ __launch_bounds__(256) void count_wide_rows(const uint32_t* __restrict__ base,
                                                        size_t total,
@@ -887,6 +1036,14 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
 // column group; and the loads of group g+1 are issued before group g is
 // decoded (two groups in flight), so a wave waits about one memory round trip
 // per group instead of two.
+//
+// The column's own row is not read (OWN = false, the default): for c != t,
+// d(c) = min over c's out-edges of w_k + d(v_k) (a shortest path to t leaves
+// c by some edge; a self loop adds w + d(c) >= d(c) and so never lowers the
+// minimum), all of them final here, and d(c) == INF exactly when every term
+// is INF — so the sets {k : w_k + d(v_k) == d(c)} follow from the neighbour
+// rows alone, bit-identical, one gather per column fewer.  OWN = true reads
+// it as before (CPD_FM_OWN=1, A/B only).
 template <int G>
 struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR pressure)
     NLoad own[G];
@@ -905,7 +1062,7 @@ struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR press
 // the same TPS x 4 targets; the groups swap their 16-B pieces through LDS so
 // that each lane stores 16 X contiguous bytes of a row (one row in X of the
 // lane's 4) — whole 64-B sectors at X = 4 instead of 16-B partial ones.
-template <int G, int S, int X = 1>
+template <int G, int S, int X = 1, bool OWN = false>
 __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ adj,
                                                       const uint32_t* __restrict__ dist,
                                                       const uint32_t* __restrict__ tgt, uint32_t B,
@@ -960,7 +1117,7 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
             const bool ok = c < n;
             const bool leaf = is_leaf(cg + j);
             if (ok && !leaf) {
-                g.own[j] = nl_issue(nr, c, grp, B4, l4);
+                if (OWN) g.own[j] = nl_issue(nr, c, grp, B4, l4);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint2 e = edge(cg + j, k);
@@ -983,18 +1140,33 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                 f2 = (g.lv[j] >> 8) & 0xFu;
                 f3 = g.lv[j] >> 12;
             } else {
-                const uint4 dn = nl_finish(g.own[j], d4, c, B4, l4);
+                uint4 dv[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint2 e = edge(cc, k);
+                    dv[k] = e.x != kNoEdge ? nl_finish(g.nb[j][k], d4, e.x, B4, l4)
+                                           : make_uint4(INF, INF, INF, INF);
+                }
+                uint4 dn = make_uint4(INF, INF, INF, INF);
+                if (OWN) {
+                    dn = nl_finish(g.own[j], d4, c, B4, l4);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint2 e = edge(cc, k);
+                        if (e.x != kNoEdge) min4(dn, dv[k], e.y);
+                    }
+                }
                 uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint2 e = edge(cc, k);
                     if (e.x == kNoEdge) continue;
-                    const uint4 dv = nl_finish(g.nb[j][k], d4, e.x, B4, l4);
                     const uint32_t we = e.y;
-                    b0 |= fm_bit(dv.x, we, dn.x, k);
-                    b1 |= fm_bit(dv.y, we, dn.y, k);
-                    b2 |= fm_bit(dv.z, we, dn.z, k);
-                    b3 |= fm_bit(dv.w, we, dn.w, k);
+                    b0 |= fm_bit(dv[k].x, we, dn.x, k);
+                    b1 |= fm_bit(dv[k].y, we, dn.y, k);
+                    b2 |= fm_bit(dv[k].z, we, dn.z, k);
+                    b3 |= fm_bit(dv[k].w, we, dn.w, k);
                 }
                 f0 = fm_final<4>(c, tc.x, dn.x, b0);
                 f1 = fm_final<4>(c, tc.y, dn.y, b1);
@@ -2134,6 +2306,13 @@ uint32_t down8_k() {  // CPD_DOWN8_K: slots per wave in the narrow down-sweep (1
     }();
     return v;
 }
+uint32_t down8_p() {  // CPD_DOWN8_P: slots whose gathers a down-sweep wave keeps in flight (1-4)
+    static const uint32_t v = [] {
+        const uint32_t p = env_u32("CPD_DOWN8_P", 1);
+        return p < 1 ? 1u : p > 4 ? 4u : p;
+    }();
+    return v;
+}
 uint32_t fm_wpb() {
     static const uint32_t v = env_u32("CPD_FM_WPB", 2);
     return v;
@@ -2159,6 +2338,10 @@ uint32_t fm_xg() {  // CPD_FM_XG: columns per gather group in the exchange kerne
 }
 uint32_t fm_g() {
     static const uint32_t v = env_u32("CPD_FM_G", 2);
+    return v;
+}
+uint32_t fm_own() {  // CPD_FM_OWN=1: the pipelined first moves also read the column's own row
+    static const uint32_t v = env_u32("CPD_FM_OWN", 0);
     return v;
 }
 
@@ -2190,11 +2373,20 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
             // (4 waves = 2048 targets: only when the slab count is even)
             const uint32_t wpb8 = down8_wpb() == 4 && slabs % 2 ? 2u : down8_wpb();
             const uint32_t tpb8 = 64u * wpb8;
-            const uint32_t K = down8_k();
+            const uint32_t P = down8_p();
+            const uint32_t K = P > 1 ? P : down8_k();
             const uint32_t ngrp = (count + K - 1u) / K;
             const dim3 g8(ngrp * slabs * 2u / wpb8), b8(tpb8);
             const uint4* d = reinterpret_cast<const uint4*>(desc);
             const uint32_t* lv = live;
+            if (P > 1) {
+                switch (P) {
+                    case 2: launch(kern::sweep_down8p<2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                    case 3: launch(kern::sweep_down8p<3>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                    default: launch(kern::sweep_down8p<4>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                }
+                return;
+            }
             switch (K) {
                 case 1: launch(kern::sweep_down8<1>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
                 case 2: launch(kern::sweep_down8<2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
@@ -2305,6 +2497,9 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
         } else if (fm_segs() == 2)
             launch(kern::first_moves_n4<2, 2>, dim3(grid.x / 2u), blk, s, adj, dist, tgt, B, n, npad,
                    r, fm, leafbits, fmleaf, nr);
+        else if (fm_own())
+            launch(kern::first_moves_n4<2, 1, 1, true>, grid, blk, s, adj, dist, tgt, B, n, npad,
+                   r, fm, leafbits, fmleaf, nr);
         else
             launch(kern::first_moves_n4<2, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm,
                    leafbits, fmleaf, nr);
@@ -2314,6 +2509,11 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
     else
         launch_first_moves_t<false>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
                                     grid, blk, s);
+}
+
+bool first_moves_reads_own(uint32_t shift, bool narrow) {
+    if (!(narrow && shift == 2 && fm_n4())) return true;  // the generic kernel
+    return fm_own() && fm_x() == 1 && fm_segs() != 2;     // only the default form has OWN
 }
 
 template <bool EMIT>

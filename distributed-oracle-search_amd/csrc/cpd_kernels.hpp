@@ -99,6 +99,9 @@ void launch_first_moves(const uint32_t* adj, uint32_t shift, const uint32_t* dis
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
                         uint32_t npad, uint32_t* fm, const uint32_t* leafbits,
                         const uint16_t* fmleaf, NarrowRows nr, hipStream_t s);
+// Whether that launch reads each computed column's own distance row (the
+// pipelined narrow kernel derives it from the neighbour rows instead).
+bool first_moves_reads_own(uint32_t shift, bool narrow);
 
 // Row width of the tiled first-move rows: npad is a multiple of this.
 constexpr uint32_t kFmTile = 2048;
