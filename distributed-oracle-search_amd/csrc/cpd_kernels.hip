@@ -347,8 +347,16 @@ __device__ __forceinline__ void narrow_store8(const NarrowRows& nr, uint4* __res
         if (head) nr.base[(size_t)grp * nr.n + col] = kWideRow;
         return;
     }
-    reinterpret_cast<uint4*>(nr.d16)[(size_t)col * B8 + l8] =
-        make_uint4(q0 | (q1 << 16), q2 | (q3 << 16), q4 | (q5 << 16), q6 | (q7 << 16));
+    const uint4 q = make_uint4(q0 | (q1 << 16), q2 | (q3 << 16), q4 | (q5 << 16), q6 | (q7 << 16));
+    uint4* const dst = reinterpret_cast<uint4*>(nr.d16) + (size_t)col * B8 + l8;
+    if (nr.nt) {  // kernel-uniform
+        __builtin_nontemporal_store(q.x, &dst->x);
+        __builtin_nontemporal_store(q.y, &dst->y);
+        __builtin_nontemporal_store(q.z, &dst->z);
+        __builtin_nontemporal_store(q.w, &dst->w);
+    } else {
+        *dst = q;
+    }
     if (head) nr.base[(size_t)grp * nr.n + col] = b;
 }
 
@@ -383,6 +391,14 @@ __device__ __forceinline__ Desc8 load_desc8(const uint4* __restrict__ desc, uint
     if (LAZY) return Desc8{dp[0], dp[1], dp[2], dp[3], {}, {}, {}};
     return Desc8{dp[0], dp[1], dp[2], dp[3], dp[4], dp[5], dp[6]};
 }
+
+// Gathers in flight per step of a long arc list (past the descriptor's
+// kDescArcs): the list tail is rare, and its registers set the kernel's
+// occupancy (8 in flight: 88 VGPRs, 5 waves per SIMD).
+#ifndef CPD_DOWN8_LONG
+#define CPD_DOWN8_LONG 4
+#endif
+constexpr int kLong = CPD_DOWN8_LONG;
 
 // One slot of the narrow down-sweep for the lane's 8 targets t.
 template <bool LAZY>
@@ -467,16 +483,16 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const uint4* __restri
         for (int i = 0; i < (int)kDescArcs; ++i)
             if (inl[i].x != kNoEdge) min8(acc, nl8_finish(pl[i], d4, inl[i].x, B4, l8), inl[i].y);
     }
-    uint32_t a = a0 + kDescArcs;  // the rest of a long list
-    for (; a + 8 <= a1; a += 8) {
-        uint2 e[8];
+    uint32_t a = a0 + kDescArcs;  // the rest of a long list (rare), kLong gathers at a time
+    for (; a + kLong <= a1; a += kLong) {
+        uint2 e[kLong];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
-        NLoad8 pl[8];
+        for (int i = 0; i < kLong; ++i) e[i] = arcs[a + i];
+        NLoad8 pl[kLong];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) pl[i] = nl8_issue(nr, e[i].x, grp, B8, l8);
+        for (int i = 0; i < kLong; ++i) pl[i] = nl8_issue(nr, e[i].x, grp, B8, l8);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) min8(acc, nl8_finish(pl[i], d4, e[i].x, B4, l8), e[i].y);
+        for (int i = 0; i < kLong; ++i) min8(acc, nl8_finish(pl[i], d4, e[i].x, B4, l8), e[i].y);
     }
     for (; a < a1; ++a) {
         const uint2 e = arcs[a];
@@ -492,8 +508,11 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const uint4* __restri
 // descriptor while the current slot's gathers are in flight, so the scalar
 // descriptor fetch leaves the critical path after the first slot.  K = 1 is
 // one slot per block.
-template <int K>
-__global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ desc,
+// PF = false: the K slots one after another, each descriptor loaded when its
+// slot starts (the wave's launch and target loads amortised over K slots,
+// nothing held across them).
+template <int K, bool PF = true>
+__global__ __launch_bounds__(256, (K > 1 && !PF) ? 5 : 1) void sweep_down8(const uint4* __restrict__ desc,
                                                    const uint2* __restrict__ arcs,
                                                    uint32_t slot0, uint32_t count, uint32_t remap,
                                                    uint32_t* __restrict__ dist,
@@ -513,6 +532,13 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ des
     if (K == 1) {
         down8_slot<false>(load_desc8<false>(desc, s0), desc, s0, t, l8, grp, B4, B8, d4, arcs,
                           cf, live, fmleaf, nr);
+        return;
+    }
+    if (!PF) {
+#pragma unroll 1
+        for (uint32_t s = s0; s < s1; ++s)
+            down8_slot<false>(load_desc8<false>(desc, s), desc, s, t, l8, grp, B4, B8, d4, arcs,
+                              cf, live, fmleaf, nr);
         return;
     }
     Desc8 cur = load_desc8<true>(desc, s0);
@@ -647,8 +673,10 @@ __device__ __forceinline__ void down8_finish(Slot8& S, const U8& t, uint32_t l8,
 // of P consecutive slots, 8 x blockDim targets), slot groups fastest,
 // XCD-remapped; every slot's descriptor and gathers are issued before the
 // first is finished.
-template <int P>
-__global__ __launch_bounds__(256) void sweep_down8p(const uint4* __restrict__ desc,
+// W = waves per SIMD asked of the register allocator (P = 2 needs ~174
+// VGPRs unbounded: 2 waves; W = 3 keeps 6 slots per SIMD in flight).
+template <int P, int W>
+__global__ __launch_bounds__(256, W) void sweep_down8p(const uint4* __restrict__ desc,
                                                     const uint2* __restrict__ arcs,
                                                     uint32_t slot0, uint32_t count, uint32_t remap,
                                                     uint32_t* __restrict__ dist,
@@ -2257,10 +2285,14 @@ namespace {
 thread_local hipEvent_t g_ev_start = nullptr, g_ev_stop = nullptr;
 
 template <typename... Args, typename F>
-void launch(F kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+void launch_shm(F kernel, dim3 grid, dim3 block, size_t shm, hipStream_t s, Args... args) {
     hipEvent_t a = g_ev_start, b = g_ev_stop;
     g_ev_start = g_ev_stop = nullptr;
-    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, a, b, 0, args...);
+    hipExtLaunchKernelGGL(kernel, grid, block, shm, s, a, b, 0, args...);
+}
+template <typename... Args, typename F>
+void launch(F kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    launch_shm(kernel, grid, block, 0, s, args...);
 }
 }  // namespace
 
@@ -2311,6 +2343,18 @@ uint32_t down8_p() {  // CPD_DOWN8_P: slots whose gathers a down-sweep wave keep
         const uint32_t p = env_u32("CPD_DOWN8_P", 1);
         return p < 1 ? 1u : p > 4 ? 4u : p;
     }();
+    return v;
+}
+uint32_t down8_pf() {  // CPD_DOWN8_PF=0: K > 1 slots per wave without the descriptor prefetch
+    static const uint32_t v = env_u32("CPD_DOWN8_PF", 1);
+    return v;
+}
+uint32_t down8_nt() {  // CPD_DOWN8_NT=1: the down-sweep's narrow rows stored non-temporal
+    static const uint32_t v = env_u32("CPD_DOWN8_NT", 0);
+    return v;
+}
+size_t down8_lds() {  // CPD_DOWN8_LDS: bytes of (unused) LDS per down-sweep workgroup (occupancy A/B)
+    static const size_t v = env_u32("CPD_DOWN8_LDS", 0);
     return v;
 }
 uint32_t fm_wpb() {
@@ -2381,14 +2425,24 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
             const uint32_t* lv = live;
             if (P > 1) {
                 switch (P) {
-                    case 2: launch(kern::sweep_down8p<2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
-                    case 3: launch(kern::sweep_down8p<3>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
-                    default: launch(kern::sweep_down8p<4>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                    case 2: launch(kern::sweep_down8p<2, 3>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                    case 3: launch(kern::sweep_down8p<3, 2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                    default: launch(kern::sweep_down8p<4, 2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                }
+                return;
+            }
+            NarrowRows nrd = nr;
+            nrd.nt = down8_nt();
+            if (!down8_pf() && K > 1) {
+                switch (K) {
+                    case 2: launch(kern::sweep_down8<2, false>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nrd); break;
+                    case 4: launch(kern::sweep_down8<4, false>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nrd); break;
+                    default: launch(kern::sweep_down8<8, false>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nrd); break;
                 }
                 return;
             }
             switch (K) {
-                case 1: launch(kern::sweep_down8<1>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
+                case 1: launch_shm(kern::sweep_down8<1>, g8, b8, down8_lds(), s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nrd); break;
                 case 2: launch(kern::sweep_down8<2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
                 case 4: launch(kern::sweep_down8<4>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
                 default: launch(kern::sweep_down8<8>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;

@@ -25,6 +25,7 @@ struct NarrowRows {
     uint32_t* base;
     uint32_t n;
     uint32_t* ovf;
+    uint32_t nt = 0;  // down-sweep stores non-temporal (set by the launcher, CPD_DOWN8_NT)
 };
 
 // One CH sweep level: `count` node slots starting at `slot0` of the
