@@ -290,7 +290,13 @@ struct U8 {
     uint4 a, b;
 };
 
-constexpr uint32_t kDescArcs = 6;  // arcs inline in a down-sweep slot descriptor
+#ifndef CPD_DOWN8_INLINE
+#define CPD_DOWN8_INLINE 6
+#endif
+// arcs inline in a down-sweep slot descriptor (4..6; a leaf's <= 4 out-edges
+// always fit), gathered together; the rest of a list streams from `arcs`
+constexpr uint32_t kDescArcs = CPD_DOWN8_INLINE;
+static_assert(kDescArcs >= 4 && kDescArcs <= 6, "descriptor arcs");
 
 __device__ __forceinline__ U8 inf8() {
     return U8{make_uint4(INF, INF, INF, INF), make_uint4(INF, INF, INF, INF)};
@@ -377,6 +383,76 @@ __device__ __forceinline__ uint32_t fm_pack4(const uint4& t, const uint4& acc, u
     return b0 | (b1 << 4) | (b2 << 8) | (b3 << 12);
 }
 
+// Leaf slot of the narrow down-sweep: d(v) = min over the out-edges (all to
+// final, higher-ranked nodes; a self loop never lowers it) and FM(v) = the
+// edges attaining it, folded per neighbour as it is decoded (argmin set: a
+// strictly smaller value restarts the set, an equal one joins it), so no
+// neighbour row is held after its fold — the slot's registers stay at one
+// pending gather set.  A self loop joins iff its weight is 0 (w + d(v) ==
+// d(v)); the wildcard at the target and at unreachable v overrides.
+// bits: the sets of 4 targets, one nibble each (target i at bits 4i..4i+3),
+// packed to keep the slot's registers low.
+template <int I>
+__device__ __forceinline__ void argmin_fold(uint32_t& a, uint32_t& bits, uint32_t val, int k) {
+    const uint32_t bit = 1u << (4 * I + k);
+    const uint32_t restart = (bits & ~(0xFu << (4 * I))) | bit;
+    bits = val < a ? restart : (val == a ? (bits | bit) : bits);
+    a = min(a, val);
+}
+
+// 4 nibbles -> the stored sets with the wildcard at the target and at
+// unreachable columns.
+__device__ __forceinline__ uint32_t fm_wild4(const uint4& t, const uint4& acc, uint32_t v,
+                                             uint32_t bits) {
+    bits |= (t.x == v || acc.x == INF) ? 0x000Fu : 0u;
+    bits |= (t.y == v || acc.y == INF) ? 0x00F0u : 0u;
+    bits |= (t.z == v || acc.z == INF) ? 0x0F00u : 0u;
+    bits |= (t.w == v || acc.w == INF) ? 0xF000u : 0u;
+    return bits;
+}
+
+__device__ __forceinline__ void leaf_finish8(const uint2* e, const NLoad8 (&pl)[kDescArcs],
+                                             uint32_t v, U8& acc, const U8& t, uint32_t l8,
+                                             uint32_t grp, uint32_t B4, uint32_t B8,
+                                             uint4* __restrict__ d4,
+                                             uint16_t* __restrict__ fmleaf, const NarrowRows& nr) {
+    uint32_t ba = 0, bb = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (e[k].x == kNoEdge || e[k].x == v) continue;
+        const U8 x = nl8_finish(pl[k], d4, e[k].x, B4, l8);
+        const uint32_t w = e[k].y;
+        argmin_fold<0>(acc.a.x, ba, sat_add(x.a.x, w), k);
+        argmin_fold<1>(acc.a.y, ba, sat_add(x.a.y, w), k);
+        argmin_fold<2>(acc.a.z, ba, sat_add(x.a.z, w), k);
+        argmin_fold<3>(acc.a.w, ba, sat_add(x.a.w, w), k);
+        argmin_fold<0>(acc.b.x, bb, sat_add(x.b.x, w), k);
+        argmin_fold<1>(acc.b.y, bb, sat_add(x.b.y, w), k);
+        argmin_fold<2>(acc.b.z, bb, sat_add(x.b.z, w), k);
+        argmin_fold<3>(acc.b.w, bb, sat_add(x.b.w, w), k);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (e[k].x == v && e[k].y == 0u) {  // zero-weight self loop (wave-uniform)
+            ba |= 0x1111u << k;
+            bb |= 0x1111u << k;
+        }
+    const uint32_t sets = fm_wild4(t.a, acc.a, v, ba) | (fm_wild4(t.b, acc.b, v, bb) << 16);
+    narrow_store8(nr, d4, v, grp, B4, B8, l8, acc);
+    reinterpret_cast<uint32_t*>(fmleaf)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
+}
+
+__device__ __forceinline__ void leaf_slot8(const uint2* e, uint32_t v, U8& acc, const U8& t,
+                                           uint32_t l8, uint32_t grp, uint32_t B4, uint32_t B8,
+                                           uint4* __restrict__ d4, uint16_t* __restrict__ fmleaf,
+                                           const NarrowRows& nr) {
+    NLoad8 pl[kDescArcs];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (e[k].x != kNoEdge && e[k].x != v) pl[k] = nl8_issue(nr, e[k].x, grp, B8, l8);
+    leaf_finish8(e, pl, v, acc, t, l8, grp, B4, B8, d4, fmleaf, nr);
+}
+
 // A down-sweep slot's descriptor (see down_desc_arcs): the 64-B head (node
 // word, arc range, first kDescArcs arcs) and, for a level-1 node, the
 // closed-form part (c0..c2).  LAZY: the closed-form part is loaded inside the
@@ -412,9 +488,12 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const uint4* __restri
     // out-edges in file order); for a level-1 node also its column and its
     // <= 4 leaf arcs (closed form)
     const uint4 i0 = D.i0, i1 = D.i1, i2 = D.i2;
-    const uint2 inl[kDescArcs] = {make_uint2(i0.x, i0.y), make_uint2(i0.z, i0.w),
-                                  make_uint2(i1.x, i1.y), make_uint2(i1.z, i1.w),
-                                  make_uint2(i2.x, i2.y), make_uint2(i2.z, i2.w)};
+    const uint2 all6[6] = {make_uint2(i0.x, i0.y), make_uint2(i0.z, i0.w),
+                           make_uint2(i1.x, i1.y), make_uint2(i1.z, i1.w),
+                           make_uint2(i2.x, i2.y), make_uint2(i2.z, i2.w)};
+    uint2 inl[kDescArcs];
+#pragma unroll
+    for (int i = 0; i < (int)kDescArcs; ++i) inl[i] = all6[i];
     const uint32_t vraw = D.h.x, a0 = D.h.y, a1 = D.h.z;
     uint32_t v;
     U8 acc;
@@ -422,30 +501,7 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const uint4* __restri
         v = vraw & kIdxMask;
         acc = U8{leaf4(t.a, v, 0u), leaf4(t.b, v, 0u)};
         if (fmleaf) {  // out-degree <= 4 (4-bit sets): all inline
-            const uint2* e = inl;
-            NLoad8 pl[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (e[k].x != kNoEdge && e[k].x != v) pl[k] = nl8_issue(nr, e[k].x, grp, B8, l8);
-            U8 x[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                x[k] = (e[k].x != kNoEdge && e[k].x != v) ? nl8_finish(pl[k], d4, e[k].x, B4, l8)
-                                                          : inf8();
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (e[k].x != kNoEdge && e[k].x != v) min8(acc, x[k], e[k].y);
-            uint32_t ba[4] = {0, 0, 0, 0}, bb[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (e[k].x == kNoEdge) continue;
-                const U8& dv = e[k].x == v ? acc : x[k];  // self loop: d(v) itself
-                fm_nib(dv.a, acc.a, e[k].y, k, ba);
-                fm_nib(dv.b, acc.b, e[k].y, k, bb);
-            }
-            const uint32_t sets = fm_pack4(t.a, acc.a, v, ba) | (fm_pack4(t.b, acc.b, v, bb) << 16);
-            narrow_store8(nr, d4, v, grp, B4, B8, l8, acc);
-            reinterpret_cast<uint32_t*>(fmleaf)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
+            leaf_slot8(inl, v, acc, t, l8, grp, B4, B8, d4, fmleaf, nr);
             return;
         }
     } else if (vraw & kL1Bit) {  // closed form from the descriptor
@@ -572,12 +628,11 @@ __device__ __forceinline__ void down8_issue(Slot8& S, const uint4* __restrict__ 
                                             const NarrowRows& nr) {
     const uint4* __restrict__ dp = desc + (size_t)slot * 8u;
     const uint4 h = dp[0], i0 = dp[1], i1 = dp[2], i2 = dp[3];
-    S.inl[0] = make_uint2(i0.x, i0.y);
-    S.inl[1] = make_uint2(i0.z, i0.w);
-    S.inl[2] = make_uint2(i1.x, i1.y);
-    S.inl[3] = make_uint2(i1.z, i1.w);
-    S.inl[4] = make_uint2(i2.x, i2.y);
-    S.inl[5] = make_uint2(i2.z, i2.w);
+    const uint2 all6[6] = {make_uint2(i0.x, i0.y), make_uint2(i0.z, i0.w),
+                           make_uint2(i1.x, i1.y), make_uint2(i1.z, i1.w),
+                           make_uint2(i2.x, i2.y), make_uint2(i2.z, i2.w)};
+#pragma unroll
+    for (int i = 0; i < (int)kDescArcs; ++i) S.inl[i] = all6[i];
     S.vraw = h.x;
     S.a0 = h.y;
     S.a1 = h.z;
@@ -624,27 +679,7 @@ __device__ __forceinline__ void down8_finish(Slot8& S, const U8& t, uint32_t l8,
                                              const NarrowRows& nr) {
     const uint32_t v = S.v;
     if ((S.vraw & kLeafBit) && fmleaf) {  // out-degree <= 4 (4-bit sets): all inline
-        U8 x[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            x[k] = (S.inl[k].x != kNoEdge && S.inl[k].x != v)
-                       ? nl8_finish(S.pl[k], d4, S.inl[k].x, B4, l8)
-                       : inf8();
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (S.inl[k].x != kNoEdge && S.inl[k].x != v) min8(S.acc, x[k], S.inl[k].y);
-        uint32_t ba[4] = {0, 0, 0, 0}, bb[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (S.inl[k].x == kNoEdge) continue;
-            const U8& dv = S.inl[k].x == v ? S.acc : x[k];  // self loop: d(v) itself
-            fm_nib(dv.a, S.acc.a, S.inl[k].y, k, ba);
-            fm_nib(dv.b, S.acc.b, S.inl[k].y, k, bb);
-        }
-        const uint32_t sets =
-            fm_pack4(t.a, S.acc.a, v, ba) | (fm_pack4(t.b, S.acc.b, v, bb) << 16);
-        narrow_store8(nr, d4, v, grp, B4, B8, l8, S.acc);
-        reinterpret_cast<uint32_t*>(fmleaf)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
+        leaf_finish8(S.inl, S.pl, v, S.acc, t, l8, grp, B4, B8, d4, fmleaf, nr);
         return;
     }
 #pragma unroll
