@@ -1131,7 +1131,13 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
                 const uint32_t p = g->pos_of[i];
                 for (uint32_t v = 0; v < n; ++v) {
                     const uint32_t c = g->order[v];
-                    const uint32_t f = (w[(size_t)p * row_words + c / per] >> (g->fmb * (c % per))) & all;
+                    // 4-bit rows are row-group interleaved (cpd_kernels.hip
+                    // fm4_piece): 16-B piece (p/4, segment c/32, p%4)
+                    const size_t wi =
+                        g->fmb == 4 ? ((((size_t)(p >> 2) * (g->npad / 32u) + c / 32u) * 4u +
+                                        (p & 3u)) * 4u + (c % 32u) / 8u)
+                                    : (size_t)p * row_words + c / per;
+                    const uint32_t f = (w[wi] >> (g->fmb * (c % per))) & all;
                     const bool wild = c == g->tgt_col[p] || h[(size_t)c * B + p] == CPD_INF;
                     fm[(size_t)i * n + v] = wild ? (uint16_t)CPD_FM_ALL : (uint16_t)f;
                 }

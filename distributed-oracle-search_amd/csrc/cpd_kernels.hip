@@ -48,6 +48,17 @@ struct FmFmt {
     static constexpr int kWords = (int)kSeg / kPer;     // words per 32-column segment (= FMB)
 };
 
+// 4-bit first-move rows are stored row-group interleaved: the 32-column
+// segment `seg` of rows 4g..4g+3 is one 64-B sector, row 4g + i's 16 B at
+// piece i.  The first-move kernels' lane owns exactly those 4 rows, so it
+// stores whole sectors (row-major 16-B pieces reached HBM as partial
+// sectors: 1.83x the algorithmic write bytes); the RLE scan's block runs the
+// 4 rows of a group in its 4 waves, which read the same sectors together.
+// fm4_piece = uint4 index of row `row`'s piece of segment `seg`.
+__device__ __forceinline__ size_t fm4_piece(uint32_t row, uint32_t nseg, uint32_t seg) {
+    return ((size_t)(row >> 2) * nseg + seg) * 4u + (row & 3u);
+}
+
 // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
 // one; MI355X_MICROARCH.md "Workgroup dispatch, XCD placement").  Remap so that
 // each XCD runs one contiguous range of logical blocks: neighbouring nodes and
@@ -1080,6 +1091,12 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
             pk[3][wi] = (pk[3][wi] & keep) | (f3 << sh);
         }
     }
+    if (FMB == 4) {  // row-group interleaved (fm4_piece): one 64-B sector
+        uint4* __restrict__ o = reinterpret_cast<uint4*>(fm) + fm4_piece(4u * l4, nseg, c0 / kSeg);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
+        return;
+    }
     const size_t row_words = npad / F::kPer;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1114,18 +1131,14 @@ struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR press
     uint32_t lv[G];
 };
 
-// S = 32-column segments per workgroup: with S = 2 a lane stores 32 contiguous
-// bytes of each of its 4 rows (two 16-B stores back to back) instead of 16,
-// so fewer partial-sector writes reach HBM (PMC writes 14.2 -> 10.1 GB per
-// 16384-row launch) — but the kernel is slower (16.0 -> 17.7 ms at 101 VGPRs,
-// 18.9 ms capped to 96 with spills): S = 1 is the default (CPD_FM_SEGS=2 to try).
-//
-// X = segments exchanged per workgroup (S = 1): the workgroup holds X wave
-// groups of TPS threads, group j computing segment j of X consecutive ones for
-// the same TPS x 4 targets; the groups swap their 16-B pieces through LDS so
-// that each lane stores 16 X contiguous bytes of a row (one row in X of the
-// lane's 4) — whole 64-B sectors at X = 4 instead of 16-B partial ones.
-template <int G, int S, int X = 1, bool OWN = false>
+// S = 32-column segments per workgroup (CPD_FM_SEGS, default 1; 2 was
+// slower in round 2 at 101 VGPRs).  The lane's 4 rows of a segment are one
+// 64-B sector of the row-group interleaved layout (fm4_piece): whole-sector
+// stores.  (Round 2 before that layout: 16-B row-major pieces, 1.83x the
+// algorithmic write bytes in PMC; an LDS exchange of X segments per
+// workgroup for 16X-B row pieces, CPD_FM_X, fixed the bytes but was slower,
+// and is gone with the layout.)
+template <int G, int S, bool OWN = false>
 __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ adj,
                                                       const uint32_t* __restrict__ dist,
                                                       const uint32_t* __restrict__ tgt, uint32_t B,
@@ -1135,18 +1148,13 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                                                       const uint16_t* __restrict__ fmleaf,
                                                       NarrowRows nr) {
     static_assert(kSeg % G == 0, "group size");
-    static_assert(X == 1 || S == 1, "exchange or wide segments, not both");
-    constexpr uint32_t TPS = 128;  // threads per segment group when X > 1
-    const uint32_t tps = X > 1 ? TPS : blockDim.x;
-    const uint32_t sgi = X > 1 ? threadIdx.x / TPS : 0u;   // this group's segment
-    const uint32_t tl = X > 1 ? threadIdx.x % TPS : threadIdx.x;
-    const uint32_t nblk = npad / (kSeg * S * X);
+    const uint32_t nseg = npad / kSeg;
+    const uint32_t nblk = nseg / S;
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t slab = L / nblk;
-    const uint32_t l4 = slab * tps + tl;  // slab = tps x 4 targets
+    const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t B4 = B / 4u;
-    const uint32_t cb0 = (L - slab * nblk) * (kSeg * S * X);
-    const uint32_t cb = cb0 + sgi * kSeg;
+    const uint32_t cb = (L - slab * nblk) * (kSeg * S);
     const uint32_t lane = threadIdx.x & 63u;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
@@ -1202,6 +1210,24 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                 f1 = (g.lv[j] >> 4) & 0xFu;
                 f2 = (g.lv[j] >> 8) & 0xFu;
                 f3 = g.lv[j] >> 12;
+            } else if (!OWN) {  // argmin set folded per neighbour (see leaf_finish8)
+                uint4 dn = make_uint4(INF, INF, INF, INF);
+                uint32_t bits = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint2 e = edge(cc, k);
+                    if (e.x == kNoEdge) continue;
+                    const uint4 dv = nl_finish(g.nb[j][k], d4, e.x, B4, l4);
+                    argmin_fold<0>(dn.x, bits, sat_add(dv.x, e.y), k);
+                    argmin_fold<1>(dn.y, bits, sat_add(dv.y, e.y), k);
+                    argmin_fold<2>(dn.z, bits, sat_add(dv.z, e.y), k);
+                    argmin_fold<3>(dn.w, bits, sat_add(dv.w, e.y), k);
+                }
+                bits = fm_wild4(tc, dn, c, bits);
+                f0 = bits & 0xFu;
+                f1 = (bits >> 4) & 0xFu;
+                f2 = (bits >> 8) & 0xFu;
+                f3 = bits >> 12;
             } else {
                 uint4 dv[4];
 #pragma unroll
@@ -1253,31 +1279,14 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
         finish(cur, cg);
         cur = nxt;
     }
-    const size_t row_words = npad / 8u;
-    if (X > 1) {
-        // xch[segment][row of 4][thread]: conflict-free 16-B LDS accesses
-        __shared__ uint4 xch[X > 1 ? X : 1][4][TPS];
+    // rows 4 l4 .. 4 l4 + 3 of segment cb/32 + sg: one 64-B sector each
+    uint4* __restrict__ o = reinterpret_cast<uint4*>(fm) + fm4_piece(4u * l4, nseg, cb / kSeg);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) xch[sgi][i][tl] = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
-        __syncthreads();
+    for (int sg = 0; sg < S; ++sg)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if ((uint32_t)i % X != sgi) continue;  // group j stores rows i == j (mod X)
-            uint4* __restrict__ o =
-                reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * row_words + cb0 / 8u);
-#pragma unroll
-            for (int sg = 0; sg < X; ++sg) o[sg] = xch[sg][i][tl];
-        }
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint4* __restrict__ o =
-            reinterpret_cast<uint4*>(fm + (size_t)(4u * l4 + (uint32_t)i) * row_words + cb / 8u);
-#pragma unroll
-        for (int sg = 0; sg < S; ++sg)
-            o[sg] = make_uint4(pk[i][4 * sg], pk[i][4 * sg + 1], pk[i][4 * sg + 2], pk[i][4 * sg + 3]);
-    }
+        for (int i = 0; i < 4; ++i)
+            o[4 * sg + i] = make_uint4(pk[i][4 * sg], pk[i][4 * sg + 1], pk[i][4 * sg + 2],
+                                       pk[i][4 * sg + 3]);
 }
 
 // One lane's greedy pass over its 32 columns (warthog graph_oracle::add_row
@@ -1342,13 +1351,17 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
     const uint32_t lane = threadIdx.x & 63u;
     if (row >= nrows) return;
     uint32_t* stage = stage_all + (EMIT ? (threadIdx.x >> 6) * kTile : 0);
+    const uint32_t nseg = npad / kSeg;
+    // this lane's 16-B pieces of the row: 4-bit rows are row-group interleaved
+    // (fm4_piece), wider ones row-major; tile t is `step` pieces further on
     const uint4* __restrict__ src =
-        reinterpret_cast<const uint4*>(fm + (size_t)row * (npad / F::kPer)) + lane * Q;
+        FMB == 4 ? reinterpret_cast<const uint4*>(fm) + fm4_piece(row, nseg, lane)
+                 : reinterpret_cast<const uint4*>(fm + (size_t)row * (npad / F::kPer)) + lane * Q;
+    const size_t step = FMB == 4 ? 64u * 4u : 64u * Q;
     uint32_t* __restrict__ out = EMIT ? runs + off[row] : nullptr;
     const bool keep = rs.st != nullptr;           // states kept (FMB == 4)
     const bool use_states = EMIT && keep;         // emit from the kept states
     const bool track_h = EMIT || keep;
-    const uint32_t nseg = npad / kSeg;
     uint32_t carry_h = 0, carry_S = F::kAll, total = 0;
     const uint32_t ntiles = npad / kTile;
     // tile t's segment of this lane (and its kept state), prefetched one tile ahead
@@ -1373,7 +1386,7 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
         const uint32_t cst = nst, crc = nrc;
         if (t + 1 < ntiles) {
 #pragma unroll
-            for (int q = 0; q < Q; ++q) nx[q] = src[(size_t)(t + 1) * (64u * Q) + q];
+            for (int q = 0; q < Q; ++q) nx[q] = src[(size_t)(t + 1) * step + q];
             if (use_states) {
                 nst = rs.st[sbase + (size_t)(t + 1) * 64u];
                 nrc = rs.rc[sbase + (size_t)(t + 1) * 64u];
@@ -2404,19 +2417,12 @@ uint32_t fm_segs() {  // CPD_FM_SEGS: 32-column segments per pipelined first-mov
     static const uint32_t v = env_u32("CPD_FM_SEGS", 1);
     return v;
 }
-uint32_t fm_x() {  // CPD_FM_X: segments exchanged per first-moves workgroup (1, 2, 4)
-    static const uint32_t v = [] {
-        const uint32_t x = env_u32("CPD_FM_X", 1);
-        return x >= 4 ? 4u : x >= 2 ? 2u : 1u;
-    }();
-    return v;
-}
-uint32_t fm_xg() {  // CPD_FM_XG: columns per gather group in the exchange kernel (1 or 2)
-    static const uint32_t v = env_u32("CPD_FM_XG", 1) >= 2 ? 2u : 1u;
-    return v;
-}
 uint32_t fm_g() {
     static const uint32_t v = env_u32("CPD_FM_G", 2);
+    return v;
+}
+uint32_t fm_n4g() {  // CPD_FM_N4G: columns per gather group of the pipelined first moves (1, 2)
+    static const uint32_t v = env_u32("CPD_FM_N4G", 2) == 1 ? 1u : 2u;
     return v;
 }
 uint32_t fm_own() {  // CPD_FM_OWN=1: the pipelined first moves also read the column's own row
@@ -2570,25 +2576,15 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     if (nr.d16 && shift == 2 && fm_n4()) {
         const uint32_t r = xcd_remap();
-        const uint32_t X = fm_x();
-        if (X > 1) {  // X groups of 128 threads, each 512 targets x one segment
-            const dim3 gx((npad / (kern::kSeg * X)) * ((rows + 1023u) / 1024u) * 2u), bx(128u * X);
-            // gather groups of 1 column keep the exchange kernel at 90 VGPRs (5
-            // waves/SIMD); 2 columns take it to 124 (4 waves)
-            if (X == 2 && fm_xg() == 2)
-                launch(kern::first_moves_n4<2, 1, 2>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
-            else if (X == 2)
-                launch(kern::first_moves_n4<1, 1, 2>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
-            else if (fm_xg() == 2)
-                launch(kern::first_moves_n4<2, 1, 4>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
-            else
-                launch(kern::first_moves_n4<1, 1, 4>, gx, bx, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
-        } else if (fm_segs() == 2)
+        if (fm_segs() == 2)
             launch(kern::first_moves_n4<2, 2>, dim3(grid.x / 2u), blk, s, adj, dist, tgt, B, n, npad,
                    r, fm, leafbits, fmleaf, nr);
         else if (fm_own())
-            launch(kern::first_moves_n4<2, 1, 1, true>, grid, blk, s, adj, dist, tgt, B, n, npad,
+            launch(kern::first_moves_n4<2, 1, true>, grid, blk, s, adj, dist, tgt, B, n, npad,
                    r, fm, leafbits, fmleaf, nr);
+        else if (fm_n4g() == 1)
+            launch(kern::first_moves_n4<1, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm,
+                   leafbits, fmleaf, nr);
         else
             launch(kern::first_moves_n4<2, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm,
                    leafbits, fmleaf, nr);
@@ -2602,7 +2598,7 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
 
 bool first_moves_reads_own(uint32_t shift, bool narrow) {
     if (!(narrow && shift == 2 && fm_n4())) return true;  // the generic kernel
-    return fm_own() && fm_x() == 1 && fm_segs() != 2;     // only the default form has OWN
+    return fm_own() && fm_segs() != 2;                      // only the default form has OWN
 }
 
 template <bool EMIT>
