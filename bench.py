@@ -177,6 +177,8 @@ def pmc_child(args):
     plan = cpd.Plan.load(plan_path(args))
     n = plan.info()["n"]
     dev = cpd.Graph(plan, device=0, batch=args.batch)
+    g = cpd.synth_road_graph(args.width, args.width, seed=args.seed, style=args.style)
+    dev.set_coords(g.x, g.y)  # lane order as in the timed run
     owned = rank_targets(args, n, 1, 0)
     targets = batch_of(owned, dev.batch, 0)
     rows = dev.build_rows(targets)
@@ -502,6 +504,9 @@ def main():
         f"{pinfo['levels_up']}+{pinfo['levels_dn']})")
 
     dev = cpd.Graph(plan, device=gpu, batch=args.batch)
+    # batch lanes along a Hilbert curve of the node coordinates (compact
+    # 256-target groups: narrow rows fit; identical rows either way)
+    dev.set_coords(g.x, g.y)
     # every rank builds the same number of rows per step (weak scaling): the
     # smallest batch any rank's free HBM allows
     (bmin,) = comm.reduce([float(dev.batch)], "MIN")

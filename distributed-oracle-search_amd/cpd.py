@@ -48,6 +48,7 @@ EXPORTED = [
     "cpd_index_set_mode", "cpd_index_get_mode", "cpd_plan_cache", "cpd_index_create_empty",
     "cpd_index_append_rows", "cpd_index_append_built_rows", "cpd_index_info",
     "cpd_synth_road_graph_ex", "cpd_query_search", "cpd_query_search_counters",
+    "cpd_graph_set_coords",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
@@ -356,6 +357,19 @@ class Graph:
     def set_batch(self, batch: int) -> None:
         """Rows per sweep (multiple of 1024; 0 = what fits in free HBM)."""
         _check(lib.cpd_graph_set_batch(self._h, C.c_uint32(batch)))
+
+    def set_coords(self, x, y) -> None:
+        """Node coordinates (node-id space; None clears them): a batch's
+        targets are laid out over the lanes along a Hilbert curve of them
+        (compact 256-target groups; identical results, fewer wide rows)."""
+        if x is None or y is None:
+            _check(lib.cpd_graph_set_coords(self._h, None, None))
+            return
+        xs = np.ascontiguousarray(x, dtype=np.int32)
+        ys = np.ascontiguousarray(y, dtype=np.int32)
+        if len(xs) != self.plan.info()["n"] or len(ys) != len(xs):
+            raise ValueError("coordinates must have one entry per node")
+        _check(lib.cpd_graph_set_coords(self._h, _ptr(xs, i32p), _ptr(ys, i32p)))
 
     def build_rows(self, targets, reuse: Rows | None = None) -> Rows:
         t = _u32(targets)

@@ -307,6 +307,9 @@ int main(int argc, char** argv) {
         cpd_graph* dg = nullptr;
         cli::check(cpd_graph_create(plan, device, &dg), "graph upload");
         cli::check(cpd_graph_set_batch(dg, (uint32_t)a.num("batch", 0)), "batch");
+        // the .xy coordinates order each batch's lanes (compact target groups)
+        if (g.x.size() == g.n && g.y.size() == g.n)
+            cli::check(cpd_graph_set_coords(dg, g.x.data(), g.y.data()), "coordinates");
         uint32_t B = 0;
         cli::check(cpd_graph_get_batch(dg, &B), "batch");
 

@@ -178,6 +178,13 @@ int  cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out);
 /* Batch width (rows built per sweep, multiple of 1024; 0 = auto from HBM). */
 int  cpd_graph_set_batch(cpd_graph* g, uint32_t batch);
 int  cpd_graph_get_batch(const cpd_graph* g, uint32_t* batch);
+/* Optional node coordinates (x[n], y[n], node-id space, e.g. the .xy file's
+ * `v id x y`; NULL clears them).  A batch's targets are then laid out over
+ * the lanes along a Hilbert curve of their coordinates instead of by column,
+ * so every 256-target lane group is spatially compact and its final
+ * distances fit the narrow rows' 16-bit offsets.  Results are identical
+ * either way; only the speed changes.                                      */
+int  cpd_graph_set_coords(cpd_graph* g, const int32_t* x, const int32_t* y);
 void cpd_graph_free(cpd_graph* g);
 
 /* ------------------------------------------------------------------------ */

@@ -31,14 +31,24 @@ def make_graph(plan, batch, narrow):
             os.environ["CPD_NARROW"] = old
 
 
-@pytest.fixture(scope="module", params=[(name, narrow) for name in sorted(GRAPHS)
-                                        for narrow in (True, False)],
-                ids=lambda p: f"{p[0]}-{'narrow' if p[1] else 'wide'}")
+# (narrow rows, lane order from coordinates): the Hilbert lane order of
+# cpd_graph_set_coords must give the same rows as the column order
+MODES = [(True, False), (False, False), (True, True)]
+
+
+@pytest.fixture(scope="module", params=[(name, narrow, xy) for name in sorted(GRAPHS)
+                                        for narrow, xy in MODES],
+                ids=lambda p: f"{p[0]}-{'narrow' if p[1] else 'wide'}{'-xy' if p[2] else ''}")
 def setup(request):
-    name, narrow = request.param
+    name, narrow, xy = request.param
     g = GRAPHS[name]()
     plan = cpd.Plan(g)
     dev = make_graph(plan, 1024, narrow)
+    if xy:  # the graph's coordinates, or seeded random ones for edge-list graphs
+        rng = np.random.default_rng(5)
+        x = g.x if g.x is not None else rng.integers(-1000, 1000, g.n, dtype=np.int32)
+        y = g.y if g.y is not None else rng.integers(-1000, 1000, g.n, dtype=np.int32)
+        dev.set_coords(x, y)
     return name, g, plan, dev
 
 

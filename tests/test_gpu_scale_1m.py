@@ -27,6 +27,7 @@ def w1m():
     g = cpd.synth_road_graph(1000, 1000, seed=1)
     plan = plan_for(g, "synth1000-s1")
     dev = cpd.Graph(plan, device=0, batch=16384)  # the bench's default batch at 1M nodes
+    dev.set_coords(g.x, g.y)  # Hilbert lane order, as the bench and make_cpd_auto run
     mine = owned(np.arange(g.n), 8, "div", 8, 0, g.n)
     yield g, plan, dev, mine
     del dev, plan
