@@ -58,8 +58,8 @@ WORKLOADS = {
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="synth1m", choices=sorted(WORKLOADS))
     ap.add_argument("--width", type=int, default=0, help="override the lattice side")
     ap.add_argument("--seed", type=int, default=0, help="override the graph seed")

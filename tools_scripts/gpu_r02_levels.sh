@@ -9,5 +9,5 @@ cd gpurun_out/lv
 timeout -k 10 300 rocprofv3 --kernel-trace -d tr --output-format csv -- python $R/bench.py --pmc-child --steps 1 --warmup 0 > tr.log 2>&1 || { tail tr.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d fe --output-format csv -- python $R/bench.py --pmc-child --steps 1 --warmup 0 > fe.log 2>&1 || { tail fe.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d wr --output-format csv -- python $R/bench.py --pmc-child --steps 1 --warmup 0 > wr.log 2>&1 || { tail wr.log; exit 1; }
-python $R/tools_scripts/level_pmc.py tr fe wr ../r02_down_levels_pmc.txt
+python $R/tools_scripts/level_pmc.py tr fe wr ../${1:-r02_down_levels_pmc.txt}
 rm -rf tr fe wr
