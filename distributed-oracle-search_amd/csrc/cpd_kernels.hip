@@ -1127,14 +1127,17 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
 template <int G>
 struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR pressure)
     NLoad own[G];
-    NLoad nb[G][4];
-    uint32_t lv[G];
+    NLoad nb[G][4];  // a leaf column's sets (fmleaf) ride in nb[j][0].q.x
 };
 
 // S = 32-column segments per workgroup (CPD_FM_SEGS, default 1; 2 was
 // slower in round 2 at 101 VGPRs).  The lane's 4 rows of a segment are one
-// 64-B sector of the row-group interleaved layout (fm4_piece): whole-sector
-// stores.  (Round 2 before that layout: 16-B row-major pieces, 1.83x the
+// 64-B sector of the row-group interleaved layout (fm4_piece), stored whole
+// by the lane.  With S = 1 each row's word goes to an LDS stage as soon as
+// its 8 columns are done (4 words live instead of 16: 8 waves per SIMD
+// instead of 6) and the sector is stored from there at the end — storing the
+// 4-B words straight to HBM measured 4x the write bytes (34 vs 8.8 GB per
+// launch: L2 does not merge them) and 24.4 vs 12.6 ms.  (Round 2 before that layout: 16-B row-major pieces, 1.83x the
 // algorithmic write bytes in PMC; an LDS exchange of X segments per
 // workgroup for 16X-B row pieces, CPD_FM_X, fixed the bytes but was slower,
 // and is gone with the layout.)
@@ -1159,6 +1162,10 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
     const uint32_t grp = wave_group(l4);
+    // S = 1: each row word is staged in LDS (64 B per lane, dynamic shared
+    // memory) as soon as its 8 columns are done, so only the current word of
+    // each row is live in registers
+    extern __shared__ uint32_t fm_stage[];
     uint32_t pk[4][4 * S];
 #pragma unroll
     for (int p = 0; p < 4 * S; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
@@ -1195,7 +1202,7 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                     if (e.x != kNoEdge) g.nb[j][k] = nl_issue(nr, e.x, grp, B4, l4);
                 }
             }
-            g.lv[j] = ok && leaf ? fmleaf[(size_t)c * B4 + l4] : 0u;
+            if (ok && leaf) g.nb[j][0].q.x = fmleaf[(size_t)c * B4 + l4];  // a leaf gathers nothing
         }
     };
     auto finish = [&](const FmGroup<G>& g, int cg) {
@@ -1206,10 +1213,11 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
             const int cc = cg + j;
             uint32_t f0, f1, f2, f3;
             if (is_leaf(cc)) {  // 4 nibbles, wildcards included
-                f0 = g.lv[j] & 0xFu;
-                f1 = (g.lv[j] >> 4) & 0xFu;
-                f2 = (g.lv[j] >> 8) & 0xFu;
-                f3 = g.lv[j] >> 12;
+                const uint32_t lv = g.nb[j][0].q.x;
+                f0 = lv & 0xFu;
+                f1 = (lv >> 4) & 0xFu;
+                f2 = (lv >> 8) & 0xFu;
+                f3 = lv >> 12;
             } else if (!OWN) {  // argmin set folded per neighbour (see leaf_finish8)
                 uint4 dn = make_uint4(INF, INF, INF, INF);
                 uint32_t bits = 0;
@@ -1271,13 +1279,26 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
         }
     };
     constexpr int NC = S * (int)kSeg;
+    static_assert(8 % G == 0, "a group never straddles a word");
     FmGroup<G> cur, nxt;
     issue(cur, 0);
 #pragma unroll
     for (int cg = 0; cg < NC; cg += G) {
         if (cg + G < NC) issue(nxt, cg + G);
         finish(cur, cg);
+        if (S == 1 && (cg + G) % 8 == 0) {  // the 4 rows' words of these 8 columns -> LDS
+            const int wi = (cg + G) / 8 - 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) fm_stage[(threadIdx.x * 4u + (uint32_t)i) * 4u + wi] = pk[i][wi];
+        }
         cur = nxt;
+    }
+    if (S == 1) {  // the lane's own staged sector: whole 64-B stores (no barrier: same lane)
+        uint4* __restrict__ o = reinterpret_cast<uint4*>(fm) + fm4_piece(4u * l4, nseg, cb / kSeg);
+        const uint4* st = reinterpret_cast<const uint4*>(fm_stage) + threadIdx.x * 4u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = st[i];
+        return;
     }
     // rows 4 l4 .. 4 l4 + 3 of segment cb/32 + sg: one 64-B sector each
     uint4* __restrict__ o = reinterpret_cast<uint4*>(fm) + fm4_piece(4u * l4, nseg, cb / kSeg);
@@ -2580,14 +2601,14 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
             launch(kern::first_moves_n4<2, 2>, dim3(grid.x / 2u), blk, s, adj, dist, tgt, B, n, npad,
                    r, fm, leafbits, fmleaf, nr);
         else if (fm_own())
-            launch(kern::first_moves_n4<2, 1, true>, grid, blk, s, adj, dist, tgt, B, n, npad,
-                   r, fm, leafbits, fmleaf, nr);
+            launch_shm(kern::first_moves_n4<2, 1, true>, grid, blk, 64u * tpb, s, adj, dist, tgt,
+                       B, n, npad, r, fm, leafbits, fmleaf, nr);
         else if (fm_n4g() == 1)
-            launch(kern::first_moves_n4<1, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm,
-                   leafbits, fmleaf, nr);
+            launch_shm(kern::first_moves_n4<1, 1>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n,
+                       npad, r, fm, leafbits, fmleaf, nr);
         else
-            launch(kern::first_moves_n4<2, 1>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm,
-                   leafbits, fmleaf, nr);
+            launch_shm(kern::first_moves_n4<2, 1>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n,
+                       npad, r, fm, leafbits, fmleaf, nr);
     } else if (nr.d16)
         launch_first_moves_t<true>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
                                    grid, blk, s);
