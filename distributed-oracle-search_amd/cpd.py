@@ -41,7 +41,7 @@ EXPORTED = [
     "cpd_plan_save", "cpd_plan_load", "cpd_plan_free", "cpd_device_count",
     "cpd_graph_create", "cpd_graph_set_batch", "cpd_graph_get_batch", "cpd_graph_free",
     "cpd_build_rows", "cpd_rows_count", "cpd_rows_export", "cpd_rows_export_range",
-    "cpd_rows_targets", "cpd_rows_free",
+    "cpd_rows_targets", "cpd_rows_wait", "cpd_rows_free",
     "cpd_debug_rows", "cpd_index_create", "cpd_index_from_rows", "cpd_index_set_weights",
     "cpd_query_batch", "cpd_query_prepare", "cpd_query_run", "cpd_query_fetch",
     "cpd_index_free", "cpd_timing_enable", "cpd_timing_reset", "cpd_timing_get",
@@ -303,6 +303,10 @@ def device_count() -> int:
 class Rows:
     def __init__(self, h):
         self._h = h
+
+    def wait(self) -> None:
+        """Finish the (possibly deferred) device work behind these rows."""
+        _check(lib.cpd_rows_wait(self._h))
 
     def count(self):
         nr, tot = C.c_uint32(), C.c_uint64()

@@ -1495,6 +1495,182 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
     }
 }
 
+// ---------------------------------------------------------------------------
+// RLE count, chunked (4-bit sets; CPD_RLE_CH, default on).  rle_scan<false>
+// gives each lane one 32-column segment of a 2048-column tile and guesses
+// the state entering it (16 look-back columns), then rescans every segment
+// whose guess was wrong — and a wave pays a whole rescan whenever any of
+// its 64 lanes needs one — about 80 column steps per 32 useful ones.  Here a
+// lane owns a chunk of CH consecutive segments of one row and scans them in
+// order, so only the chunk's entry is guessed (16 look-back columns per
+// CH x 32), and the guesses are checked afterwards by rle_fix, one wave per
+// row, which rescans the rare chunk whose guess differs from its
+// predecessor's exit.  A wave = 4 rows (one row group of the interleaved fm
+// layout: its 4 lanes of a chunk read one 64-B sector) x 16 chunks.
+// Per segment the lane keeps the entry state (RleState st, stored 8
+// segments = 32 B at a time) and the run count (rc, CH bytes stored at the
+// chunk's end), per chunk its exit state and run count (xs / cc).
+struct RleChunks {
+    uint32_t* xs;  // [nrows][nch] exit state (h << 4 | S) of the chunk
+    uint32_t* cc;  // [nrows][nch] runs ending inside the chunk
+};
+
+// the greedy scan over one 32-column segment (word v[c / 8], nibble c % 8)
+// from (h, S); returns the runs that end inside it, updates (h, S)
+__device__ __forceinline__ uint32_t seg_count4(const uint4& q, uint32_t c0, uint32_t& h,
+                                               uint32_t& S) {
+    const uint32_t v[4] = {q.x, q.y, q.z, q.w};
+    uint32_t brk = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        uint32_t word = v[w];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t f = word & 0xFu;
+            word >>= 4;
+            const uint32_t T = S & f;
+            brk |= (T == 0u ? 1u : 0u) << (8 * w + j);
+            S = T == 0u ? f : T;
+        }
+    }
+    if (brk) h = c0 + 31u - (uint32_t)__builtin_clz(brk);
+    return (uint32_t)__builtin_popcount(brk);
+}
+
+template <int CH>
+__global__ __launch_bounds__(256) void rle_count_ch(const uint32_t* __restrict__ fm,
+                                                    uint32_t npad, uint32_t nrows,
+                                                    uint32_t* __restrict__ st,
+                                                    uint8_t* __restrict__ rc, RleChunks rk) {
+    static_assert(CH % 32 == 0, "whole 32-B count stores");
+    const uint32_t nseg = npad / kSeg, nch = nseg / CH;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t rg = blockIdx.y * 4u + (threadIdx.x >> 6);  // row group of this wave
+    const uint32_t row = rg * 4u + (lane & 3u);
+    const uint32_t ch = blockIdx.x * 16u + (lane >> 2);
+    if (row >= nrows || ch >= nch) return;
+    const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
+    const uint32_t s0 = ch * CH;
+    uint32_t h = 0, S = 0xFu;  // entering column 0: head 0, wildcard set
+    if (ch > 0) {  // the guess: the previous segment's last 16 columns from a fresh run
+        const uint4 q = f4[fm4_piece(row, nseg, s0 - 1u)];
+        const uint32_t v[2] = {q.z, q.w};
+        const uint32_t c0 = s0 * kSeg - 16u;
+        h = c0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t f = (v[k / 8] >> (4 * (k % 8))) & 0xFu;
+            const uint32_t T = S & f;
+            h = T == 0u ? c0 + (uint32_t)k : h;
+            S = T == 0u ? f : T;
+        }
+    }
+    uint32_t* __restrict__ stp = st + (size_t)row * nseg + s0;
+    uint32_t total = 0;
+    uint4 nq = f4[fm4_piece(row, nseg, s0)];
+    uint2 r0 = {}, r1 = {}, r2 = {};  // counts of segments 0-7, 8-15, 16-23 of 32
+#pragma unroll 1
+    for (uint32_t s = 0; s < (uint32_t)CH; s += 8u) {  // 8 segments: 32 B of states
+        uint32_t sw[8];
+        uint2 r8 = {0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t seg = s0 + s + (uint32_t)i;
+            const uint4 q = nq;
+            if (s + (uint32_t)i + 1u < (uint32_t)CH) nq = f4[fm4_piece(row, nseg, seg + 1u)];
+            sw[i] = (h << 4) | S;
+            const uint32_t k = seg_count4(q, seg * kSeg, h, S);
+            total += k;
+            if (i < 4) r8.x |= k << (8 * i);
+            else r8.y |= k << (8 * (i - 4));
+        }
+        uint4* o = reinterpret_cast<uint4*>(stp + s);
+        o[0] = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+        o[1] = make_uint4(sw[4], sw[5], sw[6], sw[7]);
+        switch ((s / 8u) & 3u) {  // the counts go out 32 segments (32 B) at a time
+            case 0: r0 = r8; break;
+            case 1: r1 = r8; break;
+            case 2: r2 = r8; break;
+            default: {
+                uint4* orc = reinterpret_cast<uint4*>(rc + (size_t)row * nseg + s0 + s - 24u);
+                orc[0] = make_uint4(r0.x, r0.y, r1.x, r1.y);
+                orc[1] = make_uint4(r2.x, r2.y, r8.x, r8.y);
+            }
+        }
+    }
+    rk.xs[(size_t)row * nch + ch] = (h << 4) | S;
+    rk.cc[(size_t)row * nch + ch] = total;
+}
+
+// Chunk seams of rle_count_ch, one wave per row: lane j holds chunk b + j's
+// guessed entry state (its first segment's stored state), exit state and run
+// count.  A chunk whose entry differs from its predecessor's exit is rescanned
+// from the true state by its lane, segment by segment, rewriting the segment
+// states and counts, until the state meets the stored one (from there on the
+// stored states are the true ones); a chunk rescanned to its end passes a new
+// exit state on.  The lowest such chunk is fixed first, so every fix starts
+// from a true state.  counts[row] = the row's runs (+ the final one).
+template <int CH>
+__global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, uint32_t npad,
+                                              uint32_t nrows, uint32_t* __restrict__ st,
+                                              uint8_t* __restrict__ rc, RleChunks rk,
+                                              uint32_t* __restrict__ counts) {
+    const uint32_t row = blockIdx.x;
+    if (row >= nrows) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nseg = npad / kSeg, nch = nseg / CH;
+    uint32_t* __restrict__ str = st + (size_t)row * nseg;
+    uint8_t* __restrict__ rcr = rc + (size_t)row * nseg;
+    uint32_t* __restrict__ xs = rk.xs + (size_t)row * nch;
+    const uint32_t* __restrict__ cc = rk.cc + (size_t)row * nch;
+    const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
+    uint32_t carry = 0xFu;  // entering column 0: head 0, wildcard set
+    uint32_t total = 0;
+    for (uint32_t b = 0; b < nch; b += 64u) {
+        const uint32_t c = b + lane;
+        const bool valid = c < nch;
+        uint32_t in = valid ? str[(size_t)c * CH] : 0u;
+        uint32_t ex = valid ? xs[c] : 0u;
+        uint32_t cnt = valid ? cc[c] : 0u;
+        for (;;) {
+            uint32_t pred = __shfl_up(ex, 1, 64);
+            if (lane == 0) pred = carry;
+            const uint64_t m = __ballot(valid && pred != in);
+            if (!m) break;
+            const uint32_t j = (uint32_t)__builtin_ctzll(m);
+            if (lane == j) {
+                uint32_t state = pred;
+                int delta = 0;
+                bool met = false;
+                for (uint32_t s = c * CH; s < (c + 1u) * CH; ++s) {
+                    if (state == str[s]) {
+                        met = true;
+                        break;
+                    }
+                    str[s] = state;
+                    uint32_t hh = state >> 4, SS = state & 0xFu;
+                    const uint32_t k = seg_count4(f4[fm4_piece(row, nseg, s)], s * kSeg, hh, SS);
+                    delta += (int)k - (int)rcr[s];
+                    rcr[s] = (uint8_t)k;
+                    state = (hh << 4) | SS;
+                }
+                in = pred;
+                cnt = (uint32_t)((int)cnt + delta);
+                if (!met) {
+                    ex = state;
+                    xs[c] = state;
+                }
+            }
+        }
+        uint32_t sum = cnt;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        total += sum;
+        carry = __shfl(ex, 63, 64);
+    }
+    if (lane == 0) counts[row] = total + 1u;  // + the final run
+}
+
 // Table-search extraction, one lane per query.  cur/t are columns; the run for
 // column cur is found by galloping from the previous hop's run (consecutive
 // path nodes have nearby DFS columns), then binary search inside the bracket:
@@ -2638,6 +2814,38 @@ static void launch_rle(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t
 void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
                       uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s) {
     launch_rle<false>(fm, fmb, npad, nrows, counts, nullptr, nullptr, st, rc, s);
+}
+
+uint32_t rle_ch() {  // CPD_RLE_CH: segments per chunk of the chunked count (32, 64); 0 = rle_scan
+    static const uint32_t v = [] {
+        const uint32_t c = env_u32("CPD_RLE_CH", 32);
+        return c == 0 ? 0u : c >= 64 ? 64u : 32u;
+    }();
+    return v;
+}
+
+uint32_t rle_count_chunks(uint32_t npad) { return rle_ch() ? npad / kern::kSeg / rle_ch() : 0u; }
+
+void launch_rle_count_ch(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
+                         uint8_t* rc, uint32_t* xs, uint32_t* cc, hipStream_t s) {
+    if (!nrows) return;
+    const uint32_t nch = rle_count_chunks(npad);
+    const kern::RleChunks rk{xs, cc};
+    const dim3 grid((nch + 15u) / 16u, (nrows + 15u) / 16u), blk(256);
+    if (rle_ch() == 64)
+        launch(kern::rle_count_ch<64>, grid, blk, s, fm, npad, nrows, st, rc, rk);
+    else
+        launch(kern::rle_count_ch<32>, grid, blk, s, fm, npad, nrows, st, rc, rk);
+}
+
+void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
+                    uint8_t* rc, uint32_t* xs, uint32_t* cc, uint32_t* counts, hipStream_t s) {
+    if (!nrows) return;
+    const kern::RleChunks rk{xs, cc};
+    if (rle_ch() == 64)
+        launch(kern::rle_fix<64>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts);
+    else
+        launch(kern::rle_fix<32>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts);
 }
 
 void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,

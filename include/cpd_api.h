@@ -210,6 +210,11 @@ int  cpd_rows_export(const cpd_rows* r, uint64_t* offsets /* nrows+1 */,
 int  cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count,
                            uint64_t* offsets /* count+1 */, uint32_t* runs);
 int  cpd_rows_targets(const cpd_rows* r, uint32_t* targets /* nrows */);
+/* Wait for the device work behind r: a build returns once its rows' run
+ * counts are known, while the last batch's run emit may still be running
+ * (it overlaps the next build's sweeps); every accessor above waits for it,
+ * this call only waits.  The bench calls it inside its timed region. */
+int  cpd_rows_wait(const cpd_rows* r);
 void cpd_rows_free(cpd_rows* r);
 
 /* [gpu] Inspection (tests): distances d(n,t) in NODE order, n-major
