@@ -134,7 +134,8 @@ struct cpd_graph {
     DevBuf<uint64_t> row_offx[2];
     // chunk exit states / run counts of the chunked count (read by rle_fix on
     // the same stream before the next batch: one set)
-    DevBuf<uint32_t> rle_xs, rle_cc;
+    DevBuf<uint32_t> rle_xs, rle_cc, rle_hard;
+    uint32_t rle_hard_h = 0;
     std::vector<uint64_t> lane_off_h[2];  // host source of row_offx[x] (kept alive)
     // the buffer set the next batch uses, once the emit that last read it is done
     uint32_t acquire_set() {
@@ -348,6 +349,7 @@ struct cpd_graph {
         if (fmb == 4 && rle_count_chunks(npad)) {
             rle_xs.alloc((size_t)B * rle_count_chunks(npad));
             rle_cc.alloc((size_t)B * rle_count_chunks(npad));
+            rle_hard.alloc(1);
         }
         live.alloc(n);
         tmask.alloc(n);
@@ -992,13 +994,23 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     const double t1 = now_seconds();
     const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
     if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
+        HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), g->stream));
         g->timed("rle_count", (fm_row + st_row + 8.0 * nch) * k, [&] {
             launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->stream);
         });
         g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
             launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
-                           g->stream);
+                           g->rle_hard.p, g->stream);
         });
+        HIP_CHECK(hipMemcpyAsync(&g->rle_hard_h, g->rle_hard.p, sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, g->stream));
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        if (g->rle_hard_h) {  // runs too long for the seam repair: the bounded pass
+            g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
+                launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);
+            });
+            if (trace_on()) std::fprintf(stderr, "[cpd] batch re-counted by rle_scan\n");
+        }
     } else {
         g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
             launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);

@@ -1610,11 +1610,18 @@ __global__ __launch_bounds__(256) void rle_count_ch(const uint32_t* __restrict__
 // stored states are the true ones); a chunk rescanned to its end passes a new
 // exit state on.  The lowest such chunk is fixed first, so every fix starts
 // from a true state.  counts[row] = the row's runs (+ the final one).
+// A row whose rescans pass kFixBudget segments (runs far longer than the
+// look-back — never on road graphs, where a run averages 1.6 columns, but a
+// chain graph has a handful of runs per row) is given up: *hard = 1, and the
+// host re-counts the batch with rle_scan<false>, which bounds that case.
+constexpr uint32_t kFixBudget = 256;  // segments rescanned per row
+
 template <int CH>
 __global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, uint32_t npad,
                                               uint32_t nrows, uint32_t* __restrict__ st,
                                               uint8_t* __restrict__ rc, RleChunks rk,
-                                              uint32_t* __restrict__ counts) {
+                                              uint32_t* __restrict__ counts,
+                                              uint32_t* __restrict__ hard) {
     const uint32_t row = blockIdx.x;
     if (row >= nrows) return;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1625,7 +1632,7 @@ __global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, u
     const uint32_t* __restrict__ cc = rk.cc + (size_t)row * nch;
     const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
     uint32_t carry = 0xFu;  // entering column 0: head 0, wildcard set
-    uint32_t total = 0;
+    uint32_t total = 0, spent = 0;
     for (uint32_t b = 0; b < nch; b += 64u) {
         const uint32_t c = b + lane;
         const bool valid = c < nch;
@@ -1638,6 +1645,7 @@ __global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, u
             const uint64_t m = __ballot(valid && pred != in);
             if (!m) break;
             const uint32_t j = (uint32_t)__builtin_ctzll(m);
+            uint32_t nres = 0;
             if (lane == j) {
                 uint32_t state = pred;
                 int delta = 0;
@@ -1647,6 +1655,7 @@ __global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, u
                         met = true;
                         break;
                     }
+                    ++nres;
                     str[s] = state;
                     uint32_t hh = state >> 4, SS = state & 0xFu;
                     const uint32_t k = seg_count4(f4[fm4_piece(row, nseg, s)], s * kSeg, hh, SS);
@@ -1660,6 +1669,11 @@ __global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, u
                     ex = state;
                     xs[c] = state;
                 }
+            }
+            spent += __shfl(nres, (int)j, 64);  // wave-uniform
+            if (spent > kFixBudget) {
+                if (lane == 0) *hard = 1u;
+                return;
             }
         }
         uint32_t sum = cnt;
@@ -2839,13 +2853,16 @@ void launch_rle_count_ch(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint
 }
 
 void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
-                    uint8_t* rc, uint32_t* xs, uint32_t* cc, uint32_t* counts, hipStream_t s) {
+                    uint8_t* rc, uint32_t* xs, uint32_t* cc, uint32_t* counts, uint32_t* hard,
+                    hipStream_t s) {
     if (!nrows) return;
     const kern::RleChunks rk{xs, cc};
     if (rle_ch() == 64)
-        launch(kern::rle_fix<64>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts);
+        launch(kern::rle_fix<64>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts,
+               hard);
     else
-        launch(kern::rle_fix<32>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts);
+        launch(kern::rle_fix<32>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts,
+               hard);
 }
 
 void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,

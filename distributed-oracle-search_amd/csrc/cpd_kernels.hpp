@@ -121,13 +121,16 @@ void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t n
 // Chunked RLE count (4-bit sets; cpd_kernels.hip rle_count_ch): the same st /
 // rc as launch_rle_count, with each chunk of segments scanned by one lane
 // from a guessed entry state; launch_rle_fix then repairs the chunk seams and
-// writes counts[row].  xs / cc: nrows x rle_count_chunks(npad) u32 each.
+// writes counts[row], or sets *hard (zeroed by the caller) when a row's runs
+// are too long for that to be cheap: the caller then runs launch_rle_count
+// on the batch instead.  xs / cc: nrows x rle_count_chunks(npad) u32 each.
 // rle_count_chunks = 0: off (CPD_RLE_CH=0), use launch_rle_count.
 uint32_t rle_count_chunks(uint32_t npad);
 void launch_rle_count_ch(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
                          uint8_t* rc, uint32_t* xs, uint32_t* cc, hipStream_t s);
 void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
-                    uint8_t* rc, uint32_t* xs, uint32_t* cc, uint32_t* counts, hipStream_t s);
+                    uint8_t* rc, uint32_t* xs, uint32_t* cc, uint32_t* counts, uint32_t* hard,
+                    hipStream_t s);
 
 // *bad |= 1 if some row [0, nrows) of (offsets, runs) does not start at column
 // 0, has non-increasing run columns, a column >= n, or is empty.  Rows from

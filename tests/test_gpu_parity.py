@@ -12,7 +12,7 @@ import pytest
 
 import cpd
 import oracle
-from graphs import GRAPHS
+from graphs import GRAPHS, graph_from_edges
 
 pytestmark = pytest.mark.gpu
 
@@ -228,3 +228,36 @@ def test_narrow_rows_switched_off_when_mostly_wide(scale, narrow_kept):
         np.testing.assert_array_equal(runs, ref_runs)
         if rep == 1:
             assert ("group_rows" in dev.timing_get()) == narrow_kept
+
+
+def chain_graph(n, seed):
+    """A bidirectional path 0-1-...-(n-1), weights 1..3: every row has a
+    handful of runs, each spanning thousands of columns — far past the
+    chunked RLE count's 16-column look-back guess."""
+    rng = np.random.default_rng(seed)
+    edges = []
+    for v in range(n):
+        if v > 0:
+            edges.append((v, v - 1, int(rng.integers(1, 4))))
+        if v + 1 < n:
+            edges.append((v, v + 1, int(rng.integers(1, 4))))
+    return graph_from_edges(n, edges)
+
+
+@pytest.mark.parametrize("n", [5000, 20000])
+def test_long_runs_chunk_seams(n):
+    """Rows whose runs span whole chunks of the chunked RLE count: at 5000
+    nodes rle_fix rescans long stretches of each row; at 20000 a row passes
+    its rescan budget and the batch is re-counted by rle_scan<false> — the
+    rows are bit-exact against the oracle either way."""
+    g = chain_graph(n, seed=n)
+    plan = cpd.Plan(g)
+    dev = cpd.Graph(plan, batch=1024)
+    rng = np.random.default_rng(3)
+    targets = rng.choice(g.n, size=300, replace=False).astype(np.uint32)
+    rows = dev.build_rows(targets)
+    off, runs = rows.export()
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    np.testing.assert_array_equal(off, ref_off)
+    np.testing.assert_array_equal(runs, ref_runs)
+    assert int(off[-1]) < 8 * len(targets)  # a handful of runs per row
