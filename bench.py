@@ -103,7 +103,7 @@ def plan_path(args):
 KERNEL_NAMES = {"sweep_level<true": "sweep_up", "sweep_up_": "sweep_up",
                 "sweep_level<false": "sweep_down", "sweep_down8": "sweep_down",
                 "first_moves": "first_moves", "rle_scan<false": "rle_count",
-                "rle_scan<true": "rle_emit", "DenseRows": "table_search_dense",
+                "rle_scan<true": "rle_emit", "rle_count_ch": "rle_count", "rle_fix": "rle_fix", "DenseRows": "table_search_dense",
                 "RleRows": "table_search", "table_search_dense": "table_search_dense",
                 "table_search(": "table_search", "expand_rows": "expand_rows"}
 
