@@ -66,7 +66,7 @@ def parse(argv=None):
     ap.add_argument("--partmethod", default="")
     ap.add_argument("--partkey", type=int, default=0)
     ap.add_argument("--batch", type=int, default=0,
-                    help="rows per step (multiple of 1024); 0 = what fits in HBM, <= 16384")
+                    help="rows per step (multiple of 1024); 0 = what fits in HBM, <= 24576")
     ap.add_argument("--queries", type=int, default=0, help="0 = the workload's")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every host thread this job may use (OMP_NUM_THREADS or affinity)")
@@ -591,6 +591,7 @@ def main():
     ix.set_weights(w_cong)
     q_cong, q_cong_ms = time_queries("auto")
     ix.set_weights(None)
+    del ix, rows  # HBM for the search tables (the batch's runs + index: ~120 GB at 20k rows)
     # CPD-heuristic search leg: 256 rows of the index, the
     # .diff stand-in weights, hscale 1 / fscale 0.1 (10%-bounded: at fscale 0
     # a 1M-node search inserts up to ~235k nodes, a lane-serial search's

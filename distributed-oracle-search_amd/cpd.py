@@ -349,7 +349,7 @@ class Graph:
         self._h = C.c_void_p()
         self.plan = plan
         _check(lib.cpd_graph_create(plan._h, C.c_int(device), C.byref(self._h)))
-        # 0 = the largest batch that fits in free HBM (<= 16384)
+        # 0 = the largest batch that fits in free HBM (<= 24576)
         _check(lib.cpd_graph_set_batch(self._h, C.c_uint32(batch)))
 
     @property
