@@ -1380,7 +1380,9 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
                  : reinterpret_cast<const uint4*>(fm + (size_t)row * (npad / F::kPer)) + lane * Q;
     const size_t step = FMB == 4 ? 64u * 4u : 64u * Q;
     uint32_t* __restrict__ out = EMIT ? runs + off[row] : nullptr;
-    const bool keep = rs.st != nullptr;           // states kept (FMB == 4)
+    // states kept: always for FMB == 4 (the host passes them), which makes
+    // the emit's speculation code dead and frees its registers
+    const bool keep = FMB == 4 || rs.st != nullptr;
     const bool use_states = EMIT && keep;         // emit from the kept states
     const bool track_h = EMIT || keep;
     uint32_t carry_h = 0, carry_S = F::kAll, total = 0;
@@ -1478,6 +1480,7 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1  // unrolled, this copy held 145 VGPRs (3 waves per SIMD; now 50)
             for (uint32_t i = lane; i < tile_total; i += 64u) out[total + i] = stage[i];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
