@@ -1511,8 +1511,8 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
 // predecessor's exit.  A wave = 4 rows (one row group of the interleaved fm
 // layout: its 4 lanes of a chunk read one 64-B sector) x 16 chunks.
 // Per segment the lane keeps the entry state (RleState st, stored 8
-// segments = 32 B at a time) and the run count (rc, CH bytes stored at the
-// chunk's end), per chunk its exit state and run count (xs / cc).
+// segments = 32 B at a time) and the run count (rc, stored 32 segments =
+// 32 B at a time), per chunk its exit state and run count (xs / cc).
 struct RleChunks {
     uint32_t* xs;  // [nrows][nch] exit state (h << 4 | S) of the chunk
     uint32_t* cc;  // [nrows][nch] runs ending inside the chunk
