@@ -15,3 +15,10 @@ for w in melb300k synth4m synth1m-spec; do
       || { echo "bench $w failed"; tail -20 gpurun_out/${TAG}_bench_$w.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/${TAG}_bench_$w.json'));print('$w', d['value'], d['config']['rows_per_step_per_gpu'], d['roofline']['frac'], d['queries_per_s'], d['parity_sample_bit_exact'])"
 done
+if [ "$2" = "prof" ]; then
+  R=$PWD; cd /tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$TAG --output-format csv \
+      -- python3 $R/bench.py --no-pmc --no-cpu > $R/gpurun_out/prof_${TAG}_bench.json 2> $R/gpurun_out/prof_${TAG}_bench.err \
+      || { echo "rocprof failed"; tail -20 $R/gpurun_out/prof_${TAG}_bench.err; exit 1; }
+  echo prof-done
+fi
