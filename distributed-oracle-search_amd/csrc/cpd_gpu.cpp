@@ -949,7 +949,7 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k) {
                     "target " + std::to_string(targets[i]) + " out of range");
         idx[i] = i;
     }
-    if (sort_on()) {
+    if (sort_on() && k > 0) {
         // lanes by (Hilbert key, column), or by column without coordinates:
         // compact 2-D groups — a 256-lane group spans a small square, so its
         // final distances fit the narrow rows' 16-bit offsets (column order:
