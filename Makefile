@@ -30,7 +30,15 @@ TOOLS     := make_cpd_auto fifo_auto gen_distribute_conf gen_synth
 BINS      := $(addprefix bin/,$(TOOLS))
 HDRS      := include/cpd_api.h $(SRC)/cpd_internal.hpp $(SRC)/cpd_kernels.hpp $(SRC)/cpd_io.hpp
 
-.PHONY: all lib bins oracle clean
+# Build provenance: sha256 over the library's and tools' sources (sorted by
+# path, contents concatenated — cpd.src_sha() recomputes it from the shipped
+# tree), embedded in cpd_version() so a run can prove which sources its
+# libcpd.so was built from.
+PROV_SRCS := $(sort $(wildcard include/*.h $(SRC)/*.cpp $(SRC)/*.hpp $(SRC)/*.hip \
+                               $(PKG)/tools/*.cpp $(PKG)/tools/*.hpp))
+SRC_SHA    = $(shell cat $(PROV_SRCS) | sha256sum | cut -c1-16)
+
+.PHONY: all lib bins oracle clean FORCE
 all: lib bins oracle
 lib: $(LIB)
 bins: $(BINS)
@@ -41,6 +49,15 @@ $(BLD):
 
 $(BLD)/%.o: $(SRC)/%.cpp $(HDRS) | $(BLD)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+# rewritten only when the hash changes, so an unchanged tree rebuilds nothing
+$(BLD)/src_sha.h: FORCE | $(BLD)
+	@echo '#define CPD_SRC_SHA "$(SRC_SHA)"' > $@.tmp; \
+	 if cmp -s $@.tmp $@; then rm -f $@.tmp; else mv $@.tmp $@; fi
+
+$(BLD)/host_util.o: $(SRC)/host_util.cpp $(HDRS) $(BLD)/src_sha.h | $(BLD)
+	$(CXX) $(CXXFLAGS) -I$(BLD) -c $< -o $@
+
 
 $(BLD)/cpd_kernels.o: $(SRC)/cpd_kernels.hip $(SRC)/cpd_kernels.hpp | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

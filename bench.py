@@ -76,6 +76,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-partitioned", action="store_true",
                     help="skip the configs[0] mod-3 partitioned CPU run")
     ap.add_argument("--no-search", action="store_true", help="skip the cpd-search leg")
+    ap.add_argument("--no-full-build", action="store_true",
+                    help="skip the end-to-end worker build (make_cpd_auto --discard, cold plan)")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
@@ -440,6 +442,50 @@ def cpu_partitioned(threads, rows_per_worker=384, queries=20000):
 
 
 # --------------------------------------------------------------------------
+# end-to-end worker build: bin/make_cpd_auto as the
+# driver runs it (make_cpds.py:20), on a cold plan cache, every row the rank
+# owns built and copied out of HBM (--discard: the D2H export without the
+# file writes — a div-8 worker's ~312 GB of runs outgrow the box's disk)
+
+def full_build_xy(args):
+    """The workload's graph as a .xy file (bin/gen_synth, same generator and
+    seed), written once per cache."""
+    prefix = glob_xy(args)[:-3]
+    if not os.path.exists(prefix + ".xy"):
+        subprocess.run([os.path.join(ROOT, "bin", "gen_synth"), "--width", str(args.width),
+                        "--seed", str(args.seed), "--style", args.style, "--out", prefix],
+                       check=True, stdout=subprocess.DEVNULL, timeout=300)
+    return prefix + ".xy"
+
+
+def full_build(args, xy, world, rank, device):
+    """Run make_cpd_auto for worker `rank` of `world` with a fresh (cold) plan
+    cache shared by the node's ranks; returns its JSON phase line."""
+    import shutil
+    outdir = os.path.join(args.cache, f"fb-out-{world}")
+    if rank == 0:
+        shutil.rmtree(outdir, ignore_errors=True)
+        os.makedirs(outdir)
+    else:
+        while not os.path.isdir(outdir):
+            time.sleep(0.1)
+    cmd = [os.path.join(ROOT, "bin", "make_cpd_auto"), "--input", xy, "--partmethod",
+           args.partmethod, "--partkey", str(args.partkey), "--workerid", str(rank),
+           "--maxworker", str(world), "--outdir", outdir, "--device", str(device), "--discard"]
+    if args.batch:
+        cmd += ["--batch", str(args.batch)]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=900)
+    if p.returncode:
+        raise RuntimeError(f"make_cpd_auto failed: {p.stderr[-400:]}")
+    line = next(l for l in p.stdout.splitlines() if l.startswith("make_cpd_auto-json: "))
+    return json.loads(line.split(": ", 1)[1])
+
+
+def glob_xy(args):
+    style = "" if args.style == "shuffled" else f"-{args.style}"
+    return os.path.join(args.cache, f"fb-synth{args.width}-s{args.seed}{style}.xy")
+
 
 def main():
     args = parse()
@@ -475,6 +521,9 @@ def main():
     if local == 0 and not os.path.exists(ppath):
         log(f"building hierarchy for {g.n} nodes / {g.m} edges ...")
         cpd.Plan(g).save(ppath)
+    fb_xy = None
+    if not args.no_full_build and args.sample is None and local == 0:
+        fb_xy = full_build_xy(args)
     # PMC passes: children, before this process initialises the GPU
     traffic = None
     if world == 1 and not args.no_pmc:
@@ -693,9 +742,36 @@ def main():
             except Exception as e:  # reported, never fatal to the GPU numbers
                 cpu["partitioned_configs0"] = {"error": str(e)[-300:]}
 
+    # ---- end-to-end worker build: frees this process's HBM first ------------
+    fb = None
+    if not args.no_full_build and args.sample is None:
+        import gc
+        search_sample = six = None  # noqa: F841
+        del dev
+        gc.collect()
+        comm.barrier()
+        fb_xy = fb_xy or glob_xy(args)  # local rank 0 wrote it before the first barrier
+        rec = full_build(args, fb_xy, world, rank, gpu)
+        (tmax,) = comm.reduce([rec["total_s"]], "MAX")
+        tot = comm.reduce([float(rec["rows"]), float(rec["runs"]), float(rec["export_bytes"])],
+                          "SUM")
+        fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of {args.partmethod} "
+                      f"{args.partkey}, all owned rows, cold plan cache, --discard (D2H export "
+                      "into pinned host buffers, no file writes)",
+              "total_s": round(tmax, 3), "rows": int(tot[0]), "runs": int(tot[1]),
+              "rows_per_s_end_to_end": round(tot[0] / tmax, 1) if tmax else 0.0,
+              "export_GB": round(tot[2] / 1e9, 2),
+              "rank0": rec,
+              "rank0_export_GBps": round(rec["export_bytes"] / rec["export_span_s"] / 1e9, 2)
+              if rec["export_span_s"] else None}
+
     if rank == 0:
         out = assemble(args, world, (g.n, g.m), B, elapsed_max, q_totals, q_ms_max, nrows, nruns,
                        kt, cpu, parity, pinfo, traffic)
+        out["lib_src_sha"] = cpd.lib_src_sha()
+        out["tree_src_sha"] = cpd.src_sha(ROOT)
+        out["full_build"] = fb
+        out["full_build_s"] = fb["total_s"] if fb else None
         out["query_index"] = index_mode
         out["query_index_rows_per_gpu"] = index_rows
         out["query_roofline"] = query_roof

@@ -48,7 +48,8 @@ EXPORTED = [
     "cpd_index_set_mode", "cpd_index_get_mode", "cpd_plan_cache", "cpd_index_create_empty",
     "cpd_index_append_rows", "cpd_index_append_built_rows", "cpd_index_info",
     "cpd_synth_road_graph_ex", "cpd_query_search", "cpd_query_search_counters",
-    "cpd_graph_set_coords",
+    "cpd_graph_set_coords", "cpd_host_alloc", "cpd_host_free",
+    "cpd_rows_lanes",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
@@ -139,6 +140,30 @@ def _u32(a) -> np.ndarray:
 
 def version() -> str:
     return lib.cpd_version().decode()
+
+
+def lib_src_sha() -> str:
+    """The source hash libcpd.so was built from (embedded by the Makefile)."""
+    v = version()
+    return v.split("src:", 1)[1] if "src:" in v else ""
+
+
+def src_sha(root: str | None = None) -> str:
+    """sha256 (16 hex) of the library and tool sources in the tree at `root`,
+    computed exactly as the Makefile's PROV_SRCS / SRC_SHA: the files sorted by
+    repo-relative path, contents concatenated."""
+    import glob
+    import hashlib
+    root = root or os.path.dirname(_HERE)
+    pats = ["include/*.h", "distributed-oracle-search_amd/csrc/*.cpp",
+            "distributed-oracle-search_amd/csrc/*.hpp", "distributed-oracle-search_amd/csrc/*.hip",
+            "distributed-oracle-search_amd/tools/*.cpp", "distributed-oracle-search_amd/tools/*.hpp"]
+    files = sorted({os.path.relpath(f, root) for p in pats for f in glob.glob(os.path.join(root, p))})
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(root, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 # --------------------------------------------------------------------------
@@ -335,6 +360,13 @@ class Rows:
         t = np.empty(nr, np.uint32)
         _check(lib.cpd_rows_targets(self._h, _ptr(t, u32p)))
         return t
+
+    def lanes(self):
+        """The batch lane each row was built in (cpd_rows_lanes)."""
+        nr, _ = self.count()
+        a = np.empty(nr, np.uint32)
+        _check(lib.cpd_rows_lanes(self._h, _ptr(a, u32p)))
+        return a
 
     def __del__(self):
         if getattr(self, "_h", None):

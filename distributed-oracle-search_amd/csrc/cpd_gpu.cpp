@@ -310,13 +310,15 @@ struct cpd_graph {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
             // per target: dist 4n (+ 2n narrow) + two buffer sets of fm rows
-            // and RLE segment states (emit overlap) + leaf sets + one row of
-            // output runs at its worst case (4n; ~2.5n on road graphs), in
-            // 85% of free HBM; at most 24 slabs.  Larger batches amortise the
+            // and RLE segment states (emit overlap) + the chunked count's
+            // chunk states (8 B per chunk) + leaf sets + one row of output
+            // runs at its worst case (4n; ~2.5n on road graphs), in 85% of
+            // free HBM; at most 24 slabs.  Larger batches amortise the
             // latency-bound narrow levels: at 1M nodes 20480 rows per batch
             // measured 310.5k rows/s against 296.1k for 16384 (round 2).
             const double per = (narrow ? 6.0 : 4.0) * n +
                                2.0 * (fmb / 8.0 * npad + (fmb == 4 ? 5.0 / 32.0 * npad : 0.0)) +
+                               (fmb == 4 ? 8.0 * rle_count_chunks(npad) : 0.0) +
                                (leaf_fm ? 0.5 * n : 0.0) + 4.0 * n;
             const double fit = 0.85 * (double)free_b / per;
             want = (uint32_t)std::min(24576.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
@@ -326,8 +328,9 @@ struct cpd_graph {
         drain_emits();
         B = want;
         dist.alloc((size_t)n * B);
-        // the second buffer set when a quarter of free HBM still holds it
-        // after the batch's own buffers (else one set: emits do not overlap)
+        // the second buffer set when it takes under an eighth of the HBM
+        // still free after the batch's own buffers (else one set: emits do
+        // not overlap)
         const size_t set_bytes = (size_t)B * (npad / (32u / fmb)) * 4u +
                                  (fmb == 4 ? (size_t)B * (npad / 32u) * 5u : 0u) + 8u * B;
         for (int x = 0; x < 2; ++x) {
@@ -382,6 +385,7 @@ struct cpd_rows {
         }
     }
     std::vector<uint32_t> targets;   // node ids, row order
+    std::vector<uint32_t> lanes;     // batch lane of each row
     std::vector<uint64_t> offsets;   // host copy, nrows+1
     DevBuf<uint32_t> runs;
     DevBuf<uint64_t> off;
@@ -404,6 +408,7 @@ struct cpd_index {
     uint64_t cap = 0;     // run capacity of `runs` (keep_rle)
     uint64_t declared = 0;  // total runs of all rows (from the caller or the rows)
     std::vector<uint32_t> row_of_col;   // host copy
+    std::vector<uint32_t> row_targets;  // declared targets, row order
     std::vector<uint64_t> offsets;      // host copy, added + 1 (keep_rle)
     DevBuf<uint32_t> d_row_of_col, runs, adj_sel;  // adj_sel: packed adjacency, custom weights
     DevBuf<uint64_t> off;
@@ -434,6 +439,7 @@ struct cpd_index {
     DevBuf<uint8_t> sws;
     DevBuf<unsigned long long> sagg;
     bool h_ready = false, c_ready = false;
+    bool searched = false;  // qstats hold the counters of the prepared queries
     // query workspace; queries run sorted by target row (perm[i] = caller index)
     uint32_t nq = 0;
     std::vector<uint32_t> perm;
@@ -1106,6 +1112,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
                      r->runs.n);
     r->offsets.insert(r->offsets.end(), off.begin() + 1, off.end());
     r->targets.insert(r->targets.end(), targets, targets + k);
+    r->lanes.insert(r->lanes.end(), g->pos_of.begin(), g->pos_of.begin() + k);
     r->nrows += k;
     r->total = new_total;
 }
@@ -1127,6 +1134,7 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         r->nrows = 0;
         r->total = 0;
         r->targets.clear();
+        r->lanes.clear();
         r->offsets.assign(1, 0);
         for (uint32_t b = 0; b < ntargets; b += g->B) {
             uint32_t k = std::min(g->B, ntargets - b);
@@ -1190,10 +1198,30 @@ int cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count, uin
     });
 }
 
+int cpd_host_alloc(size_t bytes, void** out) {
+    return guarded([&] {
+        CPD_REQUIRE(out, CPD_E_ARG, "host alloc: null output");
+        *out = nullptr;
+        require_device();
+        HIP_CHECK(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    });
+}
+
+void cpd_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int cpd_rows_targets(const cpd_rows* r, uint32_t* targets) {
     return guarded([&] {
         CPD_REQUIRE(r && targets, CPD_E_ARG, "null argument");
         std::memcpy(targets, r->targets.data(), r->nrows * sizeof(uint32_t));
+    });
+}
+
+int cpd_rows_lanes(const cpd_rows* r, uint32_t* lanes) {
+    return guarded([&] {
+        CPD_REQUIRE(r && lanes, CPD_E_ARG, "null argument");
+        std::memcpy(lanes, r->lanes.data(), r->nrows * sizeof(uint32_t));
     });
 }
 
@@ -1282,6 +1310,7 @@ std::unique_ptr<cpd_index> index_init(cpd_graph* g, const uint32_t* row_targets,
     ix->g = g;
     ix->nrows = nrows;
     ix->row_of_col.assign(g->n, CPD_INF);
+    if (nrows) ix->row_targets.assign(row_targets, row_targets + nrows);
     for (uint32_t i = 0; i < nrows; ++i) {
         CPD_REQUIRE(row_targets[i] < g->n, CPD_E_ARG, "index: row target out of range");
         ix->row_of_col[g->order[row_targets[i]]] = i;
@@ -1402,6 +1431,14 @@ void append_built(cpd_index* ix, const cpd_rows* r) {
     r->wait();
     CPD_REQUIRE(r->nrows <= ix->nrows - ix->added, CPD_E_ARG, "index: more rows than declared");
     if (!r->nrows) return;
+    // the built rows must be the declared rows at these positions (row i of
+    // the index = row_targets[i]): a mismatch would file runs under the
+    // wrong target, undetectable once a dense index has dropped them
+    for (uint32_t i = 0; i < r->nrows; ++i)
+        CPD_REQUIRE(r->targets[i] == ix->row_targets[ix->added + i], CPD_E_ARG,
+                    "index: built row " + std::to_string(i) + " (target " +
+                        std::to_string(r->targets[i]) + ") is not the declared row " +
+                        std::to_string(ix->added + i));
     if (ix->keep_rle) {
         CPD_REQUIRE(ix->total + r->total <= ix->cap, CPD_E_ARG,
                     "index: more runs than the index was created for");
@@ -1555,6 +1592,7 @@ int cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint3
         ix->hops.alloc(nq);
         ix->fin.alloc(nq);
         ix->nq = nq;
+        ix->searched = false;
         HIP_CHECK(hipStreamSynchronize(g->stream));
     });
 }
@@ -1783,6 +1821,7 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             ag.launches++;
             ag.ms += ms;
         }
+        ix->searched = true;
         if (st) {
             st->queries = nq;
             st->expanded = h[0];
@@ -1805,7 +1844,9 @@ int cpd_query_search_counters(cpd_index* ix, uint32_t* counters) {
         ix->g->select();
         const uint32_t nq = ix->nq;
         if (!nq) return;
-        CPD_REQUIRE(ix->qstats.n >= 5ull * nq, CPD_E_ARG, "no search has run on these queries");
+        CPD_REQUIRE(ix->searched && ix->qstats.n >= 5ull * nq, CPD_E_ARG,
+                    "no search has run on these queries (cpd_query_prepare since, or only "
+                    "table-search)");
         std::vector<uint32_t> tmp(5ull * nq);
         HIP_CHECK(hipMemcpy(tmp.data(), ix->qstats.p, tmp.size() * sizeof(uint32_t),
                             hipMemcpyDeviceToHost));

@@ -365,15 +365,7 @@ __device__ __forceinline__ void narrow_store8(const NarrowRows& nr, uint4* __res
         return;
     }
     const uint4 q = make_uint4(q0 | (q1 << 16), q2 | (q3 << 16), q4 | (q5 << 16), q6 | (q7 << 16));
-    uint4* const dst = reinterpret_cast<uint4*>(nr.d16) + (size_t)col * B8 + l8;
-    if (nr.nt) {  // kernel-uniform
-        __builtin_nontemporal_store(q.x, &dst->x);
-        __builtin_nontemporal_store(q.y, &dst->y);
-        __builtin_nontemporal_store(q.z, &dst->z);
-        __builtin_nontemporal_store(q.w, &dst->w);
-    } else {
-        *dst = q;
-    }
+    reinterpret_cast<uint4*>(nr.d16)[(size_t)col * B8 + l8] = q;
     if (head) nr.base[(size_t)grp * nr.n + col] = b;
 }
 
@@ -466,16 +458,13 @@ __device__ __forceinline__ void leaf_slot8(const uint2* e, uint32_t v, U8& acc, 
 
 // A down-sweep slot's descriptor (see down_desc_arcs): the 64-B head (node
 // word, arc range, first kDescArcs arcs) and, for a level-1 node, the
-// closed-form part (c0..c2).  LAZY: the closed-form part is loaded inside the
-// level-1 branch (only those slots pay for it) instead of with the head.
+// closed-form part (c0..c2), all loaded together (one 128-B scalar fetch).
 struct Desc8 {
     uint4 h, i0, i1, i2, c0, c1, c2;
 };
 
-template <bool LAZY>
 __device__ __forceinline__ Desc8 load_desc8(const uint4* __restrict__ desc, uint32_t slot) {
     const uint4* __restrict__ dp = desc + (size_t)slot * 8u;
-    if (LAZY) return Desc8{dp[0], dp[1], dp[2], dp[3], {}, {}, {}};
     return Desc8{dp[0], dp[1], dp[2], dp[3], dp[4], dp[5], dp[6]};
 }
 
@@ -488,9 +477,7 @@ __device__ __forceinline__ Desc8 load_desc8(const uint4* __restrict__ desc, uint
 constexpr int kLong = CPD_DOWN8_LONG;
 
 // One slot of the narrow down-sweep for the lane's 8 targets t.
-template <bool LAZY>
-__device__ __forceinline__ void down8_slot(const Desc8& D, const uint4* __restrict__ desc,
-                                           uint32_t slot, const U8& t, uint32_t l8, uint32_t grp,
+__device__ __forceinline__ void down8_slot(const Desc8& D, const U8& t, uint32_t l8, uint32_t grp,
                                            uint32_t B4, uint32_t B8, uint4* __restrict__ d4,
                                            const uint2* __restrict__ arcs, const Closed& cf,
                                            const uint32_t* __restrict__ live,
@@ -516,8 +503,7 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const uint4* __restri
             return;
         }
     } else if (vraw & kL1Bit) {  // closed form from the descriptor
-        const uint4* __restrict__ dp = desc + (size_t)slot * 8u;
-        const uint4 c0 = LAZY ? dp[4] : D.c0, c1 = LAZY ? dp[5] : D.c1, c2 = LAZY ? dp[6] : D.c2;
+        const uint4 c0 = D.c0, c1 = D.c1, c2 = D.c2;
         v = c0.x;
         acc = U8{leaf4(t.a, v, 0u), leaf4(t.b, v, 0u)};
         const uint2 la[4] = {make_uint2(c0.z, c0.w), make_uint2(c1.x, c1.y),
@@ -569,17 +555,12 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const uint4* __restri
 }
 
 
-// Narrow down-sweep launch: logical block = (group of K consecutive slots,
-// 8 x blockDim targets), slot groups fastest, XCD-remapped.  A wave walks its
-// K slots for the same targets (loaded once) and loads the next slot's
-// descriptor while the current slot's gathers are in flight, so the scalar
-// descriptor fetch leaves the critical path after the first slot.  K = 1 is
-// one slot per block.
-// PF = false: the K slots one after another, each descriptor loaded when its
-// slot starts (the wave's launch and target loads amortised over K slots,
-// nothing held across them).
-template <int K, bool PF = true>
-__global__ __launch_bounds__(256, (K > 1 && !PF) ? 5 : 1) void sweep_down8(const uint4* __restrict__ desc,
+// Narrow down-sweep launch: logical block = (slot, 8 x blockDim targets),
+// slots fastest, XCD-remapped; one slot per wave.  (Round 2 measured K > 1
+// slots per wave with the next descriptor prefetched, and P slots' gathers in
+// flight per wave: no faster — the scalar descriptor fetch is not on the
+// critical path — and removed in round 3.)
+__global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ desc,
                                                    const uint2* __restrict__ arcs,
                                                    uint32_t slot0, uint32_t count, uint32_t remap,
                                                    uint32_t* __restrict__ dist,
@@ -587,165 +568,14 @@ __global__ __launch_bounds__(256, (K > 1 && !PF) ? 5 : 1) void sweep_down8(const
                                                    Closed cf, const uint32_t* __restrict__ live,
                                                    uint16_t* __restrict__ fmleaf, NarrowRows nr) {
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t ngrp = (count + K - 1) / K;
-    const uint32_t blk = L / ngrp;
-    const uint32_t s0 = slot0 + (L - blk * ngrp) * K;
-    const uint32_t s1 = min(s0 + K, slot0 + count);
+    const uint32_t blk = L / count;
+    const uint32_t s0 = slot0 + (L - blk * count);
     const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
     const uint32_t grp = l8 >> 5;                        // uniform per half-wave
     const uint32_t B8 = B4 / 2u;
     uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
     const U8 t{tgt4[2u * l8], tgt4[2u * l8 + 1u]};
-    if (K == 1) {
-        down8_slot<false>(load_desc8<false>(desc, s0), desc, s0, t, l8, grp, B4, B8, d4, arcs,
-                          cf, live, fmleaf, nr);
-        return;
-    }
-    if (!PF) {
-#pragma unroll 1
-        for (uint32_t s = s0; s < s1; ++s)
-            down8_slot<false>(load_desc8<false>(desc, s), desc, s, t, l8, grp, B4, B8, d4, arcs,
-                              cf, live, fmleaf, nr);
-        return;
-    }
-    Desc8 cur = load_desc8<true>(desc, s0);
-#pragma unroll 1
-    for (uint32_t s = s0; s < s1; ++s) {
-        Desc8 nxt = cur;
-        if (s + 1 < s1) nxt = load_desc8<true>(desc, s + 1);
-        down8_slot<true>(cur, desc, s, t, l8, grp, B4, B8, d4, arcs, cf, live, fmleaf, nr);
-        cur = nxt;
-    }
-}
-
-// The same slot computation split into issue (descriptor, own row or closed
-// form, the inline gathers) and finish (decode, minimum, leaf sets, the rest
-// of a long list, store), so that a wave keeps the gathers of P slots in
-// flight at once (sweep_down8p).  A down-sweep wave is latency-bound: it
-// lives for one descriptor load plus one gather round trip, and moves ~4 KiB
-// in that time; P slots per wave put P times the bytes behind one wait.
-struct Slot8 {
-    uint32_t vraw, v, a0, a1;
-    uint2 inl[kDescArcs];
-    U8 acc;
-    NLoad8 pl[kDescArcs];
-};
-
-__device__ __forceinline__ void down8_issue(Slot8& S, const uint4* __restrict__ desc,
-                                            uint32_t slot, const U8& t, uint32_t l8,
-                                            uint32_t grp, uint32_t B4, uint32_t B8,
-                                            const uint4* __restrict__ d4, const Closed& cf,
-                                            const uint32_t* __restrict__ live,
-                                            const NarrowRows& nr) {
-    const uint4* __restrict__ dp = desc + (size_t)slot * 8u;
-    const uint4 h = dp[0], i0 = dp[1], i1 = dp[2], i2 = dp[3];
-    const uint2 all6[6] = {make_uint2(i0.x, i0.y), make_uint2(i0.z, i0.w),
-                           make_uint2(i1.x, i1.y), make_uint2(i1.z, i1.w),
-                           make_uint2(i2.x, i2.y), make_uint2(i2.z, i2.w)};
-#pragma unroll
-    for (int i = 0; i < (int)kDescArcs; ++i) S.inl[i] = all6[i];
-    S.vraw = h.x;
-    S.a0 = h.y;
-    S.a1 = h.z;
-    if (S.vraw & kLeafBit) {
-        S.v = S.vraw & kIdxMask;
-        S.acc = U8{leaf4(t.a, S.v, 0u), leaf4(t.b, S.v, 0u)};
-    } else if (S.vraw & kL1Bit) {  // closed form from the descriptor
-        const uint4 c0 = dp[4], c1 = dp[5], c2 = dp[6];
-        S.v = c0.x;
-        U8 acc{leaf4(t.a, S.v, 0u), leaf4(t.b, S.v, 0u)};
-        const uint2 la[4] = {make_uint2(c0.z, c0.w), make_uint2(c1.x, c1.y),
-                             make_uint2(c1.z, c1.w), make_uint2(c2.x, c2.y)};
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if ((uint32_t)i < c0.y) {
-                min4(acc.a, leaf4(t.a, la[i].x, 0u), la[i].y);
-                min4(acc.b, leaf4(t.b, la[i].x, 0u), la[i].y);
-            }
-        if (c0.y > 4u) {  // more leaf arcs than fit: the ascending arrays
-            const uint32_t s1 = S.vraw & kIdxMask;
-            for (uint32_t a = cf.off[s1] + 4u; a < cf.off[s1 + 1]; ++a) {
-                const uint2 e = cf.arcs[a];
-                min4(acc.a, leaf4(t.a, e.x & kIdxMask, 0u), e.y);
-                min4(acc.b, leaf4(t.b, e.x & kIdxMask, 0u), e.y);
-            }
-        }
-        S.acc = acc;
-    } else {
-        S.v = S.vraw;
-        const bool own = !live || ((live[S.v] >> (l8 >> 7)) & 1u);  // live bits: 1024 targets
-        S.acc = own ? U8{d4[(size_t)S.v * B4 + 2u * l8], d4[(size_t)S.v * B4 + 2u * l8 + 1u]}
-                    : inf8();
-    }
-#pragma unroll
-    for (int i = 0; i < (int)kDescArcs; ++i)  // a leaf's self loop is not gathered
-        if (S.inl[i].x != kNoEdge && S.inl[i].x != S.v)
-            S.pl[i] = nl8_issue(nr, S.inl[i].x, grp, B8, l8);
-}
-
-__device__ __forceinline__ void down8_finish(Slot8& S, const U8& t, uint32_t l8, uint32_t grp,
-                                             uint32_t B4, uint32_t B8, uint4* __restrict__ d4,
-                                             const uint2* __restrict__ arcs,
-                                             uint16_t* __restrict__ fmleaf,
-                                             const NarrowRows& nr) {
-    const uint32_t v = S.v;
-    if ((S.vraw & kLeafBit) && fmleaf) {  // out-degree <= 4 (4-bit sets): all inline
-        leaf_finish8(S.inl, S.pl, v, S.acc, t, l8, grp, B4, B8, d4, fmleaf, nr);
-        return;
-    }
-#pragma unroll
-    for (int i = 0; i < (int)kDescArcs; ++i)
-        if (S.inl[i].x != kNoEdge && S.inl[i].x != v)
-            min8(S.acc, nl8_finish(S.pl[i], d4, S.inl[i].x, B4, l8), S.inl[i].y);
-    uint32_t a = S.a0 + kDescArcs;  // the rest of a long list
-    for (; a + 8 <= S.a1; a += 8) {
-        uint2 e[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = arcs[a + i];
-        NLoad8 pl[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) pl[i] = nl8_issue(nr, e[i].x, grp, B8, l8);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) min8(S.acc, nl8_finish(pl[i], d4, e[i].x, B4, l8), e[i].y);
-    }
-    for (; a < S.a1; ++a) {
-        const uint2 e = arcs[a];
-        min8(S.acc, nl8_finish(nl8_issue(nr, e.x, grp, B8, l8), d4, e.x, B4, l8), e.y);
-    }
-    narrow_store8(nr, d4, v, grp, B4, B8, l8, S.acc);
-}
-
-// Narrow down-sweep with P slots in flight per wave: logical block = (group
-// of P consecutive slots, 8 x blockDim targets), slot groups fastest,
-// XCD-remapped; every slot's descriptor and gathers are issued before the
-// first is finished.
-// W = waves per SIMD asked of the register allocator (P = 2 needs ~174
-// VGPRs unbounded: 2 waves; W = 3 keeps 6 slots per SIMD in flight).
-template <int P, int W>
-__global__ __launch_bounds__(256, W) void sweep_down8p(const uint4* __restrict__ desc,
-                                                    const uint2* __restrict__ arcs,
-                                                    uint32_t slot0, uint32_t count, uint32_t remap,
-                                                    uint32_t* __restrict__ dist,
-                                                    const uint4* __restrict__ tgt4, uint32_t B4,
-                                                    Closed cf, const uint32_t* __restrict__ live,
-                                                    uint16_t* __restrict__ fmleaf, NarrowRows nr) {
-    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t ngrp = (count + P - 1) / P;
-    const uint32_t blk = L / ngrp;
-    const uint32_t s0 = slot0 + (L - blk * ngrp) * P;
-    const uint32_t np = min((uint32_t)P, slot0 + count - s0);  // wave-uniform
-    const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
-    const uint32_t grp = l8 >> 5;                        // uniform per half-wave
-    const uint32_t B8 = B4 / 2u;
-    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
-    const U8 t{tgt4[2u * l8], tgt4[2u * l8 + 1u]};
-    Slot8 S[P];
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-        if ((uint32_t)p < np) down8_issue(S[p], desc, s0 + p, t, l8, grp, B4, B8, d4, cf, live, nr);
-#pragma unroll
-    for (int p = 0; p < P; ++p)
-        if ((uint32_t)p < np) down8_finish(S[p], t, l8, grp, B4, B8, d4, arcs, fmleaf, nr);
+    down8_slot(load_desc8(desc, s0), t, l8, grp, B4, B8, d4, arcs, cf, live, fmleaf, nr);
 }
 
 // Group rows stored wide (timing runs only): *out += #{base[i] == kWideRow}.
@@ -1117,31 +947,29 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
 // decoded (two groups in flight), so a wave waits about one memory round trip
 // per group instead of two.
 //
-// The column's own row is not read (OWN = false, the default): for c != t,
-// d(c) = min over c's out-edges of w_k + d(v_k) (a shortest path to t leaves
-// c by some edge; a self loop adds w + d(c) >= d(c) and so never lowers the
-// minimum), all of them final here, and d(c) == INF exactly when every term
-// is INF — so the sets {k : w_k + d(v_k) == d(c)} follow from the neighbour
-// rows alone, bit-identical, one gather per column fewer.  OWN = true reads
-// it as before (CPD_FM_OWN=1, A/B only).
+// The column's own row is not read: for c != t, d(c) = min over c's
+// out-edges of w_k + d(v_k) (a shortest path to t leaves c by some edge; a
+// self loop adds w + d(c) >= d(c) and so never lowers the minimum), all of
+// them final here, and d(c) == INF exactly when every term is INF — so the
+// sets {k : w_k + d(v_k) == d(c)} follow from the neighbour rows alone,
+// bit-identical, one gather per column fewer.  (Reading it, CPD_FM_OWN in
+// round 2, was slower and is gone.)
 template <int G>
 struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR pressure)
-    NLoad own[G];
     NLoad nb[G][4];  // a leaf column's sets (fmleaf) ride in nb[j][0].q.x
 };
 
-// S = 32-column segments per workgroup (CPD_FM_SEGS, default 1; 2 was
-// slower in round 2 at 101 VGPRs).  The lane's 4 rows of a segment are one
-// 64-B sector of the row-group interleaved layout (fm4_piece), stored whole
-// by the lane.  With S = 1 each row's word goes to an LDS stage as soon as
-// its 8 columns are done (4 words live instead of 16: 8 waves per SIMD
-// instead of 6) and the sector is stored from there at the end — storing the
-// 4-B words straight to HBM measured 4x the write bytes (34 vs 8.8 GB per
-// launch: L2 does not merge them) and 24.4 vs 12.6 ms.  (Round 2 before that layout: 16-B row-major pieces, 1.83x the
-// algorithmic write bytes in PMC; an LDS exchange of X segments per
-// workgroup for 16X-B row pieces, CPD_FM_X, fixed the bytes but was slower,
-// and is gone with the layout.)
-template <int G, int S, bool OWN = false>
+// One workgroup per (32-column segment, slab of 4 x blockDim targets).  The
+// lane's 4 rows of a segment are one 64-B sector of the row-group interleaved
+// layout (fm4_piece), stored whole by the lane: each row's word goes to an
+// LDS stage as soon as its 8 columns are done (4 words live instead of 16: 8
+// waves per SIMD instead of 6) and the sector is stored from there at the end
+// — storing the 4-B words straight to HBM measured 4x the write bytes (34 vs
+// 8.8 GB per launch: L2 does not merge them) and 24.4 vs 12.6 ms.  Columns
+// are gathered G = 2 at a time, the next group issued before the current one
+// is finished (G = 1 measured 16.2 against 15.3 ms; two segments per
+// workgroup, CPD_FM_SEGS = 2, 101 VGPRs and slower: both removed in round 3).
+template <int G>
 __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ adj,
                                                       const uint32_t* __restrict__ dist,
                                                       const uint32_t* __restrict__ tgt, uint32_t B,
@@ -1152,42 +980,34 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                                                       NarrowRows nr) {
     static_assert(kSeg % G == 0, "group size");
     const uint32_t nseg = npad / kSeg;
-    const uint32_t nblk = nseg / S;
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t slab = L / nblk;
+    const uint32_t slab = L / nseg;
     const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t B4 = B / 4u;
-    const uint32_t cb = (L - slab * nblk) * (kSeg * S);
+    const uint32_t cb = (L - slab * nseg) * kSeg;
     const uint32_t lane = threadIdx.x & 63u;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
     const uint32_t grp = wave_group(l4);
-    // S = 1: each row word is staged in LDS (64 B per lane, dynamic shared
-    // memory) as soon as its 8 columns are done, so only the current word of
-    // each row is live in registers
+    // each row word is staged in LDS (64 B per lane, dynamic shared memory) as
+    // soon as its 8 columns are done, so only the current word of each row is
+    // live in registers
     extern __shared__ uint32_t fm_stage[];
-    uint32_t pk[4][4 * S];
+    uint32_t pk[4][4];
 #pragma unroll
-    for (int p = 0; p < 4 * S; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
-    // the block's adjacency (S x 1 KiB) and leaf bits up front; the group
-    // pipeline then runs over all S x 32 columns without a bubble
-    uint4 sa[S];
-    uint32_t lb[S];
-#pragma unroll
-    for (int sg = 0; sg < S; ++sg) {
-        const uint32_t c0 = cb + (uint32_t)sg * kSeg;
-        lb[sg] = leafbits ? leafbits[c0 / kSeg] : 0u;
-        sa[sg] = c0 + lane / 2u < n ? reinterpret_cast<const uint4*>(adj)[(size_t)c0 * 2u + lane]
-                                    : make_uint4(kNoEdge, 0u, kNoEdge, 0u);
-    }
-    auto edge = [&](int cc, int k) -> uint2 {  // wave-uniform; cc in [0, S x 32)
-        const uint4& q = sa[cc / (int)kSeg];
-        const int ln = 2 * (cc % (int)kSeg) + (k >> 1);
-        const uint32_t x = __builtin_amdgcn_readlane((k & 1) ? q.z : q.x, ln);
-        const uint32_t w = __builtin_amdgcn_readlane((k & 1) ? q.w : q.y, ln);
+    for (int p = 0; p < 4; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
+    // the segment's adjacency (1 KiB) and leaf bits up front; the group
+    // pipeline then runs over its 32 columns without a bubble
+    const uint32_t lb = leafbits ? leafbits[cb / kSeg] : 0u;
+    const uint4 sa = cb + lane / 2u < n ? reinterpret_cast<const uint4*>(adj)[(size_t)cb * 2u + lane]
+                                        : make_uint4(kNoEdge, 0u, kNoEdge, 0u);
+    auto edge = [&](int cc, int k) -> uint2 {  // wave-uniform; cc in [0, 32)
+        const int ln = 2 * cc + (k >> 1);
+        const uint32_t x = __builtin_amdgcn_readlane((k & 1) ? sa.z : sa.x, ln);
+        const uint32_t w = __builtin_amdgcn_readlane((k & 1) ? sa.w : sa.y, ln);
         return make_uint2(x, w);
     };
-    auto is_leaf = [&](int cc) -> bool { return (lb[cc / (int)kSeg] >> (cc % (int)kSeg)) & 1u; };
+    auto is_leaf = [&](int cc) -> bool { return (lb >> cc) & 1u; };
     auto issue = [&](FmGroup<G>& g, int cg) {
 #pragma unroll
         for (int j = 0; j < G; ++j) {
@@ -1195,7 +1015,6 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
             const bool ok = c < n;
             const bool leaf = is_leaf(cg + j);
             if (ok && !leaf) {
-                if (OWN) g.own[j] = nl_issue(nr, c, grp, B4, l4);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint2 e = edge(cg + j, k);
@@ -1211,16 +1030,12 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
             const uint32_t c = cb + (uint32_t)(cg + j);
             if (c >= n) continue;  // stays the wildcard padding
             const int cc = cg + j;
-            uint32_t f0, f1, f2, f3;
+            uint32_t bits;
             if (is_leaf(cc)) {  // 4 nibbles, wildcards included
-                const uint32_t lv = g.nb[j][0].q.x;
-                f0 = lv & 0xFu;
-                f1 = (lv >> 4) & 0xFu;
-                f2 = (lv >> 8) & 0xFu;
-                f3 = lv >> 12;
-            } else if (!OWN) {  // argmin set folded per neighbour (see leaf_finish8)
+                bits = g.nb[j][0].q.x;
+            } else {  // argmin set folded per neighbour (see leaf_finish8)
                 uint4 dn = make_uint4(INF, INF, INF, INF);
-                uint32_t bits = 0;
+                bits = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint2 e = edge(cc, k);
@@ -1232,44 +1047,9 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                     argmin_fold<3>(dn.w, bits, sat_add(dv.w, e.y), k);
                 }
                 bits = fm_wild4(tc, dn, c, bits);
-                f0 = bits & 0xFu;
-                f1 = (bits >> 4) & 0xFu;
-                f2 = (bits >> 8) & 0xFu;
-                f3 = bits >> 12;
-            } else {
-                uint4 dv[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint2 e = edge(cc, k);
-                    dv[k] = e.x != kNoEdge ? nl_finish(g.nb[j][k], d4, e.x, B4, l4)
-                                           : make_uint4(INF, INF, INF, INF);
-                }
-                uint4 dn = make_uint4(INF, INF, INF, INF);
-                if (OWN) {
-                    dn = nl_finish(g.own[j], d4, c, B4, l4);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const uint2 e = edge(cc, k);
-                        if (e.x != kNoEdge) min4(dn, dv[k], e.y);
-                    }
-                }
-                uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint2 e = edge(cc, k);
-                    if (e.x == kNoEdge) continue;
-                    const uint32_t we = e.y;
-                    b0 |= fm_bit(dv[k].x, we, dn.x, k);
-                    b1 |= fm_bit(dv[k].y, we, dn.y, k);
-                    b2 |= fm_bit(dv[k].z, we, dn.z, k);
-                    b3 |= fm_bit(dv[k].w, we, dn.w, k);
-                }
-                f0 = fm_final<4>(c, tc.x, dn.x, b0);
-                f1 = fm_final<4>(c, tc.y, dn.y, b1);
-                f2 = fm_final<4>(c, tc.z, dn.z, b2);
-                f3 = fm_final<4>(c, tc.w, dn.w, b3);
             }
+            const uint32_t f0 = bits & 0xFu, f1 = (bits >> 4) & 0xFu;
+            const uint32_t f2 = (bits >> 8) & 0xFu, f3 = (bits >> 12) & 0xFu;
             const int wi = cc / 8, sh = 4 * (cc % 8);
             const uint32_t keep = ~(0xFu << sh);
             pk[0][wi] = (pk[0][wi] & keep) | (f0 << sh);
@@ -1278,7 +1058,7 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
             pk[3][wi] = (pk[3][wi] & keep) | (f3 << sh);
         }
     };
-    constexpr int NC = S * (int)kSeg;
+    constexpr int NC = (int)kSeg;
     static_assert(8 % G == 0, "a group never straddles a word");
     FmGroup<G> cur, nxt;
     issue(cur, 0);
@@ -1286,28 +1066,18 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
     for (int cg = 0; cg < NC; cg += G) {
         if (cg + G < NC) issue(nxt, cg + G);
         finish(cur, cg);
-        if (S == 1 && (cg + G) % 8 == 0) {  // the 4 rows' words of these 8 columns -> LDS
+        if ((cg + G) % 8 == 0) {  // the 4 rows' words of these 8 columns -> LDS
             const int wi = (cg + G) / 8 - 1;
 #pragma unroll
             for (int i = 0; i < 4; ++i) fm_stage[(threadIdx.x * 4u + (uint32_t)i) * 4u + wi] = pk[i][wi];
         }
         cur = nxt;
     }
-    if (S == 1) {  // the lane's own staged sector: whole 64-B stores (no barrier: same lane)
-        uint4* __restrict__ o = reinterpret_cast<uint4*>(fm) + fm4_piece(4u * l4, nseg, cb / kSeg);
-        const uint4* st = reinterpret_cast<const uint4*>(fm_stage) + threadIdx.x * 4u;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = st[i];
-        return;
-    }
-    // rows 4 l4 .. 4 l4 + 3 of segment cb/32 + sg: one 64-B sector each
+    // the lane's own staged sector: whole 64-B stores (no barrier: same lane)
     uint4* __restrict__ o = reinterpret_cast<uint4*>(fm) + fm4_piece(4u * l4, nseg, cb / kSeg);
+    const uint4* st = reinterpret_cast<const uint4*>(fm_stage) + threadIdx.x * 4u;
 #pragma unroll
-    for (int sg = 0; sg < S; ++sg)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            o[4 * sg + i] = make_uint4(pk[i][4 * sg], pk[i][4 * sg + 1], pk[i][4 * sg + 2],
-                                       pk[i][4 * sg + 3]);
+    for (int i = 0; i < 4; ++i) o[i] = st[i];
 }
 
 // One lane's greedy pass over its 32 columns (warthog graph_oracle::add_row
@@ -1688,7 +1458,7 @@ __global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, u
     if (lane == 0) counts[row] = total + 1u;  // + the final run
 }
 
-// Table-search extraction, one lane per query.  cur/t are columns; the run for
+// Table-search extraction (table_walk below).  cur/t are columns; the run for
 // column cur is found by galloping from the previous hop's run (consecutive
 // path nodes have nearby DFS columns), then binary search inside the bracket:
 // the result is always the LAST run with start <= cur — the same run warthog's
@@ -1699,68 +1469,6 @@ __global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, u
 // Per-wave sums of (cost, moves, finished) added to agg[2], agg[1], agg[0].
 __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
                            unsigned long long* __restrict__ agg);
-
-__global__ __launch_bounds__(256) void table_search(
-    const uint2* __restrict__ adj, uint32_t shift, const uint32_t* __restrict__ row_of_col,
-    const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ runs,
-    const uint32_t* __restrict__ qs, const uint32_t* __restrict__ qt, uint32_t nq,
-    int32_t kmoves, uint32_t n, uint64_t* __restrict__ cost_out,
-    uint32_t* __restrict__ hops_out, uint8_t* __restrict__ fin_out,
-    unsigned long long* __restrict__ agg) {
-    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
-    uint64_t cost = 0;
-    uint32_t hops = 0, fin = 0;
-    if (q < nq) {
-        const uint32_t t = qt[q];
-        uint32_t cur = qs[q];
-        const uint32_t row = row_of_col[t];
-        const uint32_t* __restrict__ rr = runs + offsets[row];
-        const uint32_t R = (uint32_t)(offsets[row + 1] - offsets[row]);
-        const uint32_t limit = kmoves >= 0 ? (uint32_t)kmoves : n;
-        uint32_t pos = 0;
-        while (cur != t && hops < limit && hops < n) {
-            uint32_t lo, hi;  // invariant: start(lo) <= cur < start(hi) (hi==R: +inf)
-            if ((rr[pos] >> 4) <= cur) {
-                lo = pos;
-                uint32_t step = 1;
-                hi = pos + 1;
-                while (hi < R && (rr[hi] >> 4) <= cur) {
-                    lo = hi;
-                    step <<= 1;
-                    hi = lo + step;
-                }
-                if (hi > R) hi = R;
-            } else {
-                hi = pos;
-                uint32_t step = 1;
-                lo = pos >= 1 ? pos - 1 : 0;
-                while (lo > 0 && (rr[lo] >> 4) > cur) {
-                    hi = lo;
-                    step <<= 1;
-                    lo = hi > step ? hi - step : 0;
-                }
-            }
-            while (lo + 1 < hi) {
-                const uint32_t mid = lo + ((hi - lo) >> 1);
-                if ((rr[mid] >> 4) > cur) hi = mid;
-                else lo = mid;
-            }
-            pos = lo;
-            const uint32_t mv = rr[lo] & 0xFu;
-            if (mv >> shift) break;  // names no slot of cur: malformed row
-            const uint2 e = adj[((size_t)cur << shift) + mv];
-            if (e.x == kNoEdge) break;  // move past the out-degree: malformed row
-            cost += e.y;
-            cur = e.x;
-            ++hops;
-        }
-        fin = (cur == t) ? 1u : 0u;
-        cost_out[q] = cost;
-        hops_out[q] = hops;
-        fin_out[q] = (uint8_t)fin;
-    }
-    wave_stats(cost, hops, fin, agg);
-}
 
 // Expand RLE rows into dense 4-bit move tables (8 columns per u32, column c at
 // bits 4*(c&7) of word c>>3).  One wave per (row, 2048-column tile): the runs
@@ -1836,40 +1544,6 @@ __global__ __launch_bounds__(256) void validate_rows(const uint64_t* __restrict_
         else b |= c <= (runs[i - 1] >> 4);
     }
     if (__any(b) && lane == 0) atomicOr(bad, 1u);
-}
-
-// Table-search over dense move tables: one nibble load + one packed edge load
-// per move.  Same walk, same results as table_search.
-__global__ __launch_bounds__(256) void table_search_dense(
-    const uint2* __restrict__ adj, uint32_t shift, const uint32_t* __restrict__ row_of_col,
-    const uint32_t* __restrict__ dense, uint32_t words_per_row,
-    const uint32_t* __restrict__ qs, const uint32_t* __restrict__ qt, uint32_t nq,
-    int32_t kmoves, uint32_t n, uint64_t* __restrict__ cost_out,
-    uint32_t* __restrict__ hops_out, uint8_t* __restrict__ fin_out,
-    unsigned long long* __restrict__ agg) {
-    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
-    uint64_t cost = 0;
-    uint32_t hops = 0, fin = 0;
-    if (q < nq) {
-        const uint32_t t = qt[q];
-        uint32_t cur = qs[q];
-        const uint32_t* __restrict__ row = dense + (size_t)row_of_col[t] * words_per_row;
-        const uint32_t limit = kmoves >= 0 ? (uint32_t)kmoves : n;
-        while (cur != t && hops < limit && hops < n) {
-            const uint32_t mv = (row[cur >> 3] >> (4u * (cur & 7u))) & 0xFu;
-            if (mv >> shift) break;  // names no slot of cur: malformed row
-            const uint2 e = adj[((size_t)cur << shift) + mv];
-            if (e.x == kNoEdge) break;
-            cost += e.y;
-            cur = e.x;
-            ++hops;
-        }
-        fin = (cur == t) ? 1u : 0u;
-        cost_out[q] = cost;
-        hops_out[q] = hops;
-        fin_out[q] = (uint8_t)fin;
-    }
-    wave_stats(cost, hops, fin, agg);
 }
 
 // ---------------------------------------------------------------------------
@@ -2593,54 +2267,12 @@ uint32_t down8_wpb() {  // CPD_DOWN8_WPB: 1, 2 or 4 waves per narrow down-sweep 
     }();
     return v;
 }
-uint32_t down8_k() {  // CPD_DOWN8_K: slots per wave in the narrow down-sweep (1, 2, 4, 8)
-    static const uint32_t v = [] {
-        const uint32_t k = env_u32("CPD_DOWN8_K", 1);
-        return k >= 8 ? 8u : k >= 4 ? 4u : k >= 2 ? 2u : 1u;
-    }();
-    return v;
-}
-uint32_t down8_p() {  // CPD_DOWN8_P: slots whose gathers a down-sweep wave keeps in flight (1-4)
-    static const uint32_t v = [] {
-        const uint32_t p = env_u32("CPD_DOWN8_P", 1);
-        return p < 1 ? 1u : p > 4 ? 4u : p;
-    }();
-    return v;
-}
-uint32_t down8_pf() {  // CPD_DOWN8_PF=0: K > 1 slots per wave without the descriptor prefetch
-    static const uint32_t v = env_u32("CPD_DOWN8_PF", 1);
-    return v;
-}
-uint32_t down8_nt() {  // CPD_DOWN8_NT=1: the down-sweep's narrow rows stored non-temporal
-    static const uint32_t v = env_u32("CPD_DOWN8_NT", 0);
-    return v;
-}
-size_t down8_lds() {  // CPD_DOWN8_LDS: bytes of (unused) LDS per down-sweep workgroup (occupancy A/B)
-    static const size_t v = env_u32("CPD_DOWN8_LDS", 0);
-    return v;
-}
 uint32_t fm_wpb() {
     static const uint32_t v = env_u32("CPD_FM_WPB", 2);
     return v;
 }
-uint32_t fm_n4() {  // CPD_FM_N4=0: narrow first moves without the pipelined kernel
+uint32_t fm_n4() {  // CPD_FM_N4=0: narrow first moves by the generic kernel
     static const uint32_t v = env_u32("CPD_FM_N4", 1);
-    return v;
-}
-uint32_t fm_segs() {  // CPD_FM_SEGS: 32-column segments per pipelined first-moves workgroup
-    static const uint32_t v = env_u32("CPD_FM_SEGS", 1);
-    return v;
-}
-uint32_t fm_g() {
-    static const uint32_t v = env_u32("CPD_FM_G", 2);
-    return v;
-}
-uint32_t fm_n4g() {  // CPD_FM_N4G: columns per gather group of the pipelined first moves (1, 2)
-    static const uint32_t v = env_u32("CPD_FM_N4G", 2) == 1 ? 1u : 2u;
-    return v;
-}
-uint32_t fm_own() {  // CPD_FM_OWN=1: the pipelined first moves also read the column's own row
-    static const uint32_t v = env_u32("CPD_FM_OWN", 0);
     return v;
 }
 
@@ -2672,36 +2304,9 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
             // (4 waves = 2048 targets: only when the slab count is even)
             const uint32_t wpb8 = down8_wpb() == 4 && slabs % 2 ? 2u : down8_wpb();
             const uint32_t tpb8 = 64u * wpb8;
-            const uint32_t P = down8_p();
-            const uint32_t K = P > 1 ? P : down8_k();
-            const uint32_t ngrp = (count + K - 1u) / K;
-            const dim3 g8(ngrp * slabs * 2u / wpb8), b8(tpb8);
-            const uint4* d = reinterpret_cast<const uint4*>(desc);
-            const uint32_t* lv = live;
-            if (P > 1) {
-                switch (P) {
-                    case 2: launch(kern::sweep_down8p<2, 3>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
-                    case 3: launch(kern::sweep_down8p<3, 2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
-                    default: launch(kern::sweep_down8p<4, 2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
-                }
-                return;
-            }
-            NarrowRows nrd = nr;
-            nrd.nt = down8_nt();
-            if (!down8_pf() && K > 1) {
-                switch (K) {
-                    case 2: launch(kern::sweep_down8<2, false>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nrd); break;
-                    case 4: launch(kern::sweep_down8<4, false>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nrd); break;
-                    default: launch(kern::sweep_down8<8, false>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nrd); break;
-                }
-                return;
-            }
-            switch (K) {
-                case 1: launch_shm(kern::sweep_down8<1>, g8, b8, down8_lds(), s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nrd); break;
-                case 2: launch(kern::sweep_down8<2>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
-                case 4: launch(kern::sweep_down8<4>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
-                default: launch(kern::sweep_down8<8>, g8, b8, s, d, arcs, slot0, count, xcd_remap(), dist, t4, B / 4u, cf, lv, fmleaf, nr); break;
-            }
+            const dim3 g8(count * slabs * 2u / wpb8), b8(tpb8);
+            launch(kern::sweep_down8, g8, b8, s, reinterpret_cast<const uint4*>(desc), arcs, slot0,
+                   count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live, fmleaf, nr);
         } else
             launch(kern::sweep_level<false>, grid, blk, s, nodes, arc_off, arcs, slot0, count,
                    xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live, lf);
@@ -2768,14 +2373,7 @@ static void launch_first_moves_t(const uint2* adj, uint32_t shift, const uint32_
     switch (shift) {  // SLOTS = 2^shift edges per column; G columns per gather group
         case 0: launch(kern::first_moves<1, 4, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
         case 1: launch(kern::first_moves<2, 2, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
-        case 2:
-            if (fm_g() == 4)
-                launch(kern::first_moves<4, 4, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
-            else if (fm_g() == 1)
-                launch(kern::first_moves<4, 1, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
-            else
-                launch(kern::first_moves<4, 2, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr);
-            break;
+        case 2: launch(kern::first_moves<4, 2, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
         case 3: launch(kern::first_moves<8, 1, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
         default: launch(kern::first_moves<16, 1, NARROW>, grid, blk, s, adj, dist, tgt, B, n, npad, r, fm, leafbits, fmleaf, nr); break;
     }
@@ -2789,19 +2387,8 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
     const dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u) * (256u / tpb)), blk(tpb);
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     if (nr.d16 && shift == 2 && fm_n4()) {
-        const uint32_t r = xcd_remap();
-        if (fm_segs() == 2)
-            launch(kern::first_moves_n4<2, 2>, dim3(grid.x / 2u), blk, s, adj, dist, tgt, B, n, npad,
-                   r, fm, leafbits, fmleaf, nr);
-        else if (fm_own())
-            launch_shm(kern::first_moves_n4<2, 1, true>, grid, blk, 64u * tpb, s, adj, dist, tgt,
-                       B, n, npad, r, fm, leafbits, fmleaf, nr);
-        else if (fm_n4g() == 1)
-            launch_shm(kern::first_moves_n4<1, 1>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n,
-                       npad, r, fm, leafbits, fmleaf, nr);
-        else
-            launch_shm(kern::first_moves_n4<2, 1>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n,
-                       npad, r, fm, leafbits, fmleaf, nr);
+        launch_shm(kern::first_moves_n4<2>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n, npad,
+                   xcd_remap(), fm, leafbits, fmleaf, nr);
     } else if (nr.d16)
         launch_first_moves_t<true>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
                                    grid, blk, s);
@@ -2811,8 +2398,7 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
 }
 
 bool first_moves_reads_own(uint32_t shift, bool narrow) {
-    if (!(narrow && shift == 2 && fm_n4())) return true;  // the generic kernel
-    return fm_own() && fm_segs() != 2;                      // only the default form has OWN
+    return !(narrow && shift == 2 && fm_n4());  // only the generic kernel reads it
 }
 
 template <bool EMIT>
@@ -2833,11 +2419,8 @@ void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
     launch_rle<false>(fm, fmb, npad, nrows, counts, nullptr, nullptr, st, rc, s);
 }
 
-uint32_t rle_ch() {  // CPD_RLE_CH: segments per chunk of the chunked count (32, 64); 0 = rle_scan
-    static const uint32_t v = [] {
-        const uint32_t c = env_u32("CPD_RLE_CH", 32);
-        return c == 0 ? 0u : c >= 64 ? 64u : 32u;
-    }();
+uint32_t rle_ch() {  // CPD_RLE_CH=0: count with rle_scan instead of the chunked count (32 segments)
+    static const uint32_t v = env_u32("CPD_RLE_CH", 32) == 0 ? 0u : 32u;
     return v;
 }
 
@@ -2849,10 +2432,7 @@ void launch_rle_count_ch(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint
     const uint32_t nch = rle_count_chunks(npad);
     const kern::RleChunks rk{xs, cc};
     const dim3 grid((nch + 15u) / 16u, (nrows + 15u) / 16u), blk(256);
-    if (rle_ch() == 64)
-        launch(kern::rle_count_ch<64>, grid, blk, s, fm, npad, nrows, st, rc, rk);
-    else
-        launch(kern::rle_count_ch<32>, grid, blk, s, fm, npad, nrows, st, rc, rk);
+    launch(kern::rle_count_ch<32>, grid, blk, s, fm, npad, nrows, st, rc, rk);
 }
 
 void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
@@ -2860,12 +2440,8 @@ void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t*
                     hipStream_t s) {
     if (!nrows) return;
     const kern::RleChunks rk{xs, cc};
-    if (rle_ch() == 64)
-        launch(kern::rle_fix<64>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts,
-               hard);
-    else
-        launch(kern::rle_fix<32>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts,
-               hard);
+    launch(kern::rle_fix<32>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts,
+           hard);
 }
 
 void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
@@ -2887,23 +2463,16 @@ void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t 
            npad / 8u, dense);
 }
 
-// Table-search knobs (A/B runs; results are identical under every setting):
-// CPD_TS_V1=1 runs the lane-per-query kernels without co-fetch or refill;
-// CPD_TS_ILP (1 or 2) walks per lane; the batch is cut into chunks of
-// ceil(nq / waves) queries (a multiple of 64 x ILP, at most CPD_TS_CHUNK_MAX
-// for dense rows).  Measured on the 1M-node bench (1M queries, MI355X,
-// tools_scripts/query_ab.py): dense walks want few waves that each refill
-// their lanes ~16 times (waves 1024: 88M q/s; 8192 waves, i.e. no refill:
-// 60M; lane per query: 43.7M), RLE walks — a chain of dependent loads per hop
-// — want every wave slot filled (8192); ILP 2 was slower in both.
-uint32_t ts_v1() {
-    static const uint32_t v = env_u32("CPD_TS_V1", 0);
-    return v;
-}
-uint32_t ts_ilp() {
-    static const uint32_t v = env_u32("CPD_TS_ILP", 1) >= 2 ? 2u : 1u;
-    return v;
-}
+// Table-search chunking (launch parameters only; results are identical under
+// every setting): the batch is cut into chunks of ceil(nq / waves) queries (a
+// multiple of 64, at most CPD_TS_CHUNK_MAX for dense rows), CPD_TS_WAVES
+// overriding the wave count.  Measured on the 1M-node bench (1M queries,
+// MI355X, tools_scripts/query_ab.py): dense walks want few waves that each
+// refill their lanes ~16 times (waves 1024: 88M q/s; 8192 waves, i.e. no
+// refill: 60M; round 1's lane per query: 43.7M), RLE walks — a chain of
+// dependent loads per hop — want every wave slot filled (8192).  Two walks
+// per lane (ILP 2) was slower in both forms; it and round 1's lane-per-query
+// kernels were removed in round 3.
 uint32_t ts_waves(uint32_t dflt) {
     static const uint32_t v = env_u32("CPD_TS_WAVES", 0);
     return v ? v : dflt;
@@ -2918,7 +2487,7 @@ static void launch_walk(const uint2* adj, uint32_t shift, const Rows& rows, cons
                         const uint32_t* qt, const uint32_t* qrow, uint32_t nq, uint32_t limit,
                         uint64_t* cost, uint32_t* hops, uint8_t* fin, unsigned long long* agg,
                         uint32_t waves_target, uint32_t chunk_max, hipStream_t s) {
-    const uint32_t ilp = ts_ilp(), unit = 64u * ilp;
+    constexpr uint32_t unit = 64u;
     uint64_t chunk = ((uint64_t)nq + waves_target - 1u) / waves_target;
     chunk = std::min<uint64_t>(chunk, std::max(unit, chunk_max));
     chunk = std::max<uint64_t>(unit, (chunk + unit - 1u) / unit * unit);
@@ -2928,22 +2497,12 @@ static void launch_walk(const uint2* adj, uint32_t shift, const Rows& rows, cons
 #define CPD_WALK(SH, IL)                                                                       \
     launch(kern::table_walk<SH, IL, Rows>, grid, blk, s, adj, rows, qs, qt, qrow, nq, c, limit, \
            cost, hops, fin, agg)
-    if (ilp == 2) {
-        switch (shift) {
-            case 0: CPD_WALK(0, 2); break;
-            case 1: CPD_WALK(1, 2); break;
-            case 2: CPD_WALK(2, 2); break;
-            case 3: CPD_WALK(3, 2); break;
-            default: CPD_WALK(4, 2); break;
-        }
-    } else {
-        switch (shift) {
-            case 0: CPD_WALK(0, 1); break;
-            case 1: CPD_WALK(1, 1); break;
-            case 2: CPD_WALK(2, 1); break;
-            case 3: CPD_WALK(3, 1); break;
-            default: CPD_WALK(4, 1); break;
-        }
+    switch (shift) {
+        case 0: CPD_WALK(0, 1); break;
+        case 1: CPD_WALK(1, 1); break;
+        case 2: CPD_WALK(2, 1); break;
+        case 3: CPD_WALK(3, 1); break;
+        default: CPD_WALK(4, 1); break;
     }
 #undef CPD_WALK
 }
@@ -2957,12 +2516,6 @@ void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32
                                const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
                                int32_t kmoves, uint32_t n, uint64_t* cost, uint32_t* hops,
                                uint8_t* fin, unsigned long long* agg, hipStream_t s) {
-    if (ts_v1()) {
-        launch(kern::table_search_dense, dim3((nq + 255u) / 256u), dim3(256), s,
-               reinterpret_cast<const uint2*>(adj), shift, row_of_col, dense, npad / 8u, qs, qt,
-               nq, kmoves, n, cost, hops, fin, agg);
-        return;
-    }
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::DenseRows{dense, npad / 8u}, qs,
                 qt, qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(1024),
                 ts_chunk_max(1024), s);
@@ -2973,12 +2526,6 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
                          const uint32_t* qt, const uint32_t* qrow, uint32_t nq, int32_t kmoves,
                          uint32_t n, uint64_t* cost, uint32_t* hops, uint8_t* fin,
                          unsigned long long* agg, hipStream_t s) {
-    if (ts_v1()) {
-        launch(kern::table_search, dim3((nq + 255u) / 256u), dim3(256), s,
-               reinterpret_cast<const uint2*>(adj), shift, row_of_col, offsets, runs, qs, qt, nq,
-               kmoves, n, cost, hops, fin, agg);
-        return;
-    }
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::RleRows{offsets, runs}, qs, qt,
                 qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(8192),
                 ts_chunk_max(1u << 30), s);

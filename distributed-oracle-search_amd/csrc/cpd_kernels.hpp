@@ -25,7 +25,6 @@ struct NarrowRows {
     uint32_t* base;
     uint32_t n;
     uint32_t* ovf;
-    uint32_t nt = 0;  // down-sweep stores non-temporal (set by the launcher, CPD_DOWN8_NT)
 };
 
 // One CH sweep level: `count` node slots starting at `slot0` of the
@@ -142,8 +141,7 @@ void launch_validate_rows(const uint64_t* offsets, const uint32_t* runs, uint32_
 void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,
                         uint32_t npad, uint32_t* dense, hipStream_t s);
 // table-search over dense move tables.  qs / qt: query columns, sorted by
-// target row; qrow[q]: the row of query q's target (row_of_col is only read
-// by the CPD_TS_V1=1 kernels).
+// target row; qrow[q]: the row of query q's target (row_of_col is unused).
 void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
                                const uint32_t* dense, uint32_t npad, const uint32_t* qs,
                                const uint32_t* qt, const uint32_t* qrow, uint32_t nq,

@@ -8,6 +8,7 @@
 #include <queue>
 
 #include "cpd_internal.hpp"
+#include "src_sha.h"
 
 namespace cpd {
 
@@ -292,7 +293,9 @@ extern "C" {
 
 const char* cpd_last_error(void) { return g_last_error.c_str(); }
 
-const char* cpd_version(void) { return "cpd-mi355x 0.1 gfx950"; }
+// CPD_SRC_SHA: sha256 (16 hex) of the sources this library was built from
+// (Makefile PROV_SRCS; cpd.src_sha() recomputes it from a tree).
+const char* cpd_version(void) { return "cpd-mi355x 0.3 gfx950 src:" CPD_SRC_SHA; }
 
 int cpd_partition_nbuckets(uint32_t nodenum, int method, uint32_t key,
                            uint32_t* nbuckets) {

@@ -12,6 +12,10 @@
 //                 [--no-pipeline]      build, then export, then write, per group
 //                 [--plan-only]        build / load the cached plan and exit
 //                 [--targets-from S]   only rows of targets of scenario S (q s t)
+//                 [--discard]          null sink: every row is still built and
+//                                      copied out of HBM (D2H), but no file is
+//                                      written (times the build + export path
+//                                      of a worker whose runs outgrow the disk)
 //
 // The plan (column order + hierarchy) is cached in D per graph; workers that
 // start together share it through cpd_plan_cache (one builds, the rest wait).
@@ -66,9 +70,30 @@ static void ok(int rc, const char* what) {
 // file (BucketFile), so no bucket is ever held whole in host memory.  A
 // bucket's .tmp is renamed once its last block is written.  The files are
 // byte-identical to the sequential path (--no-pipeline).
+// Destinations of the D2H copies: page-locked (cpd_host_alloc), one per
+// writer thread, grown on demand.
+struct PinnedBuf {
+    uint32_t* p = nullptr;
+    uint64_t cap = 0;
+    uint32_t* get(uint64_t n) {
+        if (n > cap) {
+            cpd_host_free(p);
+            p = nullptr;
+            cap = 0;
+            void* q = nullptr;
+            ok(cpd_host_alloc(std::max<uint64_t>(n, 1) * sizeof(uint32_t), &q), "pinned buffer");
+            p = static_cast<uint32_t*>(q);
+            cap = n;
+        }
+        return p;
+    }
+    ~PinnedBuf() { cpd_host_free(p); }
+};
+
 class Pipeline {
 public:
-    Pipeline(cpd_graph* g, uint32_t B, int threads) : g_(g), B_(B) {
+    Pipeline(cpd_graph* g, uint32_t B, int threads, bool discard)
+        : g_(g), B_(B), discard_(discard) {
         for (int i = 0; i < std::max(1, threads); ++i) pool_.emplace_back([this] { worker(); });
     }
     ~Pipeline() {
@@ -90,7 +115,7 @@ public:
         std::vector<uint64_t> bruns(nb, 0);  // runs of the bucket's rows scheduled so far
         std::vector<size_t> to_close;        // buckets finished by the block in flight
         for (size_t k = 0; k < nb; ++k)
-            if (first[k] == first[k + 1]) {  // empty bucket: header + one offset
+            if (first[k] == first[k + 1] && !discard_) {  // empty bucket: header + one offset
                 BucketFile f(paths[k], heads[k]);
                 const uint64_t zero = 0;
                 f.write_offsets(0, &zero, 1);
@@ -110,21 +135,22 @@ public:
             drain();
             t_wait += now() - tw;
             for (size_t k : to_close) {
-                files[k]->close(bruns[k]);
+                if (files[k]) files[k]->close(bruns[k]);
                 files[k].reset();
             }
             to_close.clear();
             cpd_rows* rr = r;
             for (size_t i = b0; i < b0 + cnt;) {
                 while (first[kb + 1] <= i) ++kb;
-                if (!files[kb]) files[kb] = std::make_unique<BucketFile>(paths[kb], heads[kb]);
-                BucketFile* f = files[kb].get();
+                if (!files[kb] && !discard_)
+                    files[kb] = std::make_unique<BucketFile>(paths[kb], heads[kb]);
+                BucketFile* f = files[kb].get();  // null: discard sink
                 const size_t seg_end = std::min<size_t>(first[kb + 1], b0 + cnt);
                 const uint32_t r0 = (uint32_t)(i - b0), r1 = (uint32_t)(seg_end - b0);
                 const uint32_t brow0 = (uint32_t)(i - first[kb]);
                 const uint64_t base = bruns[kb];
                 const bool last = seg_end == first[kb + 1];
-                submit([=] {  // bucket-relative offsets; the end offset with the last rows
+                if (f) submit([=] {  // bucket-relative offsets; the end offset with the last rows
                     std::vector<uint64_t> o;
                     for (uint32_t u = r0; u < r1 + (last ? 1u : 0u); ++u)
                         o.push_back(base + (*offs)[u] - (*offs)[r0]);
@@ -135,11 +161,13 @@ public:
                     while (p1 < r1 && (*offs)[p1 + 1] - (*offs)[p0] <= kPieceRuns) ++p1;
                     const uint64_t run0 = base + (*offs)[p0] - (*offs)[r0];
                     submit([=] {
-                        thread_local std::vector<uint32_t> buf;
+                        thread_local PinnedBuf buf;
                         const uint64_t nr = (*offs)[p1] - (*offs)[p0];
-                        buf.resize(nr);
-                        ok(cpd_rows_export_range(rr, p0, p1 - p0, nullptr, buf.data()), "export");
-                        f->write_runs(run0, buf.data(), nr);
+                        uint32_t* dst = buf.get(nr);
+                        const double te = now();
+                        ok(cpd_rows_export_range(rr, p0, p1 - p0, nullptr, dst), "export");
+                        note_export(te, now(), nr * sizeof(uint32_t));
+                        if (f) f->write_runs(run0, dst, nr);
                     });
                     p0 = p1;
                 }
@@ -152,13 +180,27 @@ public:
         const double tw = now();
         drain();
         t_wait += now() - tw;
-        for (size_t k : to_close) files[k]->close(bruns[k]);
+        for (size_t k : to_close)
+            if (files[k]) files[k]->close(bruns[k]);
     }
 
     double t_build = 0, t_wait = 0;
     uint64_t runs = 0;
+    // D2H copies: summed copy time over writer threads, bytes, first start /
+    // last end (their wall span)
+    double x_sum = 0, x_first = 0, x_last = 0;
+    uint64_t x_bytes = 0;
 
 private:
+    void note_export(double t0, double t1, uint64_t bytes) {
+        std::lock_guard<std::mutex> l(xmu_);
+        x_sum += t1 - t0;
+        x_bytes += bytes;
+        if (x_first == 0 || t0 < x_first) x_first = t0;
+        x_last = std::max(x_last, t1);
+    }
+    std::mutex xmu_;
+
     static constexpr uint64_t kPieceRuns = 64ull << 20;  // 256 MB of runs per copy+write
 
     void submit(std::function<void()> f) {
@@ -198,6 +240,7 @@ private:
 
     cpd_graph* g_;
     uint32_t B_;
+    bool discard_;
     cpd_rows* rows_[2] = {nullptr, nullptr};
     std::vector<std::thread> pool_;
     std::mutex mu_;
@@ -218,7 +261,7 @@ int main(int argc, char** argv) {
                      "usage: make_cpd_auto --input X.xy --partmethod {div|mod} --partkey K "
                      "--workerid I --maxworker W [--outdir D] [--device G] [--batch B] "
                      "[--threads T] [--plan P | --no-plan-cache] [--write-threads T] "
-                     "[--no-pipeline] [--plan-only] [--targets-from SCEN]\n");
+                     "[--no-pipeline] [--plan-only] [--targets-from SCEN] [--discard]\n");
         return 2;
     }
     int mcode = cli::method_code(method);
@@ -236,6 +279,7 @@ int main(int argc, char** argv) {
         std::string plan_path = a.str("plan", outdir + "/" + cpd::io::xy_stem(input) + "." + fph + ".plan");
         bool use_cache = !a.has("no-plan-cache");
         cpd_plan* plan = nullptr;
+        bool plan_loaded = false;
         double t0 = now();
         cpd_plan_opts o{};
         o.threads = (int)a.num("threads", 0);
@@ -247,6 +291,7 @@ int main(int argc, char** argv) {
             cli::check(cpd_plan_cache(plan_path.c_str(), g.row_ptr.data(), g.dst.data(), g.w.data(),
                                       g.n, g.m, &o, &plan, &status),
                        "plan");
+            plan_loaded = status == 0;
             std::printf("make_cpd_auto: %s plan %s\n",
                         status == 0 ? "loaded" : status == 1 ? "built and cached" : "built (cache not written)",
                         plan_path.c_str());
@@ -317,6 +362,12 @@ int main(int argc, char** argv) {
 
         double t_build = 0, t_io = 0;
         uint64_t rows_done = 0, runs_done = 0;
+        double x_sum = 0, x_span = 0;
+        uint64_t x_bytes = 0;
+        const bool discard = a.has("discard");
+        if (discard && a.has("no-pipeline"))
+            throw std::runtime_error("--discard needs the pipelined writer");
+        const double t_rows0 = now();
         cpd_rows* rows = nullptr;
         if (a.has("no-pipeline")) {
             size_t i = 0;
@@ -361,7 +412,7 @@ int main(int argc, char** argv) {
                 runs_done += tot;
             }
         } else {
-            Pipeline pl(dg, B, (int)a.num("write-threads", 8));
+            Pipeline pl(dg, B, (int)a.num("write-threads", 8), discard);
             std::vector<uint32_t> targets;
             std::vector<CpdBucket> heads(owned.size());
             std::vector<uint64_t> first(owned.size() + 1, 0);
@@ -387,7 +438,11 @@ int main(int argc, char** argv) {
             t_io = pl.t_wait;
             rows_done = targets.size();
             runs_done = pl.runs;
+            x_sum = pl.x_sum;
+            x_bytes = pl.x_bytes;
+            x_span = pl.x_last > pl.x_first ? pl.x_last - pl.x_first : 0.0;
         }
+        const double t_rows = now() - t_rows0;
         if (rows) cpd_rows_free(rows);
         cpd_graph_free(dg);
         cpd_plan_free(plan);
@@ -401,6 +456,19 @@ int main(int argc, char** argv) {
             t_plan, (unsigned long long)(info.ch_up_arcs + info.ch_dn_arcs), info.levels_up,
             info.levels_dn, t_build, rate, rate * g.m / 1e9, t_io,
             a.has("no-pipeline") ? "" : " (not hidden behind the build)", now() - t_start);
+        // one machine-readable line (bench.py's full-build leg reads it):
+        // rows_s = every owned row built and exported (and written, unless
+        // --discard); export = the D2H copies (summed over writer threads,
+        // and their wall span); wait = time the build loop stalled on them
+        std::printf(
+            "make_cpd_auto-json: {\"worker\": %lld, \"maxworker\": %lld, \"rows\": %llu, "
+            "\"runs\": %llu, \"batch\": %u, \"discard\": %s, \"read_s\": %.3f, \"plan_s\": %.3f, "
+            "\"plan_cached\": %s, \"rows_s\": %.3f, \"build_calls_s\": %.3f, \"wait_s\": %.3f, "
+            "\"export_bytes\": %llu, \"export_thread_s\": %.3f, \"export_span_s\": %.3f, "
+            "\"total_s\": %.3f}\n",
+            wid, W, (unsigned long long)rows_done, (unsigned long long)runs_done, B,
+            discard ? "true" : "false", t_read, t_plan, plan_loaded ? "true" : "false", t_rows,
+            t_build, t_io, (unsigned long long)x_bytes, x_sum, x_span, now() - t_start);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "make_cpd_auto: %s\n", e.what());
         return 1;

@@ -210,6 +210,15 @@ int  cpd_rows_export(const cpd_rows* r, uint64_t* offsets /* nrows+1 */,
 int  cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count,
                            uint64_t* offsets /* count+1 */, uint32_t* runs);
 int  cpd_rows_targets(const cpd_rows* r, uint32_t* targets /* nrows */);
+/* The batch lane each row was built in (lane = position in its sweep batch,
+ * 0..batch-1; rows are lane-sorted by Hilbert key with coordinates, else by
+ * column).  Results never depend on it; tests use it to cover every slab.   */
+int  cpd_rows_lanes(const cpd_rows* r, uint32_t* lanes /* nrows */);
+/* [gpu] Page-locked host memory for export destinations: a D2H copy into it
+ * runs at PCIe rate (a pageable destination is staged through a bounce
+ * buffer at a fraction of it).  Free with cpd_host_free.                    */
+int  cpd_host_alloc(size_t bytes, void** out);
+void cpd_host_free(void* p);
 /* Wait for the device work behind r: a build returns once its rows' run
  * counts are known, while the last batch's run emit may still be running
  * (it overlaps the next build's sweeps); every accessor above waits for it,

@@ -49,6 +49,19 @@ def deg8_graph():
     return graph_from_edges(n, edges)
 
 
+def ring2_graph():
+    """Out-degree <= 2 (a two-way ring with a few chords removed: 2-slot
+    adjacency, the shift-1 kernels), weights 1..5."""
+    rng = np.random.default_rng(2)
+    n = 500
+    edges = []
+    for a in range(n):
+        edges.append((a, (a + 1) % n, int(rng.integers(1, 6))))
+        if a % 7:
+            edges.append((a, (a - 1) % n, int(rng.integers(1, 6))))
+    return graph_from_edges(n, edges)
+
+
 def tie_graph():
     """Tiny weights -> many equal-cost paths (multi-bit first-move sets)."""
     g = cpd.synth_road_graph(24, 24, seed=11)
@@ -60,5 +73,6 @@ GRAPHS = {
     "ties": tie_graph,
     "irregular": irregular_graph,
     "deg8": deg8_graph,
+    "ring2": ring2_graph,
     "single": lambda: graph_from_edges(1, []),
 }

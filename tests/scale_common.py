@@ -50,3 +50,41 @@ def check_row_format(off, runs, n):
     inc[starts[1:] - 1] = True  # row boundaries
     assert np.all(inc)
     assert cols.max() < n
+
+
+def hilbert_keys(x, y):
+    """libcpd's lane key (cpd_gpu.cpp hilbert_keys): the Hilbert index of each
+    node's coordinates on a 2^16 x 2^16 grid over the bounding box."""
+    x = np.asarray(x, np.int64)
+    y = np.asarray(y, np.int64)
+    side = 1 << 16
+    x0, y0 = x.min(), y.min()
+    ext = max(x.max() - x0, y.max() - y0) + 1
+    px = (x - x0) * (side - 1) // ext
+    py = (y - y0) * (side - 1) // ext
+    d = np.zeros(len(x), np.int64)
+    s = side // 2
+    while s > 0:
+        rx = ((px & s) != 0).astype(np.int64)
+        ry = ((py & s) != 0).astype(np.int64)
+        d += s * s * ((3 * rx) ^ ry)
+        rot = ry == 0
+        flip = rot & (rx == 1)
+        px = np.where(flip, side - 1 - px, px)
+        py = np.where(flip, side - 1 - py, py)
+        px, py = np.where(rot, py, px), np.where(rot, px, py)
+        s //= 2
+    return (d & 0xFFFFFFFF).astype(np.uint64)
+
+
+def lane_of(g, order, targets):
+    """The batch lane each caller target occupies when the graph has
+    coordinates (cpd_gpu.cpp upload_targets: lanes sorted by (Hilbert key,
+    column)).  lane_of(...)[i] = lane of targets[i]."""
+    t = np.asarray(targets, np.int64)
+    keys = hilbert_keys(g.x, g.y)[t]
+    cols = np.asarray(order, np.uint64)[t]
+    idx = np.lexsort((cols, keys))  # by key, then column
+    lane = np.empty(len(t), np.int64)
+    lane[idx] = np.arange(len(t))
+    return lane

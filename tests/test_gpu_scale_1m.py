@@ -1,11 +1,14 @@
 """GPU parity at BASELINE.json configs[3]: the synthetic 1M-node / 2.5M-edge
 road graph (1000 x 1000 lattice, seed 1), partition div 8, worker 0's targets
-at the full default batch (16384 rows) — the bench's own workload.
+at the batch the bench times (auto: what free HBM holds, 21504 rows on an
+idle MI355X) — the bench's own workload and shape.
 
   - 128 rows spread over the worker's targets: bit-exact against the oracle;
-  - one full 16384-row batch: every row well formed, 8 rows (first / last /
-    interior lanes and slabs) bit-exact, then streamed into a dense index and
-    walked: free-flow cost == Dijkstra distance for every query of 16 targets;
+  - the bench's first full batch (worker 0's first B targets, Hilbert lane
+    order): every row well formed, and in EVERY 1024-lane slab the rows at
+    its first, last and one interior lane bit-exact against the oracle; then
+    the batch streamed into a dense index and walked: free-flow cost ==
+    Dijkstra distance for every query of 16 targets;
   - congested (.diff stand-in, SURVEY.md §8d: 10% of edges x U[1, 3], seed 3)
     and free-flow queries over the oracle's 128 rows, dense and RLE: cost,
     moves and finished flags bit-exact.
@@ -17,7 +20,7 @@ import pytest
 
 import cpd
 import oracle
-from scale_common import check_row_format, owned, plan_for, spread
+from scale_common import check_row_format, lane_of, owned, plan_for, spread
 
 pytestmark = pytest.mark.gpu
 
@@ -26,7 +29,7 @@ pytestmark = pytest.mark.gpu
 def w1m():
     g = cpd.synth_road_graph(1000, 1000, seed=1)
     plan = plan_for(g, "synth1000-s1")
-    dev = cpd.Graph(plan, device=0, batch=16384)  # the bench's default batch at 1M nodes
+    dev = cpd.Graph(plan, device=0)  # auto batch from free HBM, as bench.py runs
     dev.set_coords(g.x, g.y)  # Hilbert lane order, as the bench and make_cpd_auto run
     mine = owned(np.arange(g.n), 8, "div", 8, 0, g.n)
     yield g, plan, dev, mine
@@ -53,22 +56,29 @@ def test_1m_rows_bit_exact(w1m, rows128):
 def test_1m_full_batch(w1m):
     g, plan, dev, mine = w1m
     B = dev.batch
-    assert B == 16384
-    targets = mine[:B]
+    print(f"auto batch at 1M nodes: {B} rows ({B // 1024} slabs)")
+    assert B % 1024 == 0 and B >= 20480, B  # 21504 on an idle MI355X
+    targets = mine[:B]  # bench.py batch_of(owned, B, 0)
     rows = dev.build_rows(targets)
     nrows, total = rows.count()
     assert nrows == B
-    lanes = np.unique(np.concatenate([[0, 1, 1023, 1024, 8191, 8192, B - 2, B - 1],
-                                      np.arange(0, B, 997)]))
-    sample = [0, 1023, 1024, 5000, 8192, 12345, B - 2, B - 1]
-    for i in lanes:
+    for i in np.unique(np.concatenate([[0, 1, B - 2, B - 1], np.arange(0, B, 997)])):
         off, runs = rows.export_range(int(i), 1)
         check_row_format(off, runs, g.n)
+    # rows by LANE: first, last and one rotating interior lane of every slab
+    lane = lane_of(g, plan.order(), targets)
+    np.testing.assert_array_equal(rows.lanes(), lane)  # the restated lane order holds
+    row_at = np.empty(B, np.int64)
+    row_at[lane] = np.arange(B)
+    want = sorted({x for sl in range(B // 1024)
+                   for x in (1024 * sl, 1024 * sl + 1023, 1024 * sl + (397 * sl + 211) % 1024)})
+    sample = row_at[want]
+    assert len(sample) >= 3 * (B // 1024) - 2
     ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets[sample])
     for k, i in enumerate(sample):
-        off, runs = rows.export_range(i, 1)
+        off, runs = rows.export_range(int(i), 1)
         np.testing.assert_array_equal(runs, ref_runs[int(ref_off[k]):int(ref_off[k + 1])],
-                                      err_msg=f"row {i} (target {targets[i]})")
+                                      err_msg=f"row {i} lane {want[k]} (target {targets[i]})")
     # the whole batch as a streamed dense index (what fifo_auto holds), walked
     ix = cpd.Index.streamed(dev, targets, total, mode="dense")
     ix.append_rows(rows)

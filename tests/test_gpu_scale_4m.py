@@ -8,7 +8,9 @@ narrow/wide row switching and the batch sizing run at scale.
   - every row of the batch well formed (sampled lanes);
   - the batch streamed into a dense index and walked (queries: s uniform over
     the graph, t uniform over the batch, SURVEY.md §8d seed 6): every walk
-    finishes and free-flow cost == Dijkstra for every query of 8 targets.
+    finishes and free-flow cost == Dijkstra for every query of 8 targets;
+  - the worker's whole ~32.7k-row index and its share of the 10M-query batch,
+    as the bench serves them (test_4m_worker_index_serves_its_queries).
 """
 import gc
 
@@ -70,3 +72,47 @@ def test_4m_batch_bit_exact_and_walks(w4m):
         d = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, tt)
         sel = t == tt
         np.testing.assert_array_equal(cost[sel], d[s[sel]].astype(np.uint64))
+
+
+def test_4m_worker_index_serves_its_queries(w4m):
+    """configs[4] as bench.py --workload synth4m serves it: worker 0's WHOLE
+    row set (~32.7k rows, built batch by batch and streamed into one dense
+    index), then its share of the 10M-query batch (t uniform over the 256k
+    sample, s uniform, seed 6: ~1.25M queries).  Every walk finishes; for 16
+    probe targets cost == Dijkstra and cost / moves / flags are bit-exact
+    against the oracle's rows."""
+    g, plan, dev, mine = w4m
+    B = dev.batch
+    ix = cpd.Index.streamed(dev, mine, 1 << 62, mode="dense")
+    rows = None
+    for a in range(0, len(mine), B):
+        rows = dev.build_rows(mine[a:a + B], reuse=rows)
+        ix.append_rows(rows)
+    del rows
+    gc.collect()
+    assert ix.info()["added"] == len(mine)
+    qrng = np.random.default_rng(6)
+    sample = sample_targets(g.n, 262144, seed=5)
+    allt = sample[qrng.integers(0, 262144, 10_000_000)]
+    alls = qrng.integers(0, g.n, 10_000_000).astype(np.uint32)
+    sel = np.isin(allt, mine)
+    s, t = alls[sel], allt[sel].astype(np.uint32)
+    assert len(s) >= 200_000, len(s)
+    cost, hops, fin, st = ix.query(s, t)
+    assert fin.all() and st["finished"] == len(s)
+    # probes: the 16 targets with the most queries
+    uniq, cnt = np.unique(t, return_counts=True)
+    probe = np.sort(uniq[np.argsort(-cnt, kind="stable")[:16]])
+    qsel = np.isin(t, probe)
+    assert qsel.sum() >= 16
+    for tt in probe:
+        d = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, tt)
+        m = t == tt
+        np.testing.assert_array_equal(cost[m], d[s[m]].astype(np.uint64))
+    order = plan.order()
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, probe)
+    rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, order, probe, ref_off, ref_runs,
+                                     s[qsel], t[qsel])
+    np.testing.assert_array_equal(cost[qsel], rc)
+    np.testing.assert_array_equal(hops[qsel], rh)
+    np.testing.assert_array_equal(fin[qsel], rf)

@@ -28,6 +28,12 @@ def test_abi_exports_every_declared_symbol():
     assert "gfx950" in cpd.version()
 
 
+def test_library_built_from_this_tree():
+    """Build provenance: the hash libcpd.so embeds (Makefile SRC_SHA) equals the
+    hash of the sources shipped beside it."""
+    assert cpd.lib_src_sha() == cpd.src_sha()
+
+
 @pytest.mark.parametrize("method", ["mod", "div"])
 def test_partition_matches_oracle(method):
     rng = np.random.default_rng(1)
