@@ -458,9 +458,18 @@ def full_build_xy(args):
     return prefix + ".xy"
 
 
+def full_build_workers(args, world):
+    """Workers of the configuration's partition the full-build leg runs: the
+    partition key's (div 8: 8 workers, configs[3]'s "div 8"), or the rank
+    count if larger.  Rank r runs worker r, so every rank builds one whole
+    worker at any N (weak scaling, like the steps)."""
+    return max(world, args.partkey)
+
+
 def full_build(args, xy, world, rank, device):
-    """Run make_cpd_auto for worker `rank` of `world` with a fresh (cold) plan
-    cache shared by the node's ranks; returns its JSON phase line."""
+    """Run make_cpd_auto for worker `rank` of full_build_workers() with a
+    fresh (cold) plan cache shared by the node's ranks; returns its JSON phase
+    line."""
     import shutil
     outdir = os.path.join(args.cache, f"fb-out-{world}")
     if rank == 0:
@@ -471,7 +480,8 @@ def full_build(args, xy, world, rank, device):
             time.sleep(0.1)
     cmd = [os.path.join(ROOT, "bin", "make_cpd_auto"), "--input", xy, "--partmethod",
            args.partmethod, "--partkey", str(args.partkey), "--workerid", str(rank),
-           "--maxworker", str(world), "--outdir", outdir, "--device", str(device), "--discard"]
+           "--maxworker", str(full_build_workers(args, world)), "--outdir", outdir, "--device",
+           str(device), "--discard"]
     if args.batch:
         cmd += ["--batch", str(args.batch)]
     p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
@@ -755,8 +765,9 @@ def main():
         (tmax,) = comm.reduce([rec["total_s"]], "MAX")
         tot = comm.reduce([float(rec["rows"]), float(rec["runs"]), float(rec["export_bytes"])],
                           "SUM")
-        fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of {args.partmethod} "
-                      f"{args.partkey}, all owned rows, cold plan cache, --discard (D2H export "
+        fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of "
+                      f"{full_build_workers(args, world)} ({args.partmethod} {args.partkey}), one "
+                      "worker per rank: all its rows, cold plan cache, --discard (D2H export "
                       "into pinned host buffers, no file writes)",
               "total_s": round(tmax, 3), "rows": int(tot[0]), "runs": int(tot[1]),
               "rows_per_s_end_to_end": round(tot[0] / tmax, 1) if tmax else 0.0,

@@ -52,14 +52,17 @@ inline uint64_t mix(uint64_t z) {
 struct Witness {
     std::vector<uint64_t> dist;
     std::vector<uint32_t> stamp;
+    std::vector<uint32_t> tstamp;  // tstamp[v] == cur: v is a target of this search
     uint32_t cur = 0;
     std::vector<std::pair<uint64_t, uint32_t>> heap;
+    std::vector<std::pair<uint64_t, uint32_t>> tgt;  // (via, node), via descending
 
-    explicit Witness(uint32_t n) : dist(n), stamp(n, 0) {}
+    explicit Witness(uint32_t n) : dist(n), stamp(n, 0), tstamp(n, 0) {}
 
     void reset() {
         if (++cur == 0) {
             std::fill(stamp.begin(), stamp.end(), 0);
+            std::fill(tstamp.begin(), tstamp.end(), 0);
             cur = 1;
         }
         heap.clear();
@@ -70,21 +73,37 @@ struct Witness {
         dist[v] = d;
     }
     // Dijkstra from `src` over `out`, never entering `skip` or nodes with
-    // avoid[] set, until the frontier exceeds `limit_d` or `settle` nodes.
+    // avoid[] set, for the targets in `tgt` (set by the caller: (via, node),
+    // sorted by via descending).  Stops after `settle` settled nodes, or once
+    // the frontier passes the largest via of the targets not yet settled —
+    // every settled target's distance is final, and an unsettled one can no
+    // longer come in at or under its via.  (Round 2 ran on to the largest via
+    // of ALL targets; the witness decisions, get(x) <= via, are the same.)
     void run(const std::vector<std::vector<Adj>>& out, uint32_t src, uint32_t skip,
-             const uint8_t* avoid, uint64_t limit_d, uint32_t settle) {
+             const uint8_t* avoid, uint32_t settle) {
         reset();
+        for (const auto& t : tgt) tstamp[t.second] = cur;
         set(src, 0);
         heap.push_back({0, src});
         auto cmp = [](const std::pair<uint64_t, uint32_t>& a,
                       const std::pair<uint64_t, uint32_t>& b) { return a.first > b.first; };
         uint32_t settled = 0;
+        size_t open = 0;  // tgt[open..]: the targets not yet settled start here (via order)
+        auto advance = [&] {
+            while (open < tgt.size() && stamp[tgt[open].second] == cur &&
+                   tstamp[tgt[open].second] != cur)
+                ++open;
+        };
         while (!heap.empty()) {
             std::pop_heap(heap.begin(), heap.end(), cmp);
             auto [d, v] = heap.back();
             heap.pop_back();
             if (d != get(v)) continue;
-            if (d > limit_d || ++settled > settle) break;
+            if (open == tgt.size() || d > tgt[open].first || ++settled > settle) break;
+            if (tstamp[v] == cur) {  // a target settles: its distance is final
+                tstamp[v] = cur - 1;
+                advance();
+            }
             for (const Adj& a : out[v]) {
                 if (a.v == skip || (avoid && avoid[a.v])) continue;
                 uint64_t nd = d + a.w;
@@ -107,31 +126,39 @@ struct Contractor {
     uint32_t settle_contract, settle_sim;
     std::vector<Witness> scratch;
 
-    // Shortcuts needed to contract v (avoid = same-round nodes, or nullptr).
-    // If `outv` is null only counts them.
-    uint32_t shortcuts(uint32_t v, const uint8_t* avoid, uint32_t settle,
-                       std::vector<Shortcut>* outv, Witness& ws) const {
-        uint32_t count = 0;
-        const auto& ins = in[v];
+    // Shortcuts needed to contract v through its in-neighbour ins[i] (avoid =
+    // same-round nodes, or nullptr).  If `outv` is null only counts them.
+    uint32_t shortcuts_via(uint32_t v, size_t i, const uint8_t* avoid, uint32_t settle,
+                           std::vector<Shortcut>* outv, Witness& ws) const {
+        const Adj& a = in[v][i];
         const auto& outs = out[v];
-        if (ins.empty() || outs.empty()) return 0;
-        uint32_t wmax_out = 0;
-        for (const Adj& b : outs) wmax_out = std::max(wmax_out, b.w);
-        for (const Adj& a : ins) {
-            uint64_t limit = (uint64_t)a.w + wmax_out;
-            ws.run(out, a.v, v, avoid, limit, settle);
-            for (const Adj& b : outs) {
-                if (b.v == a.v) continue;
-                uint64_t via = (uint64_t)a.w + b.w;
-                if (ws.get(b.v) <= via) continue;
-                ++count;
-                if (outv) {
-                    if (via >= 0xFFFFFFFFull)
-                        throw Error(CPD_E_RANGE, "shortcut weight >= 2^32-1");
-                    outv->push_back({a.v, b.v, (uint32_t)via});
-                }
+        ws.tgt.clear();
+        for (const Adj& b : outs)
+            if (b.v != a.v) ws.tgt.push_back({(uint64_t)a.w + b.w, b.v});
+        if (ws.tgt.empty()) return 0;
+        std::sort(ws.tgt.begin(), ws.tgt.end(),
+                  [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) {
+                      return x.first != y.first ? x.first > y.first : x.second < y.second;
+                  });
+        ws.run(out, a.v, v, avoid, settle);
+        uint32_t count = 0;
+        for (const Adj& b : outs) {
+            if (b.v == a.v) continue;
+            uint64_t via = (uint64_t)a.w + b.w;
+            if (ws.get(b.v) <= via) continue;
+            ++count;
+            if (outv) {
+                if (via >= 0xFFFFFFFFull) throw Error(CPD_E_RANGE, "shortcut weight >= 2^32-1");
+                outv->push_back({a.v, b.v, (uint32_t)via});
             }
         }
+        return count;
+    }
+    uint32_t shortcuts(uint32_t v, const uint8_t* avoid, uint32_t settle,
+                       std::vector<Shortcut>* outv, Witness& ws) const {
+        if (in[v].empty() || out[v].empty()) return 0;
+        uint32_t count = 0;
+        for (size_t i = 0; i < in[v].size(); ++i) count += shortcuts_via(v, i, avoid, settle, outv, ws);
         return count;
     }
 
@@ -140,10 +167,12 @@ struct Contractor {
     // graphs (fewest arcs at ~same level count; bench/DESIGN.md).
     int64_t prio_ed = 8, prio_del = 2, prio_depth = 3;
 
-    int64_t priority(uint32_t v, Witness& ws) const {
-        int64_t sc = shortcuts(v, nullptr, settle_sim, nullptr, ws);
+    int64_t priority_of(uint32_t v, int64_t sc) const {
         int64_t ed = sc - (int64_t)in[v].size() - (int64_t)out[v].size();
         return prio_ed * ed + prio_del * (int64_t)deleted[v] + prio_depth * (int64_t)depth[v];
+    }
+    int64_t priority(uint32_t v, Witness& ws) const {
+        return priority_of(v, shortcuts(v, nullptr, settle_sim, nullptr, ws));
     }
 
     bool less_key(uint32_t a, uint32_t b) const {
@@ -216,6 +245,7 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
     std::vector<uint32_t> remaining(n);
     std::iota(remaining.begin(), remaining.end(), 0u);
 
+    const double t_init = now_seconds();
 #pragma omp parallel for schedule(dynamic, 256) num_threads(threads)
     for (int64_t i = 0; i < (int64_t)n; ++i) {
 #ifdef _OPENMP
@@ -229,7 +259,16 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
     uint32_t next_rank = 0, round = 0;
     std::vector<uint32_t> S, affected;
     std::vector<std::vector<Shortcut>> sc_local;
+    std::vector<std::pair<uint32_t, uint32_t>> pairs;  // (node, in-neighbour index)
+    std::vector<uint32_t> pair_sc;
     double t0 = now_seconds();
+    double tph[5] = {0, 0, 0, 0, 0};  // pick, contract, remove, insert, priorities (verbose)
+    double ta = t0;
+    auto phase = [&](int k) {
+        const double tb = now_seconds();
+        tph[k] += tb - ta;
+        ta = tb;
+    };
     while (!remaining.empty()) {
         // 1. independent set of local priority minima (1-hop, both directions)
         S.clear();
@@ -249,18 +288,27 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
             if (pick[i]) S.push_back(remaining[i]);
         for (uint32_t v : S) C.sel[v] = 1;
 
-        // 2. shortcuts for every selected node, avoiding all selected nodes
-        sc_local.assign(S.size(), {});
-#pragma omp parallel for schedule(dynamic, 16) num_threads(threads)
-        for (int64_t i = 0; i < (int64_t)S.size(); ++i) {
+        phase(0);
+        // 2. shortcuts for every selected node, avoiding all selected nodes:
+        // one task per (node, in-neighbour) witness search, so that the few
+        // high-degree nodes of the late rounds still spread over every thread
+        pairs.clear();
+        for (uint32_t v : S)
+            if (!C.out[v].empty())
+                for (size_t i = 0; i < C.in[v].size(); ++i) pairs.push_back({v, (uint32_t)i});
+        sc_local.assign(pairs.size(), {});
+#pragma omp parallel for schedule(dynamic, 8) num_threads(threads)
+        for (int64_t i = 0; i < (int64_t)pairs.size(); ++i) {
 #ifdef _OPENMP
             Witness& ws = C.scratch[omp_get_thread_num()];
 #else
             Witness& ws = C.scratch[0];
 #endif
-            C.shortcuts(S[i], C.sel.data(), C.settle_contract, &sc_local[i], ws);
+            C.shortcuts_via(pairs[i].first, pairs[i].second, C.sel.data(), C.settle_contract,
+                            &sc_local[i], ws);
         }
 
+        phase(1);
         // 3. record hierarchy arcs, ranks
         for (uint32_t v : S) {
             H.rank[v] = next_rank++;
@@ -303,6 +351,7 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
             std::vector<Adj>().swap(C.in[v]);
         }
 
+        phase(2);
         // 5. insert shortcuts, grouped by owner list for determinism
         std::vector<Shortcut> all;
         for (auto& l : sc_local) all.insert(all.end(), l.begin(), l.end());
@@ -342,27 +391,49 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
 
         for (uint32_t v : S) C.sel[v] = 0;
 
-        // 6. priorities of affected nodes, then drop S from `remaining`
-#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-        for (int64_t i = 0; i < (int64_t)affected.size(); ++i) {
+        phase(3);
+        // 6. priorities of affected nodes (again one task per witness search),
+        // then drop S from `remaining`
+        pairs.clear();
+        for (uint32_t u : affected)
+            if (!C.done[u] && !C.out[u].empty())
+                for (size_t i = 0; i < C.in[u].size(); ++i) pairs.push_back({u, (uint32_t)i});
+        pair_sc.assign(pairs.size(), 0);
+#pragma omp parallel for schedule(dynamic, 16) num_threads(threads)
+        for (int64_t i = 0; i < (int64_t)pairs.size(); ++i) {
 #ifdef _OPENMP
             Witness& ws = C.scratch[omp_get_thread_num()];
 #else
             Witness& ws = C.scratch[0];
 #endif
-            uint32_t u = affected[i];
-            if (!C.done[u]) C.prio[u] = C.priority(u, ws);
+            pair_sc[i] = C.shortcuts_via(pairs[i].first, pairs[i].second, nullptr, C.settle_sim,
+                                         nullptr, ws);
+        }
+        {
+            size_t k = 0;
+            for (uint32_t u : affected) {
+                if (C.done[u]) continue;
+                int64_t sc = 0;
+                while (k < pairs.size() && pairs[k].first == u) sc += pair_sc[k++];
+                C.prio[u] = C.priority_of(u, sc);
+            }
         }
         size_t k = 0;
         for (uint32_t v : remaining)
             if (!C.done[v]) remaining[k++] = v;
         remaining.resize(k);
+        phase(4);
         ++round;
-        if (verbose && (round % 50 == 0 || remaining.empty()))
-            std::fprintf(stderr, "[ch] round %u contracted %zu remaining %zu (%.1fs)\n",
-                         round, S.size(), remaining.size(), now_seconds() - t0);
+        if (verbose && (round % 10 == 0 || remaining.empty()))
+            std::fprintf(stderr, "[ch] round %u contracted %zu remaining %zu pairs %zu (%.1fs) prio %.2f\n",
+                         round, S.size(), remaining.size(), pairs.size(), now_seconds() - t0, tph[4]);
     }
     C.scratch.clear();
+    if (verbose)
+        std::fprintf(stderr,
+                     "[ch] initial priorities %.2fs; rounds: pick %.2f contract %.2f remove %.2f "
+                     "insert %.2f priorities %.2f s\n",
+                     t0 - t_init, tph[0], tph[1], tph[2], tph[3], tph[4]);
 
     // Hierarchy CSRs (node space, sorted by head for determinism).
     H.up_off.assign(n + 1, 0);
