@@ -424,6 +424,9 @@ struct cpd_index {
     DevBuf<uint32_t> stage;
     DevBuf<uint64_t> stage_off;
     DevBuf<uint32_t> flag;
+    // expand_rows work split: first run-chunk of each row being expanded
+    std::vector<uint32_t> chunk_first_h;
+    DevBuf<uint32_t> chunk_first;
 
     bool use_dense() const {
         if (stream_dense) return true;
@@ -1348,13 +1351,36 @@ void check_chunk_offsets(const uint64_t* offsets, uint32_t count) {
         CPD_REQUIRE(offsets[i + 1] > offsets[i], CPD_E_ARG, "index: empty or unsorted row");
 }
 
+// expand_rows' / validate_rows' work split for `count` rows whose host
+// offsets are h_off (count + 1 values): the first run-chunk of each row,
+// uploaded to ix->chunk_first; returns the number of chunks.  Every caller
+// syncs the stream before the next call reuses the table.
+uint32_t prepare_chunks(cpd_index* ix, const uint64_t* h_off, uint32_t count) {
+    const uint64_t per = expand_chunk_runs();
+    std::vector<uint32_t>& cf = ix->chunk_first_h;
+    cf.assign((size_t)count + 1, 0);
+    uint64_t tot = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        cf[i] = (uint32_t)tot;
+        tot += (h_off[i + 1] - h_off[i] + per - 1) / per;
+        CPD_REQUIRE(tot < (1ull << 31), CPD_E_RANGE, "index: too many runs in one append");
+    }
+    cf[count] = (uint32_t)tot;
+    ix->chunk_first.upload(cf.data(), cf.size(), ix->g->stream);
+    return (uint32_t)tot;
+}
+
 // Format check of `count` device rows (validate_rows); throws on a bad row.
-void validate_device_rows(cpd_index* ix, const uint64_t* d_off, const uint32_t* d_runs,
-                          uint32_t count) {
+// Leaves the rows' chunk table in ix->chunk_first and returns its size, for
+// expand_into.
+uint32_t validate_device_rows(cpd_index* ix, const uint64_t* d_off, const uint32_t* d_runs,
+                              const uint64_t* h_off, uint32_t count) {
     cpd_graph* g = ix->g;
+    const uint32_t chunks = prepare_chunks(ix, h_off, count);
     HIP_CHECK(hipMemsetAsync(ix->flag.p, 0, sizeof(uint32_t), g->stream));
-    g->timed("validate_rows", 0.0, [&] {
-        launch_validate_rows(d_off, d_runs, count, g->n, ix->flag.p, g->stream);
+    g->timed("validate_rows", 4.0 * (double)(h_off[count] - h_off[0]), [&] {
+        launch_validate_rows(d_off, d_runs, ix->chunk_first.p, count, chunks, g->n, ix->flag.p,
+                             g->stream);
     });
     uint32_t bad = 0;
     HIP_CHECK(hipMemcpyAsync(&bad, ix->flag.p, sizeof bad, hipMemcpyDeviceToHost, g->stream));
@@ -1362,18 +1388,23 @@ void validate_device_rows(cpd_index* ix, const uint64_t* d_off, const uint32_t* 
     CPD_REQUIRE(!bad, CPD_E_ARG,
                 "index: malformed row (must start at column 0, run columns strictly increasing "
                 "and < n)");
+    return chunks;
 }
 
-// Expand `count` rows (device offsets into d_runs) into dense rows starting
-// at index row `first`.
-void expand_into(cpd_index* ix, const uint64_t* d_off, const uint32_t* d_runs, uint32_t count,
-                 uint64_t runs_in_chunk, uint32_t first) {
+// Expand `count` rows (device offsets into d_runs; h_off = the same count + 1
+// offsets on the host) into dense rows starting at index row `first`.
+// chunks: the rows' chunk table is already in ix->chunk_first (what
+// validate_device_rows returned), or 0 to build it here.
+void expand_into(cpd_index* ix, const uint64_t* d_off, const uint32_t* d_runs,
+                 const uint64_t* h_off, uint32_t count, uint64_t runs_in_chunk, uint32_t first,
+                 uint32_t chunks = 0) {
     cpd_graph* g = ix->g;
     const size_t wpr = g->npad / 8u;
+    if (!chunks) chunks = prepare_chunks(ix, h_off, count);
     g->timed("expand_rows", 4.0 * (double)runs_in_chunk + 4.0 * (double)wpr * count + 16.0 * count,
              [&] {
-                 launch_expand_rows(d_off, d_runs, count, g->npad, ix->dense.p + first * wpr,
-                                    g->stream);
+                 launch_expand_rows(d_off, d_runs, ix->chunk_first.p, count, chunks, g->npad,
+                                    ix->dense.p + first * wpr, g->stream);
              });
 }
 
@@ -1397,7 +1428,7 @@ void append_host(cpd_index* ix, uint32_t count, const uint64_t* offsets, const u
         HIP_CHECK(hipMemcpyAsync(ix->off.p + ix->added, o.data(), o.size() * sizeof(uint64_t),
                                  hipMemcpyHostToDevice, s));
         HIP_CHECK(hipStreamSynchronize(s));
-        validate_device_rows(ix, ix->off.p + ix->added, ix->runs.p, count);
+        validate_device_rows(ix, ix->off.p + ix->added, ix->runs.p, o.data(), count);
         ix->offsets.insert(ix->offsets.end(), o.begin() + 1, o.end());
         ix->total += nr;
         ix->added += count;
@@ -1416,8 +1447,8 @@ void append_host(cpd_index* ix, uint32_t count, const uint64_t* offsets, const u
                                  hipMemcpyHostToDevice, s));
         HIP_CHECK(hipMemcpyAsync(ix->stage_off.p, o.data(), o.size() * sizeof(uint64_t),
                                  hipMemcpyHostToDevice, s));
-        validate_device_rows(ix, ix->stage_off.p, ix->stage.p, r1 - r0);
-        expand_into(ix, ix->stage_off.p, ix->stage.p, r1 - r0, pr, ix->added);
+        const uint32_t ch = validate_device_rows(ix, ix->stage_off.p, ix->stage.p, o.data(), r1 - r0);
+        expand_into(ix, ix->stage_off.p, ix->stage.p, o.data(), r1 - r0, pr, ix->added, ch);
         g->sync();  // the stage is reused by the next piece
         ix->added += r1 - r0;
         r0 = r1;
@@ -1452,7 +1483,7 @@ void append_built(cpd_index* ix, const cpd_rows* r) {
         ix->offsets.insert(ix->offsets.end(), o.begin() + 1, o.end());
         ix->total += r->total;
     } else {
-        expand_into(ix, r->off.p, r->runs.p, r->nrows, r->total, ix->added);
+        expand_into(ix, r->off.p, r->runs.p, r->offsets.data(), r->nrows, r->total, ix->added);
         g->sync();
     }
     ix->added += r->nrows;
@@ -1606,7 +1637,8 @@ void ensure_dense(cpd_index* ix) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(g->npad / kFmTile < 65536u, CPD_E_RANGE, "graph too large for dense tables");
     ix->dense.alloc((size_t)ix->nrows * (g->npad / 8u));
-    if (ix->nrows) expand_into(ix, ix->off.p, ix->runs.p, ix->nrows, ix->total, 0);
+    if (ix->nrows)
+        expand_into(ix, ix->off.p, ix->runs.p, ix->offsets.data(), ix->nrows, ix->total, 0);
     g->sync();
     ix->dense_ready = true;
 }

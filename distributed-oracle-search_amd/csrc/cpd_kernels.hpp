@@ -132,14 +132,21 @@ void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t*
                     hipStream_t s);
 
 // *bad |= 1 if some row [0, nrows) of (offsets, runs) does not start at column
-// 0, has non-increasing run columns, a column >= n, or is empty.  Rows from
-// outside the library pass this before expand_rows / the walks touch them.
-void launch_validate_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,
+// 0, has non-increasing run columns or a column >= n (empty rows: refused by
+// the caller).  Rows from outside the library pass this before expand_rows /
+// the walks touch them.  chunk_first / total_chunks as for launch_expand_rows.
+void launch_validate_rows(const uint64_t* offsets, const uint32_t* runs,
+                          const uint32_t* chunk_first, uint32_t nrows, uint32_t total_chunks,
                           uint32_t n, uint32_t* bad, hipStream_t s);
 
-// RLE rows -> dense 4-bit move tables, npad/8 words per row.
-void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, uint32_t nrows,
-                        uint32_t npad, uint32_t* dense, hipStream_t s);
+// RLE rows -> dense 4-bit move tables, npad/8 words per row.  Work is cut in
+// chunks of expand_chunk_runs() runs: chunk_first[row] (nrows + 1 values) =
+// sum over earlier rows of ceil(R / expand_chunk_runs()), total_chunks its
+// last value.  Rows must be well formed (validate_rows).
+uint32_t expand_chunk_runs();
+void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, const uint32_t* chunk_first,
+                        uint32_t nrows, uint32_t total_chunks, uint32_t npad, uint32_t* dense,
+                        hipStream_t s);
 // table-search over dense move tables.  qs / qt: query columns, sorted by
 // target row; qrow[q]: the row of query q's target (row_of_col is unused).
 void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,

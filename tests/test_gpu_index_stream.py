@@ -110,7 +110,13 @@ def test_malformed_rows_rejected(env, mode):
     bad_order[2] = bad_order[1]                 # columns not increasing
     bad_col = two.copy()
     bad_col[int(o2[1]) - 1] = (g.n << 4) | 1    # column >= n
-    for r in (bad_start, bad_order, bad_col):
+    # at the kernels' 512-run chunk seams (rows here hold ~1500 runs)
+    assert int(o2[1]) > 1100
+    seam = two.copy()
+    seam[512] = seam[511]
+    seam2 = two.copy()
+    seam2[1024] = seam2[1023] - (1 << 4)
+    for r in (bad_start, bad_order, bad_col, seam, seam2):
         ix = cpd.Index.streamed(dev, targets[:2], int(o2[-1]), mode=mode)
         with pytest.raises(cpd.CpdError) as ei:
             ix.append(o2, r)
@@ -139,3 +145,31 @@ def test_move_naming_no_edge_stops_walk(env, mode):
     np.testing.assert_array_equal(h, rh)
     np.testing.assert_array_equal(f, rf)
     assert not f.any() and not h.any()
+
+
+@pytest.mark.parametrize("mode", ["dense", "rle"])
+def test_crafted_row_lengths(env, mode):
+    """Rows of 1, 2, 511, 512, 513, 1025 and n runs (random starts, random
+    moves 0..3, some naming no edge): the dense expansion's run chunks and
+    their 8-run lookahead, against the oracle's walk over the same rows."""
+    g, plan, dev = env[:3]
+    rng = np.random.default_rng(9)
+    lens = [1, 2, 511, 512, 513, 1025, g.n]
+    targets = rng.choice(g.n, size=len(lens), replace=False).astype(np.uint32)
+    rows = []
+    for R in lens:
+        cols = np.sort(rng.choice(np.arange(1, g.n), size=R - 1, replace=False)) if R > 1 else []
+        cols = np.concatenate([[0], cols]).astype(np.uint32)
+        rows.append((cols << 4) | rng.integers(0, 4, R).astype(np.uint32))
+    off = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.uint64)
+    runs = np.concatenate(rows).astype(np.uint32)
+    ix = cpd.Index.streamed(dev, targets, int(off[-1]), mode=mode)
+    ix.append(off, runs)
+    nq = 3000
+    s = rng.integers(0, g.n, nq).astype(np.uint32)
+    t = targets[rng.integers(0, len(targets), nq)]
+    rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, plan.order(), targets, off, runs, s, t)
+    cost, hops, fin, _ = ix.query(s, t)
+    np.testing.assert_array_equal(cost, rc)
+    np.testing.assert_array_equal(hops, rh)
+    np.testing.assert_array_equal(fin, rf)
