@@ -1868,108 +1868,41 @@ __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
 // CPD-heuristic search (semantics restated in
 // oracle/cpd_oracle.c ora_cpd_search, [U]).
 //
-// Per index row r (target t), three tables over the columns, computed from
-// the dense move table by pointer jumping over the CPD's next-hop tree — the
-// CPD walk from every column at once, in log2(n) + 1 doubling rounds:
-//   hrow[r][c] = free-flow cost of the CPD path c -> t (the heuristic),
-//   crow[r][c] = its cost under the selected weights (the incumbent bound),
-//   lrow[r][c] = its moves;  INF (hrow, crow) when the walk never reaches t.
-// Jump state per (row, column): next column (kJumpBad = no path), cf, cw,
-// lw; t points to itself with zero cost (absorbing).
-constexpr uint32_t kJumpBad = 0xFFFFFFFFu;
-constexpr uint64_t kInf64 = 0xFFFFFFFFFFFFFFFFull;
-
-struct JumpState {
-    uint32_t* next;
-    uint64_t* cf;
-    uint64_t* cw;
-    uint32_t* lw;
-};
-
-__global__ __launch_bounds__(256) void jump_init(const uint32_t* __restrict__ dense,
-                                                 uint32_t wpr, const uint2* __restrict__ adj_f,
-                                                 const uint2* __restrict__ adj_w, uint32_t shift,
-                                                 const uint32_t* __restrict__ tcol, uint32_t rows,
-                                                 uint32_t n, JumpState js) {
-    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (j >= (uint64_t)rows * n) return;
-    const uint32_t r = (uint32_t)(j / n), c = (uint32_t)(j - (uint64_t)r * n);
-    uint32_t nx = kJumpBad, l = 0;
-    uint64_t f = 0, w = 0;
-    if (c == tcol[r]) {
-        nx = c;
-    } else {
-        const uint32_t mv = (dense[(size_t)r * wpr + (c >> 3)] >> (4u * (c & 7u))) & 0xFu;
-        if (!(mv >> shift)) {
-            const size_t e = ((size_t)c << shift) + mv;
-            const uint2 ef = adj_f[e];
-            if (ef.x != kNoEdge) {
-                nx = ef.x;
-                f = ef.y;
-                w = adj_w[e].y;
-                l = 1;
-            }
-        }
-    }
-    js.next[j] = nx;
-    js.cf[j] = f;
-    js.cw[j] = w;
-    js.lw[j] = l;
-}
-
-// One doubling round a -> b: b(c) = a(c) followed by a(next(c)).
-__global__ __launch_bounds__(256) void jump_round(JumpState a, JumpState b,
-                                                  const uint32_t* __restrict__ tcol, uint32_t rows,
-                                                  uint32_t n) {
-    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (j >= (uint64_t)rows * n) return;
-    const uint32_t r = (uint32_t)(j / n);
-    const uint32_t nx = a.next[j];
-    uint32_t o = nx;
-    uint64_t f = a.cf[j], w = a.cw[j];
-    uint32_t l = a.lw[j];
-    if (nx != kJumpBad && nx != tcol[r]) {
-        const uint64_t k = (uint64_t)r * n + nx;
-        o = a.next[k];
-        if (o != kJumpBad) {
-            f += a.cf[k];
-            w += a.cw[k];
-            l += a.lw[k];
-        }
-    }
-    b.next[j] = o;
-    b.cf[j] = f;
-    b.cw[j] = w;
-    b.lw[j] = l;
-}
-
-__global__ __launch_bounds__(256) void jump_final(JumpState a, const uint32_t* __restrict__ tcol,
-                                                  uint32_t rows, uint32_t n,
-                                                  uint64_t* __restrict__ hrow,
-                                                  uint64_t* __restrict__ crow,
-                                                  uint32_t* __restrict__ lrow, int write_h) {
-    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (j >= (uint64_t)rows * n) return;
-    const uint32_t r = (uint32_t)(j / n);
-    const bool ok = a.next[j] == tcol[r];
-    if (write_h) hrow[j] = ok ? a.cf[j] : kInf64;
-    crow[j] = ok ? a.cw[j] : kInf64;
-    lrow[j] = ok ? a.lw[j] : 0u;
-}
-
-// The search, one lane per query, lanes refilled from the wave's chunk of the
+// One lane per query, lanes refilled from the wave's chunk of the
 // target-sorted batch (as table_walk).  Each lane slot owns a workspace in
-// HBM: an open-addressing hash of the columns seen (tag = query + 1, column,
-// g, depth) with 2C slots, and a binary heap of C entries keyed (f, column, g)
-// — the oracle's order.  A lane advances its query by one pop per loop
-// iteration, so lanes of a wave with searches of different lengths stay busy.
-// A query whose search needs more than C nodes or heap entries stops
-// unfinished and is counted in agg[7] (overflow) — never silently wrong.
+// HBM: an open-addressing hash of the columns met (2C slots, at most C used),
+// a binary heap of C entries keyed (f, column, g) — the oracle's order — and
+// a walk stack of C entries.  A hash entry is
+//   Ent {tag, column, g lo, g hi}       tag = query + 1; g = INF: not (yet) in
+//                                       the search (only walked)
+//   Memo {hf lo, hf hi, cw lo, cw hi}   the CPD path from the column to t:
+//                                       free-flow cost, cost under the
+//                                       selected weights (INF: no path)
+//   Aux {depth, lw | state << 30}       search depth; the path's moves; state
+//                                       1 = walked, 2 = on the current walk
+// The heuristic and incumbent values come from memoised CPD walks over the
+// dense move row of t (the oracle's ora_walk): a walk follows moves until it
+// meets a walked column (or t, walked with zeros), then assigns every column
+// it passed its suffix cost, popping the walk stack; meeting a column of the
+// current walk again (a zero-weight cycle) or a move that names no edge gives
+// the whole walk INF.  Nothing is precomputed per row, so an index of any
+// size can be searched (round 2 kept 20 B per column per row of tables).
+// A search whose columns (walked or searched) outgrow C stops unfinished and
+// is counted in agg[7] (overflow) — never silently wrong.
+// Time limit (process_query.py:149-160 `time`, ns): checked with the stop
+// conditions at every pop; elapsed = wall clock since the search began
+// (s_memrealtime, 100 MHz) or, with a virtual tick (tests), tick x (expanded
+// + touched) so far — the oracle's deterministic restatement.
+constexpr uint64_t kInf64 = 0xFFFFFFFFFFFFFFFFull;
+constexpr uint32_t kOnWalk = 2u, kWalked = 1u;
+
 struct SearchWs {
-    uint4* hk;      // [slots][2C] tag, column, g lo, g hi
-    uint32_t* hd;   // [slots][2C] depth
-    uint4* he;      // [slots][C] f lo, f hi, g lo, g hi
-    uint32_t* hc;   // [slots][C] column
+    uint4* ent;     // [slots][2C]
+    uint4* memo;    // [slots][2C]
+    uint2* aux;     // [slots][2C]
+    uint4* he;      // [slots][C] heap: f lo, f hi, g lo, g hi
+    uint32_t* hc;   // [slots][C] heap: column
+    uint4* stk;     // [slots][C] walk stack: hash slot, w free, w selected, -
     uint32_t cap;   // C (power of 2)
 };
 
@@ -1977,7 +1910,8 @@ struct SearchOpt {
     double hscale, fscale;
     int32_t kmoves;
     int64_t itrs;
-    uint64_t time_ticks;  // 0 = none; else limit in 100-MHz s_memrealtime ticks
+    uint64_t time_ns;     // 0 = none
+    uint64_t tick_ns;     // 0 = wall clock, else the virtual clock's tick
 };
 
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) {
@@ -1991,25 +1925,18 @@ __device__ __forceinline__ bool hkey_less(uint64_t f1, uint32_t c1, uint64_t g1,
     return g1 < g2;
 }
 
-struct Lane {
-    uint32_t q, s, t, row, hsize, best_len, tag;
-    uint64_t ub, t0;
-    uint32_t expanded, inserted, touched, updated, surplus;
-    bool done, overflow;
-};
-
-// Hash probe: slot index of column c (found = true) or of the free slot to
-// insert it in; 2C slots at most 50% full (inserts beyond C overflow).
-__device__ __forceinline__ uint32_t hprobe(const uint4* __restrict__ hk, uint32_t mask,
-                                           uint32_t tag, uint32_t c, bool& found, uint4& ent) {
+// Hash probe: slot of column c (found = true) or the free slot to insert it
+// in (2C slots, at most C used: probes end).
+__device__ __forceinline__ uint32_t hprobe(const uint4* __restrict__ ent, uint32_t mask,
+                                           uint32_t tag, uint32_t c, bool& found) {
     uint32_t i = (c * 0x9E3779B1u) & mask;
     for (;;) {
-        ent = hk[i];
-        if (ent.x != tag) {
+        const uint4 e = ent[i];
+        if (e.x != tag) {
             found = false;
             return i;
         }
-        if (ent.y == c) {
+        if (e.y == c) {
             found = true;
             return i;
         }
@@ -2069,59 +1996,157 @@ __device__ __forceinline__ void heap_pop(uint4* __restrict__ he, uint32_t* __res
     hc[i] = lc;
 }
 
+struct Lane {
+    uint32_t q, s, t, tag, hsize, used, best_len;
+    uint64_t ub, t0;
+    uint32_t expanded, inserted, touched, updated, surplus;
+    bool done, overflow;
+};
+
+// The lane's workspace (one slot's arrays).
+struct LaneWs {
+    uint4* __restrict__ ent;
+    uint4* __restrict__ memo;
+    uint2* __restrict__ aux;
+    uint4* __restrict__ he;
+    uint32_t* __restrict__ hc;
+    uint4* __restrict__ stk;
+    uint32_t C, mask;
+};
+
+// Insert column c (absent: slot i from hprobe) as walked-only; false on
+// overflow (more than C columns).
+__device__ __forceinline__ bool ws_insert(Lane& L, const LaneWs& W, uint32_t i, uint32_t c,
+                                          uint32_t state) {
+    if (L.used >= W.C) return false;
+    ++L.used;
+    W.ent[i] = make_uint4(L.tag, c, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    W.aux[i] = make_uint2(0u, state << 30);
+    return true;
+}
+
+// Memoised CPD walk from column v (ora_walk): afterwards v's entry (returned
+// slot) is walked; false on overflow.
+template <int SHIFT>
+__device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj_f,
+                         const uint2* __restrict__ adj_w, const uint32_t* __restrict__ row,
+                         uint32_t v, uint32_t& vslot) {
+    bool found;
+    uint32_t i = hprobe(W.ent, W.mask, L.tag, v, found);
+    if (found && (W.aux[i].y >> 30) == kWalked) {
+        vslot = i;
+        return true;
+    }
+    if (!found && !ws_insert(L, W, i, v, 0u)) return false;
+    vslot = i;
+    uint32_t sp = 0, x = v, xi = i;
+    bool bad = false;
+    for (;;) {
+        const uint32_t st = W.aux[xi].y >> 30;
+        if (st == kWalked) break;
+        if (st == kOnWalk) {  // a cycle: no path to t
+            bad = true;
+            break;
+        }
+        W.aux[xi].y = (W.aux[xi].y & 0x3FFFFFFFu) | (kOnWalk << 30);
+        const uint32_t mv = (row[x >> 3] >> (4u * (x & 7u))) & 0xFu;
+        uint2 ef = make_uint2(kNoEdge, 0u), ew = make_uint2(kNoEdge, 0u);
+        if (!(mv >> SHIFT)) {
+            ef = adj_f[((size_t)x << SHIFT) + mv];
+            ew = adj_w[((size_t)x << SHIFT) + mv];
+        }
+        if (sp >= W.C) return false;
+        W.stk[sp++] = make_uint4(xi, ef.y, ew.y, 0u);
+        if (ef.x == kNoEdge) {  // names no edge of x
+            bad = true;
+            break;
+        }
+        x = ef.x;
+        xi = hprobe(W.ent, W.mask, L.tag, x, found);
+        if (!found && !ws_insert(L, W, xi, x, 0u)) return false;
+    }
+    uint64_t hf = kInf64, cw = kInf64;
+    uint32_t lw = 0;
+    if (!bad) {
+        const uint4 m = W.memo[xi];
+        hf = u64of(m.x, m.y);
+        cw = u64of(m.z, m.w);
+        lw = W.aux[xi].y & 0x3FFFFFFFu;
+    }
+    while (sp) {
+        const uint4 e = W.stk[--sp];
+        if (hf != kInf64) {
+            hf += e.y;
+            cw += e.z;
+            lw += 1u;
+        }
+        W.memo[e.x] = make_uint4((uint32_t)hf, (uint32_t)(hf >> 32), (uint32_t)cw,
+                                 (uint32_t)(cw >> 32));
+        W.aux[e.x].y = (hf == kInf64 ? 0u : lw) | (kWalked << 30);
+    }
+    return true;
+}
+
 template <int SHIFT>
 __global__ __launch_bounds__(256) void cpd_search(
-    const uint2* __restrict__ adj, const uint64_t* __restrict__ hrow,
-    const uint64_t* __restrict__ crow, const uint32_t* __restrict__ lrow, uint32_t n,
-    const uint32_t* __restrict__ qs, const uint32_t* __restrict__ qt,
-    const uint32_t* __restrict__ qrow, uint32_t nq, uint32_t chunk, SearchOpt opt,
-    SearchWs ws, uint64_t* __restrict__ cost_out, uint32_t* __restrict__ plen_out,
-    uint8_t* __restrict__ fin_out, uint32_t* __restrict__ qstats,
-    unsigned long long* __restrict__ agg) {
+    const uint2* __restrict__ adj_f, const uint2* __restrict__ adj_w,
+    const uint32_t* __restrict__ dense, uint32_t wpr, const uint32_t* __restrict__ qs,
+    const uint32_t* __restrict__ qt, const uint32_t* __restrict__ qrow, uint32_t nq,
+    uint32_t chunk, SearchOpt opt, SearchWs ws, uint64_t* __restrict__ cost_out,
+    uint32_t* __restrict__ plen_out, uint8_t* __restrict__ fin_out,
+    uint32_t* __restrict__ qstats, unsigned long long* __restrict__ agg) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t slot = wave * 64u + lane;  // this lane's workspace
     const uint64_t q0l = wave * chunk;
     const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
     const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
-    const uint32_t C = ws.cap, mask = 2u * C - 1u;
-    uint4* __restrict__ hk = ws.hk + slot * 2u * C;
-    uint32_t* __restrict__ hd = ws.hd + slot * 2u * C;
-    uint4* __restrict__ he = ws.he + slot * C;
-    uint32_t* __restrict__ hc = ws.hc + slot * C;
+    const uint32_t C = ws.cap;
+    const LaneWs W{ws.ent + slot * 2u * C, ws.memo + slot * 2u * C, ws.aux + slot * 2u * C,
+                   ws.he + slot * C, ws.hc + slot * C, ws.stk + slot * C, C, 2u * C - 1u};
     unsigned long long s_exp = 0, s_ins = 0, s_tou = 0, s_upd = 0, s_sur = 0, s_len = 0,
                        s_fin = 0, s_ovf = 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
-    // the tag of a hash slot is the query index + 1 of the search that wrote
-    // it; slots are cleared once per launch so stale tags never match
-    for (uint32_t i = 0; i < 2u * C; ++i) hk[i] = make_uint4(0u, 0u, 0u, 0u);
+    // tag = query index + 1 of the search that wrote a slot; cleared once per
+    // launch so stale tags never match
+    for (uint32_t i = 0; i < 2u * C; ++i) W.ent[i] = make_uint4(0u, 0u, 0u, 0u);
 
     Lane L;
     L.q = kIdleQ;
     L.done = false;
+    const uint32_t* row = dense;
     auto begin = [&](uint32_t q) {
         L.q = q;
         L.s = qs[q];
         L.t = qt[q];
-        L.row = qrow[q];
         L.tag = q + 1u;
         L.hsize = 0;
+        L.used = 0;
         L.ub = kInf64;
         L.best_len = 0;
         L.expanded = L.inserted = L.touched = L.updated = L.surplus = 0;
         L.done = false;
         L.overflow = false;
         L.t0 = __builtin_amdgcn_s_memrealtime();
-        const uint64_t* hr = hrow + (size_t)L.row * n;
-        const uint64_t hs = hr[L.s];
+        row = dense + (size_t)qrow[q] * wpr;
+        // t walked with zeros, then the walk from s
+        bool found;
+        const uint32_t ti = hprobe(W.ent, W.mask, L.tag, L.t, found);
+        ws_insert(L, W, ti, L.t, kWalked);
+        W.memo[ti] = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t si;
+        if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, L.s, si)) {
+            L.overflow = L.done = true;
+            return;
+        }
+        const uint4 m = W.memo[si];
+        const uint64_t hs = u64of(m.x, m.y);
         if (hs != kInf64) {
-            bool found;
-            uint4 ent;
-            const uint32_t i = hprobe(hk, mask, L.tag, L.s, found, ent);
-            hk[i] = make_uint4(L.tag, L.s, 0u, 0u);
-            hd[i] = 0u;
+            W.ent[si].z = 0u;
+            W.ent[si].w = 0u;
+            W.aux[si].x = 0u;
             L.inserted = 1;
-            heap_push(he, hc, L.hsize, (uint64_t)(opt.hscale * (double)hs), L.s, 0ull);
+            heap_push(W.he, W.hc, L.hsize, (uint64_t)(opt.hscale * (double)hs), L.s, 0ull);
         }
     };
     uint32_t next = q0;
@@ -2162,65 +2187,76 @@ __global__ __launch_bounds__(256) void cpd_search(
         // one pop of this lane's search
         uint64_t f, g;
         uint32_t v;
-        heap_pop(he, hc, L.hsize, f, v, g);
+        heap_pop(W.he, W.hc, L.hsize, f, v, g);
         bool found;
-        uint4 ent;
-        const uint32_t hi = hprobe(hk, mask, L.tag, v, found, ent);
-        if (g > u64of(ent.z, ent.w)) {  // stale entry
+        const uint32_t hi = hprobe(W.ent, W.mask, L.tag, v, found);
+        const uint4 ev = W.ent[hi];
+        if (g > u64of(ev.z, ev.w)) {  // stale entry
             ++L.surplus;
             continue;
         }
+        const uint64_t elapsed =
+            opt.tick_ns ? opt.tick_ns * ((uint64_t)L.expanded + L.touched)
+                        : 10ull * (__builtin_amdgcn_s_memrealtime() - L.t0);
         if ((double)f * (1.0 + opt.fscale) >= (double)L.ub ||
             (opt.itrs >= 0 && (int64_t)L.expanded >= opt.itrs) ||
-            (opt.time_ticks && __builtin_amdgcn_s_memrealtime() - L.t0 > opt.time_ticks)) {
+            (opt.time_ns && elapsed > opt.time_ns)) {
             L.done = true;
             continue;
         }
         ++L.expanded;
-        const size_t rb = (size_t)L.row * n;
-        const uint32_t dv = hd[hi];
-        const uint64_t cw = crow[rb + v];
-        const uint32_t lw = lrow[rb + v];
-        if (cw != kInf64 && (opt.kmoves < 0 || lw <= (uint32_t)opt.kmoves)) {
-            const uint64_t cand = g + cw;
-            if (cand < L.ub) {
-                L.ub = cand;
-                L.best_len = dv + lw;
+        const uint32_t dv = W.aux[hi].x;
+        {
+            const uint4 mv = W.memo[hi];
+            const uint64_t cw = u64of(mv.z, mv.w);
+            const uint32_t lw = W.aux[hi].y & 0x3FFFFFFFu;
+            if (cw != kInf64 && (opt.kmoves < 0 || lw <= (uint32_t)opt.kmoves)) {
+                const uint64_t cand = g + cw;
+                if (cand < L.ub) {
+                    L.ub = cand;
+                    L.best_len = dv + lw;
+                }
             }
         }
-#pragma unroll
+#pragma unroll 1
         for (int k = 0; k < (1 << SHIFT); ++k) {
-            const uint2 e = adj[((size_t)v << SHIFT) + k];
+            const uint2 e = adj_w[((size_t)v << SHIFT) + k];
             if (e.x == kNoEdge) break;  // edges are packed first
             ++L.touched;
             const uint32_t u = e.x;
             const uint64_t ng = g + e.y;
             bool fu;
-            uint4 eu;
-            const uint32_t ui = hprobe(hk, mask, L.tag, u, fu, eu);
-            if (!fu) {
-                const uint64_t hu = hrow[rb + u];
+            uint32_t ui = hprobe(W.ent, W.mask, L.tag, u, fu);
+            const bool seen = fu && !(W.ent[ui].z == 0xFFFFFFFFu && W.ent[ui].w == 0xFFFFFFFFu);
+            if (!seen) {
+                if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, u, ui)) {
+                    L.overflow = L.done = true;
+                    break;
+                }
+                const uint4 mu = W.memo[ui];
+                const uint64_t hu = u64of(mu.x, mu.y);
                 if (hu == kInf64) continue;
-                if (L.inserted >= C || L.hsize >= C) {
-                    L.overflow = true;
-                    L.done = true;
-                    break;
-                }
-                hk[ui] = make_uint4(L.tag, u, (uint32_t)ng, (uint32_t)(ng >> 32));
-                hd[ui] = dv + 1u;
-                ++L.inserted;
-                heap_push(he, hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
-            } else if (ng < u64of(eu.z, eu.w)) {
                 if (L.hsize >= C) {
-                    L.overflow = true;
-                    L.done = true;
+                    L.overflow = L.done = true;
                     break;
                 }
-                hk[ui] = make_uint4(L.tag, u, (uint32_t)ng, (uint32_t)(ng >> 32));
-                hd[ui] = dv + 1u;
+                W.ent[ui].z = (uint32_t)ng;
+                W.ent[ui].w = (uint32_t)(ng >> 32);
+                W.aux[ui].x = dv + 1u;
+                ++L.inserted;
+                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
+            } else if (ng < u64of(W.ent[ui].z, W.ent[ui].w)) {
+                if (L.hsize >= C) {
+                    L.overflow = L.done = true;
+                    break;
+                }
+                W.ent[ui].z = (uint32_t)ng;
+                W.ent[ui].w = (uint32_t)(ng >> 32);
+                W.aux[ui].x = dv + 1u;
                 ++L.updated;
-                heap_push(he, hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hrow[rb + u]), u,
-                          ng);
+                const uint4 mu = W.memo[ui];
+                heap_push(W.he, W.hc, L.hsize,
+                          ng + (uint64_t)(opt.hscale * (double)u64of(mu.x, mu.y)), u, ng);
             }
         }
     }
@@ -2563,44 +2599,6 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
                 ts_chunk_max(1u << 30), s);
 }
 
-// CPD-search tables for `rows` index rows starting at `first`: pointer
-// jumping in chunks of rows (scratch: 2 jump states of 24 B per column per
-// row of the chunk).
-void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* adj_f,
-                          const uint32_t* adj_w, uint32_t shift, const uint32_t* tcol,
-                          uint32_t rows, uint32_t n, void* scratch, uint32_t chunk_rows,
-                          uint64_t* hrow, uint64_t* crow, uint32_t* lrow, int write_h,
-                          hipStream_t s) {
-    uint32_t rounds = 1;
-    while ((1ull << (rounds - 1)) < (uint64_t)n + 1ull) ++rounds;  // 2^(rounds-1) > n hops
-    const size_t per = (size_t)chunk_rows * n;
-    char* base = static_cast<char*>(scratch);
-    auto state = [&](int k) {
-        char* p = base + (size_t)k * per * 24u;
-        return kern::JumpState{reinterpret_cast<uint32_t*>(p),
-                               reinterpret_cast<uint64_t*>(p + per * 4u),
-                               reinterpret_cast<uint64_t*>(p + per * 12u),
-                               reinterpret_cast<uint32_t*>(p + per * 20u)};
-    };
-    const kern::JumpState A = state(0), Bs = state(1);
-    const uint2* af = reinterpret_cast<const uint2*>(adj_f);
-    const uint2* aw = reinterpret_cast<const uint2*>(adj_w);
-    for (uint32_t r0 = 0; r0 < rows; r0 += chunk_rows) {
-        const uint32_t R = std::min(chunk_rows, rows - r0);
-        const uint64_t items = (uint64_t)R * n;
-        const dim3 grid((uint32_t)((items + 255u) / 256u)), blk(256);
-        launch(kern::jump_init, grid, blk, s, dense + (size_t)r0 * (npad / 8u), npad / 8u, af, aw,
-               shift, tcol + r0, R, n, A);
-        kern::JumpState a = A, b = Bs;
-        for (uint32_t k = 0; k < rounds; ++k) {
-            launch(kern::jump_round, grid, blk, s, a, b, tcol + r0, R, n);
-            std::swap(a, b);
-        }
-        launch(kern::jump_final, grid, blk, s, a, tcol + r0, R, n, hrow + (size_t)r0 * n,
-               crow + (size_t)r0 * n, lrow + (size_t)r0 * n, write_h);
-    }
-}
-
 uint32_t search_slots(uint32_t nq) {  // lanes with a workspace: whole blocks of 4 waves
     static const uint32_t waves = std::max(4u, env_u32("CPD_SEARCH_WAVES", 256));
     const uint32_t want = (nq + 63u) / 64u;
@@ -2608,28 +2606,40 @@ uint32_t search_slots(uint32_t nq) {  // lanes with a workspace: whole blocks of
     return 64u * ((w + 3u) / 4u * 4u);
 }
 
-void launch_cpd_search(const uint32_t* adj, uint32_t shift, const uint64_t* hrow,
-                       const uint64_t* crow, const uint32_t* lrow, uint32_t n, const uint32_t* qs,
+void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t shift,
+                       const uint32_t* dense, uint32_t npad, const uint32_t* qs,
                        const uint32_t* qt, const uint32_t* qrow, uint32_t nq, double hscale,
                        double fscale, int32_t kmoves, int64_t itrs, uint64_t time_ns,
-                       void* ws, uint32_t cap, uint32_t slots, uint64_t* cost, uint32_t* plen,
-                       uint8_t* fin, uint32_t* qstats, unsigned long long* agg, hipStream_t s) {
+                       uint64_t tick_ns, void* ws, uint32_t cap, uint32_t slots, uint64_t* cost,
+                       uint32_t* plen, uint8_t* fin, uint32_t* qstats, unsigned long long* agg,
+                       hipStream_t s) {
     const uint32_t waves = slots / 64u;  // a multiple of 4 (search_slots)
     char* p = static_cast<char*>(ws);
-    const size_t hs = (size_t)slots * 2u * cap, hp = (size_t)slots * cap;
-    kern::SearchWs w{reinterpret_cast<uint4*>(p), reinterpret_cast<uint32_t*>(p + hs * 16u),
-                     reinterpret_cast<uint4*>(p + hs * 20u),
-                     reinterpret_cast<uint32_t*>(p + hs * 20u + hp * 16u), cap};
-    const kern::SearchOpt o{hscale, fscale, kmoves, itrs, time_ns ? std::max<uint64_t>(1u, time_ns / 10u) : 0u};
+    const size_t h2 = (size_t)slots * 2u * cap, h1 = (size_t)slots * cap;
+    kern::SearchWs w{reinterpret_cast<uint4*>(p), reinterpret_cast<uint4*>(p + h2 * 16u),
+                     reinterpret_cast<uint2*>(p + h2 * 32u),
+                     reinterpret_cast<uint4*>(p + h2 * 40u),
+                     reinterpret_cast<uint32_t*>(p + h2 * 40u + h1 * 16u),
+                     reinterpret_cast<uint4*>(p + h2 * 40u + h1 * 20u), cap};
+    const kern::SearchOpt o{hscale, fscale, kmoves, itrs, time_ns, tick_ns};
     const dim3 grid(waves / 4u), blk(256);  // every wave has a workspace slot
     const uint32_t c2 = (uint32_t)(((uint64_t)nq + waves - 1u) / waves);
+    const uint2* af = reinterpret_cast<const uint2*>(adj_f);
+    const uint2* aw = reinterpret_cast<const uint2*>(adj_w);
+    const uint32_t wpr = npad / 8u;
+#define CPD_SEARCH(SH)                                                                      \
+    launch(kern::cpd_search<SH>, grid, blk, s, af, aw, dense, wpr, qs, qt, qrow, nq, c2, o, w, \
+           cost, plen, fin, qstats, agg)
     switch (shift) {
-        case 0: launch(kern::cpd_search<0>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
-        case 1: launch(kern::cpd_search<1>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
-        case 2: launch(kern::cpd_search<2>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
-        case 3: launch(kern::cpd_search<3>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
-        default: launch(kern::cpd_search<4>, grid, blk, s, reinterpret_cast<const uint2*>(adj), hrow, crow, lrow, n, qs, qt, qrow, nq, c2, o, w, cost, plen, fin, qstats, agg); break;
+        case 0: CPD_SEARCH(0); break;
+        case 1: CPD_SEARCH(1); break;
+        case 2: CPD_SEARCH(2); break;
+        case 3: CPD_SEARCH(3); break;
+        default: CPD_SEARCH(4); break;
     }
+#undef CPD_SEARCH
 }
+
+uint64_t search_ws_bytes_per_slot(uint32_t cap) { return 116ull * cap; }
 
 }  // namespace cpd

@@ -314,24 +314,30 @@ void cpd_index_free(cpd_index* ix);
  * free-flow cost of the CPD path to t, incumbent from the CPD path's cost
  * under the current weights (only paths of <= k_moves moves when k_moves >=
  * 0); stops when f_min x (1 + fscale) >= incumbent, after itrs expansions,
- * or after time_ns.  Runs on the queries of the last cpd_query_prepare; per
- * query results (cost, plen as hops, finished) via cpd_query_fetch.  Needs
- * 20 B per column per index row for its tables (CPD_E_OOM if they do not
- * fit) and a workspace of `capacity` nodes per concurrent search; a search
- * that needs more stops unfinished and is counted in `overflow`.          */
+ * or once time_ns have elapsed.  Runs on the queries of the last
+ * cpd_query_prepare; per query results (cost, plen as hops, finished) via
+ * cpd_query_fetch.  The CPD path values come from walks over the dense rows,
+ * memoised per search in its workspace (nothing per index row is kept, so
+ * any index can be searched); a search needs `capacity` columns of workspace
+ * (walked or searched, 116 B each) and one that needs more stops unfinished
+ * and is counted in `overflow`.  The time limit is wall clock (as fifo_auto
+ * runs it); virtual_tick_ns > 0 replaces it by a deterministic clock that
+ * advances virtual_tick_ns per expansion and per edge touched (the oracle's
+ * restatement, for tests).                                                   */
 typedef struct cpd_search_opts {
     double   hscale;       /* 1.0 */
     double   fscale;       /* 0.0 */
     int32_t  k_moves;      /* -1: whole CPD paths */
     int64_t  itrs;         /* -1: no expansion limit */
     uint64_t time_ns;      /* 0: no time limit (per query) */
-    uint32_t capacity;     /* nodes per search, power of 2 (0 = 32768) */
+    uint32_t capacity;     /* columns per search, power of 2 (0 = 32768) */
+    uint64_t virtual_tick_ns; /* 0: wall-clock time limit; else virtual clock */
 } cpd_search_opts;
 
 typedef struct cpd_search_stats {
     uint64_t queries, finished, expanded, inserted, touched, updated, surplus, plen, overflow;
     double   kernel_ms;    /* device time of the search kernel              */
-    double   tables_ms;    /* device time spent (re)building its tables     */
+    uint64_t lanes;        /* concurrent searches (workspace slots)         */
 } cpd_search_stats;
 
 int  cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st);

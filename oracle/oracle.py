@@ -136,10 +136,12 @@ def table_search(row_ptr, dst, w_sel, order, row_targets, offsets, runs, s, t, k
 
 
 def cpd_search(row_ptr, dst, w_free, w_sel, order, row_targets, offsets, runs, s, t,
-               hscale=1.0, fscale=0.0, k_moves=-1, itrs=-1, threads=0):
+               hscale=1.0, fscale=0.0, k_moves=-1, itrs=-1, time_ns=0, tick_ns=0, threads=0,
+               columns=False):
     """CPD-heuristic search (cpd_oracle.c ora_cpd_search): per query cost,
     plen, finished and stats[q] = (expanded, inserted, touched, updated,
-    surplus)."""
+    surplus); with columns=True also the distinct nodes each query met (a 6th
+    stats column).  time_ns with tick_ns > 0: the deterministic time limit."""
     row_ptr, dst, w_free, w_sel, order = map(_u32, (row_ptr, dst, w_free, w_sel, order))
     n = len(order)
     row_of_target = np.full(n, INF, np.uint32)
@@ -150,14 +152,15 @@ def cpd_search(row_ptr, dst, w_free, w_sel, order, row_targets, offsets, runs, s
     cost = np.empty(nq, np.uint64)
     plen = np.empty(nq, np.uint32)
     fin = np.empty(nq, np.uint8)
-    stats = np.empty((nq, 5), np.uint64)
+    stats = np.empty((nq, 6), np.uint64)
     L = lib()
     L.ora_cpd_search.argtypes = [C.c_uint32] + [C.c_void_p] * 10 + [
-        C.c_uint32, C.c_double, C.c_double, C.c_int32, C.c_int64] + [C.c_void_p] * 4 + [C.c_int]
+        C.c_uint32, C.c_double, C.c_double, C.c_int32, C.c_int64, C.c_uint64, C.c_uint64] + \
+        [C.c_void_p] * 4 + [C.c_int]
     rc = L.ora_cpd_search(n, _p(row_ptr), _p(dst), _p(w_free), _p(w_sel), _p(order),
                           _p(row_of_target), _p(offsets), _p(runs), _p(s), _p(t), nq,
-                          float(hscale), float(fscale), int(k_moves), int(itrs), _p(cost),
-                          _p(plen), _p(fin), _p(stats), int(threads))
+                          float(hscale), float(fscale), int(k_moves), int(itrs), int(time_ns),
+                          int(tick_ns), _p(cost), _p(plen), _p(fin), _p(stats), int(threads))
     if rc == -4:
         raise KeyError("a query target has no row")
-    return cost, plen, fin, stats
+    return cost, plen, fin, (stats if columns else stats[:, :5].copy())

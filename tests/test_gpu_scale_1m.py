@@ -97,6 +97,22 @@ def test_1m_full_batch(w1m):
         d = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, tt)
         sel = t == tt
         np.testing.assert_array_equal(cost[sel], d[s[sel]].astype(np.uint64))
+    # cpd-search over the same worker-sized index (21504 rows: round 2's
+    # per-row tables would have needed 430 GB), congested weights, fscale
+    # 0.1, queries to the rows the oracle built above: bit-exact
+    w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
+    ix.set_weights(w_cong)
+    sq = 1000
+    ss = rng.integers(0, g.n, sq).astype(np.uint32)
+    stt = targets[sample][rng.integers(0, len(sample), sq)]
+    rc, rp, rf, rs = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, plan.order(),
+                                       targets[sample], ref_off, ref_runs, ss, stt, fscale=0.1)
+    gc_, gp, gf, gcnt, gst = ix.search(ss, stt, fscale=0.1)
+    assert gst["overflow"] == 0
+    np.testing.assert_array_equal(gc_, rc)
+    np.testing.assert_array_equal(gp, rp)
+    np.testing.assert_array_equal(gf, rf)
+    np.testing.assert_array_equal(gcnt.astype(np.uint64), rs)
 
 
 @pytest.mark.parametrize("mode", ["dense", "rle"])

@@ -95,16 +95,47 @@ def test_search_overflow_is_counted(env):
     g, plan, dev, targets, off, runs, s, t, wc = env
     ix = _index(env, "dense")
     ix.set_weights(wc)
-    rc, rp, rf, rs = _oracle(env, wc)
-    need = rs[:, 1].max()  # most nodes any query inserts
-    cap = 64
-    assert need > cap
+    rc, rp, rf, rs = _oracle(env, wc, columns=True)
+    cap = 256
+    assert rs[:, 5].max() > cap  # some query's walks and search meet more columns
     cost, plen, fin, cnt, st = ix.search(s, t, capacity=cap)
     assert st["overflow"] >= 1
-    # pushes = inserted + updated bound a search's nodes and heap entries:
-    # searches below the capacity are exact, those above it stop unfinished
-    small = rs[:, 1] + rs[:, 3] < cap
+    # a search's workspace holds every column its walks and search met (the
+    # oracle's 6th stat) and its heap at most inserted + updated pushes:
+    # searches within the capacity are exact, those above it stop unfinished
+    small = (rs[:, 5] <= cap) & (rs[:, 1] + rs[:, 3] < cap)
     assert small.sum() > 100
     np.testing.assert_array_equal(cost[small], rc[small])
-    np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small])
-    assert not fin[rs[:, 1] > cap].any()
+    np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small, :5])
+    assert not fin[rs[:, 5] > cap].any()
+
+
+@pytest.mark.parametrize("time_ns,tick", [(1, 1), (40, 1), (300, 3), (5000, 7), (10**12, 1)])
+def test_search_time_limit_virtual_clock(env, time_ns, tick):
+    """The time limit under the deterministic clock (tick per expansion and
+    per touched edge, the oracle's restatement): bit-exact."""
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    rc, rp, rf, rs = _oracle(env, wc, time_ns=time_ns, tick_ns=tick)
+    cost, plen, fin, cnt, st = ix.search(s, t, time_ns=time_ns, virtual_tick_ns=tick)
+    np.testing.assert_array_equal(cost, rc)
+    np.testing.assert_array_equal(plen, rp)
+    np.testing.assert_array_equal(fin, rf)
+    np.testing.assert_array_equal(cnt.astype(np.uint64), rs)
+
+
+def test_search_time_limit_wall_clock(env):
+    """The wall-clock limit fifo_auto runs (time from the worker JSON): 1 ns
+    has passed by the first check (the walk from s alone takes longer), so
+    no search expands — the oracle at itrs = 0; a limit of 1000 s changes
+    nothing."""
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    for time_ns, ref in ((1, _oracle(env, wc, itrs=0)), (10**12, _oracle(env, wc))):
+        cost, plen, fin, cnt, st = ix.search(s, t, time_ns=time_ns)
+        np.testing.assert_array_equal(cost, ref[0])
+        np.testing.assert_array_equal(plen, ref[1])
+        np.testing.assert_array_equal(fin, ref[2])
+        np.testing.assert_array_equal(cnt.astype(np.uint64), ref[3])

@@ -202,3 +202,27 @@ def test_search_limits():
     # k_moves = 0: only t itself yields an incumbent, so the search ends at t
     np.testing.assert_array_equal(c0.astype(float), opt)
     assert np.all(st0[:, 0] >= 1)
+
+
+def test_search_virtual_time_limit():
+    """The deterministic restatement of `time`: tick_ns per expansion and per
+    touched edge.  A 1-ns budget allows exactly the first expansion (its
+    incumbent is the CPD path: the table-search cost); budgets grow the
+    search monotonically; no budget = no limit; tick 0 = not modelled."""
+    g, order, T, off, runs, s, t, wc, opt = _search_case()
+    tc, th, tf = oracle.table_search(g.row_ptr, g.dst, wc, order, T, off, runs, s, t)
+    c1, p1, f1, st1 = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t,
+                                        time_ns=1, tick_ns=1)
+    assert np.all(st1[:, 0] == 1)
+    np.testing.assert_array_equal(c1, tc)
+    prev = st1[:, 0].sum()
+    for budget in (50, 500, 5000):
+        _, _, _, stb = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t,
+                                         time_ns=budget, tick_ns=1)
+        assert stb[:, 0].sum() >= prev
+        prev = stb[:, 0].sum()
+    c0, _, _, st0 = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t)
+    for kw in (dict(time_ns=0, tick_ns=1), dict(time_ns=1, tick_ns=0)):
+        c, _, _, st = oracle.cpd_search(g.row_ptr, g.dst, g.w, wc, order, T, off, runs, s, t, **kw)
+        np.testing.assert_array_equal(c, c0)
+        np.testing.assert_array_equal(st, st0)
