@@ -49,7 +49,7 @@ EXPORTED = [
     "cpd_index_append_rows", "cpd_index_append_built_rows", "cpd_index_info",
     "cpd_synth_road_graph_ex", "cpd_query_search", "cpd_query_search_counters",
     "cpd_graph_set_coords", "cpd_host_alloc", "cpd_host_free",
-    "cpd_rows_lanes",
+    "cpd_rows_lanes", "cpd_graph_hint_next",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
@@ -416,6 +416,12 @@ class Graph:
         if reuse is not None:
             return reuse
         return Rows(h)
+
+    def hint_next(self, targets) -> None:
+        """The targets the next build_rows() call starts with: its first
+        batch's up-sweep may start during the current call (cpd_graph_hint_next)."""
+        t = _u32(targets)
+        _check(lib.cpd_graph_hint_next(self._h, _ptr(t, u32p), C.c_uint32(len(t))))
 
     def debug_rows(self, targets, want_dist=True, want_fm=True):
         t = _u32(targets)

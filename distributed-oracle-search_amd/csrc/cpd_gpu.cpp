@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -116,7 +117,7 @@ struct cpd_graph {
     // batch workspace
     uint32_t B = 0;
     uint32_t fmb = 16;  // bits per first-move set (fm_bits(adj_shift))
-    DevBuf<uint32_t> dist, tgt, counts;
+    DevBuf<uint32_t> dist, counts;
     // Emit overlap (CPD_ASYNC, default on): a batch's rle_emit runs on
     // `estream` while the next batch's sweeps start on `stream` — the sweeps'
     // narrow, latency-bound levels overlap the bandwidth-bound emit.  The
@@ -177,9 +178,34 @@ struct cpd_graph {
     }
     double n_leaf = 0, m_leaf = 0;    // leaves, their out-edges
     std::vector<double> dsc_lvl_leaves;
-    // per-level sweep counters (2 per launch: stored/own rows, gathered rows)
-    DevBuf<unsigned int> stat;
-    std::vector<unsigned int> stat_h;
+    // Per-batch state, two slots: a batch's up-sweep may run (on ustream)
+    // while the previous batch's first moves still read their own targets.
+    // tgt: the batch's target columns by lane; pos_of[i] = lane of the
+    // caller's target i; stat: per-level sweep counters (timing runs; 2 per
+    // launch: stored / own rows, gathered rows), stat_h its host copy;
+    // up_late: (level, arcs, nodes) of the up levels whose bytes wait for it.
+    struct BatchSlot {
+        DevBuf<uint32_t> tgt;
+        std::vector<uint32_t> pos_of, tgt_col;
+        DevBuf<unsigned int> stat;
+        std::vector<unsigned int> stat_h;
+        std::vector<std::array<double, 3>> up_late;
+    };
+    BatchSlot bs[2];
+    uint32_t next_slot = 0;
+    // Early up-sweep of the next batch: build_batch
+    // launches it on ustream once the current batch's down-sweep is done, so
+    // it runs beside that batch's first moves and RLE count.  prep: the slot
+    // and targets it was launched for, ev_up its end.
+    hipStream_t ustream = nullptr;
+    hipEvent_t ev_up = nullptr, ev_down = nullptr, ev_fm = nullptr;
+    bool prepped = false;
+    uint32_t prep_slot = 0;
+    std::vector<uint32_t> prep_targets, hint;
+    void drop_prep() {  // wait for an early up-sweep nobody will use
+        if (ustream) HIP_CHECK(hipStreamSynchronize(ustream));
+        prepped = false;
+    }
     DevBuf<uint32_t> asc_lvl_of, dsc_lvl_of;  // slot -> level
     // narrow upward levels (<= kNarrow nodes) run chunked: per level l,
     // items [up_item_first[l], up_item_first[l+1]) of (slot, a0, a1, 0);
@@ -189,7 +215,6 @@ struct cpd_graph {
     uint32_t n_init_cols = 0;
     // lane position of each caller target in the current batch (sorted by
     // lane_key when the caller gave coordinates, else by column)
-    std::vector<uint32_t> pos_of, tgt_col;
     std::vector<uint32_t> lane_key;  // node -> Hilbert key of its coordinates (may be empty)
     // timing
     bool timing = false;
@@ -203,6 +228,10 @@ struct cpd_graph {
             for (auto e : ev_emit)
                 if (e) (void)hipEventDestroy(e);
             if (estream) (void)hipStreamDestroy(estream);
+            if (ustream) (void)hipStreamSynchronize(ustream);
+            for (auto e : {ev_up, ev_down, ev_fm})
+                if (e) (void)hipEventDestroy(e);
+            if (ustream) (void)hipStreamDestroy(ustream);
             if (stream) (void)hipStreamSynchronize(stream);
             for (auto& p : pending) {
                 (void)hipEventDestroy(p.a);
@@ -260,17 +289,19 @@ struct cpd_graph {
     }
     Pending group;
     bool group_open = false;
-    void group_begin(const char* name) {
+    hipStream_t group_stream = nullptr;
+    void group_begin(const char* name, hipStream_t st) {
         if (!timing) return;
         group = Pending{name, get_event(), nullptr, 0.0, {}, 0};
-        HIP_CHECK(hipEventRecord(group.a, stream));
+        group_stream = st;
+        HIP_CHECK(hipEventRecord(group.a, st));
         group_open = true;
     }
     void group_end() {
         if (!group_open) return;
         group_open = false;
         group.b = get_event();
-        HIP_CHECK(hipEventRecord(group.b, stream));
+        HIP_CHECK(hipEventRecord(group.b, group_stream));
         if (group.launches) {
             pending.push_back(std::move(group));
         } else {
@@ -284,7 +315,10 @@ struct cpd_graph {
     // running on estream stay pending until a later sync.
     void sync(bool all = false) {
         HIP_CHECK(hipStreamSynchronize(stream));
-        if (all) drain_emits();
+        if (all) {
+            drain_emits();
+            if (ustream) HIP_CHECK(hipStreamSynchronize(ustream));
+        }
         std::vector<Pending> keep;
         for (auto& p : pending) {
             if (hipEventQuery(p.b) != hipSuccess) {
@@ -326,6 +360,7 @@ struct cpd_graph {
         want = (want + 1023u) / 1024u * 1024u;
         if (want == B && dist.p) return;
         drain_emits();
+        drop_prep();
         B = want;
         dist.alloc((size_t)n * B);
         // the second buffer set when it takes under an eighth of the HBM
@@ -365,7 +400,7 @@ struct cpd_graph {
             dbase.alloc((size_t)n * (B / 256u));
             ovf.alloc(1);
         }
-        tgt.alloc(B);
+        for (auto& b : bs) b.tgt.alloc(B);
         counts.alloc(B);
     }
 };
@@ -579,6 +614,9 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
         // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step)
         HIP_CHECK(hipStreamCreateWithFlags(&g->estream, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&g->ustream, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&g->ev_up, &g->ev_down, &g->ev_fm})
+            HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         for (auto& e : g->ev_emit) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         const uint32_t n = p->n, m = p->m;
         g->n = n;
@@ -687,8 +725,10 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 }
             g->leafbits.upload(lb.data(), lb.size(), s);
         }
-        g->stat.alloc(2 * (g->asc_lvl.size() + g->dsc_lvl.size()));
-        g->stat_h.assign(g->stat.n, 0);
+        for (auto& b : g->bs) {
+            b.stat.alloc(2 * (g->asc_lvl.size() + g->dsc_lvl.size()));
+            b.stat_h.assign(b.stat.n, 0);
+        }
         auto lvl_of = [n](const std::vector<uint32_t>& first) {
             std::vector<uint32_t> v(n, 0);
             for (size_t l = 0; l + 1 < first.size(); ++l)
@@ -829,8 +869,84 @@ void narrow_decide(cpd_graph* g) {
                      (unsigned long long)groups);
 }
 
-void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm) {
+// Phase U of a batch of k targets (slot's columns already uploaded), on
+// stream st: the target mask, the leaf-form init of the chunked levels and the
+// up-sweep levels.  Writes dist (up rows), live and tmask, which the previous
+// batch's down-sweep reads: the caller orders st after it.
+void launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st) {
+    const uint32_t B = g->B;
+    auto& S = g->bs[slot];
+    const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
+    const uint32_t active = slabs * 1024u;
+    uint32_t* live = live_on() ? g->live.p : nullptr;
+    unsigned int* stat = g->timing ? S.stat.p : nullptr;
+    const size_t nasc = g->asc_lvl.size();
+    S.up_late.clear();
+    if (stat) HIP_CHECK(hipMemsetAsync(stat, 0, S.stat.n * sizeof(unsigned int), st));
+    if (live) {
+        HIP_CHECK(hipMemsetAsync(g->tmask.p, 0, (size_t)g->n * sizeof(uint32_t), st));
+        launch_target_mask(S.tgt.p, active, g->tmask.p, st);
+        g->timed("sweep_up_init", 4.0 * g->n_init_cols * active, [&] {
+            launch_sweep_up_init(g->up_init_cols.p, g->n_init_cols, g->dist.p, S.tgt.p, B, slabs,
+                                 live, g->tmask.p, st);
+        });
+    }
+    // ascending sweep: each level reads lower levels' rows.  Levels 0 and 1
+    // are never materialised (closed forms, kLeafBit / kL1Bit): not launched.
+    // Dense bytes per level: gathered rows 4 B x target, row writes 4 B x
+    // target, arcs 8 B and node slot 12 B per 1024-target slab.  Sparse: 4 KiB
+    // per live (row, slab) stored and per live row gathered, arcs 8 B + their
+    // masks 4 B, node slot 12 B + masks 8 B, once per node — known once the
+    // batch's live_stats have run (added by build_batch from S.up_late).
+    g->group_begin("sweep_up", st);
+    for (size_t l = 2; l + 1 < nasc; ++l) {
+        uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
+        if (!cnt) continue;
+        double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
+        double dense = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + 8.0 * arcs_l * slabs +
+                       12.0 * cnt * slabs;
+        if (live && stat) {
+            S.up_late.push_back({(double)l, arcs_l, (double)cnt});
+            dense = 0.0;
+        }
+        const uint32_t i0 = g->up_item_first[l], ni = g->up_item_first[l + 1] - i0;
+        g->timed("sweep_up", dense, [&] {
+            if (live && ni)
+                launch_sweep_up_chunks(g->up_items.p + 4 * (size_t)i0, ni, g->asc_nodes.p,
+                                       g->asc_arcs.p, g->dist.p, S.tgt.p, B, slabs,
+                                       g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
+                                       g->tmask.p, st);
+            else
+                launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt,
+                             g->dist.p, S.tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p,
+                             g->asc_arcs.p, live, g->tmask.p, g->adj.p, g->adj_shift, nullptr,
+                             g->narrow_rows(false), nullptr, st);
+        });
+    }
+    g->group_end();
+}
+
+// The up levels' sparse bytes of a batch whose stats have arrived (S.stat_h).
+void add_up_late_bytes(cpd_graph* g, uint32_t slot) {
+    auto& S = g->bs[slot];
+    if (S.up_late.empty()) return;
+    double b = 0.0;
+    for (const auto& u : S.up_late) {
+        const size_t l = (size_t)u[0];
+        b += 4096.0 * ((double)S.stat_h[2 * l] + (double)S.stat_h[2 * l + 1]) + 12.0 * u[1] +
+             20.0 * u[2];
+    }
+    g->agg["sweep_up"].bytes += b;
+    S.up_late.clear();
+}
+
+// Phase D of the batch in `slot` (its up-sweep done or ordered before), on
+// g->stream: the down-sweep, the wide-row count (narrow; its value lands in
+// g->ovf_h), the live stats (timing runs), then ev_down; the first moves
+// into fm, then ev_fm.
+void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slot) {
     const uint32_t B = g->B, n = g->n;
+    auto& S = g->bs[slot];
     const NarrowRows nr = g->narrow_rows(narrow);
     if (narrow) HIP_CHECK(hipMemsetAsync(g->ovf.p, 0, sizeof(uint32_t), g->stream));
     // bytes per target of a final-distance row access: 4 wide; 2 + a 4-B base
@@ -839,53 +955,10 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm) {
     const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
     const uint32_t active = slabs * 1024u;
     uint32_t* live = live_on() ? g->live.p : nullptr;
-    unsigned int* stat = g->timing ? g->stat.p : nullptr;
+    unsigned int* stat = g->timing ? S.stat.p : nullptr;
     const size_t nasc = g->asc_lvl.size();
-    if (stat) HIP_CHECK(hipMemsetAsync(stat, 0, g->stat.n * sizeof(unsigned int), g->stream));
-    const std::vector<unsigned int>& sh = g->stat_h;  // filled by the batch's D2H copy
-    if (live) {
-        HIP_CHECK(hipMemsetAsync(g->tmask.p, 0, (size_t)n * sizeof(uint32_t), g->stream));
-        launch_target_mask(g->tgt.p, active, g->tmask.p, g->stream);
-        g->timed("sweep_up_init", 4.0 * g->n_init_cols * active, [&] {
-            launch_sweep_up_init(g->up_init_cols.p, g->n_init_cols, g->dist.p, g->tgt.p, B, slabs,
-                                 live, g->tmask.p, g->stream);
-        });
-    }
-    // ascending sweep: each level reads lower levels' rows.  Levels 0 and 1
-    // are never materialised (closed forms, kLeafBit / kL1Bit): not launched.
-    // Dense bytes per level: gathered rows 4 B x target, row writes 4 B x
-    // target, arcs 8 B and node slot 12 B per 1024-target slab.  Sparse: 4 KiB
-    // per live (row, slab) stored and per live row gathered, arcs 8 B + their
-    // masks 4 B, node slot 12 B + masks 8 B, once per node.
-    g->group_begin("sweep_up");
-    for (size_t l = 2; l + 1 < nasc; ++l) {
-        uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
-        if (!cnt) continue;
-        double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
-        double dense = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + 8.0 * arcs_l * slabs +
-                       12.0 * cnt * slabs;
-        std::function<double()> late;
-        if (live && stat)
-            late = [&sh, l, arcs_l, cnt] {
-                return 4096.0 * ((double)sh[2 * l] + (double)sh[2 * l + 1]) + 12.0 * arcs_l +
-                       20.0 * cnt;
-            };
-        const uint32_t i0 = g->up_item_first[l], ni = g->up_item_first[l + 1] - i0;
-        g->timed("sweep_up", dense, [&] {
-            if (live && ni)
-                launch_sweep_up_chunks(g->up_items.p + 4 * (size_t)i0, ni, g->asc_nodes.p,
-                                       g->asc_arcs.p, g->dist.p, g->tgt.p, B, slabs,
-                                       g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
-                                       g->tmask.p, g->stream);
-            else
-                launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt,
-                             g->dist.p, g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p,
-                             g->asc_arcs.p, live, g->tmask.p, g->adj.p, g->adj_shift, nullptr,
-                             g->narrow_rows(false), nullptr, g->stream);
-        }, std::move(late));
-    }
-    g->group_end();
-    g->group_begin("sweep_down");
+    const std::vector<unsigned int>& sh = S.stat_h;  // filled by the batch's D2H copy
+    g->group_begin("sweep_down", g->stream);
     for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
         uint32_t s0 = g->dsc_lvl[l], cnt = g->dsc_lvl[l + 1] - s0;
         if (!cnt) continue;
@@ -901,15 +974,18 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm) {
             };
         g->timed("sweep_down", dense, [&] {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
-                         g->tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
+                         S.tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
                          g->tmask.p, g->adj.p, g->adj_shift, g->leaf_fm ? g->fmleaf.p : nullptr,
                          nr, g->dsc_desc.p, g->stream);
         }, std::move(late));
     }
     g->group_end();
-    if (narrow && (g->timing || g->narrow_probe))
+    if (narrow) {
         launch_count_wide_rows(g->dbase.p, (size_t)n * (B / 256u),
                                reinterpret_cast<unsigned int*>(g->ovf.p), g->stream);
+        HIP_CHECK(hipMemcpyAsync(&g->ovf_h, g->ovf.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                 g->stream));
+    }
     if (live && stat && nasc > 2) {  // row counts behind the late byte counts
         g->timed("live_stats", 0.0, [&] {
             launch_live_stats(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
@@ -920,6 +996,7 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm) {
                               g->dsc_lvl_of.p, 0, n, live, stat + 2 * nasc, g->stream);
         });
     }
+    HIP_CHECK(hipEventRecord(g->ev_down, g->stream));
     // per row: own distance 4n (kernels that read it) + neighbour distances
     // 4m + first-move write npad * fmb / 8; the packed adjacency (8 B per
     // slot) is read once per 1024-target slab.  Leaf columns (leaf_fm) read
@@ -932,20 +1009,23 @@ void run_sweeps_and_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm) {
             (fslabs * 1024.0) +
         8.0 * (double)(n - nl) * (double)(1u << g->adj_shift) * fslabs + 4.0 * g->npad / 32.0;
     g->timed("first_moves", fbytes, [&] {
-        launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, g->tgt.p, B, k, n, g->npad,
+        launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, S.tgt.p, B, k, n, g->npad,
                            fm, g->leaf_fm ? g->leafbits.p : nullptr,
                            g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream);
     });
+    HIP_CHECK(hipEventRecord(g->ev_fm, g->stream));
     if (stat)
-        HIP_CHECK(hipMemcpyAsync(g->stat_h.data(), stat, g->stat.n * sizeof(unsigned int),
+        HIP_CHECK(hipMemcpyAsync(S.stat_h.data(), stat, S.stat.n * sizeof(unsigned int),
                                  hipMemcpyDeviceToHost, g->stream));
 }
 
-// Upload a batch's targets as columns.  With sorting on, lanes hold the
-// targets in column order (DFS preorder is spatially coherent, so a 1024-lane
-// slab covers one compact region and the up-sweep skips most rows);
-// g->pos_of[i] = lane of the caller's target i.
-void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k) {
+// Upload a batch's targets as columns into `slot`, on stream st.  With
+// sorting on, lanes hold the targets in column order (DFS preorder is
+// spatially coherent, so a 1024-lane slab covers one compact region and the
+// up-sweep skips most rows); pos_of[i] = lane of the caller's target i.
+void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t slot,
+                    hipStream_t st) {
+    auto& S = g->bs[slot];
     CPD_REQUIRE(g->has_ch, CPD_E_ARG,
                 "graph was created from a plan without hierarchy: it can serve queries "
                 "but not build rows");
@@ -983,14 +1063,20 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k) {
             idx.swap(it);
         }
     }
-    g->pos_of.resize(k);
+    S.pos_of.resize(k);
     for (uint32_t p = 0; p < k; ++p) {
         cols[p] = g->order[targets[idx[p]]];
-        g->pos_of[idx[p]] = p;
+        S.pos_of[idx[p]] = p;
     }
     for (uint32_t i = k; i < g->B; ++i) cols[i] = cols[0];  // padding lanes
-    g->tgt_col = cols;
-    g->tgt.upload(cols.data(), g->B, g->stream);
+    S.tgt_col = cols;
+    S.tgt.upload(S.tgt_col.data(), g->B, st);
+}
+
+// CPD_OVERLAP=0: no early up-sweep of the next batch (A/B; identical rows).
+bool overlap_on() {
+    static const bool on = env_on("CPD_OVERLAP");
+    return on;
 }
 
 // CPD_TRACE=1: host-side phase times of every batch on stderr.
@@ -1002,19 +1088,37 @@ bool trace_on() {
     return on;
 }
 
-// Build rows for one batch of k <= B targets; append to r (device).
-void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r) {
+// Build rows for one batch of k <= B targets; append to r (device).  next /
+// next_k (may be null / 0): the targets of the batch that follows; its
+// up-sweep is launched early, on ustream, as soon as this batch's down-sweep
+// is done (when this batch's first moves read no 32-bit rows, which the
+// up-sweep overwrites: narrow rows with no wide group row).
+void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
+                 const uint32_t* next, uint32_t next_k) {
     const double t0 = now_seconds();
     const uint32_t x = g->acquire_set();
     uint32_t* fm = g->fmx[x].p;
     uint32_t* rst = g->rle_stx[x].p;
     uint8_t* rrc = g->rle_rcx[x].p;
-    upload_targets(g, targets, k);
+    uint32_t slot;
+    if (g->prepped && g->prep_targets.size() == k &&
+        std::equal(targets, targets + k, g->prep_targets.begin())) {
+        slot = g->prep_slot;  // up-sweep launched by the previous batch
+        HIP_CHECK(hipStreamWaitEvent(g->stream, g->ev_up, 0));
+        g->prepped = false;
+    } else {
+        if (g->prepped) g->drop_prep();
+        slot = g->next_slot;
+        upload_targets(g, targets, k, slot, g->stream);
+        launch_up(g, k, slot, g->stream);
+    }
+    g->next_slot = slot ^ 1u;
     const uint32_t npad = g->npad;
     const double fm_row = g->fmb / 8.0 * npad;  // first-move bytes per row
     // + per 32-column segment a 4-B entry state and a 1-B count (fmb == 4)
     const double st_row = g->fmb == 4 ? 5.0 * npad / 32.0 : 0.0;
-    run_sweeps_and_fm(g, k, g->narrow, fm);
+    const bool narrow = g->narrow;
+    launch_down_fm(g, k, narrow, fm, slot);
     const double t1 = now_seconds();
     const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
     if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
@@ -1043,13 +1147,27 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     std::vector<uint32_t> counts(k);
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, g->stream));
-    const bool probe = g->narrow && g->narrow_probe && k == g->B;
-    if (g->narrow && (g->timing || probe))
-        HIP_CHECK(hipMemcpyAsync(&g->ovf_h, g->ovf.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                 g->stream));
+    // the next batch's up-sweep, beside this batch's first moves and count:
+    // after this batch's down-sweep (ev_down: it reads the up rows, live and
+    // tmask the up-sweep rewrites), and after its first moves too if they
+    // read 32-bit rows (wide group rows, or no narrow rows at all)
+    if (next && next_k && overlap_on()) {
+        const uint32_t ns = slot ^ 1u;
+        upload_targets(g, next, next_k, ns, g->ustream);
+        HIP_CHECK(hipEventSynchronize(g->ev_down));  // g->ovf_h has landed
+        HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
+        if (!narrow || g->ovf_h) HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm, 0));
+        launch_up(g, next_k, ns, g->ustream);
+        HIP_CHECK(hipEventRecord(g->ev_up, g->ustream));
+        g->prepped = true;
+        g->prep_slot = ns;
+        g->prep_targets.assign(next, next + next_k);
+    }
+    const bool probe = narrow && g->narrow_probe && k == g->B;
     g->sync();
+    add_up_late_bytes(g, slot);
     const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
-    if (g->narrow && g->timing) {  // group rows kept wide / all group rows
+    if (narrow && g->timing) {  // group rows kept wide / all group rows
         g->agg["wide_rows"].launches += g->ovf_h;
         g->agg["group_rows"].launches += groups;
     }
@@ -1062,8 +1180,9 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
     // r->total; counts[] and the emit kernel's offsets are per lane
     std::vector<uint64_t> off(k + 1), lane_off(k);
     off[0] = r->total;
+    const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
     for (uint32_t i = 0; i < k; ++i) {
-        const uint32_t p = g->pos_of[i];
+        const uint32_t p = pos_of[i];
         lane_off[p] = off[i];
         off[i + 1] = off[i] + counts[p];
     }
@@ -1112,7 +1231,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r)
                      r->runs.n);
     r->offsets.insert(r->offsets.end(), off.begin() + 1, off.end());
     r->targets.insert(r->targets.end(), targets, targets + k);
-    r->lanes.insert(r->lanes.end(), g->pos_of.begin(), g->pos_of.begin() + k);
+    r->lanes.insert(r->lanes.end(), pos_of.begin(), pos_of.begin() + k);
     r->nrows += k;
     r->total = new_total;
 }
@@ -1138,12 +1257,31 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         r->offsets.assign(1, 0);
         for (uint32_t b = 0; b < ntargets; b += g->B) {
             uint32_t k = std::min(g->B, ntargets - b);
-            build_batch(g, targets + b, k, r);
+            const uint32_t* next = nullptr;
+            uint32_t next_k = 0;
+            if (b + k < ntargets) {  // the call's own next batch
+                next = targets + b + k;
+                next_k = std::min(g->B, ntargets - b - k);
+            } else if (!g->hint.empty()) {  // the next call's first batch
+                next = g->hint.data();
+                next_k = (uint32_t)std::min<size_t>(g->B, g->hint.size());
+            }
+            build_batch(g, targets + b, k, r, next, next_k);
         }
+        g->hint.clear();
         r->off.upload(r->offsets.data(), r->offsets.size(), g->stream);
         HIP_CHECK(hipStreamSynchronize(g->stream));
         owned.release();
         *out = r;
+    });
+}
+
+int cpd_graph_hint_next(cpd_graph* g, const uint32_t* targets, uint32_t ntargets) {
+    return guarded([&] {
+        CPD_REQUIRE(g && (targets || ntargets == 0), CPD_E_ARG, "hint: null argument");
+        for (uint32_t i = 0; i < ntargets; ++i)
+            CPD_REQUIRE(targets[i] < g->n, CPD_E_ARG, "hint: target out of range");
+        g->hint.assign(targets, targets + ntargets);
     });
 }
 
@@ -1238,10 +1376,16 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
         if (!g->B) g->reserve_batch(0);
         CPD_REQUIRE(ntargets > 0 && ntargets <= g->B, CPD_E_ARG, "debug: 0 < ntargets <= batch");
         const uint32_t x = g->acquire_set();
-        upload_targets(g, targets, ntargets);
+        if (g->prepped) g->drop_prep();
+        const uint32_t slot = g->next_slot;
+        upload_targets(g, targets, ntargets, slot, g->stream);
         const bool narrow = g->narrow;
-        run_sweeps_and_fm(g, ntargets, narrow, g->fmx[x].p);
+        launch_up(g, ntargets, slot, g->stream);
+        launch_down_fm(g, ntargets, narrow, g->fmx[x].p, slot);
         g->sync();
+        g->bs[slot].up_late.clear();
+        const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
+        const std::vector<uint32_t>& tgt_col = g->bs[slot].tgt_col;
         const uint32_t n = g->n, B = g->B;
         // lane p holds the caller's target i = pos_of^-1(p)
         std::vector<uint32_t> h((size_t)n * B);
@@ -1265,7 +1409,7 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
         if (dist)
             for (uint32_t v = 0; v < n; ++v)
                 for (uint32_t i = 0; i < ntargets; ++i)
-                    dist[(size_t)v * ntargets + i] = h[(size_t)g->order[v] * B + g->pos_of[i]];
+                    dist[(size_t)v * ntargets + i] = h[(size_t)g->order[v] * B + pos_of[i]];
         if (fm) {
             // unpack fmb-bit sets; a column whose set is the wildcard (the
             // target, unreachable columns) reports CPD_FM_ALL like the oracle
@@ -1275,7 +1419,7 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
             HIP_CHECK(hipMemcpy(w.data(), g->fmx[x].p, w.size() * sizeof(uint32_t),
                                 hipMemcpyDeviceToHost));
             for (uint32_t i = 0; i < ntargets; ++i) {
-                const uint32_t p = g->pos_of[i];
+                const uint32_t p = pos_of[i];
                 for (uint32_t v = 0; v < n; ++v) {
                     const uint32_t c = g->order[v];
                     // 4-bit rows are row-group interleaved (cpd_kernels.hip
@@ -1285,7 +1429,7 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
                                         (p & 3u)) * 4u + (c % 32u) / 8u)
                                     : (size_t)p * row_words + c / per;
                     const uint32_t f = (w[wi] >> (g->fmb * (c % per))) & all;
-                    const bool wild = c == g->tgt_col[p] || h[(size_t)c * B + p] == CPD_INF;
+                    const bool wild = c == tgt_col[p] || h[(size_t)c * B + p] == CPD_INF;
                     fm[(size_t)i * n + v] = wild ? (uint16_t)CPD_FM_ALL : (uint16_t)f;
                 }
             }

@@ -126,6 +126,10 @@ public:
             const uint32_t cnt = (uint32_t)std::min<size_t>(B_, N - b0);
             cpd_rows*& r = rows_[blk & 1];
             const double tb = now();
+            if (b0 + cnt < N)  // the next block's up-sweep starts beside this block's first moves
+                ok(cpd_graph_hint_next(g_, targets.data() + b0 + cnt,
+                                       (uint32_t)std::min<size_t>(B_, N - b0 - cnt)),
+                   "hint");
             ok(cpd_build_rows(g_, targets.data() + b0, cnt, r, &r), "build");
             t_build += now() - tb;
             auto offs = std::make_shared<std::vector<uint64_t>>(cnt + 1);

@@ -199,6 +199,13 @@ void cpd_graph_free(cpd_graph* g);
  * to the host.  `reuse` (may be NULL) recycles a previous result's buffers. */
 int  cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
                     cpd_rows* reuse, cpd_rows** out);
+/* The targets the NEXT cpd_build_rows call on g will start with (its first
+ * batch; copied).  The current call's last batch then starts that batch's
+ * up-sweep early, beside its own first moves and RLE count (a call with
+ * several batches does this between its own batches without a hint).  A
+ * next call with other targets discards the early work; results never
+ * depend on the hint.  Cleared by every cpd_build_rows.                     */
+int  cpd_graph_hint_next(cpd_graph* g, const uint32_t* targets, uint32_t ntargets);
 int  cpd_rows_count(const cpd_rows* r, uint32_t* nrows, uint64_t* total_runs);
 int  cpd_rows_export(const cpd_rows* r, uint64_t* offsets /* nrows+1 */,
                      uint32_t* runs /* total_runs */);

@@ -15,6 +15,7 @@ oracle, walk queries over them dense and RLE.  What each reaches:
   CPD_ASYNC=0     the emit in line (one buffer set)
   CPD_RLE_CH=0    rle_scan<false, 4> counts (no chunked count / seam repair)
   CPD_LEAFFM=0    leaf first-move sets recomputed by first_moves
+  CPD_OVERLAP=0   each batch's up-sweep after the previous batch's first moves
 """
 import json
 import os
@@ -61,7 +62,7 @@ print(json.dumps(out))
 """
 
 SWITCHES = ["CPD_LIVE", "CPD_SORT", "CPD_LANE_KEY", "CPD_XCD", "CPD_FM_N4", "CPD_ASYNC",
-            "CPD_RLE_CH", "CPD_LEAFFM"]
+            "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP"]
 
 
 @pytest.mark.parametrize("switch", SWITCHES)

@@ -6,7 +6,7 @@ TAG=${1:-r03b}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$PWD
-timeout -k 10 700 python -u -m pytest tests/test_gpu_search.py tests/test_gpu_index_stream.py tests/test_gpu_parity.py tests/test_gpu_scale_1m.py tests/test_gpu_drivers.py -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 700 python -u -m pytest tests/test_gpu_search.py tests/test_gpu_index_stream.py tests/test_gpu_parity.py tests/test_gpu_scale_1m.py tests/test_gpu_drivers.py tests/test_gpu_switches.py tests/test_gpu_melb_standin.py -m gpu -x -v --timeout 300 --timeout-method thread \
     > gpurun_out/${TAG}_gputest.log 2>&1 || { echo "GPU TESTS FAILED"; tail -60 gpurun_out/${TAG}_gputest.log; exit 1; }
 tail -2 gpurun_out/${TAG}_gputest.log
 timeout -k 10 600 python bench.py --no-cpu --no-full-build > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
