@@ -175,17 +175,28 @@ struct Contractor {
         return priority_of(v, shortcuts(v, nullptr, settle_sim, nullptr, ws));
     }
 
+    // ids: the contraction works on internal ids (the DFS preorder: graph
+    // neighbours get nearby ids, so a witness search's scratch and lists stay
+    // in cache); orig[] maps back.  Every order that can change the result —
+    // adjacency lists, tie-breaks, the contraction order inside a round — is
+    // by ORIGINAL id, so the hierarchy is the one the node ids alone define.
+    std::vector<uint32_t> orig;
+
     bool less_key(uint32_t a, uint32_t b) const {
         if (prio[a] != prio[b]) return prio[a] < prio[b];
-        uint64_t ha = mix(a), hb = mix(b);
+        const uint32_t oa = orig[a], ob = orig[b];
+        uint64_t ha = mix(oa), hb = mix(ob);
         if (ha != hb) return ha < hb;
-        return a < b;
+        return oa < ob;
     }
 };
 
-void merge_into(std::vector<Adj>& lst, uint32_t v, uint32_t w) {
-    auto it = std::lower_bound(lst.begin(), lst.end(), v,
-                               [](const Adj& a, uint32_t key) { return a.v < key; });
+// Insert (v, w) into a list kept sorted by original id (keep the lighter
+// weight of a parallel arc).
+void merge_into(std::vector<Adj>& lst, uint32_t v, uint32_t w, const uint32_t* orig) {
+    const uint32_t ov = orig[v];
+    auto it = std::lower_bound(lst.begin(), lst.end(), ov,
+                               [orig](const Adj& a, uint32_t key) { return orig[a.v] < key; });
     if (it != lst.end() && it->v == v) {
         if (w < it->w) it->w = w;
     } else {
@@ -223,15 +234,19 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
         }
     }
 
-    // Overlay graph: no self loops, parallel edges reduced to the lightest.
+    // Internal ids (see Contractor::orig): lab[node] = DFS preorder position.
+    std::vector<uint32_t> lab(n);
+    dfs_preorder(n, row_ptr, dst, lab.data());
+    C.orig.assign(n, 0);
+    for (uint32_t v = 0; v < n; ++v) C.orig[lab[v]] = v;
+    const uint32_t* orig = C.orig.data();
+    // Overlay graph: no self loops, parallel edges reduced to the lightest;
+    // lists sorted by original id.
     for (uint32_t v = 0; v < n; ++v)
         for (uint32_t e = row_ptr[v]; e < row_ptr[v + 1]; ++e)
-            if (dst[e] != v) merge_into(C.out[v], dst[e], w[e]);
-    for (uint32_t v = 0; v < n; ++v)
-        for (const Adj& a : C.out[v]) C.in[a.v].push_back({v, a.w});
-    for (uint32_t v = 0; v < n; ++v)
-        std::sort(C.in[v].begin(), C.in[v].end(),
-                  [](const Adj& a, const Adj& b) { return a.v < b.v; });
+            if (dst[e] != v) merge_into(C.out[lab[v]], lab[dst[e]], w[e], orig);
+    for (uint32_t v = 0; v < n; ++v)  // tails in original order: in-lists come out sorted
+        for (const Adj& a : C.out[lab[v]]) C.in[a.v].push_back({lab[v], a.w});
 
     C.scratch.reserve(threads);
     for (int t = 0; t < threads; ++t) C.scratch.emplace_back(n);
@@ -242,8 +257,8 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
     std::vector<std::tuple<uint32_t, uint32_t, uint32_t>> dn;  // (u, v, w)
     dn.reserve((size_t)row_ptr[n] * 2);
 
-    std::vector<uint32_t> remaining(n);
-    std::iota(remaining.begin(), remaining.end(), 0u);
+    std::vector<uint32_t> remaining(n);  // internal ids in ORIGINAL id order
+    for (uint32_t v = 0; v < n; ++v) remaining[v] = lab[v];
 
     const double t_init = now_seconds();
 #pragma omp parallel for schedule(dynamic, 256) num_threads(threads)
@@ -311,9 +326,11 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
         phase(1);
         // 3. record hierarchy arcs, ranks
         for (uint32_t v : S) {
-            H.rank[v] = next_rank++;
-            up[v] = C.out[v];
-            for (const Adj& a : C.in[v]) dn.emplace_back(a.v, v, a.w);
+            const uint32_t ov = orig[v];
+            H.rank[ov] = next_rank++;
+            up[ov] = C.out[v];
+            for (Adj& a : up[ov]) a.v = orig[a.v];
+            for (const Adj& a : C.in[v]) dn.emplace_back(orig[a.v], ov, a.w);
         }
 
         // 4. remove S from the neighbours' lists; depth / deleted counters
@@ -370,7 +387,7 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
         for (int64_t g = 0; g < ngroups; ++g)
             for (size_t i = starts[g]; i < starts[g + 1]; ++i)
-                merge_into(C.out[all[i].u], all[i].x, all[i].w);
+                merge_into(C.out[all[i].u], all[i].x, all[i].w, orig);
         std::sort(all.begin(), all.end(), by_x);
         starts.clear();
         for (size_t i = 0; i < all.size(); ++i)
@@ -380,7 +397,7 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
         for (int64_t g = 0; g < ngroups; ++g)
             for (size_t i = starts[g]; i < starts[g + 1]; ++i)
-                merge_into(C.in[all[i].x], all[i].u, all[i].w);
+                merge_into(C.in[all[i].x], all[i].u, all[i].w, orig);
         // shortcut endpoints changed degree: their priority is stale too
         for (const Shortcut& s : all) {
             affected.push_back(s.u);
