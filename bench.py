@@ -681,6 +681,20 @@ def main():
                   "finished": int(sfin.sum()), "overflow": int(sst["overflow"]),
                   "kernel_ms": round(sst["kernel_ms"], 3), "lanes": int(sst["lanes"]),
                   "per_row_tables": "none (memoised CPD walks in each search's workspace)"}
+        # fscale 0 (optimal under the .diff weights): a 1M-node search expands
+        # ~59k nodes, so fewer queries and a 2^19-column workspace per search
+        zq = 512
+        zs, zt = ss[:zq], st_[:zq]
+        six.search(zs[:64], zt[:64], capacity=1 << 19)  # warm
+        _, _, zfin, zcnt, zst = six.search(zs, zt, capacity=1 << 19)
+        ztot = comm.reduce([float(zq), zst["kernel_ms"]], "SUM")
+        (zmax,) = comm.reduce([zst["kernel_ms"]], "MAX")
+        search["fscale0"] = {
+            "queries_per_s": round(ztot[0] / (zmax / 1e3), 1) if zmax else 0.0,
+            "queries": zq, "capacity": 1 << 19, "lanes": int(zst["lanes"]),
+            "mean_expanded": round(float(zcnt[:, 0].mean()), 1),
+            "finished": int(zfin.sum()), "overflow": int(zst["overflow"]),
+            "kernel_ms": round(zst["kernel_ms"], 3)}
         search_sample = (six, ss[:2000], st_[:2000], srows)
     # walk kernel vs its roofline: per query 8 (s, t) + 4 (row) + 13 (cost,
     # moves, flag) bytes, per move the 4-B word holding the move + the 8-B edge
@@ -743,6 +757,15 @@ def main():
                 np.array_equal(gcs, rc) and np.array_equal(gps, rp) and np.array_equal(gfs, rf)
                 and np.array_equal(gcnt.astype(np.uint64), rs))
             parity = parity and search["parity_2000_bit_exact"]
+            # fscale 0: 64 queries against the oracle
+            rc, rp, rf, rs = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, order, srows,
+                                               sref[0], sref[1], ss2[:64], st2[:64],
+                                               threads=threads)
+            gcs, gps, gfs, gcnt, _ = six.search(ss2[:64], st2[:64], capacity=1 << 19)
+            search["fscale0"]["parity_64_bit_exact"] = bool(
+                np.array_equal(gcs, rc) and np.array_equal(gps, rp) and np.array_equal(gfs, rf)
+                and np.array_equal(gcnt.astype(np.uint64), rs))
+            parity = parity and search["fscale0"]["parity_64_bit_exact"]
         cpu = {"value": round(leg["rows"] / leg["rows_s"], 3), "unit": "sources/s",
                "cores": threads, "kind": "port",
                "sample": f"{leg['rows']} CPD rows of the same graph and partition (reverse "

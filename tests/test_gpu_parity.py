@@ -183,6 +183,45 @@ def test_multi_slab_batches(width, batch):
             dist[:, i], oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, targets[i]))
 
 
+def test_next_batch_hint_and_early_up_sweep():
+    """cpd_graph_hint_next: the next call's first batch starts its up-sweep
+    during the current call.  A matching next call uses it, a different one
+    discards it, a debug build in between drops it — rows bit-exact in every
+    case; within one call, batch k + 1's up-sweep runs beside batch k's first
+    moves (several batches per call, with and without coordinates)."""
+    g = cpd.synth_road_graph(70, 70, seed=12)
+    plan = cpd.Plan(g)
+    order = plan.order()
+    rng = np.random.default_rng(12)
+    perm = rng.permutation(g.n).astype(np.uint32)
+    A, Bt, Ct = perm[:1024], perm[1024:2048], perm[2048:2900]
+    for xy in (False, True):
+        dev = cpd.Graph(plan, batch=1024)
+        if xy:
+            dev.set_coords(g.x, g.y)
+
+        def check(rows, tg):
+            off, runs = rows.export()
+            ro, rr = oracle.build_rows(g.row_ptr, g.dst, g.w, order, tg)
+            np.testing.assert_array_equal(off, ro)
+            np.testing.assert_array_equal(runs, rr)
+
+        dev.hint_next(Bt)
+        check(dev.build_rows(A), A)
+        check(dev.build_rows(Bt), Bt)      # uses the early up-sweep
+        dev.hint_next(Bt)
+        check(dev.build_rows(A), A)
+        check(dev.build_rows(Ct), Ct)      # hint mismatch: discarded
+        dev.hint_next(A)
+        check(dev.build_rows(Ct), Ct)
+        dev.debug_rows(Bt[:100], want_fm=False)  # drops the pending early up-sweep
+        check(dev.build_rows(A), A)
+        check(dev.build_rows(perm[:3500]), perm[:3500])  # 4 batches in one call
+        dev.hint_next(perm[:10])                  # a partial first batch
+        check(dev.build_rows(Bt), Bt)
+        check(dev.build_rows(perm[:10]), perm[:10])
+
+
 def test_narrow_overflow_rows_kept_wide():
     """Edge weights x700: a wave's 256 distances spread past 0xFFFF, so the
     narrow rows cannot hold them; those group rows are kept 32-bit (base =
