@@ -671,7 +671,7 @@ def main():
         sq = 20000
         ss = rng.integers(0, g.n, sq).astype(np.uint32)
         st_ = srows[rng.integers(0, len(srows), sq)]
-        six.search(ss[:256], st_[:256], fscale=0.1)  # warm
+        wst = six.search(ss[:256], st_[:256], fscale=0.1)[4]  # warm: tables built here
         _, _, sfin, scnt, sst = six.search(ss, st_, fscale=0.1)
         tot = comm.reduce([float(sq), sst["kernel_ms"]], "SUM")
         (smax,) = comm.reduce([sst["kernel_ms"]], "MAX")
@@ -680,7 +680,8 @@ def main():
                   "mean_expanded": round(float(scnt[:, 0].mean()), 1),
                   "finished": int(sfin.sum()), "overflow": int(sst["overflow"]),
                   "kernel_ms": round(sst["kernel_ms"], 3), "lanes": int(sst["lanes"]),
-                  "per_row_tables": "none (memoised CPD walks in each search's workspace)"}
+                  "form": {1: "per-row tables", 2: "memoised walks"}[sst["tables"]],
+                  "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
         # fscale 0 (optimal under the .diff weights): a 1M-node search expands
         # ~59k nodes, so fewer queries and a 2^19-column workspace per search
         zq = 512
@@ -695,6 +696,13 @@ def main():
             "mean_expanded": round(float(zcnt[:, 0].mean()), 1),
             "finished": int(zfin.sum()), "overflow": int(zst["overflow"]),
             "kernel_ms": round(zst["kernel_ms"], 3)}
+        # the fscale-0.1 queries with the memoised-walk form (what a
+        # worker-sized index, whose tables do not fit, runs)
+        _, _, _, _, wsst = six.search(ss[:4096], st_[:4096], fscale=0.1, tables="walks")
+        search["walks_form"] = {
+            "queries": 4096, "lanes": int(wsst["lanes"]), "fscale": 0.1,
+            "queries_per_s": round(4096 / (wsst["kernel_ms"] / 1e3), 1) if wsst["kernel_ms"]
+            else 0.0}
         search_sample = (six, ss[:2000], st_[:2000], srows)
     # walk kernel vs its roofline: per query 8 (s, t) + 4 (row) + 13 (cost,
     # moves, flag) bytes, per move the 4-B word holding the move + the 8-B edge

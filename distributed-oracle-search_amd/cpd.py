@@ -56,6 +56,7 @@ EXPORTED = [
 # SURVEY.md §8(d) as written (row-major ids, bidirectional, E/N/W/S order)
 SYNTH_STYLES = {"shuffled": 7, "spec": 0}
 INDEX_MODES = {"auto": 0, "rle": 1, "dense": 2}
+SEARCH_FORMS = {"auto": 0, "tables": 1, "walks": 2}
 
 
 class CpdError(RuntimeError):
@@ -84,13 +85,14 @@ class QueryStats(C.Structure):
 class SearchOpts(C.Structure):
     _fields_ = [("hscale", C.c_double), ("fscale", C.c_double), ("k_moves", C.c_int32),
                 ("itrs", C.c_int64), ("time_ns", C.c_uint64), ("capacity", C.c_uint32),
-                ("virtual_tick_ns", C.c_uint64)]
+                ("virtual_tick_ns", C.c_uint64), ("tables", C.c_int32)]
 
 
 class SearchStats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("queries", "finished", "expanded", "inserted",
                                           "touched", "updated", "surplus", "plen", "overflow")] + \
-               [("kernel_ms", C.c_double), ("lanes", C.c_uint64)]
+               [("kernel_ms", C.c_double), ("lanes", C.c_uint64), ("tables_ms", C.c_double),
+                ("tables", C.c_int32)]
 
 
 class KernelTime(C.Structure):
@@ -532,12 +534,12 @@ class Index:
         return {k: getattr(st, k) for k, _ in QueryStats._fields_}
 
     def search(self, s, t, hscale=1.0, fscale=0.0, k_moves=-1, itrs=-1, time_ns=0,
-               capacity=0, virtual_tick_ns=0):
+               capacity=0, virtual_tick_ns=0, tables="auto"):
         """CPD-heuristic search (cpd_query_search) for queries (s, t):
         (cost, plen, finished, counters[nq, 5], stats)."""
         self.prepare(s, t)
         o = SearchOpts(float(hscale), float(fscale), int(k_moves), int(itrs), int(time_ns),
-                       int(capacity), int(virtual_tick_ns))
+                       int(capacity), int(virtual_tick_ns), SEARCH_FORMS[tables])
         st = SearchStats()
         _check(lib.cpd_query_search(self._h, C.byref(o), C.byref(st)))
         nq = len(s)

@@ -470,10 +470,15 @@ struct cpd_index {
         // auto: the table whose bytes are fewer (4 B per run vs n/2 B per row)
         return nrows > 0 && 4.0 * (double)declared > (double)g->npad / 2.0 * nrows;
     }
-    // CPD-search workspace (per lane slot), per-query counters, sums
-    DevBuf<uint32_t> qstats;
+    // CPD-search: per-row tables when they fit (hrow free-flow heuristic,
+    // crow / lrow incumbent cost and moves under the current weights; rebuilt
+    // for new weights), row target columns, workspace (per lane slot),
+    // per-query counters, sums
+    DevBuf<uint64_t> hrow, crow;
+    DevBuf<uint32_t> lrow, tcol, qstats;
     DevBuf<uint8_t> sws;
     DevBuf<unsigned long long> sagg;
+    bool h_ready = false, c_ready = false;
     bool searched = false;  // qstats hold the counters of the prepared queries
     // query workspace; queries run sorted by target row (perm[i] = caller index)
     uint32_t nq = 0;
@@ -1713,6 +1718,7 @@ int cpd_index_set_weights(cpd_index* ix, const uint32_t* w) {
         cpd_graph* g = ix->g;
         g->select();
         if (!w) {
+            if (ix->custom_w) ix->c_ready = false;
             ix->custom_w = false;
             return;
         }
@@ -1722,6 +1728,7 @@ int cpd_index_set_weights(cpd_index* ix, const uint32_t* w) {
         ix->adj_sel.upload(adj.data(), adj.size(), g->stream);
         HIP_CHECK(hipStreamSynchronize(g->stream));
         ix->custom_w = true;
+        ix->c_ready = false;  // the search's incumbent tables follow the weights
     });
 }
 
@@ -1904,7 +1911,7 @@ void cpd_index_free(cpd_index* ix) {
 int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st) {
     return guarded([&] {
         CPD_REQUIRE(ix, CPD_E_ARG, "null index");
-        cpd_search_opts o{1.0, 0.0, -1, -1, 0, 0, 0};
+        cpd_search_opts o{1.0, 0.0, -1, -1, 0, 0, 0, CPD_SEARCH_AUTO};
         if (opts) o = *opts;
         if (!o.capacity) o.capacity = 32768;
         CPD_REQUIRE((o.capacity & (o.capacity - 1)) == 0 && o.capacity >= 64 &&
@@ -1913,15 +1920,61 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
         CPD_REQUIRE(o.hscale >= 0.0 && o.fscale >= 0.0, CPD_E_ARG,
                     "hscale and fscale must be >= 0");
         CPD_REQUIRE(ix->added == ix->nrows, CPD_E_ARG, "search: index incomplete");
+        CPD_REQUIRE(o.tables == CPD_SEARCH_AUTO || o.tables == CPD_SEARCH_TABLES ||
+                        o.tables == CPD_SEARCH_WALKS,
+                    CPD_E_ARG, "search tables must be CPD_SEARCH_AUTO, _TABLES or _WALKS");
         cpd_graph* g = ix->g;
         g->select();
-        const uint32_t nq = ix->nq;
+        const uint32_t n = g->n, nq = ix->nq;
         if (!ix->dense_ready) ensure_dense(ix);
-        // workspace per lane slot: search_ws_bytes_per_slot(capacity) (116 B
-        // per column of capacity); as many slots (whole blocks of 4 waves) as
-        // a quarter of free HBM holds
+        const uint32_t* adj_w = ix->custom_w ? ix->adj_sel.p : g->adj.p;
+        // per-row tables (20 B per column per row) when they fit in half of
+        // the free HBM (AUTO) or when asked for; else memoised walks
+        const size_t cells = (size_t)ix->nrows * n;
+        bool tables = o.tables == CPD_SEARCH_TABLES;
+        {
+            size_t free_b = 0, total_b = 0;
+            HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            const size_t have = ix->hrow.p ? 20u * cells : 0u;
+            const bool fits = 20u * cells - have < (free_b + have) / 2;
+            if (o.tables == CPD_SEARCH_AUTO) tables = fits;
+            CPD_REQUIRE(!tables || fits, CPD_E_OOM,
+                        "cpd-search tables need " + std::to_string((20u * cells) >> 20) +
+                            " MiB (20 B per column per index row): use the walk form");
+        }
+        hipEvent_t a = g->get_event(), b = g->get_event();
+        double tables_ms = 0.0;
+        if (tables && (!ix->h_ready || !ix->c_ready)) {
+            size_t free_b = 0, total_b = 0;
+            ix->hrow.alloc(cells);
+            ix->crow.alloc(cells);
+            ix->lrow.alloc(cells);
+            std::vector<uint32_t> tc(ix->nrows, 0);
+            for (uint32_t c = 0; c < n; ++c)
+                if (ix->row_of_col[c] != CPD_INF) tc[ix->row_of_col[c]] = c;
+            ix->tcol.upload(tc.data(), tc.size(), g->stream);
+            HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            // scratch for the doubling rounds: 48 B per column per chunk row
+            const uint32_t chunk = (uint32_t)std::max<size_t>(
+                1, std::min<size_t>(ix->nrows, (size_t)(free_b / 4) / (48ull * n + 1)));
+            DevBuf<uint8_t> scratch;
+            scratch.alloc((size_t)chunk * n * 48u);
+            HIP_CHECK(hipEventRecord(a, g->stream));
+            launch_search_tables(ix->dense.p, g->npad, g->adj.p, adj_w, g->adj_shift, ix->tcol.p,
+                                 ix->nrows, n, scratch.p, chunk, ix->hrow.p, ix->crow.p,
+                                 ix->lrow.p, ix->h_ready ? 0 : 1, g->stream);
+            HIP_CHECK(hipEventRecord(b, g->stream));
+            HIP_CHECK(hipStreamSynchronize(g->stream));
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+            tables_ms = ms;
+            ix->h_ready = ix->c_ready = true;
+        }
+        // workspace per lane slot: search_ws_bytes_per_slot(capacity, tables)
+        // (68 B per column of capacity with tables, 116 B with walks); as many
+        // slots (whole blocks of 4 waves) as a quarter of free HBM holds
         uint32_t slots = nq ? search_slots(nq) : 0u;
-        const size_t per_slot = search_ws_bytes_per_slot(o.capacity);
+        const size_t per_slot = search_ws_bytes_per_slot(o.capacity, tables);
         if (nq) {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -1935,12 +1988,11 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
         ix->qstats.alloc(5ull * std::max(1u, nq));
         ix->sagg.alloc(8);
         HIP_CHECK(hipMemsetAsync(ix->sagg.p, 0, 8 * sizeof(unsigned long long), g->stream));
-        const uint32_t* adj_w = ix->custom_w ? ix->adj_sel.p : g->adj.p;
-        hipEvent_t a = g->get_event(), b = g->get_event();
         HIP_CHECK(hipEventRecord(a, g->stream));
         (void)hipGetLastError();
         if (nq)
-            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad, ix->qs.p,
+            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad,
+                              tables ? ix->hrow.p : nullptr, ix->crow.p, ix->lrow.p, n, ix->qs.p,
                               ix->qt.p, ix->qrow.p, nq, o.hscale, o.fscale, o.k_moves, o.itrs,
                               o.time_ns, o.virtual_tick_ns, ix->sws.p, o.capacity, slots,
                               ix->cost.p, ix->hops.p, ix->fin.p, ix->qstats.p, ix->sagg.p,
@@ -1972,6 +2024,8 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             st->overflow = h[7];
             st->kernel_ms = ms;
             st->lanes = slots;
+            st->tables_ms = tables_ms;
+            st->tables = tables ? CPD_SEARCH_TABLES : CPD_SEARCH_WALKS;
         }
     });
 }

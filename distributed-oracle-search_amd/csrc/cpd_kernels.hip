@@ -1896,6 +1896,96 @@ __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
 constexpr uint64_t kInf64 = 0xFFFFFFFFFFFFFFFFull;
 constexpr uint32_t kOnWalk = 2u, kWalked = 1u;
 
+// Per-row tables (the TABLES form of the search): per index row r (target
+// t), over the columns, computed from the dense move table by pointer
+// jumping over the CPD's next-hop tree — the CPD walk from every column at
+// once, in log2(n) + 1 doubling rounds:
+//   hrow[r][c] = free-flow cost of the CPD path c -> t (the heuristic),
+//   crow[r][c] = its cost under the selected weights (the incumbent bound),
+//   lrow[r][c] = its moves;  INF (hrow, crow) when the walk never reaches t.
+// Jump state per (row, column): next column (kJumpBad = no path), cf, cw,
+// lw; t points to itself with zero cost (absorbing).
+constexpr uint32_t kJumpBad = 0xFFFFFFFFu;
+
+struct JumpState {
+    uint32_t* next;
+    uint64_t* cf;
+    uint64_t* cw;
+    uint32_t* lw;
+};
+
+__global__ __launch_bounds__(256) void jump_init(const uint32_t* __restrict__ dense,
+                                                 uint32_t wpr, const uint2* __restrict__ adj_f,
+                                                 const uint2* __restrict__ adj_w, uint32_t shift,
+                                                 const uint32_t* __restrict__ tcol, uint32_t rows,
+                                                 uint32_t n, JumpState js) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (j >= (uint64_t)rows * n) return;
+    const uint32_t r = (uint32_t)(j / n), c = (uint32_t)(j - (uint64_t)r * n);
+    uint32_t nx = kJumpBad, l = 0;
+    uint64_t f = 0, w = 0;
+    if (c == tcol[r]) {
+        nx = c;
+    } else {
+        const uint32_t mv = (dense[(size_t)r * wpr + (c >> 3)] >> (4u * (c & 7u))) & 0xFu;
+        if (!(mv >> shift)) {
+            const size_t e = ((size_t)c << shift) + mv;
+            const uint2 ef = adj_f[e];
+            if (ef.x != kNoEdge) {
+                nx = ef.x;
+                f = ef.y;
+                w = adj_w[e].y;
+                l = 1;
+            }
+        }
+    }
+    js.next[j] = nx;
+    js.cf[j] = f;
+    js.cw[j] = w;
+    js.lw[j] = l;
+}
+
+// One doubling round a -> b: b(c) = a(c) followed by a(next(c)).
+__global__ __launch_bounds__(256) void jump_round(JumpState a, JumpState b,
+                                                  const uint32_t* __restrict__ tcol, uint32_t rows,
+                                                  uint32_t n) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (j >= (uint64_t)rows * n) return;
+    const uint32_t r = (uint32_t)(j / n);
+    const uint32_t nx = a.next[j];
+    uint32_t o = nx;
+    uint64_t f = a.cf[j], w = a.cw[j];
+    uint32_t l = a.lw[j];
+    if (nx != kJumpBad && nx != tcol[r]) {
+        const uint64_t k = (uint64_t)r * n + nx;
+        o = a.next[k];
+        if (o != kJumpBad) {
+            f += a.cf[k];
+            w += a.cw[k];
+            l += a.lw[k];
+        }
+    }
+    b.next[j] = o;
+    b.cf[j] = f;
+    b.cw[j] = w;
+    b.lw[j] = l;
+}
+
+__global__ __launch_bounds__(256) void jump_final(JumpState a, const uint32_t* __restrict__ tcol,
+                                                  uint32_t rows, uint32_t n,
+                                                  uint64_t* __restrict__ hrow,
+                                                  uint64_t* __restrict__ crow,
+                                                  uint32_t* __restrict__ lrow, int write_h) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (j >= (uint64_t)rows * n) return;
+    const uint32_t r = (uint32_t)(j / n);
+    const bool ok = a.next[j] == tcol[r];
+    if (write_h) hrow[j] = ok ? a.cf[j] : kInf64;
+    crow[j] = ok ? a.cw[j] : kInf64;
+    lrow[j] = ok ? a.lw[j] : 0u;
+}
+
+
 struct SearchWs {
     uint4* ent;     // [slots][2C]
     uint4* memo;    // [slots][2C]
@@ -2087,10 +2177,21 @@ __device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj
     return true;
 }
 
-template <int SHIFT>
+// TABLES: the CPD path values come from the per-row tables (hrow / crow /
+// lrow, n per row) instead of memoised walks; the workspace then holds only
+// the searched columns (no memo, no walk stack).  Same results and counters.
+struct SearchTables {
+    const uint64_t* hrow;
+    const uint64_t* crow;
+    const uint32_t* lrow;
+    uint32_t n;
+};
+
+template <int SHIFT, bool TABLES>
 __global__ __launch_bounds__(256) void cpd_search(
     const uint2* __restrict__ adj_f, const uint2* __restrict__ adj_w,
-    const uint32_t* __restrict__ dense, uint32_t wpr, const uint32_t* __restrict__ qs,
+    const uint32_t* __restrict__ dense, uint32_t wpr, SearchTables tb,
+    const uint32_t* __restrict__ qs,
     const uint32_t* __restrict__ qt, const uint32_t* __restrict__ qrow, uint32_t nq,
     uint32_t chunk, SearchOpt opt, SearchWs ws, uint64_t* __restrict__ cost_out,
     uint32_t* __restrict__ plen_out, uint8_t* __restrict__ fin_out,
@@ -2102,8 +2203,9 @@ __global__ __launch_bounds__(256) void cpd_search(
     const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
     const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
     const uint32_t C = ws.cap;
-    const LaneWs W{ws.ent + slot * 2u * C, ws.memo + slot * 2u * C, ws.aux + slot * 2u * C,
-                   ws.he + slot * C, ws.hc + slot * C, ws.stk + slot * C, C, 2u * C - 1u};
+    const LaneWs W{ws.ent + slot * 2u * C, TABLES ? nullptr : ws.memo + slot * 2u * C,
+                   ws.aux + slot * 2u * C, ws.he + slot * C, ws.hc + slot * C,
+                   TABLES ? nullptr : ws.stk + slot * C, C, 2u * C - 1u};
     unsigned long long s_exp = 0, s_ins = 0, s_tou = 0, s_upd = 0, s_sur = 0, s_len = 0,
                        s_fin = 0, s_ovf = 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -2115,6 +2217,7 @@ __global__ __launch_bounds__(256) void cpd_search(
     L.q = kIdleQ;
     L.done = false;
     const uint32_t* row = dense;
+    size_t rb = 0;  // TABLES: the query row's first table entry
     auto begin = [&](uint32_t q) {
         L.q = q;
         L.s = qs[q];
@@ -2129,18 +2232,25 @@ __global__ __launch_bounds__(256) void cpd_search(
         L.overflow = false;
         L.t0 = __builtin_amdgcn_s_memrealtime();
         row = dense + (size_t)qrow[q] * wpr;
-        // t walked with zeros, then the walk from s
+        rb = (size_t)qrow[q] * tb.n;
         bool found;
-        const uint32_t ti = hprobe(W.ent, W.mask, L.tag, L.t, found);
-        ws_insert(L, W, ti, L.t, kWalked);
-        W.memo[ti] = make_uint4(0u, 0u, 0u, 0u);
         uint32_t si;
-        if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, L.s, si)) {
-            L.overflow = L.done = true;
-            return;
+        uint64_t hs;
+        if (TABLES) {
+            hs = tb.hrow[rb + L.s];
+            si = hprobe(W.ent, W.mask, L.tag, L.s, found);
+            if (hs != kInf64) ws_insert(L, W, si, L.s, 0u);
+        } else {  // t walked with zeros, then the walk from s
+            const uint32_t ti = hprobe(W.ent, W.mask, L.tag, L.t, found);
+            ws_insert(L, W, ti, L.t, kWalked);
+            W.memo[ti] = make_uint4(0u, 0u, 0u, 0u);
+            if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, L.s, si)) {
+                L.overflow = L.done = true;
+                return;
+            }
+            const uint4 m = W.memo[si];
+            hs = u64of(m.x, m.y);
         }
-        const uint4 m = W.memo[si];
-        const uint64_t hs = u64of(m.x, m.y);
         if (hs != kInf64) {
             W.ent[si].z = 0u;
             W.ent[si].w = 0u;
@@ -2207,9 +2317,16 @@ __global__ __launch_bounds__(256) void cpd_search(
         ++L.expanded;
         const uint32_t dv = W.aux[hi].x;
         {
-            const uint4 mv = W.memo[hi];
-            const uint64_t cw = u64of(mv.z, mv.w);
-            const uint32_t lw = W.aux[hi].y & 0x3FFFFFFFu;
+            uint64_t cw;
+            uint32_t lw;
+            if (TABLES) {
+                cw = tb.crow[rb + v];
+                lw = tb.lrow[rb + v];
+            } else {
+                const uint4 mv = W.memo[hi];
+                cw = u64of(mv.z, mv.w);
+                lw = W.aux[hi].y & 0x3FFFFFFFu;
+            }
             if (cw != kInf64 && (opt.kmoves < 0 || lw <= (uint32_t)opt.kmoves)) {
                 const uint64_t cand = g + cw;
                 if (cand < L.ub) {
@@ -2229,13 +2346,23 @@ __global__ __launch_bounds__(256) void cpd_search(
             uint32_t ui = hprobe(W.ent, W.mask, L.tag, u, fu);
             const bool seen = fu && !(W.ent[ui].z == 0xFFFFFFFFu && W.ent[ui].w == 0xFFFFFFFFu);
             if (!seen) {
-                if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, u, ui)) {
-                    L.overflow = L.done = true;
-                    break;
+                uint64_t hu;
+                if (TABLES) {
+                    hu = tb.hrow[rb + u];
+                    if (hu == kInf64) continue;
+                    if (!ws_insert(L, W, ui, u, 0u)) {
+                        L.overflow = L.done = true;
+                        break;
+                    }
+                } else {
+                    if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, u, ui)) {
+                        L.overflow = L.done = true;
+                        break;
+                    }
+                    const uint4 mu = W.memo[ui];
+                    hu = u64of(mu.x, mu.y);
+                    if (hu == kInf64) continue;
                 }
-                const uint4 mu = W.memo[ui];
-                const uint64_t hu = u64of(mu.x, mu.y);
-                if (hu == kInf64) continue;
                 if (L.hsize >= C) {
                     L.overflow = L.done = true;
                     break;
@@ -2254,9 +2381,9 @@ __global__ __launch_bounds__(256) void cpd_search(
                 W.ent[ui].w = (uint32_t)(ng >> 32);
                 W.aux[ui].x = dv + 1u;
                 ++L.updated;
-                const uint4 mu = W.memo[ui];
-                heap_push(W.he, W.hc, L.hsize,
-                          ng + (uint64_t)(opt.hscale * (double)u64of(mu.x, mu.y)), u, ng);
+                const uint64_t hu = TABLES ? tb.hrow[rb + u]
+                                           : u64of(W.memo[ui].x, W.memo[ui].y);
+                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
             }
         }
     }
@@ -2606,40 +2733,98 @@ uint32_t search_slots(uint32_t nq) {  // lanes with a workspace: whole blocks of
     return 64u * ((w + 3u) / 4u * 4u);
 }
 
+void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* adj_f,
+                          const uint32_t* adj_w, uint32_t shift, const uint32_t* tcol,
+                          uint32_t rows, uint32_t n, void* scratch, uint32_t chunk_rows,
+                          uint64_t* hrow, uint64_t* crow, uint32_t* lrow, int write_h,
+                          hipStream_t s) {
+    uint32_t rounds = 1;
+    while ((1ull << (rounds - 1)) < (uint64_t)n + 1ull) ++rounds;  // 2^(rounds-1) > n hops
+    const size_t per = (size_t)chunk_rows * n;
+    char* base = static_cast<char*>(scratch);
+    auto state = [&](int k) {
+        char* p = base + (size_t)k * per * 24u;
+        return kern::JumpState{reinterpret_cast<uint32_t*>(p),
+                               reinterpret_cast<uint64_t*>(p + per * 4u),
+                               reinterpret_cast<uint64_t*>(p + per * 12u),
+                               reinterpret_cast<uint32_t*>(p + per * 20u)};
+    };
+    const kern::JumpState A = state(0), Bs = state(1);
+    const uint2* af = reinterpret_cast<const uint2*>(adj_f);
+    const uint2* aw = reinterpret_cast<const uint2*>(adj_w);
+    for (uint32_t r0 = 0; r0 < rows; r0 += chunk_rows) {
+        const uint32_t R = std::min(chunk_rows, rows - r0);
+        const uint64_t items = (uint64_t)R * n;
+        const dim3 grid((uint32_t)((items + 255u) / 256u)), blk(256);
+        launch(kern::jump_init, grid, blk, s, dense + (size_t)r0 * (npad / 8u), npad / 8u, af, aw,
+               shift, tcol + r0, R, n, A);
+        kern::JumpState a = A, b = Bs;
+        for (uint32_t k = 0; k < rounds; ++k) {
+            launch(kern::jump_round, grid, blk, s, a, b, tcol + r0, R, n);
+            std::swap(a, b);
+        }
+        launch(kern::jump_final, grid, blk, s, a, tcol + r0, R, n, hrow + (size_t)r0 * n,
+               crow + (size_t)r0 * n, lrow + (size_t)r0 * n, write_h);
+    }
+}
+
 void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t shift,
-                       const uint32_t* dense, uint32_t npad, const uint32_t* qs,
-                       const uint32_t* qt, const uint32_t* qrow, uint32_t nq, double hscale,
-                       double fscale, int32_t kmoves, int64_t itrs, uint64_t time_ns,
-                       uint64_t tick_ns, void* ws, uint32_t cap, uint32_t slots, uint64_t* cost,
-                       uint32_t* plen, uint8_t* fin, uint32_t* qstats, unsigned long long* agg,
-                       hipStream_t s) {
+                       const uint32_t* dense, uint32_t npad, const uint64_t* hrow,
+                       const uint64_t* crow, const uint32_t* lrow, uint32_t n,
+                       const uint32_t* qs, const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
+                       double hscale, double fscale, int32_t kmoves, int64_t itrs,
+                       uint64_t time_ns, uint64_t tick_ns, void* ws, uint32_t cap,
+                       uint32_t slots, uint64_t* cost, uint32_t* plen, uint8_t* fin,
+                       uint32_t* qstats, unsigned long long* agg, hipStream_t s) {
+    const bool tables = hrow != nullptr;
     const uint32_t waves = slots / 64u;  // a multiple of 4 (search_slots)
     char* p = static_cast<char*>(ws);
     const size_t h2 = (size_t)slots * 2u * cap, h1 = (size_t)slots * cap;
-    kern::SearchWs w{reinterpret_cast<uint4*>(p), reinterpret_cast<uint4*>(p + h2 * 16u),
-                     reinterpret_cast<uint2*>(p + h2 * 32u),
-                     reinterpret_cast<uint4*>(p + h2 * 40u),
-                     reinterpret_cast<uint32_t*>(p + h2 * 40u + h1 * 16u),
-                     reinterpret_cast<uint4*>(p + h2 * 40u + h1 * 20u), cap};
+    kern::SearchWs w;
+    w.cap = cap;
+    w.ent = reinterpret_cast<uint4*>(p);
+    p += h2 * 16u;
+    if (!tables) {
+        w.memo = reinterpret_cast<uint4*>(p);
+        p += h2 * 16u;
+    } else {
+        w.memo = nullptr;
+    }
+    w.aux = reinterpret_cast<uint2*>(p);
+    p += h2 * 8u;
+    w.he = reinterpret_cast<uint4*>(p);
+    p += h1 * 16u;
+    w.stk = tables ? nullptr : reinterpret_cast<uint4*>(p);
+    if (!tables) p += h1 * 16u;
+    w.hc = reinterpret_cast<uint32_t*>(p);
     const kern::SearchOpt o{hscale, fscale, kmoves, itrs, time_ns, tick_ns};
+    const kern::SearchTables tb{hrow, crow, lrow, n};
     const dim3 grid(waves / 4u), blk(256);  // every wave has a workspace slot
     const uint32_t c2 = (uint32_t)(((uint64_t)nq + waves - 1u) / waves);
     const uint2* af = reinterpret_cast<const uint2*>(adj_f);
     const uint2* aw = reinterpret_cast<const uint2*>(adj_w);
     const uint32_t wpr = npad / 8u;
-#define CPD_SEARCH(SH)                                                                      \
-    launch(kern::cpd_search<SH>, grid, blk, s, af, aw, dense, wpr, qs, qt, qrow, nq, c2, o, w, \
-           cost, plen, fin, qstats, agg)
+#define CPD_SEARCH(SH, T)                                                                    \
+    launch(kern::cpd_search<SH, T>, grid, blk, s, af, aw, dense, wpr, tb, qs, qt, qrow, nq, c2, \
+           o, w, cost, plen, fin, qstats, agg)
+#define CPD_SEARCH_T(SH)          \
+    if (tables) CPD_SEARCH(SH, true); \
+    else CPD_SEARCH(SH, false)
     switch (shift) {
-        case 0: CPD_SEARCH(0); break;
-        case 1: CPD_SEARCH(1); break;
-        case 2: CPD_SEARCH(2); break;
-        case 3: CPD_SEARCH(3); break;
-        default: CPD_SEARCH(4); break;
+        case 0: CPD_SEARCH_T(0); break;
+        case 1: CPD_SEARCH_T(1); break;
+        case 2: CPD_SEARCH_T(2); break;
+        case 3: CPD_SEARCH_T(3); break;
+        default: CPD_SEARCH_T(4); break;
     }
+#undef CPD_SEARCH_T
 #undef CPD_SEARCH
 }
 
-uint64_t search_ws_bytes_per_slot(uint32_t cap) { return 116ull * cap; }
+// Workspace per lane slot and column of capacity: hash entries 2 x (16 + 8),
+// heap 16 + 4, and for memoised walks the memo (2 x 16) and walk stack (16).
+uint64_t search_ws_bytes_per_slot(uint32_t cap, bool tables) {
+    return (tables ? 68ull : 116ull) * cap;
+}
 
 }  // namespace cpd

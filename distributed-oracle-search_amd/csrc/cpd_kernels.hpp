@@ -165,22 +165,32 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
 
 // CPD-heuristic search (cpd_kernels.hip "CPD-heuristic search"): one search
 // per query (sorted by target row, qrow as for table-search) over the dense
-// move rows (npad/8 words per row), heuristic and incumbent from memoised CPD
-// walks; adj_f / adj_w: packed adjacency with free-flow / selected weights.
-// cost / plen / fin per query, qstats[5 q + k] = expanded, inserted, touched,
-// updated, surplus; agg[8] (zeroed by the caller) += sums of those, plen,
-// finished, overflowed.  time_ns: 0 = none; tick_ns: 0 = wall clock, else
-// the virtual clock (tick_ns per expansion and per touched edge).
+// move rows (npad/8 words per row); adj_f / adj_w: packed adjacency with
+// free-flow / selected weights.  The CPD path values come from the per-row
+// tables hrow / crow / lrow (n per row; launch_search_tables) when hrow is
+// non-null, else from CPD walks memoised in the workspace.  cost / plen / fin
+// per query, qstats[5 q + k] = expanded, inserted, touched, updated, surplus;
+// agg[8] (zeroed by the caller) += sums of those, plen, finished,
+// overflowed.  time_ns: 0 = none; tick_ns: 0 = wall clock, else the virtual
+// clock (tick_ns per expansion and per touched edge).
+// Tables for index rows [0, rows) by pointer jumping in chunks of chunk_rows
+// rows; scratch = 48 B x chunk_rows x n; tcol[r] = row r's target column.
+void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* adj_f,
+                          const uint32_t* adj_w, uint32_t shift, const uint32_t* tcol,
+                          uint32_t rows, uint32_t n, void* scratch, uint32_t chunk_rows,
+                          uint64_t* hrow, uint64_t* crow, uint32_t* lrow, int write_h,
+                          hipStream_t s);
 // Lane slots the search launches for nq queries (a multiple of 256); the
-// workspace holds search_ws_bytes_per_slot(cap) bytes per slot.
+// workspace holds search_ws_bytes_per_slot(cap, tables) bytes per slot.
 uint32_t search_slots(uint32_t nq);
-uint64_t search_ws_bytes_per_slot(uint32_t cap);
+uint64_t search_ws_bytes_per_slot(uint32_t cap, bool tables);
 void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t shift,
-                       const uint32_t* dense, uint32_t npad, const uint32_t* qs,
-                       const uint32_t* qt, const uint32_t* qrow, uint32_t nq, double hscale,
-                       double fscale, int32_t kmoves, int64_t itrs, uint64_t time_ns,
-                       uint64_t tick_ns, void* ws, uint32_t cap, uint32_t slots, uint64_t* cost,
-                       uint32_t* plen, uint8_t* fin, uint32_t* qstats, unsigned long long* agg,
-                       hipStream_t s);
+                       const uint32_t* dense, uint32_t npad, const uint64_t* hrow,
+                       const uint64_t* crow, const uint32_t* lrow, uint32_t n,
+                       const uint32_t* qs, const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
+                       double hscale, double fscale, int32_t kmoves, int64_t itrs,
+                       uint64_t time_ns, uint64_t tick_ns, void* ws, uint32_t cap,
+                       uint32_t slots, uint64_t* cost, uint32_t* plen, uint8_t* fin,
+                       uint32_t* qstats, unsigned long long* agg, hipStream_t s);
 
 }  // namespace cpd

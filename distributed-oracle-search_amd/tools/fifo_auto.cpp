@@ -255,7 +255,7 @@ int main(int argc, char** argv) {
         bool debug = json_field(conf, "debug") == "true";
         // cpd-search knobs (process_query.py:149-160): hscale, fscale, time
         // (ns; args.get_time_ns may send a float), itrs
-        cpd_search_opts so{1.0, 0.0, k_moves, -1, 0, 0, 0};  // wall-clock time limit
+        cpd_search_opts so{1.0, 0.0, k_moves, -1, 0, 0, 0, CPD_SEARCH_AUTO};  // wall-clock time limit
         if (!json_field(conf, "hscale").empty()) so.hscale = std::atof(json_field(conf, "hscale").c_str());
         if (!json_field(conf, "fscale").empty()) so.fscale = std::atof(json_field(conf, "fscale").c_str());
         if (!json_field(conf, "itrs").empty()) so.itrs = std::atoll(json_field(conf, "itrs").c_str());
@@ -318,8 +318,8 @@ int main(int argc, char** argv) {
                               (unsigned long long)ss.touched, (unsigned long long)ss.updated,
                               (unsigned long long)ss.surplus, (unsigned long long)ss.plen,
                               (unsigned long long)ss.finished, (long long)(t_receive * 1e9),
-                              (long long)(ss.kernel_ms * 1e6),
-                              (long long)(t_receive * 1e9 + ss.kernel_ms * 1e6));
+                              (long long)((ss.kernel_ms + ss.tables_ms) * 1e6),
+                              (long long)(t_receive * 1e9 + (ss.kernel_ms + ss.tables_ms) * 1e6));
             else
                 std::snprintf(buf, sizeof buf, "%llu,0,0,0,0,%llu,%llu,%lld,0,%lld",
                               (unsigned long long)st.hops, (unsigned long long)st.hops,

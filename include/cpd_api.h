@@ -323,14 +323,22 @@ void cpd_index_free(cpd_index* ix);
  * 0); stops when f_min x (1 + fscale) >= incumbent, after itrs expansions,
  * or once time_ns have elapsed.  Runs on the queries of the last
  * cpd_query_prepare; per query results (cost, plen as hops, finished) via
- * cpd_query_fetch.  The CPD path values come from walks over the dense rows,
- * memoised per search in its workspace (nothing per index row is kept, so
- * any index can be searched); a search needs `capacity` columns of workspace
- * (walked or searched, 116 B each) and one that needs more stops unfinished
- * and is counted in `overflow`.  The time limit is wall clock (as fifo_auto
- * runs it); virtual_tick_ns > 0 replaces it by a deterministic clock that
- * advances virtual_tick_ns per expansion and per edge touched (the oracle's
+ * cpd_query_fetch.  The CPD path values (heuristic, incumbent) come from
+ * per-row tables — 20 B per column per index row, built once per index and
+ * per weights by pointer jumping — when those fit in half of the free HBM
+ * (tables = CPD_SEARCH_AUTO) or when asked for (_TABLES, CPD_E_OOM if they do
+ * not fit); else (_WALKS, or AUTO on a large index) from CPD walks memoised
+ * in each search's workspace, so an index of any size can be searched.  The
+ * results and counters are the same either way.  A search's workspace holds
+ * `capacity` columns (searched ones; with walks also the walked ones; 68 /
+ * 116 B each): one that needs more stops unfinished and is counted in
+ * `overflow`.  The time limit is wall clock (as fifo_auto runs it);
+ * virtual_tick_ns > 0 replaces it by a deterministic clock that advances
+ * virtual_tick_ns per expansion and per edge touched (the oracle's
  * restatement, for tests).                                                   */
+#define CPD_SEARCH_AUTO   0
+#define CPD_SEARCH_TABLES 1
+#define CPD_SEARCH_WALKS  2
 typedef struct cpd_search_opts {
     double   hscale;       /* 1.0 */
     double   fscale;       /* 0.0 */
@@ -339,12 +347,15 @@ typedef struct cpd_search_opts {
     uint64_t time_ns;      /* 0: no time limit (per query) */
     uint32_t capacity;     /* columns per search, power of 2 (0 = 32768) */
     uint64_t virtual_tick_ns; /* 0: wall-clock time limit; else virtual clock */
+    int32_t  tables;       /* CPD_SEARCH_AUTO / _TABLES / _WALKS             */
 } cpd_search_opts;
 
 typedef struct cpd_search_stats {
     uint64_t queries, finished, expanded, inserted, touched, updated, surplus, plen, overflow;
     double   kernel_ms;    /* device time of the search kernel              */
     uint64_t lanes;        /* concurrent searches (workspace slots)         */
+    double   tables_ms;    /* device time spent (re)building the tables     */
+    int32_t  tables;       /* the form used: CPD_SEARCH_TABLES or _WALKS    */
 } cpd_search_stats;
 
 int  cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st);

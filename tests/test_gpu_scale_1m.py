@@ -97,9 +97,10 @@ def test_1m_full_batch(w1m):
         d = oracle.reverse_dijkstra(g.row_ptr, g.dst, g.w, tt)
         sel = t == tt
         np.testing.assert_array_equal(cost[sel], d[s[sel]].astype(np.uint64))
-    # cpd-search over the same worker-sized index (21504 rows: round 2's
-    # per-row tables would have needed 430 GB), congested weights, fscale
-    # 0.1, queries to the rows the oracle built above: bit-exact
+    # cpd-search over the same worker-sized index (21504 rows: per-row tables
+    # would need 430 GB, so AUTO takes the memoised walks; forcing tables is
+    # a clean CPD_E_OOM), congested weights, fscale 0.1, queries to the rows
+    # the oracle built above: bit-exact
     w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
     ix.set_weights(w_cong)
     sq = 1000
@@ -108,11 +109,14 @@ def test_1m_full_batch(w1m):
     rc, rp, rf, rs = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, plan.order(),
                                        targets[sample], ref_off, ref_runs, ss, stt, fscale=0.1)
     gc_, gp, gf, gcnt, gst = ix.search(ss, stt, fscale=0.1)
-    assert gst["overflow"] == 0
+    assert gst["overflow"] == 0 and gst["tables"] == cpd.SEARCH_FORMS["walks"]
     np.testing.assert_array_equal(gc_, rc)
     np.testing.assert_array_equal(gp, rp)
     np.testing.assert_array_equal(gf, rf)
     np.testing.assert_array_equal(gcnt.astype(np.uint64), rs)
+    with pytest.raises(cpd.CpdError) as ei:
+        ix.search(ss[:10], stt[:10], tables="tables")
+    assert ei.value.code == cpd.CPD_E_OOM
 
 
 @pytest.mark.parametrize("mode", ["dense", "rle"])

@@ -44,19 +44,22 @@ def _index(env_, mode):
     return ix
 
 
+@pytest.mark.parametrize("form", ["tables", "walks"])
 @pytest.mark.parametrize("mode", ["dense", "rle"])
 @pytest.mark.parametrize("opts", [dict(), dict(hscale=1.5), dict(fscale=0.25),
                                   dict(hscale=0.5, fscale=0.1), dict(k_moves=40),
                                   dict(itrs=7), dict(k_moves=0, itrs=200)],
                          ids=lambda o: ",".join(f"{k}={v}" for k, v in o.items()) or "default")
-def test_search_matches_oracle(env, mode, opts):
+def test_search_matches_oracle(env, mode, opts, form):
+    """Both forms of the CPD path values — per-row tables and memoised walks
+    — give the oracle's results and counters."""
     g, plan, dev, targets, off, runs, s, t, wc = env
     ix = _index(env, mode)
     for w_sel in (wc, g.w):
         ix.set_weights(None if w_sel is g.w else w_sel)
         rc, rp, rf, rs = _oracle(env, w_sel, **opts)
-        cost, plen, fin, cnt, st = ix.search(s, t, **opts)
-        assert st["overflow"] == 0
+        cost, plen, fin, cnt, st = ix.search(s, t, tables=form, **opts)
+        assert st["overflow"] == 0 and st["tables"] == cpd.SEARCH_FORMS[form]
         np.testing.assert_array_equal(cost, rc)
         np.testing.assert_array_equal(plen, rp)
         np.testing.assert_array_equal(fin, rf)
@@ -91,14 +94,33 @@ def test_search_optimal_and_bounded(env):
     assert np.all(cnt3[:, 0] == 1)
 
 
-def test_search_overflow_is_counted(env):
+def test_search_overflow_is_counted_tables(env):
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    rc, rp, rf, rs = _oracle(env, wc)
+    need = rs[:, 1].max()  # most nodes any query inserts
+    cap = 64
+    assert need > cap
+    cost, plen, fin, cnt, st = ix.search(s, t, capacity=cap, tables="tables")
+    assert st["overflow"] >= 1
+    # pushes = inserted + updated bound a search's nodes and heap entries:
+    # searches below the capacity are exact, those above it stop unfinished
+    small = rs[:, 1] + rs[:, 3] < cap
+    assert small.sum() > 100
+    np.testing.assert_array_equal(cost[small], rc[small])
+    np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small])
+    assert not fin[rs[:, 1] > cap].any()
+
+
+def test_search_overflow_is_counted_walks(env):
     g, plan, dev, targets, off, runs, s, t, wc = env
     ix = _index(env, "dense")
     ix.set_weights(wc)
     rc, rp, rf, rs = _oracle(env, wc, columns=True)
     cap = 256
     assert rs[:, 5].max() > cap  # some query's walks and search meet more columns
-    cost, plen, fin, cnt, st = ix.search(s, t, capacity=cap)
+    cost, plen, fin, cnt, st = ix.search(s, t, capacity=cap, tables="walks")
     assert st["overflow"] >= 1
     # a search's workspace holds every column its walks and search met (the
     # oracle's 6th stat) and its heap at most inserted + updated pushes:
@@ -110,31 +132,34 @@ def test_search_overflow_is_counted(env):
     assert not fin[rs[:, 5] > cap].any()
 
 
+@pytest.mark.parametrize("form", ["tables", "walks"])
 @pytest.mark.parametrize("time_ns,tick", [(1, 1), (40, 1), (300, 3), (5000, 7), (10**12, 1)])
-def test_search_time_limit_virtual_clock(env, time_ns, tick):
+def test_search_time_limit_virtual_clock(env, time_ns, tick, form):
     """The time limit under the deterministic clock (tick per expansion and
     per touched edge, the oracle's restatement): bit-exact."""
     g, plan, dev, targets, off, runs, s, t, wc = env
     ix = _index(env, "dense")
     ix.set_weights(wc)
     rc, rp, rf, rs = _oracle(env, wc, time_ns=time_ns, tick_ns=tick)
-    cost, plen, fin, cnt, st = ix.search(s, t, time_ns=time_ns, virtual_tick_ns=tick)
+    cost, plen, fin, cnt, st = ix.search(s, t, time_ns=time_ns, virtual_tick_ns=tick,
+                                         tables=form)
     np.testing.assert_array_equal(cost, rc)
     np.testing.assert_array_equal(plen, rp)
     np.testing.assert_array_equal(fin, rf)
     np.testing.assert_array_equal(cnt.astype(np.uint64), rs)
 
 
-def test_search_time_limit_wall_clock(env):
+@pytest.mark.parametrize("form", ["tables", "walks"])
+def test_search_time_limit_wall_clock(env, form):
     """The wall-clock limit fifo_auto runs (time from the worker JSON): 1 ns
-    has passed by the first check (the walk from s alone takes longer), so
-    no search expands — the oracle at itrs = 0; a limit of 1000 s changes
-    nothing."""
+    (one 100-MHz tick) has passed by the first check — the start of a search
+    reads HBM several times — so no search expands: the oracle at itrs = 0;
+    a limit of 1000 s changes nothing."""
     g, plan, dev, targets, off, runs, s, t, wc = env
     ix = _index(env, "dense")
     ix.set_weights(wc)
     for time_ns, ref in ((1, _oracle(env, wc, itrs=0)), (10**12, _oracle(env, wc))):
-        cost, plen, fin, cnt, st = ix.search(s, t, time_ns=time_ns)
+        cost, plen, fin, cnt, st = ix.search(s, t, time_ns=time_ns, tables=form)
         np.testing.assert_array_equal(cost, ref[0])
         np.testing.assert_array_equal(plen, ref[1])
         np.testing.assert_array_equal(fin, ref[2])
