@@ -1125,6 +1125,23 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     const bool narrow = g->narrow;
     launch_down_fm(g, k, narrow, fm, slot);
     const double t1 = now_seconds();
+    // the next batch's up-sweep, beside this batch's first moves and count:
+    // after this batch's down-sweep (ev_down: it reads the up rows, live and
+    // tmask the up-sweep rewrites), and after its first moves too if they
+    // read 32-bit rows (wide group rows, or no narrow rows at all)
+    auto prep_next = [&] {
+        if (!(next && next_k && overlap_on())) return;
+        const uint32_t ns = slot ^ 1u;
+        upload_targets(g, next, next_k, ns, g->ustream);
+        HIP_CHECK(hipEventSynchronize(g->ev_down));  // g->ovf_h has landed
+        HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
+        if (!narrow || g->ovf_h) HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm, 0));
+        launch_up(g, next_k, ns, g->ustream);
+        HIP_CHECK(hipEventRecord(g->ev_up, g->ustream));
+        g->prepped = true;
+        g->prep_slot = ns;
+        g->prep_targets.assign(next, next + next_k);
+    };
     const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
     if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
         HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), g->stream));
@@ -1137,6 +1154,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         });
         HIP_CHECK(hipMemcpyAsync(&g->rle_hard_h, g->rle_hard.p, sizeof(uint32_t),
                                  hipMemcpyDeviceToHost, g->stream));
+        prep_next();  // everything of this batch is queued: start the next up-sweep
         HIP_CHECK(hipStreamSynchronize(g->stream));
         if (g->rle_hard_h) {  // runs too long for the seam repair: the bounded pass
             g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
@@ -1148,26 +1166,11 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
             launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);
         });
+        prep_next();
     }
     std::vector<uint32_t> counts(k);
     HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, g->stream));
-    // the next batch's up-sweep, beside this batch's first moves and count:
-    // after this batch's down-sweep (ev_down: it reads the up rows, live and
-    // tmask the up-sweep rewrites), and after its first moves too if they
-    // read 32-bit rows (wide group rows, or no narrow rows at all)
-    if (next && next_k && overlap_on()) {
-        const uint32_t ns = slot ^ 1u;
-        upload_targets(g, next, next_k, ns, g->ustream);
-        HIP_CHECK(hipEventSynchronize(g->ev_down));  // g->ovf_h has landed
-        HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
-        if (!narrow || g->ovf_h) HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm, 0));
-        launch_up(g, next_k, ns, g->ustream);
-        HIP_CHECK(hipEventRecord(g->ev_up, g->ustream));
-        g->prepped = true;
-        g->prep_slot = ns;
-        g->prep_targets.assign(next, next + next_k);
-    }
     const bool probe = narrow && g->narrow_probe && k == g->B;
     g->sync();
     add_up_late_bytes(g, slot);
