@@ -56,6 +56,31 @@ struct DevBuf {
     }
 };
 
+// Page-locked host buffer: the staging side of every host<->device copy on
+// the build's path.  A pageable source or destination makes hipMemcpyAsync
+// wait for the device (the early up-sweep's target upload then waited for
+// the whole previous batch).
+template <class T>
+struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    HostBuf() = default;
+    HostBuf(const HostBuf&) = delete;
+    HostBuf& operator=(const HostBuf&) = delete;
+    ~HostBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    void alloc(size_t count) {
+        if (count <= n && p) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T),
+                                hipHostMallocDefault));
+        n = count;
+    }
+};
+
 // One timed interval: a single launch (events on its dispatch packet) or a
 // group of consecutive launches of one kernel (events recorded around them).
 struct Pending {
@@ -136,8 +161,9 @@ struct cpd_graph {
     // chunk exit states / run counts of the chunked count (read by rle_fix on
     // the same stream before the next batch: one set)
     DevBuf<uint32_t> rle_xs, rle_cc, rle_hard;
-    uint32_t rle_hard_h = 0;
-    std::vector<uint64_t> lane_off_h[2];  // host source of row_offx[x] (kept alive)
+    HostBuf<uint32_t> rle_hard_h;          // [1]
+    HostBuf<uint64_t> lane_off_h[2];       // host source of row_offx[x]
+    HostBuf<uint32_t> counts_h;            // [B] runs per lane
     // the buffer set the next batch uses, once the emit that last read it is done
     uint32_t acquire_set() {
         const uint32_t x = async ? cur : 0u;
@@ -169,7 +195,8 @@ struct cpd_graph {
     // the graph's lifetime — the results are identical either way
     static constexpr uint32_t kNarrowProbe = 2;
     uint32_t narrow_probe = kNarrowProbe;
-    uint32_t ovf_h = 0;
+    HostBuf<uint32_t> ovf_hb;  // [1] wide group rows of the last down-sweep
+    uint32_t ovf_h() const { return ovf_hb.p ? ovf_hb.p[0] : 0u; }
     DevBuf<uint16_t> d16;
     DevBuf<uint32_t> dbase, ovf;
     NarrowRows narrow_rows(bool on) {
@@ -187,8 +214,9 @@ struct cpd_graph {
     struct BatchSlot {
         DevBuf<uint32_t> tgt;
         std::vector<uint32_t> pos_of, tgt_col;
+        HostBuf<uint32_t> tgt_h;  // upload staging
         DevBuf<unsigned int> stat;
-        std::vector<unsigned int> stat_h;
+        HostBuf<unsigned int> stat_h;
         std::vector<std::array<double, 3>> up_late;
     };
     BatchSlot bs[2];
@@ -400,8 +428,16 @@ struct cpd_graph {
             dbase.alloc((size_t)n * (B / 256u));
             ovf.alloc(1);
         }
-        for (auto& b : bs) b.tgt.alloc(B);
+        for (auto& b : bs) {
+            b.tgt.alloc(B);
+            b.tgt_h.alloc(B);
+        }
         counts.alloc(B);
+        counts_h.alloc(B);
+        for (auto& l : lane_off_h) l.alloc(B);
+        rle_hard_h.alloc(1);
+        ovf_hb.alloc(1);
+        ovf_hb.p[0] = 0;
     }
 };
 
@@ -732,7 +768,8 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         }
         for (auto& b : g->bs) {
             b.stat.alloc(2 * (g->asc_lvl.size() + g->dsc_lvl.size()));
-            b.stat_h.assign(b.stat.n, 0);
+            b.stat_h.alloc(b.stat.n);
+            std::fill(b.stat_h.p, b.stat_h.p + b.stat.n, 0u);
         }
         auto lvl_of = [n](const std::vector<uint32_t>& first) {
             std::vector<uint32_t> v(n, 0);
@@ -864,13 +901,13 @@ bool trace_on();
 // rows off for good when most group rows had to be kept wide.
 void narrow_decide(cpd_graph* g) {
     const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
-    if (2ull * g->ovf_h <= groups) return;
+    if (2ull * g->ovf_h() <= groups) return;
     g->narrow = false;
     g->narrow_probe = 0;
     g->d16.release();
     g->dbase.release();
     if (trace_on())
-        std::fprintf(stderr, "[cpd] narrow rows off: %u of %llu group rows wide\n", g->ovf_h,
+        std::fprintf(stderr, "[cpd] narrow rows off: %u of %llu group rows wide\n", g->ovf_h(),
                      (unsigned long long)groups);
 }
 
@@ -938,7 +975,7 @@ void add_up_late_bytes(cpd_graph* g, uint32_t slot) {
     double b = 0.0;
     for (const auto& u : S.up_late) {
         const size_t l = (size_t)u[0];
-        b += 4096.0 * ((double)S.stat_h[2 * l] + (double)S.stat_h[2 * l + 1]) + 12.0 * u[1] +
+        b += 4096.0 * ((double)S.stat_h.p[2 * l] + (double)S.stat_h.p[2 * l + 1]) + 12.0 * u[1] +
              20.0 * u[2];
     }
     g->agg["sweep_up"].bytes += b;
@@ -962,7 +999,7 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
     uint32_t* live = live_on() ? g->live.p : nullptr;
     unsigned int* stat = g->timing ? S.stat.p : nullptr;
     const size_t nasc = g->asc_lvl.size();
-    const std::vector<unsigned int>& sh = S.stat_h;  // filled by the batch's D2H copy
+    const unsigned int* sh = S.stat_h.p;  // filled by the batch's D2H copy
     g->group_begin("sweep_down", g->stream);
     for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
         uint32_t s0 = g->dsc_lvl[l], cnt = g->dsc_lvl[l + 1] - s0;
@@ -974,7 +1011,7 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
         double dense = base + 4.0 * g->dsc_lvl_reads[l] * active;
         std::function<double()> late;
         if (live && stat)
-            late = [&sh, si, base, l, g, slabs] {
+            late = [sh, si, base, l, g, slabs] {
                 return base + 4096.0 * (double)sh[si] + 4.0 * g->dsc_lvl_reads[l] * slabs;
             };
         g->timed("sweep_down", dense, [&] {
@@ -988,7 +1025,7 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
     if (narrow) {
         launch_count_wide_rows(g->dbase.p, (size_t)n * (B / 256u),
                                reinterpret_cast<unsigned int*>(g->ovf.p), g->stream);
-        HIP_CHECK(hipMemcpyAsync(&g->ovf_h, g->ovf.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
+        HIP_CHECK(hipMemcpyAsync(g->ovf_hb.p, g->ovf.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                  g->stream));
     }
     if (live && stat && nasc > 2) {  // row counts behind the late byte counts
@@ -1020,7 +1057,7 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
     });
     HIP_CHECK(hipEventRecord(g->ev_fm, g->stream));
     if (stat)
-        HIP_CHECK(hipMemcpyAsync(S.stat_h.data(), stat, S.stat.n * sizeof(unsigned int),
+        HIP_CHECK(hipMemcpyAsync(S.stat_h.p, stat, S.stat.n * sizeof(unsigned int),
                                  hipMemcpyDeviceToHost, g->stream));
 }
 
@@ -1075,7 +1112,9 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t 
     }
     for (uint32_t i = k; i < g->B; ++i) cols[i] = cols[0];  // padding lanes
     S.tgt_col = cols;
-    S.tgt.upload(S.tgt_col.data(), g->B, st);
+    std::copy(cols.begin(), cols.end(), S.tgt_h.p);
+    HIP_CHECK(hipMemcpyAsync(S.tgt.p, S.tgt_h.p, (size_t)g->B * sizeof(uint32_t),
+                             hipMemcpyHostToDevice, st));
 }
 
 // CPD_OVERLAP=0: no early up-sweep of the next batch (A/B; identical rows).
@@ -1135,7 +1174,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         upload_targets(g, next, next_k, ns, g->ustream);
         HIP_CHECK(hipEventSynchronize(g->ev_down));  // g->ovf_h has landed
         HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
-        if (!narrow || g->ovf_h) HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm, 0));
+        if (!narrow || g->ovf_h()) HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm, 0));
         launch_up(g, next_k, ns, g->ustream);
         HIP_CHECK(hipEventRecord(g->ev_up, g->ustream));
         g->prepped = true;
@@ -1152,11 +1191,11 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
             launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
                            g->rle_hard.p, g->stream);
         });
-        HIP_CHECK(hipMemcpyAsync(&g->rle_hard_h, g->rle_hard.p, sizeof(uint32_t),
+        HIP_CHECK(hipMemcpyAsync(g->rle_hard_h.p, g->rle_hard.p, sizeof(uint32_t),
                                  hipMemcpyDeviceToHost, g->stream));
         prep_next();  // everything of this batch is queued: start the next up-sweep
         HIP_CHECK(hipStreamSynchronize(g->stream));
-        if (g->rle_hard_h) {  // runs too long for the seam repair: the bounded pass
+        if (g->rle_hard_h.p[0]) {  // runs too long for the seam repair: the bounded pass
             g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
                 launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);
             });
@@ -1168,15 +1207,15 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         });
         prep_next();
     }
-    std::vector<uint32_t> counts(k);
-    HIP_CHECK(hipMemcpyAsync(counts.data(), g->counts.p, k * sizeof(uint32_t),
+    const uint32_t* counts = g->counts_h.p;
+    HIP_CHECK(hipMemcpyAsync(g->counts_h.p, g->counts.p, k * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, g->stream));
     const bool probe = narrow && g->narrow_probe && k == g->B;
     g->sync();
     add_up_late_bytes(g, slot);
     const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
     if (narrow && g->timing) {  // group rows kept wide / all group rows
-        g->agg["wide_rows"].launches += g->ovf_h;
+        g->agg["wide_rows"].launches += g->ovf_h();
         g->agg["group_rows"].launches += groups;
     }
     if (probe) {
@@ -1217,8 +1256,8 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     // the next batch's up-sweep is done, so that it overlaps the down-sweep
     // instead, measured 288.5k rows/s against 293.6k: round 2.)
     hipStream_t es = g->async ? g->estream : g->stream;
-    g->lane_off_h[x].swap(lane_off);
-    g->row_offx[x].upload(g->lane_off_h[x].data(), k, es);
+    std::copy(lane_off.begin(), lane_off.end(), g->lane_off_h[x].p);
+    g->row_offx[x].upload(g->lane_off_h[x].p, k, es);
     double ebytes = (fm_row + st_row) * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
     g->timed("rle_emit", ebytes, [&] {
         launch_rle_emit(fm, g->fmb, npad, k, g->row_offx[x].p, r->runs.p, rst, rrc, es);
