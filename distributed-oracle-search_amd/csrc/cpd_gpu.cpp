@@ -97,6 +97,7 @@ struct Agg {
 };
 
 bool async_on();  // CPD_ASYNC (defined with the other switches)
+bool up_priority_on();
 bool lane_key_on();
 std::vector<uint32_t> hilbert_keys(const int32_t* x, const int32_t* y, uint32_t n);
 
@@ -655,7 +656,16 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
         // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step)
         HIP_CHECK(hipStreamCreateWithFlags(&g->estream, hipStreamNonBlocking));
-        HIP_CHECK(hipStreamCreateWithFlags(&g->ustream, hipStreamNonBlocking));
+        // the early up-sweep's stream at the highest priority: its small,
+        // latency-bound level kernels must get CUs while the first moves'
+        // 600k workgroups are queued (at equal priority they waited for all
+        // of them to be dispatched: 15 ms for a 0.7-ms init kernel)
+        {
+            int least = 0, greatest = 0;
+            HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIP_CHECK(hipStreamCreateWithPriority(&g->ustream, hipStreamNonBlocking,
+                                                  up_priority_on() ? greatest : least));
+        }
         for (hipEvent_t* e : {&g->ev_up, &g->ev_down, &g->ev_fm})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         for (auto& e : g->ev_emit) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1115,6 +1125,12 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t 
     std::copy(cols.begin(), cols.end(), S.tgt_h.p);
     HIP_CHECK(hipMemcpyAsync(S.tgt.p, S.tgt_h.p, (size_t)g->B * sizeof(uint32_t),
                              hipMemcpyHostToDevice, st));
+}
+
+// CPD_UP_PRIO=0: the early up-sweep's stream at normal priority (A/B).
+bool up_priority_on() {
+    static const bool on = env_on("CPD_UP_PRIO");
+    return on;
 }
 
 // CPD_OVERLAP=0: no early up-sweep of the next batch (A/B; identical rows).
