@@ -98,7 +98,6 @@ struct Agg {
 
 bool async_on();  // CPD_ASYNC (defined with the other switches)
 bool up_priority_on();
-uint32_t up_cu_count();
 bool lane_key_on();
 std::vector<uint32_t> hilbert_keys(const int32_t* x, const int32_t* y, uint32_t n);
 
@@ -228,14 +227,7 @@ struct cpd_graph {
     // it runs beside that batch's first moves and RLE count.  prep: the slot
     // and targets it was launched for, ev_up its end.
     hipStream_t ustream = nullptr;
-    hipEvent_t ev_up = nullptr, ev_down = nullptr, ev_fm = nullptr, ev_fsend = nullptr;
-    // CU partition (CPD_UP_CUS = k > 0): the early up-sweep runs on k CUs of
-    // its own (ustream's CU mask) and the first moves, RLE count and fix of
-    // the batch beside it on the other CUs (fstream); else fstream = stream
-    // and the two compete for every CU (the first moves' 600k workgroups
-    // then starve the up-sweep's small kernels).
-    hipStream_t fstream = nullptr;
-    bool fsplit = false;
+    hipEvent_t ev_up = nullptr, ev_down = nullptr, ev_fm = nullptr;
     bool prepped = false;
     uint32_t prep_slot = 0;
     std::vector<uint32_t> prep_targets, hint;
@@ -269,11 +261,6 @@ struct cpd_graph {
             for (auto e : {ev_up, ev_down, ev_fm})
                 if (e) (void)hipEventDestroy(e);
             if (ustream) (void)hipStreamDestroy(ustream);
-            if (fsplit && fstream) {
-                (void)hipStreamSynchronize(fstream);
-                (void)hipStreamDestroy(fstream);
-            }
-            if (ev_fsend) (void)hipEventDestroy(ev_fsend);
             if (stream) (void)hipStreamSynchronize(stream);
             for (auto& p : pending) {
                 (void)hipEventDestroy(p.a);
@@ -673,24 +660,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         // latency-bound level kernels must get CUs while the first moves'
         // 600k workgroups are queued (at equal priority they waited for all
         // of them to be dispatched: 15 ms for a 0.7-ms init kernel)
-        g->fstream = g->stream;
-        HIP_CHECK(hipEventCreateWithFlags(&g->ev_fsend, hipEventDisableTiming));
-        const uint32_t up_cus = up_cu_count();
-        hipDeviceProp_t prop{};
-        HIP_CHECK(hipGetDeviceProperties(&prop, device));
-        const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
-        if (up_cus > 0 && up_cus < ncu) {
-            // reserved CUs spread over the mask: every (ncu / up_cus)-th
-            const uint32_t words = (ncu + 31u) / 32u, stride = ncu / up_cus;
-            std::vector<uint32_t> um(words, 0u), fmk(words, 0u);
-            for (uint32_t c = 0; c < ncu; ++c) {
-                const bool up = c % stride == stride - 1u && c / stride < up_cus;
-                (up ? um : fmk)[c / 32u] |= 1u << (c % 32u);
-            }
-            HIP_CHECK(hipExtStreamCreateWithCUMask(&g->ustream, words, um.data()));
-            HIP_CHECK(hipExtStreamCreateWithCUMask(&g->fstream, words, fmk.data()));
-            g->fsplit = true;
-        } else {
+        {
             int least = 0, greatest = 0;
             HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             HIP_CHECK(hipStreamCreateWithPriority(&g->ustream, hipStreamNonBlocking,
@@ -1079,8 +1049,6 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
         });
     }
     HIP_CHECK(hipEventRecord(g->ev_down, g->stream));
-    hipStream_t fs = g->fstream;
-    if (fs != g->stream) HIP_CHECK(hipStreamWaitEvent(fs, g->ev_down, 0));
     // per row: own distance 4n (kernels that read it) + neighbour distances
     // 4m + first-move write npad * fmb / 8; the packed adjacency (8 B per
     // slot) is read once per 1024-target slab.  Leaf columns (leaf_fm) read
@@ -1095,20 +1063,12 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
     g->timed("first_moves", fbytes, [&] {
         launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, S.tgt.p, B, k, n, g->npad,
                            fm, g->leaf_fm ? g->leafbits.p : nullptr,
-                           g->leaf_fm ? g->fmleaf.p : nullptr, nr, fs);
+                           g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream);
     });
-    HIP_CHECK(hipEventRecord(g->ev_fm, fs));
+    HIP_CHECK(hipEventRecord(g->ev_fm, g->stream));
     if (stat)
         HIP_CHECK(hipMemcpyAsync(S.stat_h.p, stat, S.stat.n * sizeof(unsigned int),
-                                 hipMemcpyDeviceToHost, fs));
-}
-
-// Order g->stream after everything queued on fstream (no-op without a CU
-// partition): what follows on stream — the next down-sweep, syncs — waits.
-void join_fstream(cpd_graph* g) {
-    if (g->fstream == g->stream) return;
-    HIP_CHECK(hipEventRecord(g->ev_fsend, g->fstream));
-    HIP_CHECK(hipStreamWaitEvent(g->stream, g->ev_fsend, 0));
+                                 hipMemcpyDeviceToHost, g->stream));
 }
 
 // Upload a batch's targets as columns into `slot`, on stream st.  With
@@ -1171,15 +1131,6 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t 
 bool up_priority_on() {
     static const bool on = env_on("CPD_UP_PRIO");
     return on;
-}
-
-// CPD_UP_CUS=k: CUs reserved for the early up-sweep (0 = no partition).
-uint32_t up_cu_count() {
-    static const uint32_t v = [] {
-        const char* e = std::getenv("CPD_UP_CUS");
-        return (e && *e) ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
-    }();
-    return v;
 }
 
 // CPD_OVERLAP=0: no early up-sweep of the next batch (A/B; identical rows).
@@ -1246,37 +1197,35 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         g->prep_slot = ns;
         g->prep_targets.assign(next, next + next_k);
     };
-    hipStream_t fs = g->fstream;
     const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
     if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
-        HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), fs));
+        HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), g->stream));
         g->timed("rle_count", (fm_row + st_row + 8.0 * nch) * k, [&] {
-            launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, fs);
+            launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->stream);
         });
         g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
             launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
-                           g->rle_hard.p, fs);
+                           g->rle_hard.p, g->stream);
         });
         HIP_CHECK(hipMemcpyAsync(g->rle_hard_h.p, g->rle_hard.p, sizeof(uint32_t),
-                                 hipMemcpyDeviceToHost, fs));
+                                 hipMemcpyDeviceToHost, g->stream));
         prep_next();  // everything of this batch is queued: start the next up-sweep
-        HIP_CHECK(hipStreamSynchronize(fs));
+        HIP_CHECK(hipStreamSynchronize(g->stream));
         if (g->rle_hard_h.p[0]) {  // runs too long for the seam repair: the bounded pass
             g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
-                launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, fs);
+                launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);
             });
             if (trace_on()) std::fprintf(stderr, "[cpd] batch re-counted by rle_scan\n");
         }
     } else {
         g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
-            launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, fs);
+            launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);
         });
         prep_next();
     }
     const uint32_t* counts = g->counts_h.p;
     HIP_CHECK(hipMemcpyAsync(g->counts_h.p, g->counts.p, k * sizeof(uint32_t),
-                             hipMemcpyDeviceToHost, fs));
-    join_fstream(g);
+                             hipMemcpyDeviceToHost, g->stream));
     const bool probe = narrow && g->narrow_probe && k == g->B;
     g->sync();
     add_up_late_bytes(g, slot);
@@ -1496,7 +1445,6 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
         const bool narrow = g->narrow;
         launch_up(g, ntargets, slot, g->stream);
         launch_down_fm(g, ntargets, narrow, g->fmx[x].p, slot);
-        join_fstream(g);
         g->sync();
         g->bs[slot].up_late.clear();
         const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
