@@ -666,19 +666,24 @@ __global__ __launch_bounds__(256) void sweep_up_sparse(
 // masks with atomicOr.
 constexpr int kChunk = 16;
 
+// Grid-stride over (column, slab) rows with a small grid: the init runs on the
+// early up-sweep stream beside the previous batch's first moves, and one block
+// per 4-KiB row (~240k blocks at 1M nodes) would be dispatched round-robin
+// with first_moves' blocks and end with it, holding back every up level.
 __global__ __launch_bounds__(256) void sweep_up_init(const uint32_t* __restrict__ cols,
-                                                     uint32_t ncols, uint32_t remap,
+                                                     uint32_t ncols, uint32_t total,
                                                      uint32_t* __restrict__ dist,
                                                      const uint4* __restrict__ tgt4, uint32_t B4,
                                                      uint32_t* __restrict__ live,
                                                      const uint32_t* __restrict__ tmask,
                                                      uint32_t active) {
-    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t slab = L / ncols;
-    const uint32_t v = cols[L - slab * ncols];
-    const uint32_t l4 = slab * 256u + threadIdx.x;
-    reinterpret_cast<uint4*>(dist)[(size_t)v * B4 + l4] = leaf4(tgt4[l4], v, 0u);
-    if (slab == 0 && threadIdx.x == 0) live[v] = tmask[v] & active;
+    for (uint32_t L = blockIdx.x; L < total; L += gridDim.x) {
+        const uint32_t slab = L / ncols;
+        const uint32_t v = cols[L - slab * ncols];
+        const uint32_t l4 = slab * 256u + threadIdx.x;
+        reinterpret_cast<uint4*>(dist)[(size_t)v * B4 + l4] = leaf4(tgt4[l4], v, 0u);
+        if (slab == 0 && threadIdx.x == 0) live[v] = tmask[v] & active;
+    }
 }
 
 __global__ __launch_bounds__(256) void sweep_up_chunks(
@@ -2503,13 +2508,19 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
     }
 }
 
+static uint32_t up_init_blocks() {  // CPD_UP_INIT_BLOCKS: the init's grid (grid-stride)
+    static const uint32_t v = std::max(1u, env_u32("CPD_UP_INIT_BLOCKS", 512));
+    return v;
+}
+
 void launch_sweep_up_init(const uint32_t* cols, uint32_t ncols, uint32_t* dist,
                           const uint32_t* tgt, uint32_t B, uint32_t slabs, uint32_t* live,
                           const uint32_t* tmask, hipStream_t s) {
     if (!ncols) return;
     const uint32_t active = slabs >= 32 ? 0xFFFFFFFFu : ((1u << slabs) - 1u);
-    launch(kern::sweep_up_init, dim3(ncols * slabs), dim3(256), s, cols, ncols, xcd_remap(), dist,
-           reinterpret_cast<const uint4*>(tgt), B / 4u, live, tmask, active);
+    const uint32_t total = ncols * slabs;
+    launch(kern::sweep_up_init, dim3(std::min(total, up_init_blocks())), dim3(256), s, cols, ncols,
+           total, dist, reinterpret_cast<const uint4*>(tgt), B / 4u, live, tmask, active);
 }
 
 void launch_sweep_up_chunks(const uint32_t* items, uint32_t nitems, const uint32_t* nodes,

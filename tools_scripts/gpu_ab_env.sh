@@ -16,7 +16,7 @@ done
 for rep in 1 2; do
   for v in $vals; do
     out=gpurun_out/${tag}_${var}${v}_$rep
-    env "$var=$v" timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu --no-pmc --no-search --queries 200000 \
+    env "$var=$v" timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu --no-pmc --no-search --no-full-build --queries 200000 \
         > $out.json 2> $out.err || { echo "bench $var=$v failed"; tail -20 $out.err; exit 1; }
     python -c "import json;d=json.load(open('$out.json'));k=d['kernels'];print('$var=$v', d['value'], d['ms_per_step'], {n:round(v['ms']/10,2) for n,v in k.items() if n in ('sweep_down','sweep_up','first_moves','rle_count','rle_emit')}, d['roofline']['frac'])"
   done
