@@ -24,11 +24,12 @@ HIPFLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -I$(SRC) \
              -Wall -Wno-unused-parameter
 LDLIBS    := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
 
-HOST_OBJS := $(BLD)/host_util.o $(BLD)/ch.o $(BLD)/plan.o $(BLD)/cpd_gpu.o $(BLD)/cpd_io.o
-DEV_OBJS  := $(BLD)/cpd_kernels.o
+HOST_OBJS := $(BLD)/host_util.o $(BLD)/ch.o $(BLD)/ch_gpu.o $(BLD)/plan.o $(BLD)/cpd_gpu.o $(BLD)/cpd_io.o
+DEV_OBJS  := $(BLD)/cpd_kernels.o $(BLD)/ch_kernels.o
 TOOLS     := make_cpd_auto fifo_auto gen_distribute_conf gen_synth
 BINS      := $(addprefix bin/,$(TOOLS))
-HDRS      := include/cpd_api.h $(SRC)/cpd_internal.hpp $(SRC)/cpd_kernels.hpp $(SRC)/cpd_io.hpp
+HDRS      := include/cpd_api.h $(SRC)/cpd_internal.hpp $(SRC)/cpd_kernels.hpp $(SRC)/cpd_io.hpp \
+             $(SRC)/ch_kernels.hpp
 
 # Build provenance: sha256 over the library's and tools' sources (sorted by
 # path, contents concatenated — cpd.src_sha() recomputes it from the shipped
@@ -60,6 +61,9 @@ $(BLD)/host_util.o: $(SRC)/host_util.cpp $(HDRS) $(BLD)/src_sha.h | $(BLD)
 
 
 $(BLD)/cpd_kernels.o: $(SRC)/cpd_kernels.hip $(SRC)/cpd_kernels.hpp | $(BLD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BLD)/ch_kernels.o: $(SRC)/ch_kernels.hip $(SRC)/ch_kernels.hpp | $(BLD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(HOST_OBJS) $(DEV_OBJS)

@@ -67,7 +67,7 @@ class CpdError(RuntimeError):
 
 class PlanOpts(C.Structure):
     _fields_ = [("threads", C.c_int), ("witness_settle", C.c_uint32), ("verbose", C.c_int),
-                ("no_hierarchy", C.c_int)]
+                ("no_hierarchy", C.c_int), ("ch_gpu", C.c_int), ("ch_device", C.c_int)]
 
 
 class PlanInfo(C.Structure):
@@ -253,12 +253,15 @@ def synth_congestion(w, frac=0.1, lo=1.0, hi=3.0, seed=3) -> np.ndarray:
 
 class Plan:
     def __init__(self, g: RoadGraph | None = None, threads: int = 0, settle: int = 0,
-                 verbose: bool = False, hierarchy: bool = True, _handle=None):
+                 verbose: bool = False, hierarchy: bool = True, gpu: int | None = None,
+                 _handle=None):
+        """gpu: contract the hierarchy on this device (None: host threads)."""
         self._h = C.c_void_p()
         if _handle is not None:
             self._h = _handle
         else:
-            opts = PlanOpts(threads, settle, int(verbose), int(not hierarchy))
+            opts = PlanOpts(threads, settle, int(verbose), int(not hierarchy),
+                            int(gpu is not None), int(gpu or 0))
             _check(lib.cpd_plan_create(_ptr(g.row_ptr, u32p), _ptr(g.dst, u32p),
                                        _ptr(g.w, u32p), C.c_uint32(g.n), C.c_uint32(g.m),
                                        C.byref(opts), C.byref(self._h)))
@@ -270,13 +273,14 @@ class Plan:
         return cls(_handle=h)
 
     @classmethod
-    def cache(cls, path: str, g: RoadGraph, threads: int = 0, hierarchy: bool = True):
+    def cache(cls, path: str, g: RoadGraph, threads: int = 0, hierarchy: bool = True,
+              gpu: int | None = None):
         """(plan, status): the plan cached at `path` for this graph, built and
         saved under an flock if absent (status 0 loaded, 1 built and saved,
         2 built but not saved) — cpd_plan_cache."""
         h = C.c_void_p()
         st = C.c_int()
-        opts = PlanOpts(threads, 0, 0, int(not hierarchy))
+        opts = PlanOpts(threads, 0, 0, int(not hierarchy), int(gpu is not None), int(gpu or 0))
         _check(lib.cpd_plan_cache(path.encode(), _ptr(g.row_ptr, u32p), _ptr(g.dst, u32p),
                                   _ptr(g.w, u32p), C.c_uint32(g.n), C.c_uint32(g.m),
                                   C.byref(opts), C.byref(h), C.byref(st)))

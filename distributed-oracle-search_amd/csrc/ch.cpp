@@ -477,7 +477,21 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
         H.dn_w[i] = std::get<2>(dn[i]);
     }
 
-    // Sweep levels.
+    hierarchy_levels(H, n);
+    if (verbose)
+        std::fprintf(stderr,
+                     "[ch] %u rounds, up arcs %llu, down arcs %llu, levels up %u down %u "
+                     "(%.1fs)\n",
+                     round, (unsigned long long)H.up_off[n],
+                     (unsigned long long)H.dn_off[n], H.nlev_up, H.nlev_dn,
+                     now_seconds() - t0);
+    return H;
+}
+
+// Sweep levels of a finished hierarchy: level_up[x] = 1 + max level_up of
+// x's down-arc heads (rank ascending), level_dn[v] = 1 + max level_dn of v's
+// up-arc heads (rank descending).
+void hierarchy_levels(Hierarchy& H, uint32_t n) {
     std::vector<uint32_t> by_rank(n);
     for (uint32_t v = 0; v < n; ++v) by_rank[H.rank[v]] = v;
     H.level_up.assign(n, 0);
@@ -499,14 +513,6 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
     }
     H.nlev_up = mu + 1;
     H.nlev_dn = md + 1;
-    if (verbose)
-        std::fprintf(stderr,
-                     "[ch] %u rounds, up arcs %llu, down arcs %llu, levels up %u down %u "
-                     "(%.1fs)\n",
-                     round, (unsigned long long)H.up_off[n],
-                     (unsigned long long)H.dn_off[n], H.nlev_up, H.nlev_dn,
-                     now_seconds() - t0);
-    return H;
 }
 
 }  // namespace cpd

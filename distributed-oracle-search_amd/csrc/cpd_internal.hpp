@@ -60,6 +60,16 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr,
                           const uint32_t* dst, const uint32_t* w,
                           int threads, uint32_t settle_limit, int verbose);
 
+// The same hierarchy contracted on GPU `device` (ch_gpu.cpp, ch_kernels.hip):
+// identical rank, arcs and levels to build_hierarchy's.
+Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr,
+                              const uint32_t* dst, const uint32_t* w,
+                              int device, uint32_t settle_limit, int verbose);
+
+// Sweep levels (level_up / level_dn / nlev_*) of a hierarchy whose rank and
+// arc CSRs are set.
+void hierarchy_levels(Hierarchy& H, uint32_t n);
+
 // Upper bound on any finite shortest-path distance (u64, exact arithmetic).
 uint64_t distance_bound(uint32_t n, const uint32_t* row_ptr,
                         const uint32_t* dst, const uint32_t* w);

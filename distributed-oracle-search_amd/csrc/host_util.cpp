@@ -6,6 +6,7 @@
 #include <cstring>
 #include <numeric>
 #include <queue>
+#include <thread>
 
 #include "cpd_internal.hpp"
 #include "src_sha.h"
@@ -110,7 +111,16 @@ uint64_t distance_bound(uint32_t n, const uint32_t* row_ptr, const uint32_t* dst
     std::vector<uint64_t> off(n + 1);
     for (uint32_t v = 0; v <= n; ++v) off[v] = row_ptr[v];
     bool all_f = false, all_b = false;
-    uint64_t ef = eccentricity(n, off.data(), dst, w, 0, &all_f);
+    uint64_t ef = 0, eb = 0;
+    // the forward search runs on its own thread beside the reversal + the
+    // backward search
+    std::thread fwd([&] { ef = eccentricity(n, off.data(), dst, w, 0, &all_f); });
+    struct Join {
+        std::thread& t;
+        ~Join() {
+            if (t.joinable()) t.join();
+        }
+    } join{fwd};
     // reverse graph
     std::vector<uint64_t> roff(n + 1, 0);
     std::vector<uint32_t> rto(m), rw(m);
@@ -123,7 +133,8 @@ uint64_t distance_bound(uint32_t n, const uint32_t* row_ptr, const uint32_t* dst
             rto[p] = v;
             rw[p] = w[e];
         }
-    uint64_t eb = eccentricity(n, roff.data(), rto.data(), rw.data(), 0, &all_b);
+    eb = eccentricity(n, roff.data(), rto.data(), rw.data(), 0, &all_b);
+    fwd.join();
     if (all_f && all_b) return std::min(trivial, ef + eb);
     return trivial;
 }

@@ -8,7 +8,9 @@
 #include <atomic>
 #include <cstring>
 #include <fstream>
+#include <exception>
 #include <memory>
+#include <thread>
 
 #include "cpd_internal.hpp"
 
@@ -82,22 +84,41 @@ int cpd_plan_create(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t
         p->row_ptr.assign(row_ptr, row_ptr + n + 1);
         p->dst.assign(dst, dst + m);
         p->w.assign(w, w + m);
-        p->order.resize(n);
-        dfs_preorder(n, row_ptr, dst, p->order.data());
-        p->inv.resize(n);
-        for (uint32_t v = 0; v < n; ++v) p->inv[p->order[v]] = v;
-        p->dist_bound = distance_bound(n, row_ptr, dst, w);
-        CPD_REQUIRE(p->dist_bound < 0xFFFFFFFFull, CPD_E_RANGE,
-                    "graph distances may reach 2^32-1; the u32 distance path "
-                    "cannot represent them");
         int threads = opts ? opts->threads : 0;
         uint32_t settle = opts ? opts->witness_settle : 0;
         int verbose = opts ? opts->verbose : 0;
+        // the column order and the distance bound (a DFS and two Dijkstras,
+        // host-serial) run beside the hierarchy build, which needs neither
+        std::exception_ptr side_err;
+        std::thread side([&] {
+            try {
+                p->order.resize(n);
+                dfs_preorder(n, row_ptr, dst, p->order.data());
+                p->inv.resize(n);
+                for (uint32_t v = 0; v < n; ++v) p->inv[p->order[v]] = v;
+                p->dist_bound = distance_bound(n, row_ptr, dst, w);
+            } catch (...) {
+                side_err = std::current_exception();
+            }
+        });
+        struct Join {
+            std::thread& t;
+            ~Join() {
+                if (t.joinable()) t.join();
+            }
+        } join{side};
         if (!(opts && opts->no_hierarchy)) {
             double t0 = now_seconds();
-            p->ch = build_hierarchy(n, row_ptr, dst, w, threads, settle, verbose);
+            p->ch = opts && opts->ch_gpu
+                        ? build_hierarchy_gpu(n, row_ptr, dst, w, opts->ch_device, settle, verbose)
+                        : build_hierarchy(n, row_ptr, dst, w, threads, settle, verbose);
             p->ch_seconds = now_seconds() - t0;
         }
+        side.join();
+        if (side_err) std::rethrow_exception(side_err);
+        CPD_REQUIRE(p->dist_bound < 0xFFFFFFFFull, CPD_E_RANGE,
+                    "graph distances may reach 2^32-1; the u32 distance path "
+                    "cannot represent them");
         *out = p.release();
     });
 }

@@ -6,7 +6,8 @@
 //                 [--partition M]      README.md:89 spelling of --partmethod
 //                 [--device G]         default: I % (visible GPUs)
 //                 [--batch B]          rows per GPU sweep (multiple of 1024)
-//                 [--threads T]        host threads for the hierarchy build
+//                 [--threads T]        host threads for the hierarchy build (--ch-host)
+//                 [--ch-host]          contract the hierarchy on host threads, not the GPU
 //                 [--plan P | --no-plan-cache]
 //                 [--write-threads T]  host threads copying + writing rows (8)
 //                 [--no-pipeline]      build, then export, then write, per group
@@ -285,9 +286,16 @@ int main(int argc, char** argv) {
         cpd_plan* plan = nullptr;
         bool plan_loaded = false;
         double t0 = now();
+        int ndev = 0;
+        cli::check(cpd_device_count(&ndev), "device count");
+        const int device = ndev ? (int)a.num("device", wid % ndev) : -1;
         cpd_plan_opts o{};
         o.threads = (int)a.num("threads", 0);
         o.verbose = a.has("verbose");
+        // the hierarchy is contracted on this worker's GPU (the same hierarchy
+        // as the host build's, in a fraction of its time); --ch-host: threads
+        o.ch_gpu = ndev > 0 && !a.has("ch-host");
+        o.ch_device = std::max(device, 0);
         if (use_cache) {
             // workers started together (make_cpds.py:58-60) share one cache:
             // one builds, the others wait for it and load its plan
@@ -346,13 +354,10 @@ int main(int argc, char** argv) {
             return v;
         };
 
-        int ndev = 0;
-        cli::check(cpd_device_count(&ndev), "device count");
         if (ndev == 0) {
             std::fprintf(stderr, "make_cpd_auto: no GPU visible (this build has no CPU path)\n");
             return 1;
         }
-        int device = (int)a.num("device", wid % ndev);
         cpd_graph* dg = nullptr;
         cli::check(cpd_graph_create(plan, device, &dg), "graph upload");
         cli::check(cpd_graph_set_batch(dg, (uint32_t)a.num("batch", 0)), "batch");

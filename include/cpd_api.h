@@ -128,6 +128,10 @@ typedef struct cpd_plan_opts {
     int      verbose;          /* print CH progress to stderr                */
     int      no_hierarchy;     /* skip the CH: the plan can serve queries
                                   (fifo_auto) but cannot build rows         */
+    int      ch_gpu;           /* 1: contract the CH on GPU ch_device (the
+                                  host build's hierarchy, arc for arc;
+                                  CPD_E_HIP without a GPU); 0: host threads */
+    int      ch_device;
 } cpd_plan_opts;
 
 typedef struct cpd_plan_info {
