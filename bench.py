@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "distributed-oracle-search_amd")
 METRIC = "CPD build sources/sec + GTEPS; table-search queries/sec; % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PLAN_TAG = "ch823"      # bump when the hierarchy builder changes (cache key)
+PLAN_TAG = "ch823g"     # bump when the hierarchy builder changes (cache key)
 
 WORKLOADS = {
     "synth1m": dict(width=1000, seed=1, style="shuffled", method="div", key=8, sample=None,
@@ -317,7 +317,9 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
                         "groups": (kt or {}).get("group_rows", {}).get("launches")},
         "hierarchy": {"arcs": pinfo["ch_up_arcs"] + pinfo["ch_dn_arcs"],
                       "levels": [pinfo["levels_up"], pinfo["levels_dn"]],
-                      "build_s": round(pinfo["ch_seconds"], 1)} if pinfo else None,
+                      "build_s": round(pinfo["ch_seconds"], 2),
+                      "builder": "GPU contraction (ch_gpu.cpp), identical to the host build"}
+        if pinfo else None,
         "pmc_traffic_per_launch": {k: {"launches": v["launches"],
                                        "bytes": round(v["bytes_per_launch"], 1),
                                        "read": round(v["read_bytes_per_launch"], 1),
@@ -492,6 +494,18 @@ def full_build(args, xy, world, rank, device):
     return json.loads(line.split(": ", 1)[1])
 
 
+def build_plan_child(args, ppath, device):
+    """The workload's plan, its hierarchy contracted on GPU `device`
+    (ch_gpu.cpp: the host build's hierarchy, arc for arc), in a child process
+    so that this one initialises the GPU only after the PMC children."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import cpd\n"
+            "g = cpd.synth_road_graph(%d, %d, seed=%d, style=%r)\n"
+            "cpd.Plan(g, gpu=%d).save(%r)\n"
+            % (PKG, args.width, args.width, args.seed, args.style, device, ppath))
+    subprocess.run([sys.executable, "-c", code], check=True, timeout=600)
+
+
 def glob_xy(args):
     style = "" if args.style == "shuffled" else f"-{args.style}"
     return os.path.join(args.cache, f"fb-synth{args.width}-s{args.seed}{style}.xy")
@@ -529,8 +543,8 @@ def main():
     os.makedirs(args.cache, exist_ok=True)
     ppath = plan_path(args)
     if local == 0 and not os.path.exists(ppath):
-        log(f"building hierarchy for {g.n} nodes / {g.m} edges ...")
-        cpd.Plan(g).save(ppath)
+        log(f"building hierarchy for {g.n} nodes / {g.m} edges on GPU {local} ...")
+        build_plan_child(args, ppath, local)
     fb_xy = None
     if not args.no_full_build and args.sample is None and local == 0:
         fb_xy = full_build_xy(args)

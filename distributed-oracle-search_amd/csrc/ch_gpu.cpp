@@ -262,6 +262,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
     uint32_t lane_cap = 2048;  // pops + relaxations a lane search may take
     if (const char* e = std::getenv("CPD_CH_LANE_CAP")) lane_cap = (uint32_t)std::strtoul(e, nullptr, 10);
     uint64_t wave_searches = 0;
+    double t_lane = 0, t_wave = 0, t_big = 0;  // witness kernel wall times (verbose)
     DBuf<uint32_t> ovf3;
     auto witness = [&](uint32_t np, bool contract, uint32_t settle) {
         if (!np) return;
@@ -270,6 +271,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
         const uint32_t* list = nullptr;
         uint32_t cnt = np;
         searches += np;
+        double tw = now_seconds();
         if (np > wave_max) {
             chk::launch_witness(pairs.p, nullptr, np, overlay(), state.p, contract, settle, ws1.p,
                                 caps1, lanes1, tag1, no_wave ? 0xFFFFFFFFu : lane_cap, slots.p,
@@ -278,6 +280,8 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             read({ctr.p});
             cnt = hv.p[0];
             list = ovf.p;
+            t_lane += now_seconds() - tw;
+            tw = now_seconds();
         }
         if (cnt && !no_wave) {
             ovf2.ensure(cnt);
@@ -289,6 +293,8 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             read({ctr.p + 4});
             cnt = hv.p[0];
             list = ovf2.p;
+            t_wave += now_seconds() - tw;
+            tw = now_seconds();
         }
         read({ctr.p + 1, ctr.p + 2});
         const uint32_t err = hv.p[0], maxdeg = hv.p[1];
@@ -322,6 +328,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
         read({ctr.p + 3, ctr.p + 1});
         CPD_REQUIRE(!hv.p[0], CPD_E_HIP, "GPU contraction: witness workspace overflow");
         CPD_REQUIRE(!hv.p[1], CPD_E_RANGE, "shortcut weight >= 2^32-1");
+        t_big += now_seconds() - tw;
     };
     // priorities of list[0..k) (ch.cpp Contractor::priority / step 6)
     auto priorities = [&](const uint32_t* list, uint32_t k) {
@@ -515,12 +522,13 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
                      "workspace), "
                      "up arcs %llu, down arcs %llu, levels up %u down %u; setup %.2fs, initial "
                      "priorities %.2fs, rounds %.2fs (pick %.2f contract %.2f record %.2f lists "
-                     "%.2f priorities %.2f), assembly %.2fs\n",
+                     "%.2f priorities %.2f; witness kernels: lane %.2f wave %.2f large %.2f), "
+                     "assembly %.2fs\n",
                      round, (unsigned long long)searches, (unsigned long long)wave_searches,
                      (unsigned long long)big_searches,
                      (unsigned long long)H.up_off[n], (unsigned long long)H.dn_off[n], H.nlev_up,
                      H.nlev_dn, t_init - t0, t_prio0 - t_init, t_dev - t_prio0, tph[0], tph[1],
-                     tph[2], tph[3], tph[4], now_seconds() - t_dev);
+                     tph[2], tph[3], tph[4], t_lane, t_wave, t_big, now_seconds() - t_dev);
     return H;
 }
 

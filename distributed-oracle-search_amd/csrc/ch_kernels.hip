@@ -114,6 +114,8 @@ __global__ void k_make_pairs(const uint32_t* __restrict__ list, uint32_t k, Over
 // (1 = that target has settled).  Entries are valid when their tag is the
 // search's (tags are never reused within a workspace), so nothing is cleared.
 
+constexpr uint32_t kRelax = 8;  // arcs of a settled node relaxed per group
+
 struct Lane {
     uint4* hash;
     uint4* heap;
@@ -299,20 +301,58 @@ __global__ __launch_bounds__(256) void k_witness(
                 }
                 const uint32_t dx = g.odeg[x];
                 steps += dx;
-                for (uint32_t k = 0, o = g.ooff[x]; k < dx; ++k) {
-                    const uint2 e = arcs[o + k];
-                    if (e.x == v || (contract && state[e.x] == 1)) continue;
-                    const uint64_t nd = d + e.y;
-                    const uint32_t se = W.find(e.x);
-                    uint64_t cur = kInf;
-                    if (se <= W.hmask) {
-                        const uint4 ee = W.hash[se];
-                        cur = ((uint64_t)ee.w << 32) | ee.z;
-                    }
-                    if (nd < cur) {
-                        W.set_at(se, e.x, nd);
-                        W.push(nd, e.x);
-                        if (W.ovf) break;
+                // arcs in groups of kRelax: the group's arcs, avoid flags and
+                // home hash slots are loaded together (independent: the arcs
+                // of one list name distinct nodes), then applied in arc order
+                // — the sequential search's sets and pushes, in its order
+                const uint32_t o = g.ooff[x];
+                for (uint32_t k0 = 0; k0 < dx && !W.ovf; k0 += kRelax) {
+                    const uint32_t kn = min(kRelax, dx - k0);
+                    uint2 e[kRelax];
+                    bool live[kRelax];
+#pragma unroll
+                    for (uint32_t j = 0; j < kRelax; ++j)
+                        e[j] = j < kn ? arcs[o + k0 + j] : make_uint2(v, 0u);
+#pragma unroll
+                    for (uint32_t j = 0; j < kRelax; ++j)
+                        live[j] = e[j].x != v && !(contract && state[e[j].x] == 1);
+                    uint4 h[kRelax];
+#pragma unroll
+                    for (uint32_t j = 0; j < kRelax; ++j)
+                        h[j] = live[j] ? W.hash[W.slot0(e[j].x)] : make_uint4(0u, 0u, 0u, 0u);
+                    uint32_t ins[kRelax];  // slots inserted by this group
+                    uint32_t nins = 0;
+                    for (uint32_t j = 0; j < kn; ++j) {
+                        if (!live[j]) continue;
+                        const uint32_t y = e[j].x;
+                        // resolve the probe from the preloaded home entry
+                        uint32_t sy = W.slot0(y);
+                        uint4 ey = h[j];
+                        bool present = false;
+                        for (;;) {
+                            bool taken = ey.x == W.tag;
+                            if (!taken)  // free when loaded: an insert of this group may have taken it
+                                for (uint32_t q = 0; q < nins; ++q) taken |= ins[q] == sy;
+                            if (!taken) break;
+                            if (ey.x == W.tag && (ey.y & ~kTgtBit) == y) {
+                                present = true;
+                                break;
+                            }
+                            sy = (sy + 1u) & W.hmask;
+                            ey = W.hash[sy];
+                        }
+                        const uint64_t nd = d + e[j].y;
+                        const uint64_t cur = present ? (((uint64_t)ey.w << 32) | ey.z) : kInf;
+                        if (nd < cur) {
+                            if (present) {
+                                W.set_at(sy, y, nd);
+                            } else {
+                                W.set_at(W.hmask + 1u + sy, y, nd);
+                                ins[nins++] = sy;
+                            }
+                            W.push(nd, y);
+                            if (W.ovf) break;
+                        }
                     }
                 }
             }

@@ -359,8 +359,11 @@ int main(int argc, char** argv) {
             return 1;
         }
         cpd_graph* dg = nullptr;
+        const double t_g0 = now();
         cli::check(cpd_graph_create(plan, device, &dg), "graph upload");
+        const double t_graph = now() - t_g0;
         cli::check(cpd_graph_set_batch(dg, (uint32_t)a.num("batch", 0)), "batch");
+        const double t_batch = now() - t_g0 - t_graph;
         // the .xy coordinates order each batch's lanes (compact target groups)
         if (g.x.size() == g.n && g.y.size() == g.n)
             cli::check(cpd_graph_set_coords(dg, g.x.data(), g.y.data()), "coordinates");
@@ -377,6 +380,7 @@ int main(int argc, char** argv) {
         if (discard && a.has("no-pipeline"))
             throw std::runtime_error("--discard needs the pipelined writer");
         const double t_rows0 = now();
+        const double t_setup = t_rows0 - t_g0;
         cpd_rows* rows = nullptr;
         if (a.has("no-pipeline")) {
             size_t i = 0;
@@ -452,9 +456,11 @@ int main(int argc, char** argv) {
             x_span = pl.x_last > pl.x_first ? pl.x_last - pl.x_first : 0.0;
         }
         const double t_rows = now() - t_rows0;
+        const double t_f0 = now();
         if (rows) cpd_rows_free(rows);
         cpd_graph_free(dg);
         cpd_plan_free(plan);
+        const double t_free = now() - t_f0;
         double rate = t_build > 0 ? rows_done / t_build : 0.0;
         std::printf(
             "make_cpd_auto: worker %lld/%lld device %d: %llu rows in %zu buckets, %llu runs "
@@ -472,12 +478,13 @@ int main(int argc, char** argv) {
         std::printf(
             "make_cpd_auto-json: {\"worker\": %lld, \"maxworker\": %lld, \"rows\": %llu, "
             "\"runs\": %llu, \"batch\": %u, \"discard\": %s, \"read_s\": %.3f, \"plan_s\": %.3f, "
-            "\"plan_cached\": %s, \"rows_s\": %.3f, \"build_calls_s\": %.3f, \"wait_s\": %.3f, "
+            "\"plan_cached\": %s, \"graph_s\": %.3f, \"batch_alloc_s\": %.3f, \"setup_s\": %.3f, "
+            "\"rows_s\": %.3f, \"build_calls_s\": %.3f, \"wait_s\": %.3f, \"free_s\": %.3f, "
             "\"export_bytes\": %llu, \"export_thread_s\": %.3f, \"export_span_s\": %.3f, "
             "\"total_s\": %.3f}\n",
             wid, W, (unsigned long long)rows_done, (unsigned long long)runs_done, B,
-            discard ? "true" : "false", t_read, t_plan, plan_loaded ? "true" : "false", t_rows,
-            t_build, t_io, (unsigned long long)x_bytes, x_sum, x_span, now() - t_start);
+            discard ? "true" : "false", t_read, t_plan, plan_loaded ? "true" : "false", t_graph,
+            t_batch, t_setup, t_rows, t_build, t_io, t_free, (unsigned long long)x_bytes, x_sum, x_span, now() - t_start);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "make_cpd_auto: %s\n", e.what());
         return 1;
