@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <numeric>
 
 #ifdef _OPENMP
@@ -312,6 +313,7 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
             if (!C.out[v].empty())
                 for (size_t i = 0; i < C.in[v].size(); ++i) pairs.push_back({v, (uint32_t)i});
         sc_local.assign(pairs.size(), {});
+        std::exception_ptr err;  // an exception must not leave the parallel region
 #pragma omp parallel for schedule(dynamic, 8) num_threads(threads)
         for (int64_t i = 0; i < (int64_t)pairs.size(); ++i) {
 #ifdef _OPENMP
@@ -319,9 +321,15 @@ Hierarchy build_hierarchy(uint32_t n, const uint32_t* row_ptr, const uint32_t* d
 #else
             Witness& ws = C.scratch[0];
 #endif
-            C.shortcuts_via(pairs[i].first, pairs[i].second, C.sel.data(), C.settle_contract,
-                            &sc_local[i], ws);
+            try {
+                C.shortcuts_via(pairs[i].first, pairs[i].second, C.sel.data(), C.settle_contract,
+                                &sc_local[i], ws);
+            } catch (...) {
+#pragma omp critical(ch_err)
+                if (!err) err = std::current_exception();
+            }
         }
+        if (err) std::rethrow_exception(err);
 
         phase(1);
         // 3. record hierarchy arcs, ranks

@@ -254,12 +254,14 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
     // straight to the wave kernel when a round has few (the core rounds:
     // large searches); what outgrows a workspace moves on: lane -> wave ->
     // the large HBM workspace, which cannot overflow.
-    uint32_t wave_max = 8192, wave_blocks = 4096;
+    uint32_t wave_max = 16384, wave_blocks = 8192;
     if (const char* e = std::getenv("CPD_CH_WAVE")) wave_max = (uint32_t)std::strtoul(e, nullptr, 10);
     // test knob: no wave stage (lane -> large workspace only)
     const bool no_wave = std::getenv("CPD_CH_NOWAVE") != nullptr;
     if (no_wave) wave_max = 0;
-    uint32_t lane_cap = 2048;  // pops + relaxations a lane search may take
+    // pops + relaxations a lane search may take before a wave takes it over
+    // (A/B at 1M nodes: 512 -> 2.6 s, 2048 -> 2.4 s, none -> 2.1 s: default none)
+    uint32_t lane_cap = 0xFFFFFFFFu;
     if (const char* e = std::getenv("CPD_CH_LANE_CAP")) lane_cap = (uint32_t)std::strtoul(e, nullptr, 10);
     uint64_t wave_searches = 0;
     double t_lane = 0, t_wave = 0, t_big = 0;  // witness kernel wall times (verbose)
@@ -283,16 +285,19 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             t_lane += now_seconds() - tw;
             tw = now_seconds();
         }
-        if (cnt && !no_wave) {
-            ovf2.ensure(cnt);
+        // waves: the small LDS workspace (five workgroups per CU), then the
+        // large one (two per CU) for what outgrows it
+        for (int pass = 0; pass < 2 && cnt && !no_wave; ++pass) {
+            DBuf<uint32_t>& out = pass == 0 ? ovf2 : ovf3;
+            out.ensure(cnt);
             CH_HIP(hipMemsetAsync(ctr.p + 4, 0, 4, st));
             chk::launch_witness_wave(pairs.p, list, cnt, overlay(), state.p, contract, settle,
-                                     wave_blocks, slots.p, sflag.p, sc.p, ovf2.p, ctr.p + 4,
-                                     ctr.p + 1, st);
+                                     wave_blocks, pass == 0, slots.p, sflag.p, sc.p, out.p,
+                                     ctr.p + 4, ctr.p + 1, st);
             wave_searches += cnt;
             read({ctr.p + 4});
             cnt = hv.p[0];
-            list = ovf2.p;
+            list = out.p;
             t_wave += now_seconds() - tw;
             tw = now_seconds();
         }
@@ -319,10 +324,11 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             CH_HIP(hipMemsetAsync(ws2.p, 0, ws2.n, st));
             tag2 = 0;
         }
-        ovf3.ensure(novf);
+        DBuf<uint32_t>& lost = list == ovf.p ? ovf2 : ovf;  // not the list being read
+        lost.ensure(novf);
         CH_HIP(hipMemsetAsync(ctr.p + 3, 0, 4, st));
         chk::launch_witness(pairs.p, list, novf, overlay(), state.p, contract, settle, ws2.p,
-                            caps2, lanes2, tag2, 0xFFFFFFFFu, slots.p, sflag.p, sc.p, ovf3.p,
+                            caps2, lanes2, tag2, 0xFFFFFFFFu, slots.p, sflag.p, sc.p, lost.p,
                             ctr.p + 3, ctr.p + 1, st);
         tag2 += novf + 1;
         read({ctr.p + 3, ctr.p + 1});
@@ -331,12 +337,15 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
         t_big += now_seconds() - tw;
     };
     // priorities of list[0..k) (ch.cpp Contractor::priority / step 6)
+    uint32_t last_sim = 0;  // simulation searches of the last priorities() (verbose)
     auto priorities = [&](const uint32_t* list, uint32_t k) {
+        last_sim = 0;
         if (!k) return;
         chk::launch_sim_counts(list, k, overlay(), c[0].p, sc.p, st);
         scan(c[0].p, s[0].p, k + 1);
         read({s[0].p + k});
         const uint32_t np = hv.p[0];
+        last_sim = np;
         pairs.ensure(4ull * std::max(np, 1u));
         chk::launch_make_pairs(list, k, overlay(), s[0].p, nullptr, pairs.p, st);
         witness(np, false, settle_s);
@@ -357,6 +366,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
         tph[k] += tb - ta;
         ta = tb;
     };
+    double t_round = now_seconds();
     while (R) {
         // 1. independent set of local priority minima
         chk::launch_pick(rem.p, R, overlay(), prio.p, flag.p, st);
@@ -448,11 +458,13 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
         R = nR;
         rank0 += nS;
         ++round;
-        if (verbose && (round % 10 == 0 || R == 0))
+        if (verbose > 1 || (verbose && (round % 10 == 0 || R == 0)))
             std::fprintf(stderr,
                          "[ch-gpu] round %u contracted %u remaining %u shortcuts %u affected %u "
-                         "(%.2fs)\n",
-                         round, nS, R, K, nA, now_seconds() - t0);
+                         "searches %u + %u, %.2f ms (%.2fs)\n",
+                         round, nS, R, K, nA, np, last_sim, (now_seconds() - t_round) * 1e3,
+                         now_seconds() - t0);
+        t_round = now_seconds();
     }
 
     // Download the records and assemble the CSRs as ch.cpp does.

@@ -190,10 +190,38 @@ struct Lane {
             const uint4 value = heap[len];
             heap[len] = heap[0];
             int64_t hole = 0, second = 0;
-            while (second < (len - 1) / 2) {
-                second = 2 * (second + 1);
-                if (hd(heap[second]) > hd(heap[second - 1])) --second;
-                heap[hole] = heap[second];
+            const int64_t lim = (len - 1) / 2;
+            // libstdc++'s descent, two levels per round trip: a step loads
+            // the two children of the hole and their four children together
+            // (the lane's heap is private: nothing else writes it meanwhile)
+            while (second < lim) {
+                const int64_t c = 2 * (second + 1);
+                const uint4 a0 = heap[c - 1], a1 = heap[c];
+                uint4 gc[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int64_t gi = 2 * c - 1 + q;
+                    gc[q] = gi < len ? heap[gi] : make_uint4(0u, 0u, 0u, 0u);
+                }
+                second = c;
+                uint4 up = a1;
+                if (hd(a1) > hd(a0)) {
+                    --second;
+                    up = a0;
+                }
+                heap[hole] = up;
+                hole = second;
+                if (!(second < lim)) break;
+                const int64_t c2 = 2 * (second + 1);
+                const bool left = second == c - 1;
+                const uint4 b0 = left ? gc[0] : gc[2], b1 = left ? gc[1] : gc[3];
+                second = c2;
+                up = b1;
+                if (hd(b1) > hd(b0)) {
+                    --second;
+                    up = b0;
+                }
+                heap[hole] = up;
                 hole = second;
             }
             if ((len & 1) == 0 && second == (len - 2) / 2) {
@@ -391,9 +419,9 @@ __global__ __launch_bounds__(256) void k_witness(
 // 64-bit compare-and-swap of (tag, node) claims free slots), and the
 // improving arcs are then pushed in arc order — the host's push order, so
 // the heap, and every tie it breaks, stays the host's.
-constexpr uint32_t kWH = 2048;  // hash slots
-constexpr uint32_t kWP = 1792;  // heap slots
-constexpr uint32_t kWT = 128;   // targets
+// LDS of one wave's search: kWH hash slots, kWP heap slots, kWT targets
+// (two sizes: 27 KB, five workgroups per CU, then 55 KB for what outgrows it)
+template <uint32_t kWH, uint32_t kWP, uint32_t kWT>
 struct WaveLds {
     unsigned long long key[kWH];  // (node | target bit) << 32 | tag
     unsigned long long hdist[kWH];
@@ -405,11 +433,14 @@ struct WaveLds {
     uint32_t hn, ovf;
 };
 
+template <uint32_t kWH>
 __device__ __forceinline__ uint32_t wslot0(uint32_t node) { return (node * 0x9E3779B1u) & (kWH - 1u); }
 
 // probe for node (tag): slot index, found flag
-__device__ __forceinline__ uint32_t wfind(const WaveLds& S, uint32_t node, uint32_t tag, bool& found) {
-    uint32_t s = wslot0(node);
+template <uint32_t kWH, uint32_t kWP, uint32_t kWT>
+__device__ __forceinline__ uint32_t wfind(const WaveLds<kWH, kWP, kWT>& S, uint32_t node, uint32_t tag,
+                                          bool& found) {
+    uint32_t s = wslot0<kWH>(node);
     for (;;) {
         const unsigned long long k = S.key[s];
         if ((uint32_t)k != tag) {
@@ -426,7 +457,9 @@ __device__ __forceinline__ uint32_t wfind(const WaveLds& S, uint32_t node, uint3
 
 // insert an absent node (parallel-safe for distinct nodes): the slot, or
 // kWH when the table is full
-__device__ __forceinline__ uint32_t winsert(WaveLds& S, uint32_t nodebits, uint32_t tag, uint32_t s) {
+template <uint32_t kWH, uint32_t kWP, uint32_t kWT>
+__device__ __forceinline__ uint32_t winsert(WaveLds<kWH, kWP, kWT>& S, uint32_t nodebits, uint32_t tag,
+                                            uint32_t s) {
     const unsigned long long mine = ((unsigned long long)nodebits << 32) | tag;
     for (uint32_t probes = 0; probes < kWH; ++probes) {
         const unsigned long long k = S.key[s];
@@ -443,7 +476,9 @@ __device__ __forceinline__ uint32_t winsert(WaveLds& S, uint32_t nodebits, uint3
     return kWH;
 }
 
-__device__ __forceinline__ void wsift_up(WaveLds& S, int64_t hole, unsigned long long vd, uint32_t vn) {
+template <uint32_t kWH, uint32_t kWP, uint32_t kWT>
+__device__ __forceinline__ void wsift_up(WaveLds<kWH, kWP, kWT>& S, int64_t hole, unsigned long long vd,
+                                         uint32_t vn) {
     int64_t parent = (hole - 1) / 2;
     while (hole > 0) {
         const unsigned long long p = S.pd[parent];
@@ -457,13 +492,15 @@ __device__ __forceinline__ void wsift_up(WaveLds& S, int64_t hole, unsigned long
     S.pn[hole] = vn;
 }
 
+template <uint32_t kWH, uint32_t kWP, uint32_t kWT>
 __global__ __launch_bounds__(64) void k_witness_wave(
     const uint4* __restrict__ pairs, const uint32_t* __restrict__ plist, uint32_t np, Overlay g,
     const uint8_t* __restrict__ state, uint32_t contract, uint32_t settle, uint4* __restrict__ slots,
     uint32_t* __restrict__ sflag, uint32_t* __restrict__ sc, uint32_t* __restrict__ ovf,
     uint32_t* __restrict__ ovf_n, uint32_t* __restrict__ err) {
     extern __shared__ unsigned long long lds_raw[];
-    WaveLds& S = *reinterpret_cast<WaveLds*>(lds_raw);
+    using WL = WaveLds<kWH, kWP, kWT>;
+    WL& S = *reinterpret_cast<WL*>(lds_raw);
     const uint32_t lane = threadIdx.x;
     for (uint32_t i = lane; i < kWH; i += 64u) S.key[i] = 0ull;  // tag 0: empty
     const uint2* arcs = reinterpret_cast<const uint2*>(g.arcs);
@@ -940,24 +977,34 @@ void launch_witness(const uint32_t* pairs, const uint32_t* plist, uint32_t np, O
                        reinterpret_cast<uint4*>(slots), sflag, sc, ovf, ovf_n, err);
 }
 
-void launch_witness_wave(const uint32_t* pairs, const uint32_t* plist, uint32_t np, Overlay g,
-                         const uint8_t* state, bool contract, uint32_t settle, uint32_t blocks,
-                         uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf,
-                         uint32_t* ovf_n, uint32_t* err, hipStream_t s) {
-    if (!np) return;
-    static bool attr = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(k_witness_wave),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)sizeof(WaveLds)) == hipSuccess;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL(k_witness_wave, dim3(std::min(np, blocks)), dim3(64), sizeof(WaveLds), s,
+template <uint32_t H, uint32_t P, uint32_t T>
+void launch_ww(const uint32_t* pairs, const uint32_t* plist, uint32_t np, Overlay g,
+               const uint8_t* state, bool contract, uint32_t settle, uint32_t blocks,
+               uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf, uint32_t* ovf_n,
+               uint32_t* err, hipStream_t s) {
+    auto k = k_witness_wave<H, P, T>;
+    hipLaunchKernelGGL(k, dim3(std::min(np, blocks)), dim3(64), sizeof(WaveLds<H, P, T>), s,
                        reinterpret_cast<const uint4*>(pairs), plist, np, g, state,
                        contract ? 1u : 0u, settle, reinterpret_cast<uint4*>(slots), sflag, sc, ovf,
                        ovf_n, err);
 }
 
-uint32_t witness_wave_lds_bytes() { return (uint32_t)sizeof(WaveLds); }
+void launch_witness_wave(const uint32_t* pairs, const uint32_t* plist, uint32_t np, Overlay g,
+                         const uint8_t* state, bool contract, uint32_t settle, uint32_t blocks,
+                         bool small, uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf,
+                         uint32_t* ovf_n, uint32_t* err, hipStream_t s) {
+    if (!np) return;
+    if (small)
+        launch_ww<1024, 768, 64>(pairs, plist, np, g, state, contract, settle, blocks, slots,
+                                 sflag, sc, ovf, ovf_n, err, s);
+    else
+        launch_ww<2048, 1792, 128>(pairs, plist, np, g, state, contract, settle, blocks, slots,
+                                   sflag, sc, ovf, ovf_n, err, s);
+}
+
+uint32_t witness_wave_lds_bytes(bool small) {
+    return small ? (uint32_t)sizeof(WaveLds<1024, 768, 64>) : (uint32_t)sizeof(WaveLds<2048, 1792, 128>);
+}
 
 void launch_record(const uint32_t* S, uint32_t nS, uint32_t rank0, Overlay g, const uint32_t* upos,
                    const uint32_t* dpos, uint64_t ubase, uint64_t dbase, uint32_t* rank,

@@ -107,18 +107,28 @@ int cpd_plan_create(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t
                 if (t.joinable()) t.join();
             }
         } join{side};
+        std::exception_ptr ch_err;
         if (!(opts && opts->no_hierarchy)) {
             double t0 = now_seconds();
-            p->ch = opts && opts->ch_gpu
-                        ? build_hierarchy_gpu(n, row_ptr, dst, w, opts->ch_device, settle, verbose)
-                        : build_hierarchy(n, row_ptr, dst, w, threads, settle, verbose);
+            try {
+                p->ch = opts && opts->ch_gpu
+                            ? build_hierarchy_gpu(n, row_ptr, dst, w, opts->ch_device, settle,
+                                                  verbose)
+                            : build_hierarchy(n, row_ptr, dst, w, threads, settle, verbose);
+            } catch (...) {
+                ch_err = std::current_exception();
+            }
             p->ch_seconds = now_seconds() - t0;
         }
         side.join();
+        // the graph's own errors first (as when they were checked before the
+        // hierarchy): a distance range the u32 path cannot hold also makes
+        // the contraction fail on a shortcut weight
         if (side_err) std::rethrow_exception(side_err);
         CPD_REQUIRE(p->dist_bound < 0xFFFFFFFFull, CPD_E_RANGE,
                     "graph distances may reach 2^32-1; the u32 distance path "
                     "cannot represent them");
+        if (ch_err) std::rethrow_exception(ch_err);
         *out = p.release();
     });
 }

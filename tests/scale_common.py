@@ -11,9 +11,10 @@ CACHE = os.environ.get("CPD_TEST_CACHE", "/tmp/cpd-test-cache")
 
 def plan_for(g, tag):
     """The graph's plan, built once and cached on local disk for the session
-    (and later sessions on the same box)."""
+    (and later sessions on the same box); its hierarchy contracted on GPU 0
+    (ch_gpu.cpp: the host build's hierarchy, arc for arc — tests/test_ch_gpu.py)."""
     os.makedirs(CACHE, exist_ok=True)
-    plan, _ = cpd.Plan.cache(os.path.join(CACHE, f"{tag}.plan"), g)
+    plan, _ = cpd.Plan.cache(os.path.join(CACHE, f"{tag}.plan"), g, gpu=0)
     return plan
 
 

@@ -14,7 +14,7 @@ W = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1000
 g = cpd.synth_road_graph(W, W, seed=1)
 for rep in range(2):
     t = time.time()
-    p = cpd.Plan(g, gpu=0, verbose=True)
+    p = cpd.Plan(g, gpu=0, verbose=2 if rep == 0 else 1)  # 2: every round
     print(f"GPU plan {time.time() - t:.2f} s, CH {p.info()['ch_seconds']:.2f} s", flush=True)
 if "--host" in sys.argv:
     t = time.time()
