@@ -254,7 +254,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
     // straight to the wave kernel when a round has few (the core rounds:
     // large searches); what outgrows a workspace moves on: lane -> wave ->
     // the large HBM workspace, which cannot overflow.
-    uint32_t wave_max = 16384, wave_blocks = 8192;
+    uint32_t wave_max = 65536, wave_blocks = 8192;
     if (const char* e = std::getenv("CPD_CH_WAVE")) wave_max = (uint32_t)std::strtoul(e, nullptr, 10);
     // test knob: no wave stage (lane -> large workspace only)
     const bool no_wave = std::getenv("CPD_CH_NOWAVE") != nullptr;
@@ -285,7 +285,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             t_lane += now_seconds() - tw;
             tw = now_seconds();
         }
-        // waves: the small LDS workspace (five workgroups per CU), then the
+        // waves: the small LDS workspace (four workgroups per CU), then the
         // large one (two per CU) for what outgrows it
         for (int pass = 0; pass < 2 && cnt && !no_wave; ++pass) {
             DBuf<uint32_t>& out = pass == 0 ? ovf2 : ovf3;

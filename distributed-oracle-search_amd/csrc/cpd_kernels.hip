@@ -1479,20 +1479,25 @@ __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
 // bits 4*(c&7) of word c>>3; column c's move = the move of the last run that
 // starts at or before c — copied, never recomputed).
 //
-// Work is cut by RUNS: chunks of kExpandRuns consecutive runs of one row
-// (chunk_first[row] = the row's first chunk, a prefix over rows of
-// ceil(R / kExpandRuns)); a wave takes kExpandCpw consecutive chunks and
-// stages each (plus the next 8 runs) in LDS, coalesced.  Each output word is
-// written by the run that holds its first column, one lane per run: the
-// words wholly inside a run are its move repeated (a run's interior of more
-// than 64 words is written by the whole wave, coalesced), the word where the
-// run ends takes its other columns from the <= 7 runs that follow.  Round 3's
-// first form (lane per output word, a 9-step binary search over the staged
-// runs per word, one chunk per wave: 6.5M workgroups at 1M nodes) ran at 0.2
-// of HBM peak; round 2's (wave per 2048-column tile, two ~20-step binary
-// searches over the whole row) at 0.12.
+// Work is cut by RUNS, not columns: chunks of kExpandRuns consecutive runs of
+// one row (chunk_first[row] = the row's first chunk, a prefix over rows of
+// ceil(R / kExpandRuns)); a wave takes cpw consecutive chunks (CPD_EXP_CPW,
+// default kExpandCpw), loads each plus the next 8 runs (coalesced, into LDS)
+// and writes the output words whose first column lies in the chunk:
+// [ceil(start(r0) / 8), ceil(start(r1) / 8)) — the first chunk of a row from
+// word 0, the last to the end of the row — a lane per word (the last staged
+// run at or before its first column by binary search, then its 8 columns).
+// A word's 8 columns are covered by at most 8 runs past r1, so the lookahead
+// completes every owned word and each word has exactly one writer.  Round 2's
+// form (wave per 2048-column tile, two ~20-step binary searches over the row's
+// runs per wave) read 1.6x its algorithmic bytes at 0.12 of HBM peak; one
+// chunk per wave (round 3's first form) ran 6.5M workgroups at 1M nodes (42.9 ms
+// per 21504 rows; 4 chunks: 35.2; 16: 32.8).
+// (A lane per RUN instead — each word written by the run holding its first
+// column, interiors as a segmented fill — measured 100 ms against 39 for
+// 21504 rows: five times as many lanes' worth of work as words.)
 constexpr uint32_t kExpandRuns = 512;
-constexpr uint32_t kExpandCpw = 4;
+constexpr uint32_t kExpandCpw = 16;
 
 __global__ __launch_bounds__(256) void expand_rows(const uint64_t* __restrict__ offsets,
                                                    const uint32_t* __restrict__ runs,
@@ -1502,14 +1507,11 @@ __global__ __launch_bounds__(256) void expand_rows(const uint64_t* __restrict__ 
                                                    uint32_t* __restrict__ dense) {
     constexpr uint32_t kLook = 8;
     __shared__ uint32_t cr_all[4][kExpandRuns + kLook];
-    __shared__ uint32_t seg_all[4][2][64];  // per run of the group: first interior word, prefix
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t c_begin = (blockIdx.x * 4u + wv) * cpw;
     if (c_begin >= total_chunks) return;  // wave-uniform; no block barrier below
     const uint32_t c_end = min(total_chunks, c_begin + cpw);
     uint32_t* cr = cr_all[wv];
-    uint32_t* sfa = seg_all[wv][0];
-    uint32_t* spre = seg_all[wv][1];
     // the first chunk's row: the last row whose first chunk is <= it (uniform)
     uint32_t lo = 0, hi = nrows;
     while (lo + 1 < hi) {
@@ -1531,55 +1533,26 @@ __global__ __launch_bounds__(256) void expand_rows(const uint64_t* __restrict__ 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t w0 = r0 == 0 ? 0u : ((cr[0] >> 4) + 7u) >> 3;
+        const uint32_t w1 = r1 == R ? words_per_row : ((cr[r1 - r0] >> 4) + 7u) >> 3;
         uint32_t* __restrict__ out = dense + (size_t)row * words_per_row;
-        const uint32_t end_col = words_per_row * 8u;  // the row's last run runs to here
-        for (uint32_t j0 = 0; j0 < r1 - r0; j0 += 64u) {
-            const uint32_t j = j0 + lane;
-            uint32_t fa = 0, nf = 0;  // this run's interior words [fa, fa + nf)
-            if (j < r1 - r0) {
-                const uint32_t s0 = cr[j] >> 4;
-                const uint32_t e0 = r0 + j + 1 < R ? cr[j + 1] >> 4 : end_col;
-                const uint32_t wa = (s0 + 7u) >> 3, wb = (e0 + 7u) >> 3;  // words owned
-                if (wa < wb) {
-                    // the last owned word: columns past e0 belong to the next runs
-                    const uint32_t wl = wb - 1u, c0 = wl * 8u;
-                    uint32_t word = 0, a = j;
+        uint32_t a0 = 0;  // this lane's previous word's run: its next word starts there or later
+        for (uint32_t w = w0 + lane; w < w1; w += 64u) {
+            const uint32_t c0 = w * 8u;
+            uint32_t a = a0, b = nl;  // last staged run with start <= c0
+            while (a + 1 < b) {
+                const uint32_t mid = (a + b) >> 1;
+                if ((cr[mid] >> 4) > c0) b = mid;
+                else a = mid;
+            }
+            a0 = a;
+            uint32_t word = 0;
 #pragma unroll
-                    for (uint32_t k = 0; k < 8u; ++k) {
-                        while (a + 1 < nl && (cr[a + 1] >> 4) <= c0 + k) ++a;
-                        word |= (cr[a] & 0xFu) << (4u * k);
-                    }
-                    out[wl] = word;
-                    fa = wa;
-                    nf = wl - wa;
-                }
+            for (uint32_t k = 0; k < 8u; ++k) {
+                while (a + 1 < nl && (cr[a + 1] >> 4) <= c0 + k) ++a;
+                word |= (cr[a] & 0xFu) << (4u * k);
             }
-            // interior words (the run's move repeated) of the group's 64 runs:
-            // consecutive in the row, so dealt out over the lanes as one
-            // segmented fill — coalesced stores whatever the run lengths
-            uint32_t pre = nf;  // inclusive prefix over the lanes
-#pragma unroll
-            for (uint32_t d = 1; d < 64u; d <<= 1) {
-                const uint32_t y = __shfl_up(pre, d, 64);
-                if (lane >= d) pre += y;
-            }
-            const uint32_t total = __shfl(pre, 63, 64);
-            if (!total) continue;
-            __builtin_amdgcn_wave_barrier();
-            sfa[lane] = fa;
-            spre[lane] = pre - nf;  // exclusive
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            for (uint32_t idx = lane; idx < total; idx += 64u) {
-                uint32_t a = 0, b = 64;  // last lane whose exclusive prefix <= idx
-                while (a + 1 < b) {
-                    const uint32_t mid = (a + b) >> 1;
-                    if (spre[mid] <= idx) a = mid;
-                    else b = mid;
-                }
-                out[sfa[a] + (idx - spre[a])] = (cr[j0 + a] & 0xFu) * 0x11111111u;
-            }
+            out[w] = word;
         }
     }
 }
