@@ -285,7 +285,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             t_lane += now_seconds() - tw;
             tw = now_seconds();
         }
-        // waves: the small LDS workspace (four workgroups per CU), then the
+        // waves: the small LDS workspace (five workgroups per CU), then the
         // large one (two per CU) for what outgrows it
         for (int pass = 0; pass < 2 && cnt && !no_wave; ++pass) {
             DBuf<uint32_t>& out = pass == 0 ? ovf2 : ovf3;

@@ -420,14 +420,13 @@ __global__ __launch_bounds__(256) void k_witness(
 // improving arcs are then pushed in arc order — the host's push order, so
 // the heap, and every tie it breaks, stays the host's.
 // LDS of one wave's search: kWH hash slots, kWP heap slots, kWT targets
-// (two sizes: 33 KB, four workgroups per CU, then 63 KB for what outgrows it)
+// (two sizes: 27 KB, five workgroups per CU, then 55 KB for what outgrows it)
 template <uint32_t kWH, uint32_t kWP, uint32_t kWT>
 struct WaveLds {
     unsigned long long key[kWH];  // (node | target bit) << 32 | tag
     unsigned long long hdist[kWH];
     unsigned long long pd[kWP];  // heap: dist
     uint32_t pn[kWP];            //       node
-    unsigned long long pa[kWP];  //       its list: (out-degree << 32) | first arc
     unsigned long long tv[kWT];  // targets: via (descending), node, settled
     uint32_t tn[kWT];
     uint32_t ts[kWT];
@@ -479,20 +478,18 @@ __device__ __forceinline__ uint32_t winsert(WaveLds<kWH, kWP, kWT>& S, uint32_t 
 
 template <uint32_t kWH, uint32_t kWP, uint32_t kWT>
 __device__ __forceinline__ void wsift_up(WaveLds<kWH, kWP, kWT>& S, int64_t hole, unsigned long long vd,
-                                         uint32_t vn, unsigned long long va) {
+                                         uint32_t vn) {
     int64_t parent = (hole - 1) / 2;
     while (hole > 0) {
         const unsigned long long p = S.pd[parent];
         if (!(p > vd)) break;
         S.pd[hole] = p;
         S.pn[hole] = S.pn[parent];
-        S.pa[hole] = S.pa[parent];
         hole = parent;
         parent = (hole - 1) / 2;
     }
     S.pd[hole] = vd;
     S.pn[hole] = vn;
-    S.pa[hole] = va;
 }
 
 template <uint32_t kWH, uint32_t kWP, uint32_t kWT>
@@ -583,7 +580,6 @@ __global__ __launch_bounds__(64) void k_witness_wave(
             if (!bad) {
                 S.pd[0] = 0ull;  // every lane writes the same words
                 S.pn[0] = a.x;
-                S.pa[0] = ((unsigned long long)g.odeg[a.x] << 32) | g.ooff[a.x];
                 L = 1;
             }
             uint32_t settled = 0, open = 0;
@@ -593,46 +589,38 @@ __global__ __launch_bounds__(64) void k_witness_wave(
                     const int64_t len = (int64_t)L - 1;
                     const unsigned long long vd = S.pd[len];
                     const uint32_t vn = S.pn[len];
-                    const unsigned long long va = S.pa[len];
                     const unsigned long long td = S.pd[0];
                     const uint32_t tn0 = S.pn[0];
-                    const unsigned long long ta = S.pa[0];
                     __syncthreads();
                     S.pd[len] = td;
                     S.pn[len] = tn0;
-                    S.pa[len] = ta;
                     int64_t hole = 0, second = 0;
                     while (second < (len - 1) / 2) {
                         second = 2 * (second + 1);
                         if (S.pd[second] > S.pd[second - 1]) --second;
                         const unsigned long long cd = S.pd[second];
                         const uint32_t cn = S.pn[second];
-                        const unsigned long long ca = S.pa[second];
                         __syncthreads();
                         S.pd[hole] = cd;
                         S.pn[hole] = cn;
-                        S.pa[hole] = ca;
                         hole = second;
                     }
                     if ((len & 1) == 0 && second == (len - 2) / 2) {
                         second = 2 * (second + 1);
                         const unsigned long long cd = S.pd[second - 1];
                         const uint32_t cn = S.pn[second - 1];
-                        const unsigned long long ca = S.pa[second - 1];
                         __syncthreads();
                         S.pd[hole] = cd;
                         S.pn[hole] = cn;
-                        S.pa[hole] = ca;
                         hole = second - 1;
                     }
                     __syncthreads();
-                    wsift_up(S, hole, vd, vn, va);
+                    wsift_up(S, hole, vd, vn);
                 }
                 __syncthreads();
                 --L;
                 const unsigned long long d = S.pd[L];
                 const uint32_t x = S.pn[L];
-                const unsigned long long xa = S.pa[L];
                 bool fx;
                 const uint32_t sx = wfind(S, x, tag, fx);
                 const unsigned long long kx = S.key[sx];
@@ -651,18 +639,15 @@ __global__ __launch_bounds__(64) void k_witness_wave(
                             break;
                         }
                 }
-                // the settled node's list came with its heap entry: no load
-                const uint32_t ox = (uint32_t)xa, dx = (uint32_t)(xa >> 32);
+                const uint32_t ox = g.ooff[x], dx = g.odeg[x];
                 for (uint32_t k0 = 0; k0 < dx && !bad; k0 += 64u) {
                     const uint32_t k = k0 + lane;
                     bool imp = false;
-                    unsigned long long nd = 0, ya = 0;
+                    unsigned long long nd = 0;
                     uint32_t y = 0;
                     if (k < dx) {
                         const uint2 e = arcs[ox + k];
                         y = e.x;
-                        // the neighbour's list, loaded beside its other lookups
-                        ya = ((unsigned long long)g.odeg[y] << 32) | g.ooff[y];
                         if (!(e.x == v || (contract && state[e.x] == 1))) {
                             nd = d + e.y;
                             bool f;
@@ -687,9 +672,8 @@ __global__ __launch_bounds__(64) void k_witness_wave(
                         m &= m - 1ull;
                         const unsigned long long jd = __shfl(nd, j, 64);
                         const uint32_t jn = __shfl(y, j, 64);
-                        const unsigned long long ja = __shfl(ya, j, 64);
                         ++L;
-                        wsift_up(S, (int64_t)L - 1, jd, jn, ja);
+                        wsift_up(S, (int64_t)L - 1, jd, jn);
                         __syncthreads();
                     }
                 }
@@ -1014,12 +998,12 @@ void launch_witness_wave(const uint32_t* pairs, const uint32_t* plist, uint32_t 
         launch_ww<1024, 768, 64>(pairs, plist, np, g, state, contract, settle, blocks, slots,
                                  sflag, sc, ovf, ovf_n, err, s);
     else
-        launch_ww<2048, 1400, 128>(pairs, plist, np, g, state, contract, settle, blocks, slots,
+        launch_ww<2048, 1792, 128>(pairs, plist, np, g, state, contract, settle, blocks, slots,
                                    sflag, sc, ovf, ovf_n, err, s);
 }
 
 uint32_t witness_wave_lds_bytes(bool small) {
-    return small ? (uint32_t)sizeof(WaveLds<1024, 768, 64>) : (uint32_t)sizeof(WaveLds<2048, 1400, 128>);
+    return small ? (uint32_t)sizeof(WaveLds<1024, 768, 64>) : (uint32_t)sizeof(WaveLds<2048, 1792, 128>);
 }
 
 void launch_record(const uint32_t* S, uint32_t nS, uint32_t rank0, Overlay g, const uint32_t* upos,

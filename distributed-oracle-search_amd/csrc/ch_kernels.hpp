@@ -62,7 +62,7 @@ void launch_witness(const uint32_t* pairs, const uint32_t* plist, uint32_t np, O
                     uint32_t* ovf_n, uint32_t* err, hipStream_t s);
 // The same searches, one wave each with the search's table and heap in LDS
 // (witness_wave_lds_bytes(small) per workgroup; small: 1024 table / 768 heap
-// slots / 64 targets, else 2048 / 1400 / 128): for the core rounds' large
+// slots / 64 targets, else 2048 / 1792 / 128): for the core rounds' large
 // searches.  A search that outgrows LDS goes to ovf as above.
 void launch_witness_wave(const uint32_t* pairs, const uint32_t* plist, uint32_t np, Overlay g,
                          const uint8_t* state, bool contract, uint32_t settle, uint32_t blocks,
