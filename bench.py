@@ -260,19 +260,25 @@ def batch_of(owned, B, i):
 def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows, nruns,
              kt, cpu, parity, pinfo, traffic=None):
     """Rank 0's JSON line.  value = rows built by ALL ranks / max rank time.
-    roofline: the kernel with the most device time; achieved = its algorithmic
-    bytes (SURVEY.md §8d model, counted per launch by libcpd) / its summed
-    event time; traffic = PMC bytes per launch of the same kernel (or None)."""
+    roofline: the dominant kernel = the one moving the most algorithmic bytes
+    (SURVEY.md §8d model, counted per launch by libcpd); achieved = those
+    bytes / its summed event time; traffic = PMC bytes per launch of the same
+    kernel (or None).  Not the kernel with the most device time: the next
+    batch's up-sweep runs on its own stream beside this batch's first moves,
+    and its ~190 small latency-bound launches wait there behind the first
+    moves' workgroups (summed, ~31 ms of events per step for ~10 GB), so
+    event time would name a kernel that is stretched, not heavy."""
     n, m = graph_info
     total_rows = world * args.steps * B
     value = total_rows / elapsed_max
     roof = None
     if kt:
         name, k = max(((a, b) for a, b in kt.items() if a not in _COUNTERS),
-                      key=lambda kv: kv[1]["ms"])
+                      key=lambda kv: kv[1]["bytes"])
         achieved = k["bytes"] / (k["ms"] / 1e3) / 1e9 if k["ms"] > 0 else 0.0
         t = (traffic or {}).get(name)
-        roof = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+        roof = {"bound": "hbm", "kernel": name, "chosen_by": "most algorithmic bytes",
+                "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": round(t["bytes_per_launch"], 1) if t else None,
                 "traffic_unit": "bytes/launch (PMC: 2*FETCH_SIZE + WRITE_SIZE, KiB->B)",

@@ -255,6 +255,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
     // large searches); what outgrows a workspace moves on: lane -> wave ->
     // the large HBM workspace, which cannot overflow.
     uint32_t wave_max = 65536, wave_blocks = 8192;
+    const bool tiny_on = std::getenv("CPD_CH_TINY") && *std::getenv("CPD_CH_TINY") == '1';
     if (const char* e = std::getenv("CPD_CH_WAVE")) wave_max = (uint32_t)std::strtoul(e, nullptr, 10);
     // test knob: no wave stage (lane -> large workspace only)
     const bool no_wave = std::getenv("CPD_CH_NOWAVE") != nullptr;
@@ -285,15 +286,17 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             t_lane += now_seconds() - tw;
             tw = now_seconds();
         }
-        // waves: the small LDS workspace (five workgroups per CU), then the
-        // large one (two per CU) for what outgrows it
-        for (int pass = 0; pass < 2 && cnt && !no_wave; ++pass) {
-            DBuf<uint32_t>& out = pass == 0 ? ovf2 : ovf3;
+        // waves: LDS workspaces of 13 KB (CPD_CH_TINY=1: simulations only,
+        // twelve workgroups per CU), 27 KB (five) and 55 KB (two), each
+        // taking what outgrew the one before
+        const int first = tiny_on && !contract ? 0 : 1;
+        for (int size = first; size < 3 && cnt && !no_wave; ++size) {
+            DBuf<uint32_t>& out = size == first ? ovf2 : (list == ovf2.p ? ovf3 : ovf2);
             out.ensure(cnt);
             CH_HIP(hipMemsetAsync(ctr.p + 4, 0, 4, st));
             chk::launch_witness_wave(pairs.p, list, cnt, overlay(), state.p, contract, settle,
-                                     wave_blocks, pass == 0, slots.p, sflag.p, sc.p, out.p,
-                                     ctr.p + 4, ctr.p + 1, st);
+                                     wave_blocks, size, slots.p, sflag.p, sc.p, out.p, ctr.p + 4,
+                                     ctr.p + 1, st);
             wave_searches += cnt;
             read({ctr.p + 4});
             cnt = hv.p[0];

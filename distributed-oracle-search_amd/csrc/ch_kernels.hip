@@ -991,10 +991,13 @@ void launch_ww(const uint32_t* pairs, const uint32_t* plist, uint32_t np, Overla
 
 void launch_witness_wave(const uint32_t* pairs, const uint32_t* plist, uint32_t np, Overlay g,
                          const uint8_t* state, bool contract, uint32_t settle, uint32_t blocks,
-                         bool small, uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf,
+                         int size, uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf,
                          uint32_t* ovf_n, uint32_t* err, hipStream_t s) {
     if (!np) return;
-    if (small)
+    if (size == 0)
+        launch_ww<512, 384, 32>(pairs, plist, np, g, state, contract, settle, blocks, slots,
+                                sflag, sc, ovf, ovf_n, err, s);
+    else if (size == 1)
         launch_ww<1024, 768, 64>(pairs, plist, np, g, state, contract, settle, blocks, slots,
                                  sflag, sc, ovf, ovf_n, err, s);
     else
@@ -1002,8 +1005,10 @@ void launch_witness_wave(const uint32_t* pairs, const uint32_t* plist, uint32_t 
                                    sflag, sc, ovf, ovf_n, err, s);
 }
 
-uint32_t witness_wave_lds_bytes(bool small) {
-    return small ? (uint32_t)sizeof(WaveLds<1024, 768, 64>) : (uint32_t)sizeof(WaveLds<2048, 1792, 128>);
+uint32_t witness_wave_lds_bytes(int size) {
+    return size == 0 ? (uint32_t)sizeof(WaveLds<512, 384, 32>)
+           : size == 1 ? (uint32_t)sizeof(WaveLds<1024, 768, 64>)
+                       : (uint32_t)sizeof(WaveLds<2048, 1792, 128>);
 }
 
 void launch_record(const uint32_t* S, uint32_t nS, uint32_t rank0, Overlay g, const uint32_t* upos,

@@ -61,14 +61,14 @@ void launch_witness(const uint32_t* pairs, const uint32_t* plist, uint32_t np, O
                     uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf,
                     uint32_t* ovf_n, uint32_t* err, hipStream_t s);
 // The same searches, one wave each with the search's table and heap in LDS
-// (witness_wave_lds_bytes(small) per workgroup; small: 1024 table / 768 heap
-// slots / 64 targets, else 2048 / 1792 / 128): for the core rounds' large
-// searches.  A search that outgrows LDS goes to ovf as above.
+// (witness_wave_lds_bytes(size) per workgroup; size 0: 512 table / 384 heap
+// slots / 32 targets, 1: 1024 / 768 / 64, 2: 2048 / 1792 / 128): for the
+// core rounds' large searches.  A search that outgrows LDS goes to ovf as above.
 void launch_witness_wave(const uint32_t* pairs, const uint32_t* plist, uint32_t np, Overlay g,
                          const uint8_t* state, bool contract, uint32_t settle, uint32_t blocks,
-                         bool small, uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf,
+                         int size, uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf,
                          uint32_t* ovf_n, uint32_t* err, hipStream_t s);
-uint32_t witness_wave_lds_bytes(bool small);
+uint32_t witness_wave_lds_bytes(int size);
 // Record the contracted nodes S (ranks rank0 + i): rank[v], rec_* per rank,
 // their out-/in-lists copied to the up / down pools at upos / dpos (+ base),
 // neighbours' deleted / depth / aff updated, state[v] = 2.

@@ -1495,10 +1495,11 @@ __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
 // per 21504 rows; 4 chunks: 35.2; 16: 32.8).
 // (A lane per RUN instead — each word written by the run holding its first
 // column, interiors as a segmented fill — measured 100 ms against 39 for
-// 21504 rows: five times as many lanes' worth of work as words.)
+// 21504 rows: five times as many lanes' worth of work as words.  A bitmap of
+// the chunk's run starts with prefix popcounts in place of the binary
+// search: 38.8 ms against 32.8.)
 constexpr uint32_t kExpandRuns = 512;
 constexpr uint32_t kExpandCpw = 16;
-constexpr uint32_t kExpandSpan = 8192;  // chunk column spans the bitmap path takes
 
 __global__ __launch_bounds__(256) void expand_rows(const uint64_t* __restrict__ offsets,
                                                    const uint32_t* __restrict__ runs,
@@ -1508,11 +1509,8 @@ __global__ __launch_bounds__(256) void expand_rows(const uint64_t* __restrict__ 
                                                    uint32_t* __restrict__ dense) {
     constexpr uint32_t kLook = 8;
     __shared__ uint32_t cr_all[4][kExpandRuns + kLook];
-    __shared__ uint32_t bm_all[4][kExpandSpan / 32u], pc_all[4][kExpandSpan / 32u];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t c_begin = (blockIdx.x * 4u + wv) * cpw;
-    uint32_t* bm = bm_all[wv];
-    uint32_t* pc = pc_all[wv];
     if (c_begin >= total_chunks) return;  // wave-uniform; no block barrier below
     const uint32_t c_end = min(total_chunks, c_begin + cpw);
     uint32_t* cr = cr_all[wv];
@@ -1540,62 +1538,6 @@ __global__ __launch_bounds__(256) void expand_rows(const uint64_t* __restrict__ 
         const uint32_t w0 = r0 == 0 ? 0u : ((cr[0] >> 4) + 7u) >> 3;
         const uint32_t w1 = r1 == R ? words_per_row : ((cr[r1 - r0] >> 4) + 7u) >> 3;
         uint32_t* __restrict__ out = dense + (size_t)row * words_per_row;
-        const uint32_t cb = w0 * 8u, span = (w1 - w0) * 8u;  // the chunk's columns
-        if (span && span <= kExpandSpan) {
-            // run index of every column by a bitmap of the run starts in
-            // (cb, cb + span) and its prefix popcounts: b0 = the last run
-            // starting at or before cb (one of the first 8: w0 = ceil(start / 8))
-            const uint32_t nw = (span + 31u) >> 5;
-            for (uint32_t i = lane; i < nw; i += 64u) bm[i] = 0u;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const uint32_t sl = lane < nl ? cr[lane] >> 4 : 0xFFFFFFFFu;
-            const uint32_t b0 = (uint32_t)__popcll(__ballot(lane < 8u && sl <= cb)) - 1u;
-            for (uint32_t i = lane; i < nl; i += 64u) {
-                const uint32_t p = (cr[i] >> 4) - cb;  // wraps (huge) for starts <= cb
-                if (p - 1u < span - 1u) atomicOr(&bm[p >> 5], 1u << (p & 31u));
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            // exclusive prefix of the words' popcounts, kExpandSpan / 32 / 64 words per lane
-            constexpr uint32_t kPer = kExpandSpan / 32u / 64u;
-            uint32_t pcs[kPer], tot = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < kPer; ++q) {
-                const uint32_t i = lane * kPer + q;
-                pcs[q] = tot;
-                tot += i < nw ? (uint32_t)__popc(bm[i]) : 0u;
-            }
-            uint32_t incl = tot;
-#pragma unroll
-            for (uint32_t d = 1; d < 64u; d <<= 1) {
-                const uint32_t y = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += y;
-            }
-#pragma unroll
-            for (uint32_t q = 0; q < kPer; ++q) {
-                const uint32_t i = lane * kPer + q;
-                if (i < nw) pc[i] = pcs[q] + incl - tot;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            for (uint32_t w = w0 + lane; w < w1; w += 64u) {
-                const uint32_t p = (w - w0) * 8u;  // 8 columns inside one bitmap word
-                const uint32_t bw = bm[p >> 5], base = b0 + pc[p >> 5];
-                uint32_t word = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < 8u; ++k) {
-                    const uint32_t bit = (p & 31u) + k;  // bits (.., bit] of this word
-                    const uint32_t m = bit == 31u ? 0xFFFFFFFFu : ((2u << bit) - 1u);
-                    word |= (cr[base + (uint32_t)__popc(bw & m)] & 0xFu) << (4u * k);
-                }
-                out[w] = word;
-            }
-            continue;
-        }
         uint32_t a0 = 0;  // this lane's previous word's run: its next word starts there or later
         for (uint32_t w = w0 + lane; w < w1; w += 64u) {
             const uint32_t c0 = w * 8u;

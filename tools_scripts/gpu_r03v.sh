@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$PWD
-timeout -k 10 600 python -u -m pytest tests/test_gpu_index_stream.py tests/test_gpu_drivers.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_index_stream.py tests/test_gpu_drivers.py tests/test_gpu_parity.py tests/test_ch_gpu.py -x -q --timeout 300 --timeout-method thread \
     > gpurun_out/r03v_tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 gpurun_out/r03v_tests.log; exit 1; }
 tail -2 gpurun_out/r03v_tests.log
 cd /tmp
@@ -17,3 +17,8 @@ import sys,csv
 for r in csv.reader(sys.stdin): print('expand_rows calls', r[1], 'avg_us %.1f' % (float(r[3]) / 1e3))"
 python3 -c "import json;d=json.load(open('$R/gpurun_out/prof_r03v.json'));print('parity', d['parity_sample_bit_exact'], d['queries_per_s'])"
 cd $R && bash tools_scripts/gpu_r03u.sh
+cd $R
+for t in 0 1; do
+  CPD_CH_TINY=$t timeout -k 10 200 python tools_scripts/ch_gpu_time.py > gpurun_out/r03v_time_tiny$t.log 2>&1 || { echo "timing tiny=$t failed"; exit 1; }
+  echo "tiny=$t"; grep -E "ch-gpu\] [0-9]+ rounds|GPU plan" gpurun_out/r03v_time_tiny$t.log | tail -2
+done
