@@ -240,7 +240,10 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             caps1 = {a, b, c};
     }
     const uint64_t lb1 = chk::witness_lane_bytes(caps1);
-    const uint32_t lanes1 = 131072;
+    // lanes: up to 131072 (2048 waves: 3.2 GB of workspaces), fewer for small
+    // graphs (a round has at most ~4n searches)
+    const uint32_t lanes1 =
+        (uint32_t)std::min<uint64_t>(131072, std::max<uint64_t>(256, (4ull * n + 255) / 256 * 256));
     DBuf<uint8_t> ws1, ws2;
     ws1.ensure(lb1 * lanes1);
     CH_HIP(hipMemsetAsync(ws1.p, 0, ws1.n, st));
@@ -255,7 +258,9 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
     // large searches); what outgrows a workspace moves on: lane -> wave ->
     // the large HBM workspace, which cannot overflow.
     uint32_t wave_max = 65536, wave_blocks = 8192;
-    const bool tiny_on = std::getenv("CPD_CH_TINY") && *std::getenv("CPD_CH_TINY") == '1';
+    // the 13-KB stage for simulation searches (1M: 1.15 against 1.26 s);
+    // CPD_CH_TINY=0 skips it (A/B)
+    const bool tiny_on = !(std::getenv("CPD_CH_TINY") && *std::getenv("CPD_CH_TINY") == '0');
     if (const char* e = std::getenv("CPD_CH_WAVE")) wave_max = (uint32_t)std::strtoul(e, nullptr, 10);
     // test knob: no wave stage (lane -> large workspace only)
     const bool no_wave = std::getenv("CPD_CH_NOWAVE") != nullptr;
@@ -286,9 +291,9 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
             t_lane += now_seconds() - tw;
             tw = now_seconds();
         }
-        // waves: LDS workspaces of 13 KB (CPD_CH_TINY=1: simulations only,
-        // twelve workgroups per CU), 27 KB (five) and 55 KB (two), each
-        // taking what outgrew the one before
+        // waves: LDS workspaces of 13 KB (simulations only, twelve
+        // workgroups per CU), 27 KB (five) and 55 KB (two), each taking
+        // what outgrew the one before
         const int first = tiny_on && !contract ? 0 : 1;
         for (int size = first; size < 3 && cnt && !no_wave; ++size) {
             DBuf<uint32_t>& out = size == first ? ovf2 : (list == ovf2.p ? ovf3 : ovf2);

@@ -59,7 +59,7 @@ def test_ch_gpu_identical_spec_graph():
 @pytest.mark.parametrize("env", [{"CPD_CH_WS": "16,8,2"},
                                  {"CPD_CH_WS": "16,8,2", "CPD_CH_NOWAVE": "1"},
                                  {"CPD_CH_WAVE": "0"}, {"CPD_CH_WAVE": "1000000000"},
-                                 {"CPD_CH_WAVE": "1000000000", "CPD_CH_TINY": "1"}])
+                                 {"CPD_CH_WAVE": "1000000000", "CPD_CH_TINY": "0"}])
 def test_ch_gpu_search_routes(env):
     """Every route a witness search can take — the lane workspace (here tiny,
     so most searches overflow it), the wave kernel's LDS, the large HBM

@@ -6,7 +6,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for pr in 8,2,3 8,2,6 8,2,12 4,2,3; do
+for pr in ${PRIOS:-8,2,3 8,2,6 8,2,12 4,2,3}; do
   tag=$(echo $pr | tr , _)
   CPD_CH_PRIO=$pr CPD_BENCH_CACHE=/tmp/cpd-prio-$tag timeout -k 10 400 python bench.py --steps 10 --warmup 2 --no-cpu --no-pmc --no-search --no-full-build --queries 200000 \
       > gpurun_out/r03u_$tag.json 2> gpurun_out/r03u_$tag.err || { echo "bench $pr failed"; tail -20 gpurun_out/r03u_$tag.err; exit 1; }
