@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "distributed-oracle-search_amd")
 METRIC = "CPD build sources/sec + GTEPS; table-search queries/sec; % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-PLAN_TAG = "ch823g"     # bump when the hierarchy builder changes (cache key)
+PLAN_TAG = "ch8212g"    # bump when the hierarchy builder changes (cache key)
 
 WORKLOADS = {
     "synth1m": dict(width=1000, seed=1, style="shuffled", method="div", key=8, sample=None,

@@ -164,9 +164,12 @@ struct Contractor {
     }
 
     // priority = a*edge difference + b*contracted neighbours + c*depth; depth
-    // bounds the sweep levels.  8,2,3 measured best on the synthetic road
-    // graphs (fewest arcs at ~same level count; bench/DESIGN.md).
-    int64_t prio_ed = 8, prio_del = 2, prio_depth = 3;
+    // bounds the sweep levels.  Round 3 (profiles/ch_prio_ab/): 8,2,12 —
+    // 166 + 159 levels, 5.20M arcs, 343k rows/s on the 1M bench graph —
+    // against round 2's 8,2,3 (189 + 194 levels, 5.09M arcs, 338k rows/s):
+    // fewer latency-bound narrow levels outweigh 2% more arcs (8,2,20 / 8,2,30:
+    // 343-345k / 345.6k, with the down-sweep's arcs and time growing).
+    int64_t prio_ed = 8, prio_del = 2, prio_depth = 12;
 
     int64_t priority_of(uint32_t v, int64_t sc) const {
         int64_t ed = sc - (int64_t)in[v].size() - (int64_t)out[v].size();

@@ -1,7 +1,7 @@
 // Contraction hierarchy built on the GPU (kernels: ch_kernels.hip).
 //
 // The same parallel independent-set contraction as ch.cpp — same priority
-// (8 x edge difference + 2 x contracted neighbours + 3 x depth, ties by a
+// (8 x edge difference + 2 x contracted neighbours + 12 x depth, ties by a
 // hash of the node id), same independent set, same bounded witness searches
 // (settle limits, via bounds, heap order), same lightest-arc shortcut merges
 // — so the hierarchy is the host's, rank for rank and arc for arc
@@ -100,7 +100,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
     const double t0 = now_seconds();
     const uint32_t settle_c = settle_limit ? settle_limit : 400;
     const uint32_t settle_s = std::max<uint32_t>(50, settle_c / 4);
-    int64_t pa = 8, pb = 2, pc = 3;  // ch.cpp Contractor::prio_* (CPD_CH_PRIO as there)
+    int64_t pa = 8, pb = 2, pc = 12;  // ch.cpp Contractor::prio_* (CPD_CH_PRIO as there)
     if (const char* e = std::getenv("CPD_CH_PRIO")) {
         long a, b, c;
         if (std::sscanf(e, "%ld,%ld,%ld", &a, &b, &c) == 3) {
