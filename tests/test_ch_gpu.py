@@ -91,3 +91,34 @@ def test_ch_gpu_identical_1m():
     print(f"\n1M CH: host {t_host:.2f} s ({a.info()['ch_seconds']:.2f} s CH), "
           f"GPU {t_gpu:.2f} s ({b.info()['ch_seconds']:.2f} s CH)")
     same_hierarchy(a.export_ch(), b.export_ch())
+
+
+@pytest.mark.gpu
+def test_make_cpd_auto_ch_gpu_and_host_same_files(tmp_path):
+    """The drop-in executable: a worker whose plan is contracted on its GPU
+    (the default) and one told --ch-host write byte-identical bucket files
+    and column order, and save the same plan."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    binp = os.path.join(root, "bin")
+    prefix = str(tmp_path / "g")
+    subprocess.run([os.path.join(binp, "gen_synth"), "--width", "60", "--height", "50", "--seed",
+                    "3", "--out", prefix], check=True, capture_output=True, timeout=120)
+    digests = {}
+    for mode in ("gpu", "host"):
+        out = tmp_path / mode
+        out.mkdir()
+        cmd = [os.path.join(binp, "make_cpd_auto"), "--input", prefix + ".xy", "--partmethod",
+               "div", "--partkey", "4", "--workerid", "1", "--maxworker", "4", "--outdir",
+               str(out), "--device", "0", "--plan", str(out / "g.plan")]
+        if mode == "host":
+            cmd.append("--ch-host")
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-2000:]
+        files = sorted(f for f in os.listdir(out) if f.endswith(".cpd") or f.endswith(".order"))
+        assert any(f.endswith(".cpd") for f in files)
+        digests[mode] = {f: hashlib.sha256(open(out / f, "rb").read()).hexdigest() for f in files}
+        a = cpd.Plan.load(str(out / "g.plan")).export_ch()
+        digests[mode]["plan"] = hashlib.sha256(
+            b"".join(np.ascontiguousarray(a[k]).tobytes() for k in KEYS)).hexdigest()
+    assert digests["gpu"] == digests["host"]
