@@ -788,7 +788,11 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             return v;
         };
         {
-            constexpr uint32_t kNarrow = 1024;
+            // up levels of at most kNarrow nodes run chunked (CPD_UP_NARROW: A/B)
+            static const uint32_t kNarrow = [] {
+                const char* e = std::getenv("CPD_UP_NARROW");
+                return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1024u;
+            }();
             const uint32_t C = sweep_chunk_arcs();
             std::vector<uint32_t> items, cols;
             g->up_item_first.assign(g->asc_lvl.size(), 0);
