@@ -242,8 +242,10 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
     const uint64_t lb1 = chk::witness_lane_bytes(caps1);
     // lanes: up to 131072 (2048 waves: 3.2 GB of workspaces), fewer for small
     // graphs (a round has at most ~4n searches)
+    uint64_t lane_max = 131072;  // CPD_CH_LANES: A/B
+    if (const char* e = std::getenv("CPD_CH_LANES")) lane_max = std::max(256ul, std::strtoul(e, nullptr, 10));
     const uint32_t lanes1 =
-        (uint32_t)std::min<uint64_t>(131072, std::max<uint64_t>(256, (4ull * n + 255) / 256 * 256));
+        (uint32_t)std::min<uint64_t>(lane_max, std::max<uint64_t>(256, (4ull * n + 255) / 256 * 256));
     DBuf<uint8_t> ws1, ws2;
     ws1.ensure(lb1 * lanes1);
     CH_HIP(hipMemsetAsync(ws1.p, 0, ws1.n, st));

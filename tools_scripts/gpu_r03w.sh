@@ -14,3 +14,7 @@ for nw in 256 1024 4096; do
       > gpurun_out/r03w_narrow$nw.json 2> gpurun_out/r03w_narrow$nw.err || { echo "bench narrow $nw failed"; tail -20 gpurun_out/r03w_narrow$nw.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/r03w_narrow$nw.json'));k=d['kernels'];print('narrow=$nw', d['value'], d['ms_per_step'], {n:round(v['ms']/10,2) for n,v in k.items() if n in ('sweep_down','sweep_up','first_moves','rle_count','rle_emit')})"
 done
+for ln in 65536 131072 262144; do
+  CPD_CH_LANES=$ln timeout -k 10 200 python tools_scripts/ch_gpu_time.py > gpurun_out/r03w_lanes$ln.log 2>&1 || { echo "timing lanes $ln failed"; exit 1; }
+  echo "lanes=$ln"; grep -E "ch-gpu\] [0-9]+ rounds|GPU plan" gpurun_out/r03w_lanes$ln.log | tail -2
+done
