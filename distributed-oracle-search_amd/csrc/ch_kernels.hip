@@ -595,48 +595,15 @@ __global__ __launch_bounds__(64) void k_witness_wave(
                     S.pd[len] = td;
                     S.pn[len] = tn0;
                     int64_t hole = 0, second = 0;
-                    const int64_t lim = (len - 1) / 2;
-                    // two levels per step: the hole's children and their
-                    // children read together (as the lane search's pop)
-                    while (second < lim) {
-                        const int64_t c = 2 * (second + 1);
-                        const unsigned long long a0 = S.pd[c - 1], a1 = S.pd[c];
-                        const uint32_t n0 = S.pn[c - 1], n1 = S.pn[c];
-                        unsigned long long gd[4];
-                        uint32_t gn[4];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int64_t gi = 2 * c - 1 + q;
-                            gd[q] = gi < len ? S.pd[gi] : 0ull;
-                            gn[q] = gi < len ? S.pn[gi] : 0u;
-                        }
+                    while (second < (len - 1) / 2) {
+                        second = 2 * (second + 1);
+                        if (S.pd[second] > S.pd[second - 1]) --second;
+                        const unsigned long long cd = S.pd[second];
+                        const uint32_t cn = S.pn[second];
                         __syncthreads();
-                        second = c;
-                        unsigned long long ud = a1;
-                        uint32_t un = n1;
-                        if (a1 > a0) {
-                            --second;
-                            ud = a0;
-                            un = n0;
-                        }
-                        S.pd[hole] = ud;
-                        S.pn[hole] = un;
+                        S.pd[hole] = cd;
+                        S.pn[hole] = cn;
                         hole = second;
-                        if (!(second < lim)) break;
-                        const int64_t c2 = 2 * (second + 1);
-                        const int o = second == c - 1 ? 0 : 2;
-                        second = c2;
-                        ud = gd[o + 1];
-                        un = gn[o + 1];
-                        if (gd[o + 1] > gd[o]) {
-                            --second;
-                            ud = gd[o];
-                            un = gn[o];
-                        }
-                        S.pd[hole] = ud;
-                        S.pn[hole] = un;
-                        hole = second;
-                        __syncthreads();
                     }
                     if ((len & 1) == 0 && second == (len - 2) / 2) {
                         second = 2 * (second + 1);
