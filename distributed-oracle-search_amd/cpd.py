@@ -49,7 +49,8 @@ EXPORTED = [
     "cpd_index_append_rows", "cpd_index_append_built_rows", "cpd_index_info",
     "cpd_synth_road_graph_ex", "cpd_query_search", "cpd_query_search_counters",
     "cpd_graph_set_coords", "cpd_host_alloc", "cpd_host_free",
-    "cpd_rows_lanes", "cpd_graph_hint_next",
+    "cpd_rows_lanes", "cpd_graph_hint_next", "cpd_graph_set_hbm_reserve",
+    "cpd_device_mem_info",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
@@ -332,6 +333,13 @@ def device_count() -> int:
     return c.value
 
 
+def device_mem_info(device: int = 0):
+    """(free, total) HBM bytes of `device` (cpd_device_mem_info)."""
+    f, t = C.c_uint64(), C.c_uint64()
+    _check(lib.cpd_device_mem_info(C.c_int(device), C.byref(f), C.byref(t)))
+    return f.value, t.value
+
+
 class Rows:
     def __init__(self, h):
         self._h = h
@@ -384,11 +392,13 @@ class Rows:
 class Graph:
     """A plan resident on one GPU."""
 
-    def __init__(self, plan: Plan, device: int = 0, batch: int = 0):
+    def __init__(self, plan: Plan, device: int = 0, batch: int = 0, hbm_reserve: int = 0):
         self._h = C.c_void_p()
         self.plan = plan
         _check(lib.cpd_graph_create(plan._h, C.c_int(device), C.byref(self._h)))
-        # 0 = the largest batch that fits in free HBM (<= 24576)
+        if hbm_reserve:
+            self.set_hbm_reserve(hbm_reserve)
+        # 0 = the largest batch that fits in free HBM above the reserve (<= 24576)
         _check(lib.cpd_graph_set_batch(self._h, C.c_uint32(batch)))
 
     @property
@@ -400,6 +410,11 @@ class Graph:
     def set_batch(self, batch: int) -> None:
         """Rows per sweep (multiple of 1024; 0 = what fits in free HBM)."""
         _check(lib.cpd_graph_set_batch(self._h, C.c_uint32(batch)))
+
+    def set_hbm_reserve(self, nbytes: int) -> None:
+        """HBM the auto batch leaves free for what follows on this GPU
+        (cpd_graph_set_hbm_reserve); applies at the next set_batch(0)."""
+        _check(lib.cpd_graph_set_hbm_reserve(self._h, C.c_uint64(nbytes)))
 
     def set_coords(self, x, y) -> None:
         """Node coordinates (node-id space; None clears them): a batch's

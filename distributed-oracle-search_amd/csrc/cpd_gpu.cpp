@@ -368,6 +368,7 @@ struct cpd_graph {
     }
     void select() const { HIP_CHECK(hipSetDevice(device)); }
 
+    uint64_t hbm_reserve = 0;  // cpd_graph_set_hbm_reserve
     void reserve_batch(uint32_t want) {
         if (want == 0) {
             size_t free_b = 0, total_b = 0;
@@ -383,7 +384,11 @@ struct cpd_graph {
                                2.0 * (fmb / 8.0 * npad + (fmb == 4 ? 5.0 / 32.0 * npad : 0.0)) +
                                (fmb == 4 ? 8.0 * rle_count_chunks(npad) : 0.0) +
                                (leaf_fm ? 0.5 * n : 0.0) + 4.0 * n;
-            const double fit = 0.85 * (double)free_b / per;
+            const double avail = free_b > hbm_reserve ? (double)(free_b - hbm_reserve) : 0.0;
+            const double fit = 0.85 * avail / per;
+            CPD_REQUIRE(hbm_reserve == 0 || fit >= 1024.0, CPD_E_OOM,
+                        "HBM reserve of " + std::to_string(hbm_reserve >> 20) + " MiB leaves " +
+                            std::to_string((size_t)avail >> 20) + " MiB: too little for a 1024-row batch");
             want = (uint32_t)std::min(24576.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
         }
         want = (want + 1023u) / 1024u * 1024u;
@@ -401,7 +406,7 @@ struct cpd_graph {
             if (x == 1) {
                 size_t free_b = 0, total_b = 0;
                 HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-                async = async_on() && set_bytes * 8 < free_b;
+                async = async_on() && set_bytes * 8 < (free_b > hbm_reserve ? free_b - hbm_reserve : 0);
                 if (!async) {
                     fmx[1].release();
                     rle_stx[1].release();
@@ -645,6 +650,21 @@ int cpd_device_count(int* count) {
     });
 }
 
+int cpd_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes) {
+    return guarded([&] {
+        CPD_REQUIRE(free_bytes && total_bytes, CPD_E_ARG, "null argument");
+        require_device();
+        int count = 0;
+        HIP_CHECK(hipGetDeviceCount(&count));
+        CPD_REQUIRE(device >= 0 && device < count, CPD_E_ARG, "no such device");
+        HIP_CHECK(hipSetDevice(device));
+        size_t f = 0, t = 0;
+        HIP_CHECK(hipMemGetInfo(&f, &t));
+        *free_bytes = f;
+        *total_bytes = t;
+    });
+}
+
 int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
     return guarded([&] {
         CPD_REQUIRE(p && out, CPD_E_ARG, "graph: null argument");
@@ -828,6 +848,13 @@ int cpd_graph_set_batch(cpd_graph* g, uint32_t batch) {
         g->select();
         HIP_CHECK(hipStreamSynchronize(g->stream));
         g->reserve_batch(batch);
+    });
+}
+
+int cpd_graph_set_hbm_reserve(cpd_graph* g, uint64_t bytes) {
+    return guarded([&] {
+        CPD_REQUIRE(g, CPD_E_ARG, "null graph");
+        g->hbm_reserve = bytes;
     });
 }
 

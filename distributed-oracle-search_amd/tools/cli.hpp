@@ -42,6 +42,10 @@ struct Args {
         std::string s = str(k);
         return s.empty() ? def : std::atoll(s.c_str());
     }
+    double real(const std::string& k, double def) const {
+        std::string s = str(k);
+        return s.empty() ? def : std::atof(s.c_str());
+    }
     const std::vector<std::string>& list(const std::string& k) const {
         static const std::vector<std::string> empty;
         auto it = kv.find(k);

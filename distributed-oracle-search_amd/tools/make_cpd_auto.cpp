@@ -266,7 +266,8 @@ int main(int argc, char** argv) {
                      "usage: make_cpd_auto --input X.xy --partmethod {div|mod} --partkey K "
                      "--workerid I --maxworker W [--outdir D] [--device G] [--batch B] "
                      "[--threads T] [--plan P | --no-plan-cache] [--write-threads T] "
-                     "[--no-pipeline] [--plan-only] [--targets-from SCEN] [--discard]\n");
+                     "[--no-pipeline] [--plan-only] [--targets-from SCEN] [--discard] "
+                     "[--hbm-reserve GIB]\n");
         return 2;
     }
     int mcode = cli::method_code(method);
@@ -362,6 +363,11 @@ int main(int argc, char** argv) {
         const double t_g0 = now();
         cli::check(cpd_graph_create(plan, device, &dg), "graph upload");
         const double t_graph = now() - t_g0;
+        // --hbm-reserve GIB: HBM the auto batch leaves to what shares this GPU
+        // (a fifo_auto serving beside the build)
+        if (a.has("hbm-reserve"))
+            cli::check(cpd_graph_set_hbm_reserve(dg, (uint64_t)(a.real("hbm-reserve", 0.0) * (1ull << 30))),
+                       "hbm reserve");
         cli::check(cpd_graph_set_batch(dg, (uint32_t)a.num("batch", 0)), "batch");
         const double t_batch = now() - t_g0 - t_graph;
         // the .xy coordinates order each batch's lanes (compact target groups)

@@ -177,11 +177,23 @@ void cpd_plan_free(cpd_plan* p);
 /* ------------------------------------------------------------------------ */
 /* [gpu] Devices and graphs. */
 int  cpd_device_count(int* count);
+/* Free and total HBM bytes of `device` (hipMemGetInfo there): what a caller
+ * sizes cpd_graph_set_hbm_reserve against.                                 */
+int  cpd_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes);
 /* Upload a plan to `device` (column-space CSR, CH arcs, levels). */
 int  cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out);
 /* Batch width (rows built per sweep, multiple of 1024; 0 = auto from HBM). */
 int  cpd_graph_set_batch(cpd_graph* g, uint32_t batch);
 int  cpd_graph_get_batch(const cpd_graph* g, uint32_t* batch);
+/* HBM bytes the auto batch (batch 0) leaves free for what follows on this
+ * GPU: an index built from the rows on the same handle, or a fifo_auto
+ * serving beside a make_cpd_auto.  The auto batch takes 85% of the free HBM
+ * above the reserve (default 0), both emit buffer sets included.  Takes
+ * effect at the next cpd_graph_set_batch(g, 0), or at the first build when
+ * the batch was never set.  With a reserve set, that call fails with
+ * CPD_E_OOM when what is left cannot hold a 1024-row batch.  Explicit batch
+ * widths ignore the reserve.                                               */
+int  cpd_graph_set_hbm_reserve(cpd_graph* g, uint64_t bytes);
 /* Optional node coordinates (x[n], y[n], node-id space, e.g. the .xy file's
  * `v id x y`; NULL clears them).  A batch's targets are then laid out over
  * the lanes along a Hilbert curve of their coordinates instead of by column,

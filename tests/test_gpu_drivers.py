@@ -148,23 +148,31 @@ def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key):
                     "5", "--out", prefix, "--queries", "10"], check=True, capture_output=True)
     xy = prefix + ".xy"
     dirs = {}
-    for mode, extra in [("seq", ["--no-pipeline"]), ("pipe", ["--write-threads", "3"])]:
+    # "reserve": the auto batch above a 1-GiB HBM reserve (cpd_graph_set_hbm_reserve)
+    for mode, extra in [("seq", ["--no-pipeline", "--batch", "1024"]),
+                        ("pipe", ["--write-threads", "3", "--batch", "1024"]),
+                        ("reserve", ["--hbm-reserve", "1"]), ("too_much", ["--hbm-reserve", "1e7"])]:
         out = str(tmp_path / mode)
         p = subprocess.run([os.path.join(BIN, "make_cpd_auto"), "--input", xy, "--partmethod",
                             method, "--partkey", str(key), "--workerid", "1", "--maxworker", "2",
-                            "--outdir", out, "--device", "0", "--batch", "1024",
+                            "--outdir", out, "--device", "0",
                             "--plan", str(tmp_path / "g.plan")] + extra,
                            capture_output=True, text=True, timeout=300)
+        if mode == "too_much":  # a reserve past the free HBM: refused, nothing built
+            assert p.returncode != 0 and "HBM reserve" in p.stderr, p.stderr
+            continue
         assert p.returncode == 0, p.stderr
         dirs[mode] = out
     seq = sorted(f for f in os.listdir(dirs["seq"]) if f.endswith(".cpd"))
     pipe = sorted(f for f in os.listdir(dirs["pipe"]) if f.endswith(".cpd"))
     assert seq == pipe and len(seq) == key // 2
     assert not [f for f in os.listdir(dirs["pipe"]) if f.endswith(".tmp")]
+    assert sorted(f for f in os.listdir(dirs["reserve"]) if f.endswith(".cpd")) == seq
     for f in seq:
         a = open(os.path.join(dirs["seq"], f), "rb").read()
         b = open(os.path.join(dirs["pipe"], f), "rb").read()
         assert a == b, f
+        assert open(os.path.join(dirs["reserve"], f), "rb").read() == a, f
     # one bucket against the CPU oracle
     g = cpd.synth_road_graph(64, 48, seed=5)
     order = oracle.dfs_preorder(g.row_ptr, g.dst)

@@ -1,0 +1,50 @@
+"""The auto batch's HBM headroom (cpd_graph_set_hbm_reserve; VERDICT r02
+"the batch chooser ignores what follows the build"): with a reserve set, the
+auto batch leaves it free, shrinks to fit above it, fails with CPD_E_OOM when
+no 1024-row batch fits, and the rows it builds stay bit-exact."""
+import numpy as np
+import pytest
+
+import cpd
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+
+def test_hbm_reserve_bounds_the_auto_batch():
+    g = cpd.synth_road_graph(60, 60, seed=4)
+    plan = cpd.Plan(g)
+    dev = cpd.Graph(plan, batch=0)
+    full = dev.batch
+    assert full == 24576  # a 3600-node graph: the cap, far below free HBM
+
+    free0, _ = cpd.device_mem_info(0)
+    dev.set_hbm_reserve(free0 + (1 << 30))
+    with pytest.raises(cpd.CpdError) as ei:
+        dev.set_batch(0)
+    assert ei.value.code == cpd.CPD_E_OOM
+
+    free0, _ = cpd.device_mem_info(0)
+    reserve = free0 - 256 * MiB
+    dev.set_hbm_reserve(reserve)
+    dev.set_batch(0)
+    b = dev.batch
+    assert 1024 <= b < full and b % 1024 == 0
+    free1, _ = cpd.device_mem_info(0)
+    assert free1 >= reserve
+
+    rng = np.random.default_rng(8)
+    targets = rng.permutation(g.n).astype(np.uint32)[: b + 700]  # two sweeps
+    off, runs = dev.build_rows(targets).export()
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    np.testing.assert_array_equal(off, ref_off)
+    np.testing.assert_array_equal(runs, ref_runs)
+
+    # an explicit width ignores the reserve; reserve 0 restores the auto cap
+    dev.set_batch(2048)
+    assert dev.batch == 2048
+    dev.set_hbm_reserve(0)
+    dev.set_batch(0)
+    assert dev.batch == full
