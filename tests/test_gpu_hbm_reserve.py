@@ -48,3 +48,11 @@ def test_hbm_reserve_bounds_the_auto_batch():
     dev.set_hbm_reserve(0)
     dev.set_batch(0)
     assert dev.batch == full
+
+
+def test_device_mem_info():
+    free, total = cpd.device_mem_info(0)
+    assert 0 < free <= total
+    with pytest.raises(cpd.CpdError) as ei:
+        cpd.device_mem_info(cpd.device_count())
+    assert ei.value.code == cpd.CPD_E_ARG

@@ -179,6 +179,9 @@ def test_gpu_entry_points_fail_loudly_without_gpu():
     with pytest.raises(cpd.CpdError) as e:
         cpd.Graph(cpd.Plan(g))
     assert e.value.code == cpd.CPD_E_HIP and "no CPU fallback" in str(e.value)
+    with pytest.raises(cpd.CpdError) as e:
+        cpd.device_mem_info(0)
+    assert e.value.code == cpd.CPD_E_HIP
 
 
 def test_tools_roundtrip_and_fail_loudly(tmp_path):
