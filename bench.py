@@ -77,7 +77,9 @@ def parse(argv=None):
                     help="skip the configs[0] mod-3 partitioned CPU run")
     ap.add_argument("--no-search", action="store_true", help="skip the cpd-search leg")
     ap.add_argument("--no-full-build", action="store_true",
-                    help="skip the end-to-end worker build (make_cpd_auto --discard, cold plan)")
+                    help="skip the end-to-end worker build (make_cpd_auto, cold plan)")
+    ap.add_argument("--full-build-discard", action="store_true",
+                    help="full-build leg without file writes (make_cpd_auto --discard)")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
@@ -104,8 +106,9 @@ def plan_path(args):
 # rocprofv3 kernel names -> the library's timing names
 KERNEL_NAMES = {"sweep_level<true": "sweep_up", "sweep_up_": "sweep_up",
                 "sweep_level<false": "sweep_down", "sweep_down8": "sweep_down",
-                "first_moves": "first_moves", "rle_scan<false": "rle_count",
-                "rle_scan<true": "rle_emit", "rle_count_ch": "rle_count", "rle_fix": "rle_fix", "DenseRows": "table_search_dense",
+                "first_moves": "first_moves", "rle_scan<": "rle_count",
+                "rle_moves": "rle_moves", "rle_count_ch": "rle_count", "rle_fix": "rle_fix",
+                "moves_runs": "moves_runs", "DenseRows": "table_search_dense",
                 "RleRows": "table_search", "table_search_dense": "table_search_dense",
                 "table_search(": "table_search", "expand_rows": "expand_rows"}
 
@@ -450,10 +453,12 @@ def cpu_partitioned(threads, rows_per_worker=384, queries=20000):
 
 
 # --------------------------------------------------------------------------
-# end-to-end worker build: bin/make_cpd_auto as the
-# driver runs it (make_cpds.py:20), on a cold plan cache, every row the rank
-# owns built and copied out of HBM (--discard: the D2H export without the
-# file writes — a div-8 worker's ~312 GB of runs outgrow the box's disk)
+# end-to-end worker build: bin/make_cpd_auto
+# as the driver runs it (make_cpds.py:20), on a cold plan cache, every row the
+# rank owns built, copied out of HBM and written to its bucket files in the
+# compact layout (DOSCPD02: a 4-bit move per column, n/2 bytes per row); then
+# bin/fifo_auto (make_fifos.py:21) loads those files and answers a request
+# through the reference's FIFO protocol, checked against the oracle
 
 def full_build_xy(args):
     """The workload's graph as a .xy file (bin/gen_synth, same generator and
@@ -474,22 +479,33 @@ def full_build_workers(args, world):
     return max(world, args.partkey)
 
 
-def full_build(args, xy, world, rank, device):
+def full_build_dir(args, world):
+    return os.path.join(args.cache, f"fb-out-{world}")
+
+
+def full_build(args, xy, world, rank, device, comm):
     """Run make_cpd_auto for worker `rank` of full_build_workers() with a
     fresh (cold) plan cache shared by the node's ranks; returns its JSON phase
-    line."""
+    line.  Rank 0 writes its bucket files (DOSCPD02) into the cache directory
+    on the box's disk; the other ranks run the same worker path with
+    --discard (D2H export, no file writes): eight 62.5-GB workers would
+    outgrow one node's disk."""
+    import glob
     import shutil
-    outdir = os.path.join(args.cache, f"fb-out-{world}")
-    if rank == 0:
-        shutil.rmtree(outdir, ignore_errors=True)
+    outdir = full_build_dir(args, world)
+    if rank == 0:  # the previous runs' outputs (and plan caches) go first
+        for d in glob.glob(os.path.join(args.cache, "fb-out-*")):
+            shutil.rmtree(d, ignore_errors=True)
         os.makedirs(outdir)
-    else:
-        while not os.path.isdir(outdir):
-            time.sleep(0.1)
+    # no rank starts before the cold directory exists (ADVICE r03: a rank
+    # that only polled for the directory could reuse a stale plan cache or
+    # race rank 0's removal)
+    comm.barrier()
+    write = rank == 0 and not args.full_build_discard
     cmd = [os.path.join(ROOT, "bin", "make_cpd_auto"), "--input", xy, "--partmethod",
            args.partmethod, "--partkey", str(args.partkey), "--workerid", str(rank),
            "--maxworker", str(full_build_workers(args, world)), "--outdir", outdir, "--device",
-           str(device), "--discard"]
+           str(device), "--format", "moves"] + ([] if write else ["--discard"])
     if args.batch:
         cmd += ["--batch", str(args.batch)]
     p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
@@ -497,7 +513,89 @@ def full_build(args, xy, world, rank, device):
     if p.returncode:
         raise RuntimeError(f"make_cpd_auto failed: {p.stderr[-400:]}")
     line = next(l for l in p.stdout.splitlines() if l.startswith("make_cpd_auto-json: "))
-    return json.loads(line.split(": ", 1)[1])
+    rec = json.loads(line.split(": ", 1)[1])
+    if write:
+        rec["files_bytes"] = sum(os.path.getsize(os.path.join(outdir, f))
+                                 for f in os.listdir(outdir) if f.endswith(".cpd"))
+    return rec
+
+
+def _read_ready(p, deadline):
+    """fifo_auto's load record and its "listening" line (select with a
+    deadline: a server that never comes up fails the leg, not the bench)."""
+    import select
+    rec, buf = None, ""
+    while time.time() < deadline:
+        r, _, _ = select.select([p.stdout], [], [], 1.0)
+        if r:
+            line = p.stdout.readline()
+            if not line:
+                break
+            buf += line
+            if line.startswith("fifo_auto-json: "):
+                rec = json.loads(line.split(": ", 1)[1])
+            if "listening" in line:
+                return rec
+        if p.poll() is not None:
+            break
+    raise RuntimeError(f"fifo_auto did not come up: {buf[-300:]} {p.stderr.read()[-300:]}")
+
+
+def serve_probe(args, xy, outdir, W, device, g, order, threads, nq=4000, nprobe=4):
+    """bin/fifo_auto (make_fifos.py:21) on the bucket files worker 0 just
+    wrote, one request through the reference's protocol (process_query.py:
+    66-111: query file, answer FIFO, JSON config with debug on for the
+    per-query side file), answers checked against the oracle's rows of
+    `nprobe` of the worker's targets."""
+    import numpy as np
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpd
+    import oracle
+    fifo = os.path.join(outdir, "worker0.fifo")
+    cmd = [os.path.join(ROOT, "bin", "fifo_auto"), "--input", xy, "--partmethod",
+           args.partmethod, "--partkey", str(args.partkey), "--workerid", "0", "--maxworker",
+           str(W), "--outdir", outdir, "--alg", "table-search", "--device", str(device),
+           "--fifo", fifo, "--once"]
+    t0 = time.time()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        rec = _read_ready(p, t0 + 300)
+        ready = time.time() - t0
+        rng = np.random.default_rng(7)
+        mine = cpd.owned_nodes(g.n, W, args.partmethod, args.partkey, 0)
+        probes = np.sort(rng.choice(mine, nprobe, replace=False)).astype(np.uint32)
+        s = rng.integers(0, g.n, nq).astype(np.uint32)
+        t = probes[rng.integers(0, nprobe, nq)]
+        qfile = os.path.join(outdir, "query.localhost0")
+        with open(qfile, "w") as f:  # process_query.py:93-96
+            f.write(f"{nq}\n" + "".join(f"{a} {b}\n" for a, b in zip(s, t)))
+        answer = os.path.join(outdir, "answer.localhost0")
+        os.mkfifo(answer)
+        conf = {"hscale": 1.0, "fscale": 0.0, "time": 0, "itrs": -1, "k_moves": -1, "threads": 0,
+                "verbose": False, "debug": True, "thread_alloc": False, "no_cache": False}
+        t1 = time.time()
+        with open(fifo, "w") as f:  # process_query.py:89
+            f.write(json.dumps(conf) + "\n" + f"{qfile} {answer} -\n")
+        with open(answer) as f:
+            line = f.read().strip()
+        answered = time.time() - t1
+        p.wait(timeout=60)
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+    res = np.loadtxt(qfile + ".res", dtype=np.uint64, ndmin=2)
+    off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, probes, threads=threads)
+    rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, order, probes, off, runs, s, t,
+                                     threads=threads)
+    exact = bool(len(res) == nq and np.array_equal(res[:, 0], s) and np.array_equal(res[:, 2], rc)
+                 and np.array_equal(res[:, 3], rh) and np.array_equal(res[:, 4], rf))
+    return {"what": "bin/fifo_auto on worker 0's bucket files, one request through the "
+                    "reference FIFO protocol (debug side file), vs the oracle",
+            "ready_s": round(ready, 3), "load": rec, "request_s": round(answered, 3),
+            "queries": nq, "probe_targets": nprobe, "answer": line,
+            "bit_exact": exact}
 
 
 def build_plan_child(args, ppath, device):
@@ -817,20 +915,32 @@ def main():
         gc.collect()
         comm.barrier()
         fb_xy = fb_xy or glob_xy(args)  # local rank 0 wrote it before the first barrier
-        rec = full_build(args, fb_xy, world, rank, gpu)
+        rec = full_build(args, fb_xy, world, rank, gpu, comm)
         (tmax,) = comm.reduce([rec["total_s"]], "MAX")
         tot = comm.reduce([float(rec["rows"]), float(rec["runs"]), float(rec["export_bytes"])],
                           "SUM")
-        fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of "
-                      f"{full_build_workers(args, world)} ({args.partmethod} {args.partkey}), one "
-                      "worker per rank: all its rows, cold plan cache, --discard (D2H export "
-                      "into pinned host buffers, no file writes)",
+        W = full_build_workers(args, world)
+        fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of {W} ({args.partmethod} "
+                      f"{args.partkey}), one worker per rank: all its rows, cold plan cache, "
+                      "compact bucket files (DOSCPD02) written by rank 0, --discard (D2H export "
+                      "only) on the other ranks",
               "total_s": round(tmax, 3), "rows": int(tot[0]), "runs": int(tot[1]),
               "rows_per_s_end_to_end": round(tot[0] / tmax, 1) if tmax else 0.0,
               "export_GB": round(tot[2] / 1e9, 2),
               "rank0": rec,
               "rank0_export_GBps": round(rec["export_bytes"] / rec["export_span_s"] / 1e9, 2)
               if rec["export_span_s"] else None}
+        if rank == 0 and "files_bytes" in rec:
+            fb["files_GB"] = round(rec["files_bytes"] / 1e9, 2)
+            try:
+                fb["serve"] = serve_probe(args, fb_xy, full_build_dir(args, world), W, gpu, g,
+                                          plan.order(), host_threads(args))
+            except Exception as e:  # reported, never fatal to the GPU numbers
+                fb["serve"] = {"error": str(e)[-400:]}
+        comm.barrier()
+        if rank == 0:  # the box's disk: the worker's files go once checked
+            import shutil
+            shutil.rmtree(full_build_dir(args, world), ignore_errors=True)
 
     if rank == 0:
         out = assemble(args, world, (g.n, g.m), B, elapsed_max, q_totals, q_ms_max, nrows, nruns,

@@ -50,7 +50,8 @@ EXPORTED = [
     "cpd_synth_road_graph_ex", "cpd_query_search", "cpd_query_search_counters",
     "cpd_graph_set_coords", "cpd_host_alloc", "cpd_host_free",
     "cpd_rows_lanes", "cpd_graph_hint_next", "cpd_graph_set_hbm_reserve",
-    "cpd_device_mem_info",
+    "cpd_device_mem_info", "cpd_rows_move_words", "cpd_rows_export_moves",
+    "cpd_index_append_moves",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
@@ -370,6 +371,22 @@ class Rows:
                                          None, _ptr(runs, u32p)))
         return off, runs
 
+    def move_words(self) -> int:
+        """Words per row of the compact form (ceil(n / 8))."""
+        w = C.c_uint32()
+        _check(lib.cpd_rows_move_words(self._h, C.byref(w)))
+        return w.value
+
+    def export_moves(self, first: int = 0, count: int | None = None) -> np.ndarray:
+        """Rows [first, first+count) as 4-bit move tables: (count, ceil(n/8))
+        u32, column c in bits 4*(c%8) of word c//8 (cpd_rows_export_moves)."""
+        if count is None:
+            count = self.count()[0] - first
+        out = np.empty((count, self.move_words()), np.uint32)
+        _check(lib.cpd_rows_export_moves(self._h, C.c_uint32(first), C.c_uint32(count),
+                                         _ptr(out, u32p)))
+        return out
+
     def targets(self):
         nr, _ = self.count()
         t = np.empty(nr, np.uint32)
@@ -504,6 +521,14 @@ class Index:
         rn = _u32(runs)
         _check(lib.cpd_index_append_rows(self._h, C.c_uint32(len(off) - 1), _ptr(off, u64p),
                                          _ptr(rn, u32p)))
+
+    def append_moves(self, moves) -> None:
+        """Host rows in the compact form: (count, ceil(n/8)) u32 move tables
+        (cpd_index_append_moves)."""
+        mv = np.ascontiguousarray(moves, np.uint32)
+        if mv.ndim != 2:
+            raise ValueError("moves must be (rows, words)")
+        _check(lib.cpd_index_append_moves(self._h, C.c_uint32(mv.shape[0]), _ptr(mv, u32p)))
 
     def append_rows(self, rows: Rows) -> None:
         _check(lib.cpd_index_append_built_rows(self._h, rows._h))

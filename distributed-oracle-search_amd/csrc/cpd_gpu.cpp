@@ -10,6 +10,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <type_traits>
@@ -144,26 +145,26 @@ struct cpd_graph {
     uint32_t B = 0;
     uint32_t fmb = 16;  // bits per first-move set (fm_bits(adj_shift))
     DevBuf<uint32_t> dist, counts;
-    // Emit overlap (CPD_ASYNC, default on): a batch's rle_emit runs on
-    // `estream` while the next batch's sweeps start on `stream` — the sweeps'
-    // narrow, latency-bound levels overlap the bandwidth-bound emit.  The
-    // buffers emit reads (first-move rows, RLE states, lane offsets) are
-    // doubled: set x serves every other batch and is reused only after the
-    // emit that read it (ev_emit[x]) has finished.
+    // Emit overlap (CPD_ASYNC, default on): a batch's move-table emit
+    // (rle_moves) runs on `estream` while the next batch's sweeps start on
+    // `stream` — the sweeps' narrow, latency-bound levels overlap the emit.
+    // The buffers the emit reads (first-move rows, RLE segment states, lane ->
+    // row map) are doubled: set x serves every other batch and is reused only
+    // after the emit that read it (ev_emit[x]) has finished.
     hipStream_t estream = nullptr;
     bool async = false;
     uint32_t cur = 0;
     hipEvent_t ev_emit[2] = {nullptr, nullptr};
     bool emit_pending[2] = {false, false};
     DevBuf<uint32_t> fmx[2];      // [B][npad] fmb-bit sets
-    DevBuf<uint32_t> rle_stx[2];  // [B][npad/32] RLE segment entry states (fmb == 4)
+    DevBuf<uint32_t> rle_stx[2];  // [B][npad/32] RLE segment entry states
     DevBuf<uint8_t> rle_rcx[2];   // [B][npad/32] runs ending in each segment
-    DevBuf<uint64_t> row_offx[2];
+    DevBuf<uint32_t> lane_rowx[2];  // [B] table row of each batch lane
     // chunk exit states / run counts of the chunked count (read by rle_fix on
     // the same stream before the next batch: one set)
     DevBuf<uint32_t> rle_xs, rle_cc, rle_hard;
     HostBuf<uint32_t> rle_hard_h;          // [1]
-    HostBuf<uint64_t> lane_off_h[2];       // host source of row_offx[x]
+    HostBuf<uint32_t> lane_row_h[2];       // host source of lane_rowx[x]
     HostBuf<uint32_t> counts_h;            // [B] runs per lane
     // the buffer set the next batch uses, once the emit that last read it is done
     uint32_t acquire_set() {
@@ -367,6 +368,7 @@ struct cpd_graph {
         pending.swap(keep);
     }
     void select() const { HIP_CHECK(hipSetDevice(device)); }
+    uint32_t wpr() const { return npad / 8u; }  // words per move-table row
 
     uint64_t hbm_reserve = 0;  // cpd_graph_set_hbm_reserve
     void reserve_batch(uint32_t want) {
@@ -375,15 +377,16 @@ struct cpd_graph {
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
             // per target: dist 4n (+ 2n narrow) + two buffer sets of fm rows
             // and RLE segment states (emit overlap) + the chunked count's
-            // chunk states (8 B per chunk) + leaf sets + one row of output
-            // runs at its worst case (4n; ~2.5n on road graphs), in 85% of
-            // free HBM; at most 24 slabs.  Larger batches amortise the
-            // latency-bound narrow levels: at 1M nodes 20480 rows per batch
-            // measured 310.5k rows/s against 296.1k for 16384 (round 2).
+            // chunk states (8 B per chunk) + leaf sets + two rows of move
+            // tables (npad / 2 each: the row set being built and the one a
+            // caller such as make_cpd_auto is exporting), in 85% of free HBM;
+            // at most 24 slabs.  Larger batches amortise the latency-bound
+            // narrow levels: at 1M nodes 20480 rows per batch measured 310.5k
+            // rows/s against 296.1k for 16384 (round 2).
             const double per = (narrow ? 6.0 : 4.0) * n +
-                               2.0 * (fmb / 8.0 * npad + (fmb == 4 ? 5.0 / 32.0 * npad : 0.0)) +
+                               2.0 * (fmb / 8.0 * npad + 5.0 / 32.0 * npad) +
                                (fmb == 4 ? 8.0 * rle_count_chunks(npad) : 0.0) +
-                               (leaf_fm ? 0.5 * n : 0.0) + 4.0 * n;
+                               (leaf_fm ? 0.5 * n : 0.0) + 2.0 * 0.5 * npad;
             const double avail = free_b > hbm_reserve ? (double)(free_b - hbm_reserve) : 0.0;
             const double fit = 0.85 * avail / per;
             CPD_REQUIRE(hbm_reserve == 0 || fit >= 1024.0, CPD_E_OOM,
@@ -401,7 +404,7 @@ struct cpd_graph {
         // still free after the batch's own buffers (else one set: emits do
         // not overlap)
         const size_t set_bytes = (size_t)B * (npad / (32u / fmb)) * 4u +
-                                 (fmb == 4 ? (size_t)B * (npad / 32u) * 5u : 0u) + 8u * B;
+                                 (size_t)B * (npad / 32u) * 5u + 4u * B;
         for (int x = 0; x < 2; ++x) {
             if (x == 1) {
                 size_t free_b = 0, total_b = 0;
@@ -411,14 +414,14 @@ struct cpd_graph {
                     fmx[1].release();
                     rle_stx[1].release();
                     rle_rcx[1].release();
+                    lane_rowx[1].release();
                     break;
                 }
             }
             fmx[x].alloc((size_t)B * (npad / (32u / fmb)));
-            if (fmb == 4) {
-                rle_stx[x].alloc((size_t)B * (npad / 32u));
-                rle_rcx[x].alloc((size_t)B * (npad / 32u));
-            }
+            rle_stx[x].alloc((size_t)B * (npad / 32u));
+            rle_rcx[x].alloc((size_t)B * (npad / 32u));
+            lane_rowx[x].alloc(B);
         }
         cur = 0;
         if (fmb == 4 && rle_count_chunks(npad)) {
@@ -440,7 +443,7 @@ struct cpd_graph {
         }
         counts.alloc(B);
         counts_h.alloc(B);
-        for (auto& l : lane_off_h) l.alloc(B);
+        for (auto& l : lane_row_h) l.alloc(B);
         rle_hard_h.alloc(1);
         ovf_hb.alloc(1);
         ovf_hb.p[0] = 0;
@@ -450,8 +453,8 @@ struct cpd_graph {
 struct cpd_rows {
     int device = 0;
     uint32_t nrows = 0;
-    uint64_t total = 0;
-    hipEvent_t done = nullptr;  // after the last emit into `runs` (emit overlap)
+    uint64_t total = 0;         // runs of all rows
+    hipEvent_t done = nullptr;  // after the last emit into `moves` (emit overlap)
     void wait() const {
         if (done) HIP_CHECK(hipEventSynchronize(done));
     }
@@ -463,9 +466,29 @@ struct cpd_rows {
     }
     std::vector<uint32_t> targets;   // node ids, row order
     std::vector<uint32_t> lanes;     // batch lane of each row
-    std::vector<uint64_t> offsets;   // host copy, nrows+1
-    DevBuf<uint32_t> runs;
+    std::vector<uint64_t> offsets;   // run offsets (host), nrows+1
+    // The rows in their compact form: 4-bit move tables, wpr = npad / 8 words
+    // per row (rle_moves) — the RLE row expanded, 5x smaller than its runs on
+    // the bench graphs.  Run words are decoded from them on demand
+    // (moves_runs, at `off`).
+    uint32_t n = 0, wpr = 0;
+    DevBuf<uint32_t> moves;
     DevBuf<uint64_t> off;
+    // device staging for decoded runs, one buffer per concurrent exporter
+    // (make_cpd_auto's writer threads), kept until the rows are freed
+    mutable std::mutex stage_mu;
+    mutable std::vector<std::unique_ptr<DevBuf<uint32_t>>> stages;
+    std::unique_ptr<DevBuf<uint32_t>> acquire_stage() const {
+        std::lock_guard<std::mutex> l(stage_mu);
+        if (stages.empty()) return std::make_unique<DevBuf<uint32_t>>();
+        auto b = std::move(stages.back());
+        stages.pop_back();
+        return b;
+    }
+    void release_stage(std::unique_ptr<DevBuf<uint32_t>> b) const {
+        std::lock_guard<std::mutex> l(stage_mu);
+        stages.push_back(std::move(b));
+    }
 };
 
 // A table-search index: nrows rows (row i = target row_targets[i]) that arrive
@@ -544,6 +567,20 @@ bool env_on(const char* name) {
     const char* e = std::getenv(name);
     return !(e && *e == '0');
 }
+
+// One non-blocking stream per (host thread, device), kept for the thread's
+// lifetime: exports from several host threads never queue behind a build's
+// stream or each other.
+hipStream_t thread_stream(int device) {
+    thread_local std::vector<hipStream_t> streams;
+    if (streams.size() <= (size_t)device) streams.resize(device + 1, nullptr);
+    hipStream_t& st = streams[device];
+    if (!st) HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    return st;
+}
+
+// Runs decoded per export piece (a longer row alone): 256 MB of staging.
+constexpr uint64_t kDecodeRuns = 64ull << 20;
 
 void require_device() {
     int count = 0;
@@ -1207,7 +1244,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     const uint32_t npad = g->npad;
     const double fm_row = g->fmb / 8.0 * npad;  // first-move bytes per row
     // + per 32-column segment a 4-B entry state and a 1-B count (fmb == 4)
-    const double st_row = g->fmb == 4 ? 5.0 * npad / 32.0 : 0.0;
+    const double st_row = 5.0 * npad / 32.0;
     const bool narrow = g->narrow;
     launch_down_fm(g, k, narrow, fm, slot);
     const double t1 = now_seconds();
@@ -1270,44 +1307,36 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         narrow_decide(g);
     }
     const double t2 = now_seconds();
-    // row offsets for this batch in the caller's order, appended after
-    // r->total; counts[] and the emit kernel's offsets are per lane
-    std::vector<uint64_t> off(k + 1), lane_off(k);
+    // run offsets in the caller's order, appended after r->total (counts[]
+    // are per lane); the batch's rows become table rows r->nrows + i, written
+    // by lane pos_of[i]
+    std::vector<uint64_t> off(k + 1);
     off[0] = r->total;
     const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
+    uint32_t* lrow = g->lane_row_h[x].p;
     for (uint32_t i = 0; i < k; ++i) {
         const uint32_t p = pos_of[i];
-        lane_off[p] = off[i];
+        lrow[p] = r->nrows + i;
         off[i + 1] = off[i] + counts[p];
     }
-    uint64_t new_total = off[k];
-    if (new_total > r->runs.n) {  // grow, preserving the rows already built
-        g->drain_emits();  // an earlier batch's emit may still write the old buffer
-        // 25% headroom: batches differ by a few runs, and re-allocating tens of
-        // GB costs ~1 s, so a reused buffer must not grow again per batch
-        size_t want = std::max<size_t>(new_total + new_total / 4, r->runs.n + r->runs.n / 2);
-        uint32_t* np = nullptr;
-        HIP_CHECK(hipMalloc(&np, std::max<size_t>(want, 1) * sizeof(uint32_t)));
-        if (r->total)
-            HIP_CHECK(hipMemcpyAsync(np, r->runs.p, r->total * sizeof(uint32_t),
-                                     hipMemcpyDeviceToDevice, g->stream));
-        HIP_CHECK(hipStreamSynchronize(g->stream));
-        r->runs.release();
-        r->runs.p = np;
-        r->runs.n = want;
-    }
+    const uint64_t new_total = off[k];
+    CPD_REQUIRE(r->moves.n >= (size_t)(r->nrows + k) * g->wpr(), CPD_E_ARG,
+                "rows: move table capacity");
     const double t3 = now_seconds();
     // the emit: on estream (the next batch's sweeps start meanwhile on
     // stream), or in line when overlap is off; everything it reads came from
     // `stream`, which the count sync above has drained.  (Deferring it until
     // the next batch's up-sweep is done, so that it overlaps the down-sweep
-    // instead, measured 288.5k rows/s against 293.6k: round 2.)
+    // instead, measured 288.5k rows/s against 293.6k: round 2, run-word emit.)
     hipStream_t es = g->async ? g->estream : g->stream;
-    std::copy(lane_off.begin(), lane_off.end(), g->lane_off_h[x].p);
-    g->row_offx[x].upload(g->lane_off_h[x].p, k, es);
-    double ebytes = (fm_row + st_row) * k + 8.0 * k + 4.0 * (double)(new_total - r->total);
-    g->timed("rle_emit", ebytes, [&] {
-        launch_rle_emit(fm, g->fmb, npad, k, g->row_offx[x].p, r->runs.p, rst, rrc, es);
+    HIP_CHECK(hipMemcpyAsync(g->lane_rowx[x].p, lrow, k * sizeof(uint32_t), hipMemcpyHostToDevice,
+                             es));
+    // per row: the sets (fm_row), the segment states (4 B per 32 columns;
+    // the run counts are read only where the look-ahead needs them), the
+    // table (npad / 2)
+    const double ebytes = (fm_row + 4.0 * npad / 32.0 + 0.5 * npad) * k + 4.0 * k;
+    g->timed("rle_moves", ebytes, [&] {
+        launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, r->moves.p, es);
     });
     if (!r->done) HIP_CHECK(hipEventCreateWithFlags(&r->done, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(r->done, es));
@@ -1318,11 +1347,10 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     g->sync();
     if (trace_on())
         std::fprintf(stderr,
-                     "[cpd] batch %u rows: launch sweeps+fm %.2f ms, to counts %.2f ms, grow %.2f "
-                     "ms, emit %.2f ms, runs %llu (cap %zu)\n",
+                     "[cpd] batch %u rows: launch sweeps+fm %.2f ms, to counts %.2f ms, offsets "
+                     "%.2f ms, emit %.2f ms, runs %llu\n",
                      k, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3,
-                     (now_seconds() - t3) * 1e3, (unsigned long long)(new_total - r->total),
-                     r->runs.n);
+                     (now_seconds() - t3) * 1e3, (unsigned long long)(new_total - r->total));
     r->offsets.insert(r->offsets.end(), off.begin() + 1, off.end());
     r->targets.insert(r->targets.end(), targets, targets + k);
     r->lanes.insert(r->lanes.end(), pos_of.begin(), pos_of.begin() + k);
@@ -1349,6 +1377,12 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         r->targets.clear();
         r->lanes.clear();
         r->offsets.assign(1, 0);
+        r->n = g->n;
+        r->wpr = g->wpr();
+        if (r->moves.n < (size_t)ntargets * r->wpr) {
+            r->wait();  // an earlier build's emit may still write the old table
+            r->moves.alloc((size_t)ntargets * r->wpr);
+        }
         for (uint32_t b = 0; b < ntargets; b += g->B) {
             uint32_t k = std::min(g->B, ntargets - b);
             const uint32_t* next = nullptr;
@@ -1396,14 +1430,7 @@ int cpd_rows_wait(const cpd_rows* r) {
 }
 
 int cpd_rows_export(const cpd_rows* r, uint64_t* offsets, uint32_t* runs) {
-    return guarded([&] {
-        CPD_REQUIRE(r, CPD_E_ARG, "null rows");
-        HIP_CHECK(hipSetDevice(r->device));
-        r->wait();
-        if (offsets) std::memcpy(offsets, r->offsets.data(), (r->nrows + 1) * sizeof(uint64_t));
-        if (runs && r->total)
-            HIP_CHECK(hipMemcpy(runs, r->runs.p, r->total * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    });
+    return cpd_rows_export_range(r, 0, r ? r->nrows : 0, offsets, runs);
 }
 
 int cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count, uint64_t* offsets,
@@ -1418,14 +1445,47 @@ int cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count, uin
         if (!runs || end == base) return;
         HIP_CHECK(hipSetDevice(r->device));
         r->wait();
-        // one non-blocking stream per (host thread, device), kept for the
-        // thread's lifetime: exports never queue behind a build's stream
-        thread_local std::vector<hipStream_t> streams;
-        if (streams.size() <= (size_t)r->device) streams.resize(r->device + 1, nullptr);
-        hipStream_t& st = streams[r->device];
-        if (!st) HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-        HIP_CHECK(hipMemcpyAsync(runs, r->runs.p + base, (end - base) * sizeof(uint32_t),
-                                 hipMemcpyDeviceToHost, st));
+        hipStream_t st = thread_stream(r->device);
+        // decode piece by piece (<= kDecodeRuns runs, a longer row alone) into
+        // a staging buffer of the rows' pool, then copy out
+        auto stage = r->acquire_stage();
+        for (uint32_t p0 = first; p0 < first + count;) {
+            uint32_t p1 = p0 + 1;
+            while (p1 < first + count && r->offsets[p1 + 1] - r->offsets[p0] <= kDecodeRuns) ++p1;
+            const uint64_t nr = r->offsets[p1] - r->offsets[p0];
+            stage->alloc(std::max<uint64_t>(nr, std::min<uint64_t>(end - base, kDecodeRuns)));
+            launch_moves_runs(r->moves.p + (size_t)p0 * r->wpr, r->wpr, r->n, p1 - p0,
+                              r->off.p + p0, r->offsets[p0], stage->p, st);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(runs + (r->offsets[p0] - base), stage->p, nr * sizeof(uint32_t),
+                                     hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            p0 = p1;
+        }
+        r->release_stage(std::move(stage));
+    });
+}
+
+int cpd_rows_move_words(const cpd_rows* r, uint32_t* words) {
+    return guarded([&] {
+        CPD_REQUIRE(r && words, CPD_E_ARG, "null argument");
+        *words = (r->n + 7u) / 8u;
+    });
+}
+
+int cpd_rows_export_moves(const cpd_rows* r, uint32_t first, uint32_t count, uint32_t* moves) {
+    return guarded([&] {
+        CPD_REQUIRE(r && (moves || count == 0), CPD_E_ARG, "null argument");
+        CPD_REQUIRE(first <= r->nrows && count <= r->nrows - first, CPD_E_ARG,
+                    "export range: rows out of range");
+        if (!count) return;
+        HIP_CHECK(hipSetDevice(r->device));
+        r->wait();
+        hipStream_t st = thread_stream(r->device);
+        const size_t w = (r->n + 7u) / 8u;  // the compact row: ceil(n / 8) words
+        HIP_CHECK(hipMemcpy2DAsync(moves, w * sizeof(uint32_t), r->moves.p + (size_t)first * r->wpr,
+                                   (size_t)r->wpr * sizeof(uint32_t), w * sizeof(uint32_t), count,
+                                   hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
     });
 }
@@ -1690,7 +1750,10 @@ void append_host(cpd_index* ix, uint32_t count, const uint64_t* offsets, const u
     }
 }
 
-// Append every row of a device-built cpd_rows (no host round trip).
+// Append every row of a device-built cpd_rows (no host round trip): the
+// move tables are copied as they are into a dense index, decoded into run
+// words for an RLE one (and, for an index created from these rows whose
+// AUTO mode resolves to dense, copied too).
 void append_built(cpd_index* ix, const cpd_rows* r) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(r->device == g->device, CPD_E_ARG, "index: rows live on another device");
@@ -1705,23 +1768,80 @@ void append_built(cpd_index* ix, const cpd_rows* r) {
                     "index: built row " + std::to_string(i) + " (target " +
                         std::to_string(r->targets[i]) + ") is not the declared row " +
                         std::to_string(ix->added + i));
+    CPD_REQUIRE(r->wpr == g->wpr(), CPD_E_ARG, "index: rows built for another graph");
+    const size_t wpr = g->wpr();
+    if (ix->dense.p && (ix->stream_dense || !ix->keep_rle || ix->dense_ready))
+        HIP_CHECK(hipMemcpyAsync(ix->dense.p + (size_t)ix->added * wpr, r->moves.p,
+                                 (size_t)r->nrows * wpr * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                 g->stream));
     if (ix->keep_rle) {
         CPD_REQUIRE(ix->total + r->total <= ix->cap, CPD_E_ARG,
                     "index: more runs than the index was created for");
         std::vector<uint64_t> o(r->nrows + 1);
         for (uint32_t i = 0; i <= r->nrows; ++i) o[i] = ix->total + r->offsets[i];
-        HIP_CHECK(hipMemcpyAsync(ix->runs.p + ix->total, r->runs.p, r->total * sizeof(uint32_t),
-                                 hipMemcpyDeviceToDevice, g->stream));
+        g->timed("moves_runs", 0.5 * (double)g->npad * r->nrows + 4.0 * (double)r->total, [&] {
+            launch_moves_runs(r->moves.p, r->wpr, r->n, r->nrows, r->off.p, 0,
+                              ix->runs.p + ix->total, g->stream);
+        });
         HIP_CHECK(hipMemcpyAsync(ix->off.p + ix->added, o.data(), o.size() * sizeof(uint64_t),
                                  hipMemcpyHostToDevice, g->stream));
         HIP_CHECK(hipStreamSynchronize(g->stream));
         ix->offsets.insert(ix->offsets.end(), o.begin() + 1, o.end());
         ix->total += r->total;
-    } else {
-        expand_into(ix, r->off.p, r->runs.p, r->offsets.data(), r->nrows, r->total, ix->added);
-        g->sync();
     }
+    g->sync();
     ix->added += r->nrows;
+}
+
+// Append `count` host rows in the compact form (ceil(n / 8) words each).  A
+// dense index takes them as they are (one 2-D copy to the table stride); an
+// RLE index decodes them on the GPU, counting first.  No format check is
+// needed: every nibble is some move, and a move naming no out-edge of its
+// column stops the walk (unfinished) like the oracle's.
+void append_moves(cpd_index* ix, uint32_t count, const uint32_t* moves) {
+    cpd_graph* g = ix->g;
+    CPD_REQUIRE(count <= ix->nrows - ix->added, CPD_E_ARG, "index: more rows than declared");
+    if (!count) return;
+    CPD_REQUIRE(moves, CPD_E_ARG, "index: null move rows");
+    const size_t w = (g->n + 7u) / 8u, wpr = g->wpr();
+    hipStream_t s = g->stream;
+    if (!ix->keep_rle) {
+        HIP_CHECK(hipMemcpy2DAsync(ix->dense.p + (size_t)ix->added * wpr, wpr * sizeof(uint32_t),
+                                   moves, w * sizeof(uint32_t), w * sizeof(uint32_t), count,
+                                   hipMemcpyHostToDevice, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        ix->added += count;
+        return;
+    }
+    // RLE: pieces of <= 1 GiB of tables staged at the table stride
+    const uint32_t piece = (uint32_t)std::max<size_t>(1, ((size_t)1 << 28) / wpr);
+    for (uint32_t r0 = 0; r0 < count; r0 += piece) {
+        const uint32_t nr = std::min(piece, count - r0);
+        ix->stage.alloc((size_t)std::min(piece, count) * wpr);
+        ix->flag.alloc(std::max<size_t>(ix->flag.n, (size_t)std::min(piece, count)));
+        HIP_CHECK(hipMemcpy2DAsync(ix->stage.p, wpr * sizeof(uint32_t), moves + (size_t)r0 * w,
+                                   w * sizeof(uint32_t), w * sizeof(uint32_t), nr,
+                                   hipMemcpyHostToDevice, s));
+        launch_moves_count(ix->stage.p, (uint32_t)wpr, g->n, nr, ix->flag.p, s);
+        HIP_CHECK(hipGetLastError());
+        std::vector<uint32_t> cnt(nr);
+        HIP_CHECK(hipMemcpyAsync(cnt.data(), ix->flag.p, nr * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        std::vector<uint64_t> o(nr + 1);
+        o[0] = ix->total;
+        for (uint32_t i = 0; i < nr; ++i) o[i + 1] = o[i] + cnt[i];
+        CPD_REQUIRE(o[nr] <= ix->cap, CPD_E_ARG, "index: more runs than the index was created for");
+        HIP_CHECK(hipMemcpyAsync(ix->off.p + ix->added, o.data(), o.size() * sizeof(uint64_t),
+                                 hipMemcpyHostToDevice, s));
+        launch_moves_runs(ix->stage.p, (uint32_t)wpr, g->n, nr, ix->off.p + ix->added, 0,
+                          ix->runs.p, s);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(s));
+        ix->offsets.insert(ix->offsets.end(), o.begin() + 1, o.end());
+        ix->total = o[nr];
+        ix->added += nr;
+    }
 }
 
 }  // namespace
@@ -1750,6 +1870,11 @@ int cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out) {
         auto ix = index_init(g, r->targets.data(), r->nrows);
         ix->declared = r->total;
         index_keep_rle(ix.get(), r->total);
+        if (ix->use_dense()) {  // AUTO resolves dense: the rows' tables, copied
+            CPD_REQUIRE(g->npad / kFmTile < 65536u, CPD_E_RANGE, "graph too large for dense tables");
+            ix->dense.alloc((size_t)ix->nrows * g->wpr());
+            ix->dense_ready = true;
+        }
         append_built(ix.get(), r);
         *out = ix.release();
     });
@@ -1779,6 +1904,14 @@ int cpd_index_append_rows(cpd_index* ix, uint32_t count, const uint64_t* offsets
         CPD_REQUIRE(ix, CPD_E_ARG, "index: null argument");
         ix->g->select();
         append_host(ix, count, offsets, runs);
+    });
+}
+
+int cpd_index_append_moves(cpd_index* ix, uint32_t count, const uint32_t* moves) {
+    return guarded([&] {
+        CPD_REQUIRE(ix, CPD_E_ARG, "index: null argument");
+        ix->g->select();
+        append_moves(ix, count, moves);
     });
 }
 

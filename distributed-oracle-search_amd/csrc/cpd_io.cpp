@@ -71,6 +71,7 @@ uint32_t to_u32(int64_t v, const std::string& what) {
 
 const char kBucketMagic[8] = {'D', 'O', 'S', 'C', 'P', 'D', '0', '1'};
 const char kOrderMagic[8] = {'D', 'O', 'S', 'O', 'R', 'D', '0', '1'};
+const char kMoveBucketMagic[8] = {'D', 'O', 'S', 'C', 'P', 'D', '0', '2'};
 
 }  // namespace
 
@@ -423,6 +424,139 @@ CpdBucket read_bucket(const std::string& path) {
     if (!f) throw Error(CPD_E_IO, path + ": truncated body");
     if (b.offsets[0] != 0 || b.offsets[nrows] != total) throw Error(CPD_E_IO, path + ": bad offsets");
     return b;
+}
+
+int bucket_format(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw Error(CPD_E_IO, "cannot open " + path);
+    char magic[8];
+    f.read(magic, 8);
+    if (f && std::memcmp(magic, kBucketMagic, 8) == 0) return 1;
+    if (f && std::memcmp(magic, kMoveBucketMagic, 8) == 0) return 2;
+    throw Error(CPD_E_IO, path + ": not a CPD bucket file");
+}
+
+// DOSCPD02 layout: magic 8 | 8 x u32 | total u64 | fingerprint u64 (= 56 B) |
+// targets | counts | pad | rows from rows_offset()
+static constexpr uint64_t kMoveHeader = 8 + 32 + 8 + 8;
+static constexpr uint64_t kMoveRowsAlign = 4096;
+
+uint64_t MoveBucket::rows_offset() const {
+    const uint64_t end = kMoveHeader + 8ull * targets.size();
+    return (end + kMoveRowsAlign - 1) / kMoveRowsAlign * kMoveRowsAlign;
+}
+
+MoveBucketFile::MoveBucketFile(const std::string& path, const MoveBucket& b)
+    : path_(path), tmp_(path + ".tmp"), nrows_((uint32_t)b.targets.size()), words_(b.words),
+      rows_off_(b.rows_offset()) {
+    if (b.words != (b.n + 7u) / 8u) throw Error(CPD_E_ARG, "move bucket: words != ceil(n / 8)");
+    fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd_ < 0) throw Error(CPD_E_IO, "cannot write " + tmp_);
+    std::vector<char> h(rows_off_, 0);  // header, targets, zero counts, pad
+    std::memcpy(h.data(), kMoveBucketMagic, 8);
+    const uint32_t h32[8] = {b.n, nrows_, b.bid, b.method, b.key, b.maxworker, b.words, 0u};
+    std::memcpy(h.data() + 8, h32, sizeof h32);
+    std::memcpy(h.data() + 48, &b.fingerprint, 8);  // total (h + 40) is written by close()
+    std::memcpy(h.data() + kMoveHeader, b.targets.data(), 4ull * nrows_);
+    pwrite_all(h.data(), h.size(), 0);
+}
+
+MoveBucketFile::~MoveBucketFile() {
+    if (fd_ >= 0) {
+        ::close(fd_);
+        ::unlink(tmp_.c_str());
+    }
+}
+
+void MoveBucketFile::pwrite_all(const void* p, size_t bytes, uint64_t pos) {
+    const char* c = static_cast<const char*>(p);
+    while (bytes > 0) {
+        const ssize_t k = ::pwrite(fd_, c, std::min<size_t>(bytes, size_t(1) << 30), (off_t)pos);
+        if (k <= 0) throw Error(CPD_E_IO, "write failed: " + tmp_);
+        c += k;
+        pos += (uint64_t)k;
+        bytes -= (size_t)k;
+    }
+}
+
+void MoveBucketFile::write_counts(uint32_t first_row, const uint32_t* counts, uint32_t count) {
+    if (first_row > nrows_ || count > nrows_ - first_row)
+        throw Error(CPD_E_ARG, "bucket counts out of range: " + tmp_);
+    pwrite_all(counts, 4ull * count, kMoveHeader + 4ull * nrows_ + 4ull * first_row);
+}
+
+void MoveBucketFile::write_rows(uint32_t first_row, const uint32_t* rows, uint32_t count) {
+    if (first_row > nrows_ || count > nrows_ - first_row)
+        throw Error(CPD_E_ARG, "bucket rows out of range: " + tmp_);
+    pwrite_all(rows, 4ull * words_ * count, rows_off_ + 4ull * words_ * first_row);
+}
+
+void MoveBucketFile::close(uint64_t total_runs) {
+    pwrite_all(&total_runs, 8, 40);
+    const int fd = fd_;
+    fd_ = -1;
+    if (::close(fd) != 0) throw Error(CPD_E_IO, "close failed: " + tmp_);
+    if (std::rename(tmp_.c_str(), path_.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path_);
+}
+
+MoveBucket read_move_bucket_head(const std::string& path) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f) throw Error(CPD_E_IO, "cannot open " + path);
+    const uint64_t size = (uint64_t)f.tellg();
+    f.seekg(0);
+    char magic[8];
+    f.read(magic, 8);
+    if (!f || std::memcmp(magic, kMoveBucketMagic, 8) != 0)
+        throw Error(CPD_E_IO, path + ": not a compact (DOSCPD02) CPD bucket file");
+    MoveBucket b;
+    uint32_t h32[8];
+    f.read(reinterpret_cast<char*>(h32), sizeof h32);
+    f.read(reinterpret_cast<char*>(&b.total_runs), 8);
+    f.read(reinterpret_cast<char*>(&b.fingerprint), 8);
+    if (!f) throw Error(CPD_E_IO, path + ": truncated header");
+    b.n = h32[0];
+    const uint32_t nrows = h32[1];
+    b.bid = h32[2];
+    b.method = h32[3];
+    b.key = h32[4];
+    b.maxworker = h32[5];
+    b.words = h32[6];
+    if (b.words != (b.n + 7u) / 8u) throw Error(CPD_E_IO, path + ": row width does not match n");
+    b.targets.resize(nrows);
+    b.counts.resize(nrows);
+    if (size != b.rows_offset() + 4ull * b.words * nrows)
+        throw Error(CPD_E_IO, path + ": size does not match its header");
+    f.read(reinterpret_cast<char*>(b.targets.data()), nrows * 4ull);
+    f.read(reinterpret_cast<char*>(b.counts.data()), nrows * 4ull);
+    if (!f) throw Error(CPD_E_IO, path + ": truncated body");
+    uint64_t tot = 0;
+    for (uint32_t c : b.counts) {
+        if (c == 0) throw Error(CPD_E_IO, path + ": a row without runs");
+        tot += c;
+    }
+    if (tot != b.total_runs) throw Error(CPD_E_IO, path + ": run counts do not add up");
+    return b;
+}
+
+void read_move_bucket_rows(const std::string& path, const MoveBucket& head, uint32_t first,
+                           uint32_t count, uint32_t* out) {
+    if ((uint64_t)first + count > head.targets.size()) throw Error(CPD_E_ARG, path + ": rows out of range");
+    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) throw Error(CPD_E_IO, "cannot open " + path);
+    uint64_t pos = head.rows_offset() + 4ull * head.words * first;
+    char* c = reinterpret_cast<char*>(out);
+    uint64_t left = 4ull * head.words * count;
+    while (left) {
+        const ssize_t k = ::pread(fd, c, std::min<uint64_t>(left, 1ull << 30), (off_t)pos);
+        if (k <= 0) {
+            ::close(fd);
+            throw Error(CPD_E_IO, path + ": truncated rows");
+        }
+        c += k;
+        pos += (uint64_t)k;
+        left -= (uint64_t)k;
+    }
+    ::close(fd);
 }
 
 void write_order(const std::string& path, uint64_t fp, const std::vector<uint32_t>& order) {

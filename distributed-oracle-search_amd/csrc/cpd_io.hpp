@@ -10,6 +10,9 @@
 //   query  "{n}\n" then n lines "s t" (process_query.send_queries, :93-96).
 //   .cpd   one file per partition bucket (README.md:86-93 "one or more CPDs"),
 //          our own layout == the HBM layout, so a load is one read + one copy.
+//          DOSCPD02 (default): the rows in their compact form, a 4-bit move
+//          per column (cpd_rows_export_moves), n/2 bytes per row; DOSCPD01
+//          (make_cpd_auto --format rle): RLE run words, 4 B per run.
 //   .order the DFS column order shared by every bucket of a graph.
 #pragma once
 #include <cstdint>
@@ -88,6 +91,48 @@ CpdBucket read_bucket(const std::string& path);
 CpdBucket read_bucket_head(const std::string& path);
 void read_bucket_runs(const std::string& path, const CpdBucket& head, uint64_t first,
                       uint64_t count, uint32_t* out);
+// Which layout a bucket file has: 1 (DOSCPD01, run words) or 2 (DOSCPD02,
+// move tables); throws CPD_E_IO for anything else.
+int bucket_format(const std::string& path);
+
+// DOSCPD02 — compact bucket: the rows as 4-bit move tables (bijective with
+// the greedy RLE rows; cpd_api.h cpd_rows_export_moves):
+//   magic "DOSCPD02" | n nrows bid method key maxworker words pad (8 x u32) |
+//   total_runs u64 | fingerprint u64 | targets u32[nrows] |
+//   runs u32[nrows] (run count of each row) | zero pad to a 4-KiB boundary |
+//   rows u32[nrows][words], words = ceil(n / 8)
+struct MoveBucket {
+    uint32_t n = 0, bid = 0, method = 0, key = 0, maxworker = 0, words = 0;
+    uint64_t fingerprint = 0, total_runs = 0;
+    std::vector<uint32_t> targets, counts;
+    uint64_t rows_offset() const;
+};
+// Written in pieces from several threads, in any order (positional writes);
+// close() writes the run total and renames the .tmp into place.
+class MoveBucketFile {
+public:
+    // `b` supplies the header fields and targets (counts / total unused)
+    MoveBucketFile(const std::string& path, const MoveBucket& b);
+    ~MoveBucketFile();  // without close(): the .tmp is removed
+    MoveBucketFile(const MoveBucketFile&) = delete;
+    MoveBucketFile& operator=(const MoveBucketFile&) = delete;
+    void write_counts(uint32_t first_row, const uint32_t* counts, uint32_t count);
+    void write_rows(uint32_t first_row, const uint32_t* rows, uint32_t count);
+    void close(uint64_t total_runs);
+
+private:
+    void pwrite_all(const void* p, size_t bytes, uint64_t pos);
+    std::string path_, tmp_;
+    int fd_ = -1;
+    uint32_t nrows_ = 0, words_ = 0;
+    uint64_t rows_off_ = 0;
+};
+// Header, targets and counts (the file size checked against the header);
+// rows [first, first + count) then read by position.
+MoveBucket read_move_bucket_head(const std::string& path);
+void read_move_bucket_rows(const std::string& path, const MoveBucket& head, uint32_t first,
+                           uint32_t count, uint32_t* out);
+
 void write_order(const std::string& path, uint64_t fingerprint, const std::vector<uint32_t>& order);
 std::vector<uint32_t> read_order(const std::string& path, uint64_t fingerprint);
 

@@ -8,7 +8,9 @@
 //                          FMB = max(4, slots of the packed adjacency) >= the
 //                          max out-degree: 4 bits on road lattices, a quarter
 //                          of a u16; columns >= n are padded with the wildcard
-//   runs  u32 words, rows back to back at off[row] (count pass, then emit)
+//   moves [row][npad/8] u32  the rows as 4-bit move tables (rle_moves); RLE
+//                          words (column << 4 | move) are decoded from them
+//                          on demand (moves_runs)
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -1089,18 +1091,14 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
 // [U]: keep S = AND of the current run's first-move sets; a column that would
 // empty S ends the run — word (head << 4 | lowest bit of S) — and starts a new
 // one at that column).  v holds the segment's 32 FMB-bit sets, 32/FMB per word.
-template <bool EMIT, int FMB>
+template <int FMB>
 __device__ __forceinline__ void seg_pass(const uint32_t (&v)[FmFmt<FMB>::kWords], uint32_t c0,
-                                         uint32_t& h, uint32_t& S, uint32_t& cnt,
-                                         uint32_t* stage) {
+                                         uint32_t& h, uint32_t& S, uint32_t& cnt) {
     using F = FmFmt<FMB>;
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         const uint32_t f = (v[k / F::kPer] >> (FMB * (k % F::kPer))) & F::kAll;
         const bool brk = (S & f) == 0u;
-        if (EMIT) {
-            if (brk) stage[cnt] = (h << 4) | (uint32_t)__builtin_ctz(S);
-        }
         cnt += brk ? 1u : 0u;
         h = brk ? c0 + (uint32_t)k : h;
         S = brk ? f : (S & f);
@@ -1114,39 +1112,39 @@ __device__ __forceinline__ uint32_t set_at(const uint32_t (&v)[FmFmt<FMB>::kWord
 }
 
 // Per-(row, 32-column segment) RLE entry states, written by the count pass
-// and read by the emit pass so that it needs no speculation of its own
-// (4-bit sets: the state (head, S) packs into head << 4 | S):
-//   st[row * nseg + seg] = state of the greedy scan entering the segment,
-//   rc[row * nseg + seg] = runs that end inside the segment (<= 32).
-// st == nullptr: not kept (wider sets); the emit pass then speculates too.
+// and read by the move-table emit (rle_moves), which needs no speculation of
+// its own:
+//   st[row * nseg + seg] = state of the greedy scan entering the segment:
+//                          head << 4 | S for 4-bit sets (rle_fix compares
+//                          whole states), S alone for wider ones,
+//   rc[row * nseg + seg] = runs that end inside the segment (<= 32) = the
+//                          columns of the segment where a new run starts.
 struct RleState {
     uint32_t* st;
     uint8_t* rc;
 };
 
-// Greedy RLE, one row per wave, 2048-column tiles (lane l owns columns
+// Greedy RLE count, one row per wave, 2048-column tiles (lane l owns columns
 // 32l..32l+31 of the tile).  The scan is sequential by definition, so each
 // lane guesses the state entering its segment — the predecessor lane's last
 // 16 columns scanned from a fresh run: the greedy state forgets its past
 // within a few runs, so the guess is usually exact — runs its segment from
 // the guess, then re-runs from its predecessor's end state until no lane's
-// input changes (exact for any input: at most 64 rounds).  The count needs
-// the entry set only; the head matters once the states are kept or emitted.
-// COUNT: counts[row] = runs in the row (+ entry states if rs.st).  EMIT: runs
-// written at off[row], staged per tile in LDS and stored coalesced.
-template <bool EMIT, int FMB>
+// input changes (exact for any input: at most 64 rounds).  counts[row] =
+// runs in the row; the segment entry states and counts go to rs.  (The
+// chunked count rle_count_ch + rle_fix replaces this for 4-bit sets; this
+// pass serves wider sets and rows whose long runs the seam repair gives up
+// on.)
+template <int FMB>
 __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm, uint32_t npad,
                                                 uint32_t nrows, uint32_t* __restrict__ counts,
-                                                const uint64_t* __restrict__ off,
-                                                uint32_t* __restrict__ runs, RleState rs) {
+                                                RleState rs) {
     using F = FmFmt<FMB>;
     constexpr int Q = F::kWords / 4;  // 16-B loads per lane per tile
     constexpr int LB = CPD_RLE_LOOKBACK;  // lookback columns
-    __shared__ uint32_t stage_all[EMIT ? 4 * kTile : 1];
     const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     if (row >= nrows) return;
-    uint32_t* stage = stage_all + (EMIT ? (threadIdx.x >> 6) * kTile : 0);
     const uint32_t nseg = npad / kSeg;
     // this lane's 16-B pieces of the row: 4-bit rows are row-group interleaved
     // (fm4_piece), wider ones row-major; tile t is `step` pieces further on
@@ -1154,24 +1152,14 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
         FMB == 4 ? reinterpret_cast<const uint4*>(fm) + fm4_piece(row, nseg, lane)
                  : reinterpret_cast<const uint4*>(fm + (size_t)row * (npad / F::kPer)) + lane * Q;
     const size_t step = FMB == 4 ? 64u * 4u : 64u * Q;
-    uint32_t* __restrict__ out = EMIT ? runs + off[row] : nullptr;
-    // states kept: always for FMB == 4 (the host passes them), which makes
-    // the emit's speculation code dead and frees its registers
-    const bool keep = FMB == 4 || rs.st != nullptr;
-    const bool use_states = EMIT && keep;         // emit from the kept states
-    const bool track_h = EMIT || keep;
+    const bool keep = rs.st != nullptr;
+    const bool track_h = keep && FMB == 4;  // heads matter only in packed 4-bit states
     uint32_t carry_h = 0, carry_S = F::kAll, total = 0;
     const uint32_t ntiles = npad / kTile;
-    // tile t's segment of this lane (and its kept state), prefetched one tile ahead
-    uint4 nx[Q];
-    uint32_t nst = 0, nrc = 0;
     const size_t sbase = (size_t)row * nseg + lane;
+    uint4 nx[Q];  // tile t's segment of this lane, prefetched one tile ahead
 #pragma unroll
     for (int q = 0; q < Q; ++q) nx[q] = src[q];
-    if (use_states) {
-        nst = rs.st[sbase];
-        nrc = rs.rc[sbase];
-    }
     for (uint32_t t = 0; t < ntiles; ++t) {
         uint32_t v[F::kWords];
 #pragma unroll
@@ -1181,96 +1169,288 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
             v[4 * q + 2] = nx[q].z;
             v[4 * q + 3] = nx[q].w;
         }
-        const uint32_t cst = nst, crc = nrc;
         if (t + 1 < ntiles) {
 #pragma unroll
             for (int q = 0; q < Q; ++q) nx[q] = src[(size_t)(t + 1) * step + q];
-            if (use_states) {
-                nst = rs.st[sbase + (size_t)(t + 1) * 64u];
-                nrc = rs.rc[sbase + (size_t)(t + 1) * 64u];
-            }
         }
         const uint32_t c0 = t * kTile + lane * kSeg;
-        uint32_t in_h, in_S, eh, eS, cnt;
-        if (use_states) {
-            in_h = cst >> 4;
-            in_S = cst & 0xFu;
-            cnt = crc;
-        } else {
-            // guess: the predecessor's last LB columns from a fresh run
-            constexpr int PW = LB / F::kPer;  // words holding those columns
-            static_assert(LB % F::kPer == 0 && PW <= F::kWords, "lookback: whole words");
-            uint32_t pv[PW];
+        // guess: the predecessor's last LB columns from a fresh run
+        constexpr int PW = LB / F::kPer;  // words holding those columns
+        static_assert(LB % F::kPer == 0 && PW <= F::kWords, "lookback: whole words");
+        uint32_t pv[PW];
 #pragma unroll
-            for (int i = 0; i < PW; ++i) pv[i] = __shfl_up(v[F::kWords - PW + i], 1, 64);
-            uint32_t gh = c0 - LB, gS = F::kAll;
+        for (int i = 0; i < PW; ++i) pv[i] = __shfl_up(v[F::kWords - PW + i], 1, 64);
+        uint32_t gh = c0 - LB, gS = F::kAll;
 #pragma unroll
-            for (int k = 0; k < LB; ++k) {
-                const uint32_t f = (pv[k / F::kPer] >> (FMB * (k % F::kPer))) & F::kAll;
-                const bool brk = (gS & f) == 0u;
-                gh = brk ? c0 - LB + (uint32_t)k : gh;
-                gS = brk ? f : (gS & f);
+        for (int k = 0; k < LB; ++k) {
+            const uint32_t f = (pv[k / F::kPer] >> (FMB * (k % F::kPer))) & F::kAll;
+            const bool brk = (gS & f) == 0u;
+            gh = brk ? c0 - LB + (uint32_t)k : gh;
+            gS = brk ? f : (gS & f);
+        }
+        uint32_t in_h = lane == 0 ? carry_h : gh;
+        uint32_t in_S = lane == 0 ? carry_S : gS;
+        uint32_t eh = in_h, eS = in_S, cnt = 0;
+        seg_pass<FMB>(v, c0, eh, eS, cnt);
+        for (int round = 0; round < 64; ++round) {
+            uint32_t nh = __shfl_up(eh, 1, 64), nS = __shfl_up(eS, 1, 64);
+            if (lane == 0) {
+                nh = carry_h;
+                nS = carry_S;
             }
-            in_h = lane == 0 ? carry_h : gh;
-            in_S = lane == 0 ? carry_S : gS;
-            eh = in_h;
-            eS = in_S;
-            cnt = 0;
-            seg_pass<false, FMB>(v, c0, eh, eS, cnt, nullptr);
-            for (int round = 0; round < 64; ++round) {
-                uint32_t nh = __shfl_up(eh, 1, 64), nS = __shfl_up(eS, 1, 64);
-                if (lane == 0) {
-                    nh = carry_h;
-                    nS = carry_S;
-                }
-                const bool need = nS != in_S || (track_h && nh != in_h);
-                if (!__any(need)) break;
-                if (need) {
-                    in_h = nh;
-                    in_S = nS;
-                    eh = nh;
-                    eS = nS;
-                    cnt = 0;
-                    seg_pass<false, FMB>(v, c0, eh, eS, cnt, nullptr);
-                }
-            }
-            if (!EMIT && keep) {  // coalesced: 64 lanes x 4 B + 64 x 1 B per tile
-                rs.st[sbase + (size_t)t * 64u] = (in_h << 4) | in_S;
-                rs.rc[sbase + (size_t)t * 64u] = (uint8_t)cnt;
+            const bool need = nS != in_S || (track_h && nh != in_h);
+            if (!__any(need)) break;
+            if (need) {
+                in_h = nh;
+                in_S = nS;
+                eh = nh;
+                eS = nS;
+                cnt = 0;
+                seg_pass<FMB>(v, c0, eh, eS, cnt);
             }
         }
-        // inclusive scan of per-lane run counts
+        if (keep) {  // coalesced: 64 lanes x 4 B + 64 x 1 B per tile
+            rs.st[sbase + (size_t)t * 64u] = FMB == 4 ? (in_h << 4) | in_S : in_S;
+            rs.rc[sbase + (size_t)t * 64u] = (uint8_t)cnt;
+        }
+        uint32_t sum = cnt;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        total += sum;
+        carry_h = __shfl(eh, 63, 64);
+        carry_S = __shfl(eS, 63, 64);
+    }
+    if (lane == 0) counts[row] = total + 1;  // + the final run
+}
+
+// ---------------------------------------------------------------------------
+// Compact rows: the greedy RLE row as a 4-bit move table.
+//
+// Every column of a run gets the run's move (lowest set bit of the AND of the
+// run's sets, taken where the run closes), and consecutive runs always carry
+// different moves: a run closes at column c only when S & FM(c) == 0, its move
+// lies in S and the next run's in FM(c).  So the table is the RLE row
+// expanded — n/2 bytes per row against 4 B per run (R ~ 0.62 n on the bench
+// graphs: 5x smaller) — and the runs come back exactly as
+// {0} U {c : move(c) != move(c - 1)} (moves_runs below).  Column c of a row
+// is nibble c % 8 of word c / 8: the dense table the walks read, so an index
+// takes the rows as they are.
+//
+// A column's move depends on where its run CLOSES, to its right; the scan
+// state depends on the columns to its left, which the count pass has already
+// resolved (st: every segment's entry state).  So a wave takes kMoveTiles
+// consecutive 2048-column tiles of one row and walks them right to left,
+// carrying the move of the run still open at the right edge:
+//   forward (per lane, 32 columns from the segment's entry set): the break
+//     mask and L_k = lowest bit of the running set after column k; the run
+//     entering the segment closes at its first break b, with move F = L_{b-1}
+//     (the entry set's lowest bit when b = 0);
+//   resolve (per wave): a lane's open tail run closes in the first lane to
+//     its right that has a break (that lane's F), else right of the tile
+//     (the carry);
+//   backward (per lane): column k takes the move of the run holding it.
+// The carry entering the chunk comes from a look-ahead to the first segment
+// right of it whose count rc is non-zero (one uniform segment scan); when no
+// run closes right of the chunk, the open run is the row's last, and its move
+// is the lowest bit of the set at the row's end.  One 16-B store per lane per
+// tile: a wave writes 1 KiB contiguous.
+constexpr uint32_t kMoveTiles = 16;
+
+__device__ __forceinline__ uint32_t low_bit(uint32_t S) {
+    return (uint32_t)__builtin_ctz(S | 0x8000u);  // S != 0: every set is non-empty
+}
+
+// nibble i (runtime index) of a 32-nibble value held in 4 words
+__device__ __forceinline__ uint32_t nib_at(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3,
+                                           uint32_t i) {
+    const uint32_t x = i < 16u ? (i < 8u ? w0 : w1) : (i < 24u ? w2 : w3);
+    return (x >> (4u * (i & 7u))) & 0xFu;
+}
+
+struct SegMoves {
+    uint32_t brk;   // bit k: a new run starts at column k
+    uint32_t L[4];  // nibble k: lowest set bit of the running set after column k
+    uint32_t S;     // the running set after column 31
+};
+
+template <int FMB>
+__device__ __forceinline__ SegMoves seg_moves(const uint32_t (&v)[FmFmt<FMB>::kWords],
+                                              uint32_t S) {
+    SegMoves r;
+    r.brk = 0;
+    r.L[0] = r.L[1] = r.L[2] = r.L[3] = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t f = set_at<FMB>(v, k);
+        const uint32_t T = S & f;
+        const bool b = T == 0u;
+        r.brk |= (b ? 1u : 0u) << k;
+        S = b ? f : T;
+        r.L[k >> 3] |= low_bit(S) << (4 * (k & 7));
+    }
+    r.S = S;
+    return r;
+}
+
+// move of the run entering the segment (it closes at the first break)
+__device__ __forceinline__ uint32_t seg_entry_move(const SegMoves& r, uint32_t Sin) {
+    const uint32_t b0 = (uint32_t)__builtin_ctz(r.brk | 0x80000000u);
+    return b0 == 0u ? low_bit(Sin) : nib_at(r.L[0], r.L[1], r.L[2], r.L[3], b0 - 1u);
+}
+
+template <int FMB>
+__device__ __forceinline__ void load_seg(const uint32_t* __restrict__ fm, uint32_t npad,
+                                         uint32_t row, uint32_t seg,
+                                         uint32_t (&v)[FmFmt<FMB>::kWords]) {
+    using F = FmFmt<FMB>;
+    const uint32_t nseg = npad / kSeg;
+    if (FMB == 4) {
+        const uint4 q = reinterpret_cast<const uint4*>(fm)[fm4_piece(row, nseg, seg)];
+        v[0] = q.x;
+        v[1] = q.y;
+        v[2] = q.z;
+        v[3] = q.w;
+    } else {
+        constexpr int Q = F::kWords / 4;
+        const uint4* s =
+            reinterpret_cast<const uint4*>(fm + (size_t)row * (npad / F::kPer)) + (size_t)seg * Q;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint4 x = s[q];
+            v[4 * q] = x.x;
+            v[4 * q + 1] = x.y;
+            v[4 * q + 2] = x.z;
+            v[4 * q + 3] = x.w;
+        }
+    }
+}
+
+// Batch row `brow` (fm / st / rc row) goes to table row out_row[brow].
+template <int FMB>
+__global__ __launch_bounds__(256) void rle_moves(const uint32_t* __restrict__ fm, uint32_t npad,
+                                                 uint32_t nrows, const uint32_t* __restrict__ st,
+                                                 const uint8_t* __restrict__ rc,
+                                                 const uint32_t* __restrict__ out_row,
+                                                 uint32_t* __restrict__ dense) {
+    using F = FmFmt<FMB>;
+    const uint32_t brow = blockIdx.y * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (brow >= nrows) return;  // wave-uniform
+    const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
+    const uint32_t t0 = blockIdx.x * kMoveTiles;
+    if (t0 >= ntiles) return;
+    const uint32_t t1 = min(ntiles, t0 + kMoveTiles);
+    constexpr uint32_t smask = FMB == 4 ? 0xFu : F::kAll;  // 4-bit states carry the head
+    const uint32_t* __restrict__ strow = st + (size_t)brow * nseg;
+    const uint8_t* __restrict__ rcrow = rc + (size_t)brow * nseg;
+    // carry: the move of the run open at the right edge of the tile in hand
+    uint32_t carry = 0;
+    bool have = false;  // wave-uniform
+    for (uint32_t s0 = t1 * 64u; s0 < nseg && !have; s0 += 64u) {
+        const uint64_t m = __ballot(s0 + lane < nseg && rcrow[s0 + lane] != 0);
+        if (m) {
+            const uint32_t sj = s0 + (uint32_t)__builtin_ctzll(m);
+            uint32_t v[F::kWords];
+            load_seg<FMB>(fm, npad, brow, sj, v);
+            const uint32_t Sin = strow[sj] & smask;
+            carry = seg_entry_move(seg_moves<FMB>(v, Sin), Sin);
+            have = true;
+        }
+    }
+    if (!have) {  // no run closes right of the chunk: the row's final run
+        uint32_t v[F::kWords];
+        load_seg<FMB>(fm, npad, brow, nseg - 1u, v);
+        carry = low_bit(seg_moves<FMB>(v, strow[nseg - 1u] & smask).S);
+    }
+    uint4* __restrict__ orow = reinterpret_cast<uint4*>(dense + (size_t)out_row[brow] * (npad / 8u));
+    for (uint32_t t = t1; t-- > t0;) {
+        const uint32_t seg = t * 64u + lane;
+        uint32_t v[F::kWords];
+        load_seg<FMB>(fm, npad, brow, seg, v);
+        const uint32_t Sin = strow[seg] & smask;
+        const SegMoves r = seg_moves<FMB>(v, Sin);
+        const uint32_t fl = seg_entry_move(r, Sin);
+        const uint64_t m = __ballot(r.brk != 0u);
+        const uint64_t right = lane == 63u ? 0ull : (m >> (lane + 1u)) << (lane + 1u);
+        const uint32_t j = right ? (uint32_t)__builtin_ctzll(right) : lane;
+        const uint32_t fj = (uint32_t)__shfl((int)fl, (int)j, 64);
+        uint32_t mv = right ? fj : carry;
+        uint32_t o[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 31; k >= 0; --k) {
+            o[k >> 3] |= mv << (4 * (k & 7));
+            if (k > 0 && ((r.brk >> k) & 1u)) mv = (r.L[(k - 1) >> 3] >> (4 * ((k - 1) & 7))) & 0xFu;
+        }
+        orow[(size_t)t * 64u + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
+    }
+}
+
+// Move tables -> RLE words, the inverse of rle_moves: a row's runs start at
+// column 0 and at every column whose move differs from its left neighbour's,
+// word = column << 4 | move (warthog rle_run32 [U]); columns >= n are
+// ignored.  EMIT = false: counts[r] = the row's runs; EMIT = true: the runs at
+// runs[off[r] - base].  A wave per row, 2048-column tiles left to right, runs
+// staged per tile in LDS and stored coalesced.  Row r's table at
+// dense + r * stride (stride: words, a multiple of 4).
+template <bool EMIT>
+__global__ __launch_bounds__(256) void moves_runs(const uint32_t* __restrict__ dense,
+                                                  uint32_t stride, uint32_t n, uint32_t nrows,
+                                                  const uint64_t* __restrict__ off, uint64_t base,
+                                                  uint32_t* __restrict__ runs,
+                                                  uint32_t* __restrict__ counts) {
+    __shared__ uint32_t stage_all[EMIT ? 4 * kTile : 1];
+    const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (row >= nrows) return;
+    uint32_t* stage = stage_all + (EMIT ? (threadIdx.x >> 6) * kTile : 0u);
+    const uint4* __restrict__ rowp = reinterpret_cast<const uint4*>(dense + (size_t)row * stride);
+    uint32_t* __restrict__ out = EMIT ? runs + (off[row] - base) : nullptr;
+    const uint32_t ntiles = (n + kTile - 1u) / kTile;
+    uint32_t prev = 0x10u;  // no nibble: column 0 always starts a run
+    uint32_t total = 0;
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        const uint32_t c0 = t * kTile + lane * kSeg;
+        uint4 q = make_uint4(0u, 0u, 0u, 0u);
+        if (c0 < n) q = rowp[(size_t)t * 64u + lane];
+        const uint32_t x[4] = {q.x, q.y, q.z, q.w};
+        uint32_t pl = (uint32_t)__shfl_up((int)(x[3] >> 28), 1, 64);
+        if (lane == 0) pl = prev;
+        uint32_t chg = 0;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const uint32_t mv = (x[k >> 3] >> (4 * (k & 7))) & 0xFu;
+            const uint32_t pv = k == 0 ? pl : (x[(k - 1) >> 3] >> (4 * ((k - 1) & 7))) & 0xFu;
+            chg |= (mv != pv ? 1u : 0u) << k;
+        }
+        if (c0 + kSeg > n) chg &= c0 >= n ? 0u : (uint32_t)((1ull << (n - c0)) - 1ull);
+        const uint32_t cnt = (uint32_t)__builtin_popcount(chg);
         uint32_t incl = cnt;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
             if (lane >= (uint32_t)o) incl += y;
         }
-        const uint32_t tile_total = __shfl(incl, 63, 64);
+        const uint32_t tile_total = (uint32_t)__shfl((int)incl, 63, 64);
         if (EMIT) {
-            uint32_t h = in_h, S = in_S, k = 0;
-            seg_pass<true, FMB>(v, c0, h, S, k, stage + (incl - cnt));
-            eh = h;
-            eS = S;
+            uint32_t p = incl - cnt;
+            for (uint32_t b = chg; b; b &= b - 1u) {
+                const uint32_t k = (uint32_t)__builtin_ctz(b);
+                stage[p++] = ((c0 + k) << 4) | nib_at(q.x, q.y, q.z, q.w, k);
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 1  // unrolled, this copy held 145 VGPRs (3 waves per SIMD; now 50)
+#pragma unroll 1
             for (uint32_t i = lane; i < tile_total; i += 64u) out[total + i] = stage[i];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         total += tile_total;
-        carry_h = __shfl(eh, 63, 64);
-        carry_S = __shfl(eS, 63, 64);
+        prev = (uint32_t)__shfl((int)(x[3] >> 28), 63, 64);
     }
-    if (lane == 0) {
-        if (EMIT)
-            out[total] = (carry_h << 4) | (uint32_t)__builtin_ctz(carry_S);
-        else
-            counts[row] = total + 1;  // + the final run
-    }
+    if (!EMIT && lane == 0) counts[row] = total;
 }
 
 // ---------------------------------------------------------------------------
@@ -2619,22 +2799,16 @@ bool first_moves_reads_own(uint32_t shift, bool narrow) {
     return !(narrow && shift == 2 && fm_n4());  // only the generic kernel reads it
 }
 
-template <bool EMIT>
-static void launch_rle(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                       uint32_t* counts, const uint64_t* off, uint32_t* runs, uint32_t* st,
-                       uint8_t* rc, hipStream_t s) {
-    const dim3 grid((nrows + 3u) / 4u), block(256);
-    const kern::RleState rs{fmb == 4 ? st : nullptr, fmb == 4 ? rc : nullptr};
-    switch (fmb) {
-        case 4: launch(kern::rle_scan<EMIT, 4>, grid, block, s, fm, npad, nrows, counts, off, runs, rs); break;
-        case 8: launch(kern::rle_scan<EMIT, 8>, grid, block, s, fm, npad, nrows, counts, off, runs, rs); break;
-        default: launch(kern::rle_scan<EMIT, 16>, grid, block, s, fm, npad, nrows, counts, off, runs, rs); break;
-    }
-}
-
 void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
                       uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s) {
-    launch_rle<false>(fm, fmb, npad, nrows, counts, nullptr, nullptr, st, rc, s);
+    if (!nrows) return;
+    const dim3 grid((nrows + 3u) / 4u), block(256);
+    const kern::RleState rs{st, rc};
+    switch (fmb) {
+        case 4: launch(kern::rle_scan<4>, grid, block, s, fm, npad, nrows, counts, rs); break;
+        case 8: launch(kern::rle_scan<8>, grid, block, s, fm, npad, nrows, counts, rs); break;
+        default: launch(kern::rle_scan<16>, grid, block, s, fm, npad, nrows, counts, rs); break;
+    }
 }
 
 uint32_t rle_ch() {  // CPD_RLE_CH=0: count with rle_scan instead of the chunked count (32 segments)
@@ -2662,10 +2836,32 @@ void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t*
            hard);
 }
 
-void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                     const uint64_t* off, uint32_t* runs, uint32_t* st, uint8_t* rc,
-                     hipStream_t s) {
-    launch_rle<true>(fm, fmb, npad, nrows, nullptr, off, runs, st, rc, s);
+void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
+                      const uint32_t* st, const uint8_t* rc, const uint32_t* out_row,
+                      uint32_t* dense, hipStream_t s) {
+    if (!nrows) return;
+    const uint32_t ntiles = npad / kern::kTile;
+    const dim3 grid((ntiles + kern::kMoveTiles - 1u) / kern::kMoveTiles, (nrows + 3u) / 4u),
+        block(256);
+    switch (fmb) {
+        case 4: launch(kern::rle_moves<4>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
+        case 8: launch(kern::rle_moves<8>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
+        default: launch(kern::rle_moves<16>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
+    }
+}
+
+void launch_moves_count(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,
+                        uint32_t* counts, hipStream_t s) {
+    if (!nrows) return;
+    launch(kern::moves_runs<false>, dim3((nrows + 3u) / 4u), dim3(256), s, dense, stride, n, nrows,
+           (const uint64_t*)nullptr, (uint64_t)0, (uint32_t*)nullptr, counts);
+}
+
+void launch_moves_runs(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,
+                       const uint64_t* off, uint64_t base, uint32_t* runs, hipStream_t s) {
+    if (!nrows) return;
+    launch(kern::moves_runs<true>, dim3((nrows + 3u) / 4u), dim3(256), s, dense, stride, n, nrows,
+           off, base, runs, (uint32_t*)nullptr);
 }
 
 void launch_validate_rows(const uint64_t* offsets, const uint32_t* runs,

@@ -106,16 +106,27 @@ bool first_moves_reads_own(uint32_t shift, bool narrow);
 // Row width of the tiled first-move rows: npad is a multiple of this.
 constexpr uint32_t kFmTile = 2048;
 
-// Greedy RLE scan, one wave per row: runs per row, then the runs themselves
-// written at off[row] (uint64 offsets into `runs`).  fmb = fm_bits(shift).
-// st / rc ([nrows][npad/32] u32 / u8, used when fmb == 4): the count pass
-// stores each segment's entry state and run count there, the emit pass reads
-// them instead of speculating again.
+// Greedy RLE count, one wave per row: counts[row] = runs per row, and per
+// 32-column segment the scan's entry state and the runs ending inside it
+// (st / rc, [nrows][npad/32] u32 / u8).  fmb = fm_bits(shift).
 void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
                       uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s);
-void launch_rle_emit(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                     const uint64_t* off, uint32_t* runs, uint32_t* st, uint8_t* rc,
-                     hipStream_t s);
+
+// The compact row form: each row's greedy RLE row as a 4-bit move table
+// (column c = nibble c % 8 of word c / 8, npad / 8 words per row — the dense
+// table the walks read), from the first-move sets and the count pass's
+// segment states st / rc; batch row r goes to dense row out_row[r].
+void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
+                      const uint32_t* st, const uint8_t* rc, const uint32_t* out_row,
+                      uint32_t* dense, hipStream_t s);
+// Move tables (row r at dense + r * stride words, stride % 4 == 0) back to
+// RLE words: runs start at column 0 and wherever the move changes (columns
+// >= n ignored).  count: counts[r] = runs of row r; runs: row r's words at
+// runs[off[r] - base].
+void launch_moves_count(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,
+                        uint32_t* counts, hipStream_t s);
+void launch_moves_runs(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,
+                       const uint64_t* off, uint64_t base, uint32_t* runs, hipStream_t s);
 
 // Chunked RLE count (4-bit sets; cpd_kernels.hip rle_count_ch): the same st /
 // rc as launch_rle_count, with each chunk of segments scanned by one lane

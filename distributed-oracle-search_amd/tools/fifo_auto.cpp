@@ -33,6 +33,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <future>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -175,44 +176,95 @@ int main(int argc, char** argv) {
         cli::check(cpd_plan_order(plan, order.data()), "order");
         std::vector<uint32_t> stored = cpd::io::read_order(cpd::io::order_path(outdir, xy), fp);
         if (stored != order) throw std::runtime_error("stored column order differs from this build's");
-        // this worker's buckets: headers first (targets, offsets, run totals)
+        const double t_graph0 = now();
+        // this worker's buckets: headers first (targets, offsets or run
+        // counts, run totals); DOSCPD02 (compact move tables, what
+        // make_cpd_auto writes by default) or DOSCPD01 (run words)
         uint32_t nb = 0;
         cli::check(cpd_partition_nbuckets(g.n, mcode, (uint32_t)key, &nb), "buckets");
         std::vector<std::string> paths;
+        std::vector<int> formats;
         std::vector<cpd::io::CpdBucket> heads;
+        std::vector<cpd::io::MoveBucket> mheads;
         std::vector<uint32_t> targets;
-        uint64_t total_runs = 0;
+        uint64_t total_runs = 0, compact_bytes = 0;
         for (uint32_t b = 0; b < nb; ++b) {
             if (b % (uint32_t)W != (uint32_t)wid) continue;
             paths.push_back(cpd::io::bucket_path(outdir, xy, method, (uint32_t)key, b));
-            heads.push_back(cpd::io::read_bucket_head(paths.back()));
-            const auto& bk = heads.back();
-            if (bk.fingerprint != fp || bk.key != (uint32_t)key || bk.method != (uint32_t)mcode)
+            formats.push_back(cpd::io::bucket_format(paths.back()));
+            uint64_t bfp = 0;
+            uint32_t bkey = 0, bmethod = 0;
+            if (formats.back() == 1) {
+                heads.push_back(cpd::io::read_bucket_head(paths.back()));
+                mheads.emplace_back();
+                const auto& bk = heads.back();
+                bfp = bk.fingerprint, bkey = bk.key, bmethod = bk.method;
+                targets.insert(targets.end(), bk.targets.begin(), bk.targets.end());
+                total_runs += bk.offsets.back();
+            } else {
+                mheads.push_back(cpd::io::read_move_bucket_head(paths.back()));
+                heads.emplace_back();
+                const auto& bk = mheads.back();
+                bfp = bk.fingerprint, bkey = bk.key, bmethod = bk.method;
+                if (bk.n != g.n) throw std::runtime_error("bucket " + std::to_string(b) + " has another node count");
+                targets.insert(targets.end(), bk.targets.begin(), bk.targets.end());
+                total_runs += bk.total_runs;
+                compact_bytes += 4ull * bk.words * bk.targets.size();
+            }
+            if (bfp != fp || bkey != (uint32_t)key || bmethod != (uint32_t)mcode)
                 throw std::runtime_error("bucket " + std::to_string(b) + " was built for another graph/partition");
-            targets.insert(targets.end(), bk.targets.begin(), bk.targets.end());
-            total_runs += bk.offsets.back();
         }
         int ndev = 0;
         cli::check(cpd_device_count(&ndev), "device count");
         if (ndev == 0) throw std::runtime_error("no GPU visible (this build has no CPU path)");
         int device = (int)a.num("device", wid % ndev);
         cli::check(cpd_graph_create(plan, device, &dg), "graph upload");
-        // then the runs, streamed in pieces of <= kPieceRuns (a longer row
+        // then the rows, streamed in pieces of <= kPiece words (a longer row
         // alone): a dense index never holds the worker's runs in HBM or RAM
         const std::string im = a.str("index", "auto");
         const int imode = im == "rle" ? CPD_INDEX_RLE : im == "dense" ? CPD_INDEX_DENSE : CPD_INDEX_AUTO;
         cli::check(cpd_index_create_empty(dg, targets.data(), (uint32_t)targets.size(), imode,
                                           total_runs, &ix),
                    "index");
-        constexpr uint64_t kPieceRuns = 64ull << 20;  // 256 MB
+        const double t_rows0 = now();
+        constexpr uint64_t kPiece = 64ull << 20;  // 256 MB
         std::vector<uint32_t> buf;
         std::vector<uint64_t> rel;
-        for (size_t k = 0; k < heads.size(); ++k) {
+        // compact buckets: pieces read into two page-locked buffers by a
+        // reader thread while the previous piece is appended (uploaded)
+        uint32_t* pin[2] = {nullptr, nullptr};
+        for (size_t k = 0; k < paths.size(); ++k) {
+            if (formats[k] == 2) {
+                const auto& mh = mheads[k];
+                const uint32_t nr = (uint32_t)mh.targets.size();
+                if (!nr) continue;
+                const uint32_t per = (uint32_t)std::max<uint64_t>(1, kPiece / mh.words);
+                for (auto& p : pin)
+                    if (!p) {
+                        void* q = nullptr;
+                        cli::check(cpd_host_alloc(4ull * mh.words * per, &q), "pinned buffer");
+                        p = static_cast<uint32_t*>(q);
+                    }
+                auto read = [&, k, per, nr](uint32_t r0, int slot) {
+                    cpd::io::read_move_bucket_rows(paths[k], mheads[k], r0, std::min(per, nr - r0), pin[slot]);
+                };
+                std::future<void> rd = std::async(std::launch::async, read, 0u, 0);
+                for (uint32_t r0 = 0, i = 0; r0 < nr; r0 += per, ++i) {
+                    rd.get();  // piece i is in pin[i & 1] (a read error is rethrown here)
+                    if (r0 + per < nr) rd = std::async(std::launch::async, read, r0 + per, (int)((i + 1) & 1u));
+                    const int rc = cpd_index_append_moves(ix, std::min(per, nr - r0), pin[i & 1u]);
+                    if (rc != CPD_OK) {
+                        if (rd.valid()) rd.wait();
+                        cli::check(rc, "index rows");
+                    }
+                }
+                continue;
+            }
             const auto& off = heads[k].offsets;
             const uint32_t nr = (uint32_t)heads[k].targets.size();
             for (uint32_t r0 = 0; r0 < nr;) {
                 uint32_t r1 = r0 + 1;
-                while (r1 < nr && off[r1 + 1] - off[r0] <= kPieceRuns) ++r1;
+                while (r1 < nr && off[r1 + 1] - off[r0] <= kPiece) ++r1;
                 buf.resize(off[r1] - off[r0]);
                 cpd::io::read_bucket_runs(paths[k], heads[k], off[r0], buf.size(), buf.data());
                 rel.resize(r1 - r0 + 1);
@@ -221,8 +273,17 @@ int main(int argc, char** argv) {
                 r0 = r1;
             }
         }
+        for (auto p : pin) cpd_host_free(p);
+        const double t_rows = now() - t_rows0;
         int mode = 0;
         cli::check(cpd_index_get_mode(ix, &mode), "index mode");
+        // one machine-readable line (bench.py's full-build leg reads it)
+        std::printf("fifo_auto-json: {\"worker\": %lld, \"rows\": %zu, \"runs\": %llu, "
+                    "\"index\": \"%s\", \"compact_bytes\": %llu, \"read_plan_s\": %.3f, "
+                    "\"graph_s\": %.3f, \"rows_s\": %.3f, \"ready_s\": %.3f}\n",
+                    wid, targets.size(), (unsigned long long)total_runs,
+                    mode == CPD_INDEX_DENSE ? "dense" : "rle", (unsigned long long)compact_bytes,
+                    t_graph0 - t0, t_rows0 - t_graph0, t_rows, now() - t0);
         std::printf("fifo_auto: worker %lld: %zu rows, %llu runs (%s index) on device %d, ready in "
                     "%.3fs; listening on %s\n",
                     wid, targets.size(), (unsigned long long)total_runs,

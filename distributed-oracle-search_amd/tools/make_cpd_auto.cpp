@@ -13,10 +13,14 @@
 //                 [--no-pipeline]      build, then export, then write, per group
 //                 [--plan-only]        build / load the cached plan and exit
 //                 [--targets-from S]   only rows of targets of scenario S (q s t)
+//                 [--format moves|rle] bucket file layout: moves (default) =
+//                                      DOSCPD02, the rows as 4-bit move tables
+//                                      (n/2 bytes per row); rle = DOSCPD01,
+//                                      the run words (4 B per run)
 //                 [--discard]          null sink: every row is still built and
 //                                      copied out of HBM (D2H), but no file is
 //                                      written (times the build + export path
-//                                      of a worker whose runs outgrow the disk)
+//                                      without the disk)
 //
 // The plan (column order + hierarchy) is cached in D per graph; workers that
 // start together share it through cpd_plan_cache (one builds, the rest wait).
@@ -93,8 +97,8 @@ struct PinnedBuf {
 
 class Pipeline {
 public:
-    Pipeline(cpd_graph* g, uint32_t B, int threads, bool discard)
-        : g_(g), B_(B), discard_(discard) {
+    Pipeline(cpd_graph* g, uint32_t B, int threads, bool discard, bool moves)
+        : g_(g), B_(B), discard_(discard), moves_(moves) {
         for (int i = 0; i < std::max(1, threads); ++i) pool_.emplace_back([this] { worker(); });
     }
     ~Pipeline() {
@@ -111,17 +115,33 @@ public:
     void run(const std::vector<uint32_t>& targets, const std::vector<uint64_t>& first,
              const std::vector<CpdBucket>& heads, const std::vector<std::string>& paths) {
         using cpd::io::BucketFile;
+        using cpd::io::MoveBucketFile;
         const size_t N = targets.size(), nb = heads.size();
         std::vector<std::unique_ptr<BucketFile>> files(nb);
+        std::vector<std::unique_ptr<MoveBucketFile>> mfiles(nb);
         std::vector<uint64_t> bruns(nb, 0);  // runs of the bucket's rows scheduled so far
         std::vector<size_t> to_close;        // buckets finished by the block in flight
+        auto open_bucket = [&](size_t k) {
+            if (discard_) return;
+            if (moves_) mfiles[k] = std::make_unique<MoveBucketFile>(paths[k], move_head(heads[k]));
+            else files[k] = std::make_unique<BucketFile>(paths[k], heads[k]);
+        };
+        auto close_bucket = [&](size_t k) {
+            if (files[k]) files[k]->close(bruns[k]);
+            if (mfiles[k]) mfiles[k]->close(bruns[k]);
+            files[k].reset();
+            mfiles[k].reset();
+        };
         for (size_t k = 0; k < nb; ++k)
-            if (first[k] == first[k + 1] && !discard_) {  // empty bucket: header + one offset
-                BucketFile f(paths[k], heads[k]);
-                const uint64_t zero = 0;
-                f.write_offsets(0, &zero, 1);
-                f.close(0);
+            if (first[k] == first[k + 1] && !discard_) {  // empty bucket: header (+ one offset)
+                open_bucket(k);
+                if (files[k]) {
+                    const uint64_t zero = 0;
+                    files[k]->write_offsets(0, &zero, 1);
+                }
+                close_bucket(k);
             }
+        uint32_t words = 0;  // compact row width
         size_t kb = 0;
         for (size_t b0 = 0, blk = 0; b0 < N; b0 += B_, ++blk) {
             const uint32_t cnt = (uint32_t)std::min<size_t>(B_, N - b0);
@@ -135,47 +155,26 @@ public:
             t_build += now() - tb;
             auto offs = std::make_shared<std::vector<uint64_t>>(cnt + 1);
             ok(cpd_rows_export_range(r, 0, cnt, offs->data(), nullptr), "export offsets");
+            if (!words) ok(cpd_rows_move_words(r, &words), "move words");
             // block k-1 written (it read the other cpd_rows): close what it finished
             const double tw = now();
             drain();
             t_wait += now() - tw;
-            for (size_t k : to_close) {
-                if (files[k]) files[k]->close(bruns[k]);
-                files[k].reset();
-            }
+            for (size_t k : to_close) close_bucket(k);
             to_close.clear();
             cpd_rows* rr = r;
             for (size_t i = b0; i < b0 + cnt;) {
                 while (first[kb + 1] <= i) ++kb;
-                if (!files[kb] && !discard_)
-                    files[kb] = std::make_unique<BucketFile>(paths[kb], heads[kb]);
-                BucketFile* f = files[kb].get();  // null: discard sink
+                if (!files[kb] && !mfiles[kb]) open_bucket(kb);
                 const size_t seg_end = std::min<size_t>(first[kb + 1], b0 + cnt);
                 const uint32_t r0 = (uint32_t)(i - b0), r1 = (uint32_t)(seg_end - b0);
                 const uint32_t brow0 = (uint32_t)(i - first[kb]);
                 const uint64_t base = bruns[kb];
                 const bool last = seg_end == first[kb + 1];
-                if (f) submit([=] {  // bucket-relative offsets; the end offset with the last rows
-                    std::vector<uint64_t> o;
-                    for (uint32_t u = r0; u < r1 + (last ? 1u : 0u); ++u)
-                        o.push_back(base + (*offs)[u] - (*offs)[r0]);
-                    f->write_offsets(brow0, o.data(), (uint32_t)o.size());
-                });
-                for (uint32_t p0 = r0; p0 < r1;) {
-                    uint32_t p1 = p0 + 1;
-                    while (p1 < r1 && (*offs)[p1 + 1] - (*offs)[p0] <= kPieceRuns) ++p1;
-                    const uint64_t run0 = base + (*offs)[p0] - (*offs)[r0];
-                    submit([=] {
-                        thread_local PinnedBuf buf;
-                        const uint64_t nr = (*offs)[p1] - (*offs)[p0];
-                        uint32_t* dst = buf.get(nr);
-                        const double te = now();
-                        ok(cpd_rows_export_range(rr, p0, p1 - p0, nullptr, dst), "export");
-                        note_export(te, now(), nr * sizeof(uint32_t));
-                        if (f) f->write_runs(run0, dst, nr);
-                    });
-                    p0 = p1;
-                }
+                if (moves_)
+                    schedule_moves(rr, mfiles[kb].get(), offs, r0, r1, brow0, words);
+                else
+                    schedule_runs(rr, files[kb].get(), offs, r0, r1, brow0, base, last);
                 bruns[kb] += (*offs)[r1] - (*offs)[r0];
                 if (last) to_close.push_back(kb);
                 i = seg_end;
@@ -185,18 +184,91 @@ public:
         const double tw = now();
         drain();
         t_wait += now() - tw;
-        for (size_t k : to_close)
-            if (files[k]) files[k]->close(bruns[k]);
+        for (size_t k : to_close) close_bucket(k);
     }
 
     double t_build = 0, t_wait = 0;
     uint64_t runs = 0;
     // D2H copies: summed copy time over writer threads, bytes, first start /
-    // last end (their wall span)
-    double x_sum = 0, x_first = 0, x_last = 0;
+    // last end (their wall span); file writes: summed time over threads
+    double x_sum = 0, x_first = 0, x_last = 0, w_sum = 0;
     uint64_t x_bytes = 0;
 
 private:
+    static cpd::io::MoveBucket move_head(const CpdBucket& h) {
+        cpd::io::MoveBucket m;
+        m.n = h.n;
+        m.bid = h.bid;
+        m.method = h.method;
+        m.key = h.key;
+        m.maxworker = h.maxworker;
+        m.words = (h.n + 7u) / 8u;
+        m.fingerprint = h.fingerprint;
+        m.targets = h.targets;
+        return m;
+    }
+
+    // DOSCPD01: bucket-relative offsets (the end offset with the last rows),
+    // then the run words in pieces of <= kPieceRuns
+    void schedule_runs(cpd_rows* rr, cpd::io::BucketFile* f,
+                       const std::shared_ptr<std::vector<uint64_t>>& offs, uint32_t r0, uint32_t r1,
+                       uint32_t brow0, uint64_t base, bool last) {
+        if (f) submit([=] {
+            std::vector<uint64_t> o;
+            for (uint32_t u = r0; u < r1 + (last ? 1u : 0u); ++u)
+                o.push_back(base + (*offs)[u] - (*offs)[r0]);
+            f->write_offsets(brow0, o.data(), (uint32_t)o.size());
+        });
+        for (uint32_t p0 = r0; p0 < r1;) {
+            uint32_t p1 = p0 + 1;
+            while (p1 < r1 && (*offs)[p1 + 1] - (*offs)[p0] <= kPieceRuns) ++p1;
+            const uint64_t run0 = base + (*offs)[p0] - (*offs)[r0];
+            submit([=] {
+                thread_local PinnedBuf buf;
+                const uint64_t nr = (*offs)[p1] - (*offs)[p0];
+                uint32_t* dst = buf.get(nr);
+                const double te = now();
+                ok(cpd_rows_export_range(rr, p0, p1 - p0, nullptr, dst), "export");
+                const double tx = now();
+                note_export(te, tx, nr * sizeof(uint32_t));
+                if (f) {
+                    f->write_runs(run0, dst, nr);
+                    note_write(now() - tx);
+                }
+            });
+            p0 = p1;
+        }
+    }
+
+    // DOSCPD02: the rows' run counts, then the move tables in pieces of
+    // <= kPieceRuns words
+    void schedule_moves(cpd_rows* rr, cpd::io::MoveBucketFile* f,
+                        const std::shared_ptr<std::vector<uint64_t>>& offs, uint32_t r0,
+                        uint32_t r1, uint32_t brow0, uint32_t words) {
+        if (f) submit([=] {
+            std::vector<uint32_t> c(r1 - r0);
+            for (uint32_t u = r0; u < r1; ++u) c[u - r0] = (uint32_t)((*offs)[u + 1] - (*offs)[u]);
+            f->write_counts(brow0, c.data(), r1 - r0);
+        });
+        const uint32_t per = (uint32_t)std::max<uint64_t>(1, kPieceRuns / words);
+        for (uint32_t p0 = r0; p0 < r1; p0 += per) {
+            const uint32_t p1 = std::min(r1, p0 + per);
+            submit([=] {
+                thread_local PinnedBuf buf;
+                const uint64_t nw = (uint64_t)words * (p1 - p0);
+                uint32_t* dst = buf.get(nw);
+                const double te = now();
+                ok(cpd_rows_export_moves(rr, p0, p1 - p0, dst), "export moves");
+                const double tx = now();
+                note_export(te, tx, nw * sizeof(uint32_t));
+                if (f) {
+                    f->write_rows(brow0 + (p0 - r0), dst, p1 - p0);
+                    note_write(now() - tx);
+                }
+            });
+        }
+    }
+
     void note_export(double t0, double t1, uint64_t bytes) {
         std::lock_guard<std::mutex> l(xmu_);
         x_sum += t1 - t0;
@@ -204,9 +276,13 @@ private:
         if (x_first == 0 || t0 < x_first) x_first = t0;
         x_last = std::max(x_last, t1);
     }
+    void note_write(double dt) {
+        std::lock_guard<std::mutex> l(xmu_);
+        w_sum += dt;
+    }
     std::mutex xmu_;
 
-    static constexpr uint64_t kPieceRuns = 64ull << 20;  // 256 MB of runs per copy+write
+    static constexpr uint64_t kPieceRuns = 64ull << 20;  // 256 MB of runs / words per copy+write
 
     void submit(std::function<void()> f) {
         {
@@ -245,7 +321,7 @@ private:
 
     cpd_graph* g_;
     uint32_t B_;
-    bool discard_;
+    bool discard_, moves_;
     cpd_rows* rows_[2] = {nullptr, nullptr};
     std::vector<std::thread> pool_;
     std::mutex mu_;
@@ -267,10 +343,16 @@ int main(int argc, char** argv) {
                      "--workerid I --maxworker W [--outdir D] [--device G] [--batch B] "
                      "[--threads T] [--plan P | --no-plan-cache] [--write-threads T] "
                      "[--no-pipeline] [--plan-only] [--targets-from SCEN] [--discard] "
-                     "[--hbm-reserve GIB]\n");
+                     "[--hbm-reserve GIB] [--format moves|rle]\n");
         return 2;
     }
     int mcode = cli::method_code(method);
+    const std::string format = a.str("format", "moves");
+    if (format != "moves" && format != "rle") {
+        std::fprintf(stderr, "make_cpd_auto: --format must be moves or rle\n");
+        return 2;
+    }
+    const bool moves = format == "moves";
     std::string outdir = a.str("outdir", dir_of(input));
     ::mkdir(outdir.c_str(), 0755);
     double t_start = now();
@@ -380,7 +462,7 @@ int main(int argc, char** argv) {
 
         double t_build = 0, t_io = 0;
         uint64_t rows_done = 0, runs_done = 0;
-        double x_sum = 0, x_span = 0;
+        double x_sum = 0, x_span = 0, w_sum = 0;
         uint64_t x_bytes = 0;
         const bool discard = a.has("discard");
         if (discard && a.has("no-pipeline"))
@@ -404,15 +486,43 @@ int main(int argc, char** argv) {
                 first.push_back(targets.size());
                 double tb = now();
                 cli::check(cpd_build_rows(dg, targets.data(), (uint32_t)targets.size(), rows, &rows), "build");
-                uint32_t nr = 0;
+                uint32_t nr = 0, words = 0;
                 uint64_t tot = 0;
                 cli::check(cpd_rows_count(rows, &nr, &tot), "rows");
+                cli::check(cpd_rows_move_words(rows, &words), "move words");
                 std::vector<uint64_t> off(nr + 1);
-                std::vector<uint32_t> runs(tot);
-                cli::check(cpd_rows_export(rows, off.data(), runs.data()), "export");
+                std::vector<uint32_t> runs(moves ? 0 : tot), mv(moves ? (size_t)nr * words : 0);
+                if (moves) {
+                    cli::check(cpd_rows_export_range(rows, 0, nr, off.data(), nullptr), "offsets");
+                    cli::check(cpd_rows_export_moves(rows, 0, nr, mv.data()), "export moves");
+                } else {
+                    cli::check(cpd_rows_export(rows, off.data(), runs.data()), "export");
+                }
                 t_build += now() - tb;
                 double ti = now();
                 for (size_t k = 0; k < group.size(); ++k) {
+                    const std::string path =
+                        cpd::io::bucket_path(outdir, input, method, (uint32_t)key, group[k]);
+                    if (moves) {
+                        cpd::io::MoveBucket b;
+                        b.n = g.n;
+                        b.bid = group[k];
+                        b.method = (uint32_t)mcode;
+                        b.key = (uint32_t)key;
+                        b.maxworker = (uint32_t)W;
+                        b.words = words;
+                        b.fingerprint = fp;
+                        b.targets.assign(targets.begin() + first[k], targets.begin() + first[k + 1]);
+                        const uint32_t nb = (uint32_t)b.targets.size();
+                        std::vector<uint32_t> c(nb);
+                        for (uint32_t r = 0; r < nb; ++r)
+                            c[r] = (uint32_t)(off[first[k] + r + 1] - off[first[k] + r]);
+                        cpd::io::MoveBucketFile f(path, b);
+                        f.write_counts(0, c.data(), nb);
+                        f.write_rows(0, mv.data() + first[k] * (size_t)words, nb);
+                        f.close(off[first[k + 1]] - off[first[k]]);
+                        continue;
+                    }
                     CpdBucket b;
                     b.n = g.n;
                     b.bid = group[k];
@@ -424,14 +534,14 @@ int main(int argc, char** argv) {
                     uint64_t base = off[first[k]];
                     for (size_t r = first[k]; r <= first[k + 1]; ++r) b.offsets.push_back(off[r] - base);
                     b.runs.assign(runs.begin() + base, runs.begin() + off[first[k + 1]]);
-                    cpd::io::write_bucket(cpd::io::bucket_path(outdir, input, method, (uint32_t)key, group[k]), b);
+                    cpd::io::write_bucket(path, b);
                 }
                 t_io += now() - ti;
                 rows_done += nr;
                 runs_done += tot;
             }
         } else {
-            Pipeline pl(dg, B, (int)a.num("write-threads", 8), discard);
+            Pipeline pl(dg, B, (int)a.num("write-threads", 8), discard, moves);
             std::vector<uint32_t> targets;
             std::vector<CpdBucket> heads(owned.size());
             std::vector<uint64_t> first(owned.size() + 1, 0);
@@ -460,6 +570,7 @@ int main(int argc, char** argv) {
             x_sum = pl.x_sum;
             x_bytes = pl.x_bytes;
             x_span = pl.x_last > pl.x_first ? pl.x_last - pl.x_first : 0.0;
+            w_sum = pl.w_sum;
         }
         const double t_rows = now() - t_rows0;
         const double t_f0 = now();
@@ -487,10 +598,11 @@ int main(int argc, char** argv) {
             "\"plan_cached\": %s, \"graph_s\": %.3f, \"batch_alloc_s\": %.3f, \"setup_s\": %.3f, "
             "\"rows_s\": %.3f, \"build_calls_s\": %.3f, \"wait_s\": %.3f, \"free_s\": %.3f, "
             "\"export_bytes\": %llu, \"export_thread_s\": %.3f, \"export_span_s\": %.3f, "
-            "\"total_s\": %.3f}\n",
+            "\"write_thread_s\": %.3f, \"format\": \"%s\", \"total_s\": %.3f}\n",
             wid, W, (unsigned long long)rows_done, (unsigned long long)runs_done, B,
             discard ? "true" : "false", t_read, t_plan, plan_loaded ? "true" : "false", t_graph,
-            t_batch, t_setup, t_rows, t_build, t_io, t_free, (unsigned long long)x_bytes, x_sum, x_span, now() - t_start);
+            t_batch, t_setup, t_rows, t_build, t_io, t_free, (unsigned long long)x_bytes, x_sum, x_span,
+            w_sum, format.c_str(), now() - t_start);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "make_cpd_auto: %s\n", e.what());
         return 1;

@@ -211,8 +211,12 @@ void cpd_graph_free(cpd_graph* g);
  * the first-move sets FM_t(n) = {k : w(n->v_k) + d(v_k,t) = d(n,t)}
  * (t itself and unreachable nodes: wildcard), and the greedy run-length row
  * over the DFS column order with the lowest-set-bit tie-break
- * (warthog graph_oracle::add_row [U]).  Rows stay in HBM; export copies them
- * to the host.  `reuse` (may be NULL) recycles a previous result's buffers. */
+ * (warthog graph_oracle::add_row [U]).  Rows stay in HBM in their compact
+ * form — the RLE row expanded into a 4-bit move per column, which under the
+ * greedy rule is a bijection (consecutive runs always carry different moves,
+ * so the runs are column 0 and every column whose move differs from its left
+ * neighbour's) — and are exported either as run words or in that form.
+ * `reuse` (may be NULL) recycles a previous result's buffers.               */
 int  cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
                     cpd_rows* reuse, cpd_rows** out);
 /* The targets the NEXT cpd_build_rows call on g will start with (its first
@@ -223,6 +227,8 @@ int  cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
  * depend on the hint.  Cleared by every cpd_build_rows.                     */
 int  cpd_graph_hint_next(cpd_graph* g, const uint32_t* targets, uint32_t ntargets);
 int  cpd_rows_count(const cpd_rows* r, uint32_t* nrows, uint64_t* total_runs);
+/* Run words (start_column << 4 | move), decoded on the GPU from the compact
+ * rows: the rows of warthog's rle_run32 form [U], byte for byte.            */
 int  cpd_rows_export(const cpd_rows* r, uint64_t* offsets /* nrows+1 */,
                      uint32_t* runs /* total_runs */);
 /* Rows [first, first + count) of r: offsets relative to row `first`
@@ -232,6 +238,13 @@ int  cpd_rows_export(const cpd_rows* r, uint64_t* offsets /* nrows+1 */,
  * (the overlapped writer of bin/make_cpd_auto).  Either output may be NULL. */
 int  cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count,
                            uint64_t* offsets /* count+1 */, uint32_t* runs);
+/* The compact form (DOSCPD02 bucket files, cpd_index_append_moves): a row is
+ * *words = ceil(n / 8) u32, column c's move in bits 4*(c%8)..+3 of word
+ * c/8; the nibbles past column n-1 repeat the last run's move.  Rows
+ * [first, first + count) back to back, on the calling thread's stream.      */
+int  cpd_rows_move_words(const cpd_rows* r, uint32_t* words);
+int  cpd_rows_export_moves(const cpd_rows* r, uint32_t first, uint32_t count,
+                           uint32_t* moves /* count * words */);
 int  cpd_rows_targets(const cpd_rows* r, uint32_t* targets /* nrows */);
 /* The batch lane each row was built in (lane = position in its sweep batch,
  * 0..batch-1; rows are lane-sorted by Hilbert key with coordinates, else by
@@ -281,6 +294,12 @@ int  cpd_index_create_empty(cpd_graph* g, const uint32_t* row_targets, uint32_t 
 int  cpd_index_append_rows(cpd_index* ix, uint32_t count, const uint64_t* offsets,
                            const uint32_t* runs);
 int  cpd_index_append_built_rows(cpd_index* ix, const cpd_rows* r);
+/* Rows in the compact form (cpd_rows_export_moves layout, count rows of
+ * ceil(n / 8) words): a DENSE index takes them as they are, an RLE index
+ * decodes them into run words on the GPU (total_runs of the create call must
+ * cover them).  No format check is needed: a nibble naming no out-edge of its
+ * column stops a walk there, unfinished, as the oracle's walk does.          */
+int  cpd_index_append_moves(cpd_index* ix, uint32_t count, const uint32_t* moves);
 /* Rows declared / appended, runs resident in HBM, bytes of dense tables.     */
 int  cpd_index_info(const cpd_index* ix, uint32_t* nrows, uint32_t* added,
                     uint64_t* runs_resident, uint64_t* dense_bytes);

@@ -114,6 +114,40 @@ def build_rows(row_ptr, dst, w, order, targets, threads=0):
     return off, runs
 
 
+def moves_from_runs(offsets, runs, n):
+    """The compact form of RLE rows (the checker of cpd_rows_export_moves /
+    DOSCPD02): (nrows, ceil(n/8)) u32, column c's move — that of the last run
+    starting at or before c (get_move) — in bits 4*(c%8) of word c//8; the
+    nibbles past column n-1 repeat the last run's move."""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    runs = _u32(runs)
+    nrows, w = len(offsets) - 1, (n + 7) // 8
+    out = np.zeros((nrows, w), np.uint32)
+    cols = np.arange(8 * w, dtype=np.int64)
+    for r in range(nrows):
+        rr = runs[int(offsets[r]):int(offsets[r + 1])]
+        starts = (rr >> 4).astype(np.int64)
+        idx = np.searchsorted(starts, cols, side="right") - 1  # last run starting <= c
+        nib = (rr[idx] & 0xF).astype(np.uint32).reshape(w, 8)
+        out[r] = (nib << (4 * np.arange(8, dtype=np.uint32))).sum(axis=1, dtype=np.uint64)
+    return out
+
+
+def runs_from_moves(moves, n):
+    """Inverse of moves_from_runs under the greedy rule: a run starts at
+    column 0 and wherever the move differs from the left neighbour's."""
+    moves = _u32(moves)
+    nrows = moves.shape[0]
+    off = np.zeros(nrows + 1, np.uint64)
+    out = []
+    for r in range(nrows):
+        nib = ((moves[r][:, None] >> (4 * np.arange(8, dtype=np.uint32))) & 0xF).ravel()[:n]
+        starts = np.flatnonzero(np.concatenate(([True], nib[1:] != nib[:-1])))
+        out.append(((starts.astype(np.uint32) << 4) | nib[starts]).astype(np.uint32))
+        off[r + 1] = off[r] + len(starts)
+    return off, (np.concatenate(out) if out else np.empty(0, np.uint32))
+
+
 def table_search(row_ptr, dst, w_sel, order, row_targets, offsets, runs, s, t, k_moves=-1,
                  threads=0):
     row_ptr, dst, w_sel, order = map(_u32, (row_ptr, dst, w_sel, order))

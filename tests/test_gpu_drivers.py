@@ -48,8 +48,11 @@ def _wait_ready(proc, timeout=60):
     raise AssertionError(f"fifo_auto did not come up: {buf} {proc.stderr.read()}")
 
 
-@pytest.mark.parametrize("method,key", [("mod", 3), ("div", 5)])
-def test_drivers_end_to_end(tmp_path, method, key):
+@pytest.mark.parametrize("method,key,fmt", [("mod", 3, "moves"), ("div", 5, "moves"),
+                                            ("mod", 3, "rle")])
+def test_drivers_end_to_end(tmp_path, method, key, fmt):
+    """fmt: the bucket layout make_cpd_auto writes (DOSCPD02 move tables by
+    default, DOSCPD01 run words with --format rle); fifo_auto reads either."""
     W = 3
     prefix = str(tmp_path / "g")
     subprocess.run([os.path.join(BIN, "gen_synth"), "--width", "30", "--height", "24", "--seed",
@@ -59,8 +62,8 @@ def test_drivers_end_to_end(tmp_path, method, key):
     for wid in range(W):
         p = subprocess.run([os.path.join(BIN, "make_cpd_auto"), "--input", xy, "--partmethod", method,
                             "--partkey", str(key), "--workerid", str(wid), "--maxworker", str(W),
-                            "--outdir", outdir, "--device", "0"], capture_output=True, text=True,
-                           timeout=300)
+                            "--outdir", outdir, "--device", "0", "--format", fmt],
+                           capture_output=True, text=True, timeout=300)
         assert p.returncode == 0, p.stderr
         assert "rows/s" in p.stdout
     g = cpd.synth_road_graph(30, 24, seed=2)
@@ -137,12 +140,30 @@ def _read_bucket(path):
     return targets, off, runs
 
 
+def _read_move_bucket(path):
+    """The compact bucket layout of csrc/cpd_io.cpp (DOSCPD02, MoveBucketFile)."""
+    raw = open(path, "rb").read()
+    assert raw[:8] == b"DOSCPD02"
+    n, nrows, bid, method, key, maxworker, words, _ = (int(x) for x in np.frombuffer(raw, np.uint32, 8, 8))
+    assert words == (n + 7) // 8
+    total = int(np.frombuffer(raw, np.uint64, 1, 40)[0])
+    p = 56
+    targets = np.frombuffer(raw, np.uint32, nrows, p)
+    counts = np.frombuffer(raw, np.uint32, nrows, p + 4 * nrows)
+    rows_at = -(-(p + 8 * nrows) // 4096) * 4096
+    assert len(raw) == rows_at + 4 * words * nrows and int(counts.sum()) == total
+    moves = np.frombuffer(raw, np.uint32, nrows * words, rows_at).reshape(nrows, words)
+    return targets, counts, moves
+
+
+@pytest.mark.parametrize("fmt", ["moves", "rle"])
 @pytest.mark.parametrize("method,key", [("mod", 5), ("div", 7)])
-def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key):
+def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key, fmt):
     """The overlapped writer (build block k+1 while a pool copies block k out
     of HBM and writes it in place) gives byte-identical bucket files to the
-    sequential path; with --batch 1024 the blocks straddle bucket boundaries
-    and --write-threads 3 interleaves pieces of several buckets."""
+    sequential path, in both layouts (DOSCPD02 move tables, the default, and
+    DOSCPD01 run words); with --batch 1024 the blocks straddle bucket
+    boundaries and --write-threads 3 interleaves pieces of several buckets."""
     prefix = str(tmp_path / "g")
     subprocess.run([os.path.join(BIN, "gen_synth"), "--width", "64", "--height", "48", "--seed",
                     "5", "--out", prefix, "--queries", "10"], check=True, capture_output=True)
@@ -155,7 +176,7 @@ def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key):
         out = str(tmp_path / mode)
         p = subprocess.run([os.path.join(BIN, "make_cpd_auto"), "--input", xy, "--partmethod",
                             method, "--partkey", str(key), "--workerid", "1", "--maxworker", "2",
-                            "--outdir", out, "--device", "0",
+                            "--outdir", out, "--device", "0", "--format", fmt,
                             "--plan", str(tmp_path / "g.plan")] + extra,
                            capture_output=True, text=True, timeout=300)
         if mode == "too_much":  # a reserve past the free HBM: refused, nothing built
@@ -176,7 +197,13 @@ def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key):
     # one bucket against the CPU oracle
     g = cpd.synth_road_graph(64, 48, seed=5)
     order = oracle.dfs_preorder(g.row_ptr, g.dst)
-    targets, off, runs = _read_bucket(os.path.join(dirs["pipe"], pipe[0]))
-    o_off, o_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, np.array(targets))
-    np.testing.assert_array_equal(off, o_off)
-    np.testing.assert_array_equal(runs, o_runs)
+    if fmt == "rle":
+        targets, off, runs = _read_bucket(os.path.join(dirs["pipe"], pipe[0]))
+        o_off, o_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, np.array(targets))
+        np.testing.assert_array_equal(off, o_off)
+        np.testing.assert_array_equal(runs, o_runs)
+    else:
+        targets, counts, moves = _read_move_bucket(os.path.join(dirs["pipe"], pipe[0]))
+        o_off, o_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, np.array(targets))
+        np.testing.assert_array_equal(counts, np.diff(o_off))
+        np.testing.assert_array_equal(moves, oracle.moves_from_runs(o_off, o_runs, g.n))

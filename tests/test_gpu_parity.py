@@ -74,6 +74,41 @@ def test_rows_bit_exact(setup):
     np.testing.assert_array_equal(runs, ref_runs, err_msg=name)
 
 
+def test_compact_rows_bit_exact(setup):
+    """The rows' compact form (4-bit move per column, what DOSCPD02 files and
+    dense indexes hold) against the oracle's RLE rows expanded, and both index
+    forms loaded from it walk like the oracle."""
+    name, g, plan, dev = setup
+    rng = np.random.default_rng(6)
+    targets = rng.permutation(g.n)[: min(g.n, 1500)].astype(np.uint32)
+    rows = dev.build_rows(targets)
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    mv = rows.export_moves()
+    np.testing.assert_array_equal(mv, oracle.moves_from_runs(ref_off, ref_runs, g.n), err_msg=name)
+    # a range, and the decoded runs of a range
+    a, b = len(targets) // 3, len(targets) // 3 + 7
+    np.testing.assert_array_equal(rows.export_moves(a, b - a), mv[a:b])
+    o, r = rows.export_range(a, b - a)
+    np.testing.assert_array_equal(r, ref_runs[int(ref_off[a]):int(ref_off[b])])
+    np.testing.assert_array_equal(o, ref_off[a:b + 1] - ref_off[a])
+    s = rng.integers(0, g.n, 3000).astype(np.uint32)
+    t = targets[rng.integers(0, len(targets), 3000)]
+    rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, plan.order(), targets, ref_off,
+                                     ref_runs, s, t)
+    for mode in ("dense", "rle"):
+        ix = cpd.Index.streamed(dev, targets, int(ref_off[-1]), mode=mode)
+        half = len(targets) // 2
+        ix.append_moves(mv[:half])
+        ix.append_moves(mv[half:])
+        assert ix.mode == mode
+        cost, hops, fin, _ = ix.query(s, t)
+        np.testing.assert_array_equal(cost, rc, err_msg=f"{name} {mode}")
+        np.testing.assert_array_equal(hops, rh, err_msg=f"{name} {mode}")
+        np.testing.assert_array_equal(fin, rf, err_msg=f"{name} {mode}")
+        if mode == "rle":
+            assert ix.info()["runs_resident"] == int(ref_off[-1])
+
+
 @pytest.mark.parametrize("mode", ["rle", "dense", "auto"])
 def test_queries_free_flow_and_congested(setup, mode):
     name, g, plan, dev = setup

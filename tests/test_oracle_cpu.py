@@ -88,6 +88,27 @@ def test_rle_rows_properties(graphs):
                 assert oracle.get_move(row, col) == (row[j] & 0xF)
 
 
+def test_compact_rows_are_the_rle_rows(graphs):
+    """The compact row form (DOSCPD02, cpd_rows_export_moves) is bijective
+    with the greedy RLE row: consecutive runs always carry different moves
+    (a run closes at c only when S & FM(c) is empty; its move lies in S, the
+    next one's in FM(c)), so the runs are exactly column 0 and every column
+    whose move differs from its left neighbour's."""
+    rng = np.random.default_rng(4)
+    for name, g in graphs.items():
+        order = oracle.dfs_preorder(g.row_ptr, g.dst)
+        targets = rng.choice(g.n, size=min(g.n, 40), replace=False)
+        off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, targets)
+        for i in range(len(targets)):
+            row = runs[off[i]:off[i + 1]]
+            assert np.all(np.diff((row & 0xF).astype(np.int64)) != 0), name
+        mv = oracle.moves_from_runs(off, runs, g.n)
+        assert mv.shape == (len(targets), (g.n + 7) // 8)
+        off2, runs2 = oracle.runs_from_moves(mv, g.n)
+        np.testing.assert_array_equal(off2, off, err_msg=name)
+        np.testing.assert_array_equal(runs2, runs, err_msg=name)
+
+
 def _ka_graph(case):
     from graphs import graph_from_edges
     return graph_from_edges(case["n"], [tuple(e) for e in case["edges"]])
