@@ -164,7 +164,10 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
     PinnedWords hv;
     CH_HIP(hipHostMalloc(reinterpret_cast<void**>(&hv.p), 64 * sizeof(uint32_t), hipHostMallocDefault));
 
-    size_t arena_cap = std::max<size_t>(16ull * M, 1u << 22);  // arcs
+    // arena offsets are 32-bit (the merge kernel takes them as u32)
+    CPD_REQUIRE(2ull * M < (1ull << 32), CPD_E_RANGE, "GPU contraction: graph has >= 2^31 arcs");
+    size_t arena_cap = std::min<size_t>(std::max<size_t>(16ull * M, 1u << 22),
+                                        (1ull << 32) - 1);  // arcs
     DBuf<uint32_t> arena, arena2;
     arena.ensure(2 * arena_cap);
     CH_HIP(hipMemcpyAsync(arena.p, arena0.data(), arena0.size() * 4, hipMemcpyHostToDevice, st));
@@ -283,6 +286,10 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
         searches += np;
         double tw = now_seconds();
         if (np > wave_max) {
+            if ((uint64_t)tag1 + np + 1 >= (1ull << 32)) {  // tags would wrap: clear the tables
+                CH_HIP(hipMemsetAsync(ws1.p, 0, ws1.n, st));
+                tag1 = 0;
+            }
             chk::launch_witness(pairs.p, nullptr, np, overlay(), state.p, contract, settle, ws1.p,
                                 caps1, lanes1, tag1, no_wave ? 0xFFFFFFFFu : lane_cap, slots.p,
                                 sflag.p, sc.p, ovf.p, ctr.p, ctr.p + 1, st);
@@ -325,11 +332,13 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
                     "GPU contraction: witness workspace too large");
         const chk::WitnessCaps caps2{(uint32_t)hash, (uint32_t)heap, std::max(maxdeg, 1u)};
         const uint64_t lb2 = chk::witness_lane_bytes(caps2);
+        // as many lanes as searches (whole waves), at most what 8 GB holds;
+        // the kernel strides over the searches when there are fewer lanes
         const uint64_t budget = 8ull << 30;
         const uint32_t lanes2 =
-            (uint32_t)std::max<uint64_t>(256, std::min<uint64_t>((novf + 255) / 256 * 256,
-                                                                 budget / lb2 / 256 * 256));
-        if (ws2.n < lb2 * lanes2) {
+            (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>((novf + 63) / 64 * 64,
+                                                                budget / lb2 / 64 * 64));
+        if (ws2.n < lb2 * lanes2 || (uint64_t)tag2 + novf + 1 >= (1ull << 32)) {
             ws2.ensure(lb2 * lanes2);
             CH_HIP(hipMemsetAsync(ws2.p, 0, ws2.n, st));
             tag2 = 0;
@@ -454,6 +463,7 @@ Hierarchy build_hierarchy_gpu(uint32_t n, const uint32_t* row_ptr, const uint32_
         bk_o.ensure(2ull * std::max(K, 1u));
         bk_i.ensure(2ull * std::max(K, 1u));
         chk::launch_fill_buckets(sclist.p, K, bo_o.p, bo_i.p, cur_o.p, cur_i.p, bk_o.p, bk_i.p, st);
+        CPD_REQUIRE(top + to + ti < (1ull << 32), CPD_E_RANGE, "GPU contraction: overlay too large");
         chk::launch_merge(Al.p, nA, d_ooff.p, d_odeg.p, d_ioff.p, d_ideg.p, arena.p, state.p,
                           s[0].p, s[1].p, (uint32_t)top, (uint32_t)(top + to), bo_o.p, bo_i.p,
                           cnt_o.p, cnt_i.p, bk_o.p, bk_i.p, ctr.p + 2, st);

@@ -969,8 +969,10 @@ void launch_witness(const uint32_t* pairs, const uint32_t* plist, uint32_t np, O
                     uint32_t* slots, uint32_t* sflag, uint32_t* sc, uint32_t* ovf,
                     uint32_t* ovf_n, uint32_t* err, hipStream_t s) {
     if (!np) return;
-    const uint32_t l = std::min<uint32_t>(lanes, ((np + 255u) / 256u) * 256u);
-    hipLaunchKernelGGL(k_witness, dim3(l / 256u), dim3(256), 0, s,
+    // lanes: a multiple of 64 (whole waves; 256-thread blocks when it allows)
+    const uint32_t l = std::min<uint32_t>(lanes, ((np + 63u) / 64u) * 64u);
+    const uint32_t tpb = l % 256u == 0 ? 256u : 64u;
+    hipLaunchKernelGGL(k_witness, dim3(l / tpb), dim3(tpb), 0, s,
                        reinterpret_cast<const uint4*>(pairs), plist, np, g, state,
                        contract ? 1u : 0u, settle, static_cast<uint8_t*>(ws), caps,
                        witness_lane_bytes(caps), tag_base, step_cap,

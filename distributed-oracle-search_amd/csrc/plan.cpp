@@ -111,10 +111,25 @@ int cpd_plan_create(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t
         if (!(opts && opts->no_hierarchy)) {
             double t0 = now_seconds();
             try {
-                p->ch = opts && opts->ch_gpu
-                            ? build_hierarchy_gpu(n, row_ptr, dst, w, opts->ch_device, settle,
-                                                  verbose)
-                            : build_hierarchy(n, row_ptr, dst, w, threads, settle, verbose);
+                if (opts && opts->ch_gpu) {
+                    try {
+                        p->ch = build_hierarchy_gpu(n, row_ptr, dst, w, opts->ch_device, settle,
+                                                    verbose);
+                    } catch (const Error& e) {
+                        // the GPU contraction ran out of device memory or
+                        // failed at run time: the host build gives the same
+                        // hierarchy.  No device at all stays an
+                        // error (ch_gpu asks for the GPU).
+                        const bool no_device =
+                            std::string(e.what()).find("no HIP device") != std::string::npos;
+                        if (!(e.code == CPD_E_OOM || (e.code == CPD_E_HIP && !no_device))) throw;
+                        std::fprintf(stderr, "[cpd] GPU contraction failed (%s); contracting on "
+                                             "host threads\n", e.what());
+                        p->ch = build_hierarchy(n, row_ptr, dst, w, threads, settle, verbose);
+                    }
+                } else {
+                    p->ch = build_hierarchy(n, row_ptr, dst, w, threads, settle, verbose);
+                }
             } catch (...) {
                 ch_err = std::current_exception();
             }

@@ -2,9 +2,9 @@
 # One GPU call on the current tree: the full -m gpu suite, smoke(), the
 # driver's default bench line (with the end-to-end worker build), and a
 # rocprofv3 kernel-trace --stats of the bench workload.
-#   tools_scripts/gpu_r03.sh TAG [skip-tests] [skip-prof]
+#   tools_scripts/gpu_round.sh TAG [skip-tests] [skip-prof]
 set -o pipefail
-TAG=${1:-r03}
+TAG=${1:-round}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$PWD
