@@ -121,7 +121,7 @@ int cpd_plan_create(const uint32_t* row_ptr, const uint32_t* dst, const uint32_t
                         // hierarchy.  No device at all stays an
                         // error (ch_gpu asks for the GPU).
                         const bool no_device =
-                            std::string(e.what()).find("no HIP device") != std::string::npos;
+                            std::string(e.what()).find("no GPU visible") != std::string::npos;
                         if (!(e.code == CPD_E_OOM || (e.code == CPD_E_HIP && !no_device))) throw;
                         std::fprintf(stderr, "[cpd] GPU contraction failed (%s); contracting on "
                                              "host threads\n", e.what());
