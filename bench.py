@@ -395,6 +395,9 @@ def cpu_worker(spec):
     sp = json.loads(spec)
     g = cpd.synth_road_graph(sp["width"], sp["width"], seed=sp["seed"], style=sp["style"])
     order = oracle.dfs_preorder(g.row_ptr, g.dst)
+    if sp.get("kind") == "search":
+        cpu_search_leg(sp, g, order)
+        return
     rng = np.random.default_rng(sp.get("qseed", 10 + sp.get("wid", 0)))
     if sp.get("targets_npy"):
         targets = np.load(sp["targets_npy"]).astype(np.uint32)
@@ -412,6 +415,38 @@ def cpu_worker(spec):
     print(json.dumps({"rows_s": t1 - t0, "queries_s": t2 - t1, "rows": len(targets),
                       "queries": len(s), "runs": int(off[-1]), "hops": int(hops.sum()),
                       "n": g.n, "m": g.m}), flush=True)
+
+
+def cpu_search_leg(sp, g, order):
+    """CPD-heuristic search on the host: the oracle's
+    ora_cpd_search (the restated warthog cpd_search, OpenMP over queries) on
+    the bench's 256 search rows and .diff stand-in weights, for each leg the
+    first queries of the GPU's query list in chunks until a time budget is
+    spent (so the default bench stays within minutes); q/s = queries done /
+    their time."""
+    import numpy as np
+    import cpd
+    import oracle
+    srows = np.load(sp["targets_npy"]).astype(np.uint32)
+    q = np.load(sp["queries_npy"]).astype(np.uint32)
+    s, t = q[0], q[1]
+    w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
+    off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, srows, threads=sp["threads"])
+    out = {}
+    for leg in sp["legs"]:
+        done, secs, expanded = 0, 0.0, 0
+        while done < leg["queries"] and secs < leg["budget_s"]:
+            k = min(leg["chunk"], leg["queries"] - done)
+            t0 = time.perf_counter()
+            _, _, _, st = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, order, srows, off, runs,
+                                            s[done:done + k], t[done:done + k],
+                                            fscale=leg["fscale"], threads=sp["threads"])
+            secs += time.perf_counter() - t0
+            expanded += int(st[:, 0].sum())
+            done += k
+        out[leg["name"]] = {"queries": done, "s": secs, "queries_per_s": done / secs if secs else 0.0,
+                            "mean_expanded": expanded / max(1, done)}
+    print(json.dumps(out), flush=True)
 
 
 def run_cpu_worker(spec, threads, timeout=900):
@@ -773,7 +808,15 @@ def main():
     ix.set_weights(w_cong)
     q_cong, q_cong_ms = time_queries("auto")
     ix.set_weights(None)
-    del ix, rows  # HBM for the search tables (the batch's runs + index: ~120 GB at 20k rows)
+    del ix, rows
+    # The build's batch buffers (~190 GB at 1M nodes) are not used past this
+    # point: the search, CPU-baseline and parity legs run on a graph with
+    # 1024-row batches, which leaves the HBM to the search workspaces.
+    import gc
+    del dev
+    gc.collect()
+    dev = cpd.Graph(plan, device=gpu, batch=1024)
+    dev.set_coords(g.x, g.y)
     # CPD-heuristic search leg: 256 rows of the index, the
     # .diff stand-in weights, hscale 1 / fscale 0.1 (10%-bounded: at fscale 0
     # a 1M-node search inserts up to ~235k nodes, a lane-serial search's
@@ -801,19 +844,27 @@ def main():
                   "form": {1: "per-row tables", 2: "memoised walks"}[sst["tables"]],
                   "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
         # fscale 0 (optimal under the .diff weights): a 1M-node search expands
-        # ~59k nodes, so fewer queries and a 2^19-column workspace per search
-        zq = 512
-        zs, zt = ss[:zq], st_[:zq]
-        six.search(zs[:64], zt[:64], capacity=1 << 19)  # warm
-        _, _, zfin, zcnt, zst = six.search(zs, zt, capacity=1 << 19)
+        # ~48k nodes into a 2^19-column workspace (36 MB per lane with
+        # tables); as many searches as lanes fit in 60% of the free HBM run at
+        # once (round 3 ran 512)
+        cap0 = 1 << 19
+        free_b, _ = cpd.device_mem_info(gpu)
+        zq = int(max(512, min(8192, (0.6 * free_b / (68 * cap0)) // 256 * 256)))
+        zs = rng.integers(0, g.n, zq).astype(np.uint32)
+        zt = srows[rng.integers(0, len(srows), zq)]
+        six.search(zs[:64], zt[:64], capacity=cap0)  # warm
+        _, _, zfin, zcnt, zst = six.search(zs, zt, capacity=cap0, workspace_frac=0.6)
         ztot = comm.reduce([float(zq), zst["kernel_ms"]], "SUM")
         (zmax,) = comm.reduce([zst["kernel_ms"]], "MAX")
         search["fscale0"] = {
             "queries_per_s": round(ztot[0] / (zmax / 1e3), 1) if zmax else 0.0,
-            "queries": zq, "capacity": 1 << 19, "lanes": int(zst["lanes"]),
+            "queries": zq, "capacity": cap0, "lanes": int(zst["lanes"]),
             "mean_expanded": round(float(zcnt[:, 0].mean()), 1),
             "finished": int(zfin.sum()), "overflow": int(zst["overflow"]),
-            "kernel_ms": round(zst["kernel_ms"], 3)}
+            "kernel_ms": round(zst["kernel_ms"], 3),
+            # per-lane latency: one search's expansions in series
+            "us_per_expansion_per_lane": round(zst["kernel_ms"] * 1e3 * int(zst["lanes"]) /
+                                               max(1.0, float(zcnt[:, 0].sum())), 2)}
         # the fscale-0.1 queries with the memoised-walk form (what a
         # worker-sized index, whose tables do not fit, runs)
         _, _, _, _, wsst = six.search(ss[:4096], st_[:4096], fscale=0.1, tables="walks")
@@ -821,7 +872,7 @@ def main():
             "queries": 4096, "lanes": int(wsst["lanes"]), "fscale": 0.1,
             "queries_per_s": round(4096 / (wsst["kernel_ms"] / 1e3), 1) if wsst["kernel_ms"]
             else 0.0}
-        search_sample = (six, ss[:2000], st_[:2000], srows)
+        search_sample = (six, ss[:2000], st_[:2000], srows, ss, st_, zs, zt)
     # walk kernel vs its roofline: per query 8 (s, t) + 4 (row) + 13 (cost,
     # moves, flag) bytes, per move the 4-B word holding the move + the 8-B edge
     qbytes = 25.0 * q_totals[0] + 12.0 * q_totals[2]
@@ -873,7 +924,38 @@ def main():
             parity = parity and bool(np.array_equal(gc_, rc) and np.array_equal(gh, rh))
         del gix, grows
         if search:
-            six, ss2, st2, srows = search_sample
+            six, ss2, st2, srows, ss_all, st_all, zs, zt = search_sample
+            # the same searches on the host (child process, every job thread)
+            snpy = os.path.join(args.cache, f"cpu-search-{os.getpid()}.npy")
+            qnpy = os.path.join(args.cache, f"cpu-search-q-{os.getpid()}.npy")
+            np.save(snpy, srows)
+            try:
+                legs = []
+                for name, qs_, qt_, fs, chunk, budget in (("fscale0.1", ss_all, st_all, 0.1, 500, 8.0),
+                                                          ("fscale0", zs, zt, 0.0, 2 * threads, 12.0)):
+                    np.save(qnpy, np.stack([qs_, qt_]))
+                    r = collect(run_cpu_worker({"kind": "search", "width": args.width,
+                                                "seed": args.seed, "style": args.style,
+                                                "targets_npy": snpy, "queries_npy": qnpy,
+                                                "legs": [{"name": name, "fscale": fs,
+                                                          "queries": len(qs_), "chunk": chunk,
+                                                          "budget_s": budget}]}, threads))
+                    legs.append(r[name])
+                gpu_q = (search["queries_per_s"], search["fscale0"]["queries_per_s"])
+                search["cpu_baseline"] = {
+                    "kind": "port", "cores": threads,
+                    "what": "oracle ora_cpd_search (restated cpd_search, OpenMP over queries) in "
+                            "a child process, the GPU legs' first queries until a time budget",
+                    "fscale0.1": dict(legs[0], gpu_over_cpu=round(gpu_q[0] / legs[0]["queries_per_s"], 2)
+                                      if legs[0]["queries_per_s"] else None),
+                    "fscale0": dict(legs[1], gpu_over_cpu=round(gpu_q[1] / legs[1]["queries_per_s"], 2)
+                                    if legs[1]["queries_per_s"] else None)}
+            except Exception as e:  # reported, never fatal to the GPU numbers
+                search["cpu_baseline"] = {"error": str(e)[-300:]}
+            finally:
+                for f in (snpy, qnpy):
+                    if os.path.exists(f):
+                        os.remove(f)
             sref = oracle.build_rows(g.row_ptr, g.dst, g.w, order, srows, threads=threads)
             rc, rp, rf, rs = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, order, srows,
                                                sref[0], sref[1], ss2, st2, fscale=0.1,

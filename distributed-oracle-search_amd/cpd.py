@@ -87,7 +87,8 @@ class QueryStats(C.Structure):
 class SearchOpts(C.Structure):
     _fields_ = [("hscale", C.c_double), ("fscale", C.c_double), ("k_moves", C.c_int32),
                 ("itrs", C.c_int64), ("time_ns", C.c_uint64), ("capacity", C.c_uint32),
-                ("virtual_tick_ns", C.c_uint64), ("tables", C.c_int32)]
+                ("virtual_tick_ns", C.c_uint64), ("tables", C.c_int32),
+                ("workspace_frac", C.c_double)]
 
 
 class SearchStats(C.Structure):
@@ -578,12 +579,13 @@ class Index:
         return {k: getattr(st, k) for k, _ in QueryStats._fields_}
 
     def search(self, s, t, hscale=1.0, fscale=0.0, k_moves=-1, itrs=-1, time_ns=0,
-               capacity=0, virtual_tick_ns=0, tables="auto"):
+               capacity=0, virtual_tick_ns=0, tables="auto", workspace_frac=0.0):
         """CPD-heuristic search (cpd_query_search) for queries (s, t):
         (cost, plen, finished, counters[nq, 5], stats)."""
         self.prepare(s, t)
         o = SearchOpts(float(hscale), float(fscale), int(k_moves), int(itrs), int(time_ns),
-                       int(capacity), int(virtual_tick_ns), SEARCH_FORMS[tables])
+                       int(capacity), int(virtual_tick_ns), SEARCH_FORMS[tables],
+                       float(workspace_frac))
         st = SearchStats()
         _check(lib.cpd_query_search(self._h, C.byref(o), C.byref(st)))
         nq = len(s)

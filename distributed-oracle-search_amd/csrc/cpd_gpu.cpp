@@ -2133,7 +2133,7 @@ void cpd_index_free(cpd_index* ix) {
 int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st) {
     return guarded([&] {
         CPD_REQUIRE(ix, CPD_E_ARG, "null index");
-        cpd_search_opts o{1.0, 0.0, -1, -1, 0, 0, 0, CPD_SEARCH_AUTO};
+        cpd_search_opts o{1.0, 0.0, -1, -1, 0, 0, 0, CPD_SEARCH_AUTO, 0.0};
         if (opts) o = *opts;
         if (!o.capacity) o.capacity = 32768;
         CPD_REQUIRE((o.capacity & (o.capacity - 1)) == 0 && o.capacity >= 64 &&
@@ -2141,6 +2141,9 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
                     CPD_E_ARG, "search capacity must be a power of 2 in [64, 2^24]");
         CPD_REQUIRE(o.hscale >= 0.0 && o.fscale >= 0.0, CPD_E_ARG,
                     "hscale and fscale must be >= 0");
+        CPD_REQUIRE(o.workspace_frac >= 0.0 && o.workspace_frac <= 0.9, CPD_E_ARG,
+                    "workspace_frac must be in [0, 0.9]");
+        const double wfrac = o.workspace_frac > 0.0 ? o.workspace_frac : 0.25;
         CPD_REQUIRE(ix->added == ix->nrows, CPD_E_ARG, "search: index incomplete");
         CPD_REQUIRE(o.tables == CPD_SEARCH_AUTO || o.tables == CPD_SEARCH_TABLES ||
                         o.tables == CPD_SEARCH_WALKS,
@@ -2194,14 +2197,15 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
         }
         // workspace per lane slot: search_ws_bytes_per_slot(capacity, tables)
         // (68 B per column of capacity with tables, 116 B with walks); as many
-        // slots (whole blocks of 4 waves) as a quarter of free HBM holds
+        // slots (whole blocks of 4 waves) as wfrac of the free HBM holds
         uint32_t slots = nq ? search_slots(nq) : 0u;
         const size_t per_slot = search_ws_bytes_per_slot(o.capacity, tables);
         if (nq) {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
             const size_t per_block = 256ull * per_slot;
-            const size_t fit = std::max<size_t>(1, (free_b / 4 + ix->sws.n) / per_block);
+            const size_t fit =
+                std::max<size_t>(1, (size_t)(wfrac * (double)(free_b + ix->sws.n)) / per_block);
             CPD_REQUIRE((free_b + ix->sws.n) / 2 >= per_block, CPD_E_OOM,
                         "search workspace of 256 lanes x capacity does not fit in HBM");
             slots = (uint32_t)std::min<size_t>(slots, fit * 256u);

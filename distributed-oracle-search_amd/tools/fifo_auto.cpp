@@ -316,7 +316,7 @@ int main(int argc, char** argv) {
         bool debug = json_field(conf, "debug") == "true";
         // cpd-search knobs (process_query.py:149-160): hscale, fscale, time
         // (ns; args.get_time_ns may send a float), itrs
-        cpd_search_opts so{1.0, 0.0, k_moves, -1, 0, 0, 0, CPD_SEARCH_AUTO};  // wall-clock time limit
+        cpd_search_opts so{1.0, 0.0, k_moves, -1, 0, 0, 0, CPD_SEARCH_AUTO, 0.0};  // wall-clock time limit
         if (!json_field(conf, "hscale").empty()) so.hscale = std::atof(json_field(conf, "hscale").c_str());
         if (!json_field(conf, "fscale").empty()) so.fscale = std::atof(json_field(conf, "fscale").c_str());
         if (!json_field(conf, "itrs").empty()) so.itrs = std::atoll(json_field(conf, "itrs").c_str());

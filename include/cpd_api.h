@@ -383,6 +383,8 @@ typedef struct cpd_search_opts {
     uint32_t capacity;     /* columns per search, power of 2 (0 = 32768) */
     uint64_t virtual_tick_ns; /* 0: wall-clock time limit; else virtual clock */
     int32_t  tables;       /* CPD_SEARCH_AUTO / _TABLES / _WALKS             */
+    double   workspace_frac; /* share of the free HBM the lanes' workspaces may
+                                take (0 = 0.25); more lanes search at once   */
 } cpd_search_opts;
 
 typedef struct cpd_search_stats {
