@@ -803,6 +803,17 @@ def main():
         q_rle, q_rle_ms = time_queries("rle")
     q_totals, q_ms_max = time_queries("auto")
     index_mode = ix.mode
+    # end to end: host arrays in, host arrays out —
+    # cpd_query_batch = prepare (upload, target sort on the GPU) + walk +
+    # fetch (results back in caller order), by the host clock
+    ix.query(qs, qt)  # warm
+    te = time.perf_counter()
+    for _ in range(3):
+        ix.query(qs, qt)
+    e2e_s = time.perf_counter() - te
+    (e2e_max,) = comm.reduce([e2e_s], "MAX")
+    (e2e_q,) = comm.reduce([float(3 * nq)], "SUM")
+    ix.prepare(qs, qt)
     # congested leg (configs[2]): the .diff stand-in of SURVEY.md §8d — 10% of
     # edges x U[1, 3], rounded up — sent with the batch as fifo_auto does
     ix.set_weights(w_cong)
@@ -1039,6 +1050,10 @@ def main():
             out["queries_per_s_rle"] = round(q_rle[0] / (q_rle_ms / 1e3), 1)
         out["queries_per_s_congested"] = (round(q_cong[0] / (q_cong_ms / 1e3), 1)
                                           if q_cong_ms else 0.0)
+        out["queries_per_s_e2e"] = round(e2e_q / e2e_max, 1) if e2e_max else 0.0
+        out["queries_e2e_note"] = ("cpd_query_batch by the host clock: (s, t) upload, target sort "
+                                   "and gather on the GPU, walk, results scattered back and "
+                                   "copied out")
         out.update(extra)
         print(json.dumps(out), flush=True)
     if world > 1:

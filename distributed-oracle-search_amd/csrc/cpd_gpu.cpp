@@ -110,6 +110,7 @@ struct cpd_graph {
     uint32_t n = 0, m = 0, npad = 0;
     std::vector<uint32_t> order;       // node -> column
     std::vector<uint32_t> inv;         // column -> node
+    DevBuf<uint32_t> order_d;          // node -> column (query preparation)
     std::vector<uint32_t> edge_perm;   // column-space edge -> file edge
     std::vector<uint32_t> w_free_col;  // free-flow weights, column-space edges
     std::vector<uint32_t> rowc_host;   // column-space row_ptr (host copy)
@@ -545,9 +546,11 @@ struct cpd_index {
     DevBuf<unsigned long long> sagg;
     bool h_ready = false, c_ready = false;
     bool searched = false;  // qstats hold the counters of the prepared queries
-    // query workspace; queries run sorted by target row (perm[i] = caller index)
+    // query workspace; queries run sorted by target row (qperm[i] = caller
+    // index of sorted query i), all of it prepared on the GPU
     uint32_t nq = 0;
-    std::vector<uint32_t> perm;
+    DevBuf<uint32_t> qin_s, qin_t, qkey, qkey2, qval, qperm, qbad;
+    DevBuf<uint8_t> qsort_tmp, qout;
     DevBuf<uint32_t> qs, qt, qrow, hops;
     DevBuf<uint64_t> cost;
     DevBuf<uint8_t> fin;
@@ -757,6 +760,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         while ((1u << g->adj_shift) < maxdeg) ++g->adj_shift;
         g->fmb = fm_bits(g->adj_shift);
         hipStream_t s = g->stream;
+        g->order_d.upload(g->order.data(), n, s);
         g->row_ptr.upload(g->rowc_host.data(), n + 1, s);
         g->dst.upload(dstc.data(), m, s);
         g->w.upload(g->w_free_col.data(), m, s);
@@ -1962,37 +1966,48 @@ int cpd_query_prepare(cpd_index* ix, const uint32_t* s, const uint32_t* t, uint3
                         std::to_string(ix->nrows) + " rows appended)");
         cpd_graph* g = ix->g;
         g->select();
-        // counting sort by target row: a wave's lanes then walk the same row
-        std::vector<uint32_t> bucket(ix->nrows + 1, 0);
-        for (uint32_t q = 0; q < nq; ++q) {
-            CPD_REQUIRE(s[q] < g->n && t[q] < g->n, CPD_E_ARG, "query node out of range");
-            uint32_t r = ix->row_of_col[g->order[t[q]]];
-            if (r == CPD_INF)
-                throw Error(CPD_E_NOROW, "target " + std::to_string(t[q]) +
-                                             " has no CPD row in this index");
-            bucket[r + 1]++;
-        }
-        for (uint32_t r = 0; r < ix->nrows; ++r) bucket[r + 1] += bucket[r];
-        ix->perm.resize(nq);
-        std::vector<uint32_t> sc(nq), tc(nq), rq(nq);
-        for (uint32_t q = 0; q < nq; ++q) {
-            uint32_t tcol = g->order[t[q]];
-            const uint32_t row = ix->row_of_col[tcol];
-            uint32_t i = bucket[row]++;
-            ix->perm[i] = q;
-            tc[i] = tcol;
-            sc[i] = g->order[s[q]];
-            rq[i] = row;
-        }
-        ix->qs.upload(sc.data(), nq, g->stream);
-        ix->qt.upload(tc.data(), nq, g->stream);
-        ix->qrow.upload(rq.data(), nq, g->stream);
-        ix->cost.alloc(nq);
-        ix->hops.alloc(nq);
-        ix->fin.alloc(nq);
-        ix->nq = nq;
+        hipStream_t st = g->stream;
+        // on the GPU: columns and target rows of the queries, a stable radix
+        // sort by row (a wave's lanes then walk the same row), the sorted
+        // columns; the caller's order comes back in cpd_query_fetch
+        ix->nq = 0;
         ix->searched = false;
-        HIP_CHECK(hipStreamSynchronize(g->stream));
+        const size_t m = std::max<uint32_t>(nq, 1u);
+        for (DevBuf<uint32_t>* b : {&ix->qin_s, &ix->qin_t, &ix->qkey, &ix->qkey2, &ix->qval,
+                                    &ix->qperm, &ix->qs, &ix->qt, &ix->qrow, &ix->hops})
+            b->alloc(m);
+        ix->qbad.alloc(1);
+        ix->cost.alloc(m);
+        ix->fin.alloc(m);
+        if (nq) {
+            HIP_CHECK(hipMemcpyAsync(ix->qin_s.p, s, nq * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipMemcpyAsync(ix->qin_t.p, t, nq * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+            HIP_CHECK(hipMemsetAsync(ix->qbad.p, 0, sizeof(uint32_t), st));
+            launch_query_keys(ix->qin_s.p, ix->qin_t.p, nq, g->n, g->order_d.p, ix->d_row_of_col.p,
+                              ix->qkey.p, ix->qval.p, ix->qbad.p, st);
+            HIP_CHECK(hipGetLastError());
+            uint32_t bad = 0;
+            HIP_CHECK(hipMemcpyAsync(&bad, ix->qbad.p, sizeof bad, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            if (bad) {  // name the first offending query (error path only)
+                for (uint32_t q = 0; q < nq; ++q) {
+                    CPD_REQUIRE(s[q] < g->n && t[q] < g->n, CPD_E_ARG, "query node out of range");
+                    if (ix->row_of_col[g->order[t[q]]] == CPD_INF)
+                        throw Error(CPD_E_NOROW, "target " + std::to_string(t[q]) +
+                                                     " has no CPD row in this index");
+                }
+            }
+            const size_t tb = query_sort_bytes(nq);
+            ix->qsort_tmp.alloc(tb);
+            launch_query_sort(ix->qsort_tmp.p, ix->qsort_tmp.n, ix->qkey.p, ix->qkey2.p, ix->qval.p,
+                              ix->qperm.p, nq, std::max(1u, ix->nrows), st);
+            HIP_CHECK(hipGetLastError());
+            launch_query_gather(ix->qin_s.p, ix->qin_t.p, g->order_d.p, ix->qkey2.p, ix->qperm.p,
+                                nq, ix->qs.p, ix->qt.p, ix->qrow.p, st);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipStreamSynchronize(st));
+        }
+        ix->nq = nq;
     });
 }
 
@@ -2097,18 +2112,30 @@ int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
 int cpd_query_fetch(cpd_index* ix, uint64_t* cost, uint32_t* hops, uint8_t* finished) {
     return guarded([&] {
         CPD_REQUIRE(ix, CPD_E_ARG, "null index");
-        ix->g->select();
+        cpd_graph* g = ix->g;
+        g->select();
         const uint32_t nq = ix->nq;
-        // results come back in target-sorted order; undo the permutation
-        auto fetch = [&](auto* out, auto* dev) {
-            using T = std::remove_pointer_t<decltype(out)>;
-            std::vector<T> tmp(nq);
-            HIP_CHECK(hipMemcpy(tmp.data(), dev, nq * sizeof(T), hipMemcpyDeviceToHost));
-            for (uint32_t i = 0; i < nq; ++i) out[ix->perm[i]] = tmp[i];
-        };
-        if (cost && nq) fetch(cost, ix->cost.p);
-        if (hops && nq) fetch(hops, ix->hops.p);
-        if (finished && nq) fetch(finished, ix->fin.p);
+        if (!nq) return;
+        // results come back in target-sorted order: scattered to the
+        // caller's order on the GPU, then copied out
+        hipStream_t st = g->stream;
+        ix->qout.alloc((size_t)nq * 8u);
+        if (cost) {
+            launch_scatter_u64(ix->cost.p, ix->qperm.p, nq, reinterpret_cast<uint64_t*>(ix->qout.p), st);
+            HIP_CHECK(hipMemcpyAsync(cost, ix->qout.p, nq * 8ull, hipMemcpyDeviceToHost, st));
+        }
+        if (hops) {
+            HIP_CHECK(hipStreamSynchronize(st));  // qout is reused
+            launch_scatter_u32(ix->hops.p, ix->qperm.p, nq, 1u, reinterpret_cast<uint32_t*>(ix->qout.p), st);
+            HIP_CHECK(hipMemcpyAsync(hops, ix->qout.p, nq * 4ull, hipMemcpyDeviceToHost, st));
+        }
+        if (finished) {
+            HIP_CHECK(hipStreamSynchronize(st));
+            launch_scatter_u8(ix->fin.p, ix->qperm.p, nq, ix->qout.p, st);
+            HIP_CHECK(hipMemcpyAsync(finished, ix->qout.p, nq, hipMemcpyDeviceToHost, st));
+        }
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipStreamSynchronize(st));
     });
 }
 
@@ -2265,11 +2292,13 @@ int cpd_query_search_counters(cpd_index* ix, uint32_t* counters) {
         CPD_REQUIRE(ix->searched && ix->qstats.n >= 5ull * nq, CPD_E_ARG,
                     "no search has run on these queries (cpd_query_prepare since, or only "
                     "table-search)");
-        std::vector<uint32_t> tmp(5ull * nq);
-        HIP_CHECK(hipMemcpy(tmp.data(), ix->qstats.p, tmp.size() * sizeof(uint32_t),
-                            hipMemcpyDeviceToHost));
-        for (uint32_t i = 0; i < nq; ++i)
-            std::memcpy(counters + 5ull * ix->perm[i], tmp.data() + 5ull * i, 5 * sizeof(uint32_t));
+        hipStream_t st = ix->g->stream;
+        ix->qout.alloc(20ull * nq);
+        launch_scatter_u32(ix->qstats.p, ix->qperm.p, nq, 5u, reinterpret_cast<uint32_t*>(ix->qout.p),
+                           st);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(counters, ix->qout.p, 20ull * nq, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
     });
 }
 

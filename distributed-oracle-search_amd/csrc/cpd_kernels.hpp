@@ -158,6 +158,29 @@ uint32_t expand_chunk_runs();
 void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, const uint32_t* chunk_first,
                         uint32_t nrows, uint32_t total_chunks, uint32_t npad, uint32_t* dense,
                         hipStream_t s);
+// Query batches on the GPU (cpd_query_prepare / _fetch): key[q] = row of
+// t[q]'s column (row_of_col[order[t[q]]]), val[q] = q, *bad |= 1 for a node
+// >= n, 2 for a target without a row; a stable radix sort of (key, val) by
+// the low ceil(log2 nrows) bits (tmp: query_sort_bytes(nq) bytes); the
+// sorted queries' columns and rows; results back to the caller's order
+// (out[perm[i] * k + j] = in[i * k + j]).
+void launch_query_keys(const uint32_t* s, const uint32_t* t, uint32_t nq, uint32_t n,
+                       const uint32_t* order, const uint32_t* row_of_col, uint32_t* key,
+                       uint32_t* val, uint32_t* bad, hipStream_t st);
+size_t query_sort_bytes(uint32_t nq);
+void launch_query_sort(void* tmp, size_t tmp_bytes, const uint32_t* key_in, uint32_t* key_out,
+                       const uint32_t* val_in, uint32_t* val_out, uint32_t nq, uint32_t nrows,
+                       hipStream_t st);
+void launch_query_gather(const uint32_t* s, const uint32_t* t, const uint32_t* order,
+                         const uint32_t* key, const uint32_t* val, uint32_t nq, uint32_t* qs,
+                         uint32_t* qt, uint32_t* qrow, hipStream_t st);
+void launch_scatter_u64(const uint64_t* in, const uint32_t* perm, uint32_t nq, uint64_t* out,
+                        hipStream_t st);
+void launch_scatter_u32(const uint32_t* in, const uint32_t* perm, uint32_t nq, uint32_t k,
+                        uint32_t* out, hipStream_t st);
+void launch_scatter_u8(const uint8_t* in, const uint32_t* perm, uint32_t nq, uint8_t* out,
+                       hipStream_t st);
+
 // table-search over dense move tables.  qs / qt: query columns, sorted by
 // target row; qrow[q]: the row of query q's target (row_of_col is unused).
 void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
