@@ -518,7 +518,7 @@ def full_build_dir(args, world):
     return os.path.join(args.cache, f"fb-out-{world}")
 
 
-def full_build(args, xy, world, rank, device, comm):
+def full_build(args, xy, world, rank, device, comm, runner=subprocess.run):
     """Run make_cpd_auto for worker `rank` of full_build_workers() with a
     fresh (cold) plan cache shared by the node's ranks; returns its JSON phase
     line.  Rank 0 writes its bucket files (DOSCPD02) into the cache directory
@@ -543,8 +543,7 @@ def full_build(args, xy, world, rank, device, comm):
            str(device), "--format", "moves"] + ([] if write else ["--discard"])
     if args.batch:
         cmd += ["--batch", str(args.batch)]
-    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                       timeout=900)
+    p = runner(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
     if p.returncode:
         raise RuntimeError(f"make_cpd_auto failed: {p.stderr[-400:]}")
     line = next(l for l in p.stdout.splitlines() if l.startswith("make_cpd_auto-json: "))
@@ -553,6 +552,29 @@ def full_build(args, xy, world, rank, device, comm):
         rec["files_bytes"] = sum(os.path.getsize(os.path.join(outdir, f))
                                  for f in os.listdir(outdir) if f.endswith(".cpd"))
     return rec
+
+
+def full_build_leg(args, xy, world, rank, device, comm, runner=subprocess.run):
+    """full_build() on every rank, then the node's figures: the slowest
+    worker's time, rows / runs / exported bytes summed over ranks (rank 0's
+    phase record kept whole)."""
+    rec = full_build(args, xy, world, rank, device, comm, runner)
+    (tmax,) = comm.reduce([rec["total_s"]], "MAX")
+    tot = comm.reduce([float(rec["rows"]), float(rec["runs"]), float(rec["export_bytes"])], "SUM")
+    W = full_build_workers(args, world)
+    fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of {W} ({args.partmethod} "
+                  f"{args.partkey}), one worker per rank: all its rows, cold plan cache, "
+                  "compact bucket files (DOSCPD02) written by rank 0, --discard (D2H export "
+                  "only) on the other ranks",
+          "total_s": round(tmax, 3), "rows": int(tot[0]), "runs": int(tot[1]),
+          "rows_per_s_end_to_end": round(tot[0] / tmax, 1) if tmax else 0.0,
+          "export_GB": round(tot[2] / 1e9, 2),
+          "rank0": rec,
+          "rank0_export_GBps": round(rec["export_bytes"] / rec["export_span_s"] / 1e9, 2)
+          if rec.get("export_span_s") else None}
+    if "files_bytes" in rec:
+        fb["files_GB"] = round(rec["files_bytes"] / 1e9, 2)
+    return fb, rec
 
 
 def _read_ready(p, deadline):
@@ -1008,23 +1030,9 @@ def main():
         gc.collect()
         comm.barrier()
         fb_xy = fb_xy or glob_xy(args)  # local rank 0 wrote it before the first barrier
-        rec = full_build(args, fb_xy, world, rank, gpu, comm)
-        (tmax,) = comm.reduce([rec["total_s"]], "MAX")
-        tot = comm.reduce([float(rec["rows"]), float(rec["runs"]), float(rec["export_bytes"])],
-                          "SUM")
+        fb, rec = full_build_leg(args, fb_xy, world, rank, gpu, comm)
         W = full_build_workers(args, world)
-        fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of {W} ({args.partmethod} "
-                      f"{args.partkey}), one worker per rank: all its rows, cold plan cache, "
-                      "compact bucket files (DOSCPD02) written by rank 0, --discard (D2H export "
-                      "only) on the other ranks",
-              "total_s": round(tmax, 3), "rows": int(tot[0]), "runs": int(tot[1]),
-              "rows_per_s_end_to_end": round(tot[0] / tmax, 1) if tmax else 0.0,
-              "export_GB": round(tot[2] / 1e9, 2),
-              "rank0": rec,
-              "rank0_export_GBps": round(rec["export_bytes"] / rec["export_span_s"] / 1e9, 2)
-              if rec["export_span_s"] else None}
         if rank == 0 and "files_bytes" in rec:
-            fb["files_GB"] = round(rec["files_bytes"] / 1e9, 2)
             try:
                 fb["serve"] = serve_probe(args, fb_xy, full_build_dir(args, world), W, gpu, g,
                                           plan.order(), host_threads(args))

@@ -67,3 +67,74 @@ def test_two_rank_gloo_aggregation(tmp_path):
     for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "higher_is_better",
               "vs_baseline", "dtype", "data", "config"):
         assert k in out
+
+
+FB_WORKER = r'''
+import json, os, sys, time, types
+sys.path.insert(0, os.environ["ROOT"])
+import torch.distributed as dist
+import bench
+
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+cache = os.environ["CACHE"]
+args = bench.parse(["--width", "40", "--cache", cache])
+comm = bench.Comm(world, rank, rank, device=None)
+if rank == 0:  # a stale directory from an earlier run, with a stale plan cache
+    stale = bench.full_build_dir(args, world)
+    os.makedirs(stale, exist_ok=True)
+    open(os.path.join(stale, "stale.plan"), "w").write("old")
+seen = {}
+
+def fake_make_cpd_auto(cmd, **kw):
+    """Stands in for bin/make_cpd_auto: records what it was asked to do."""
+    a = dict(zip(cmd[1::2], cmd[2::2]))
+    outdir = a["--outdir"]
+    seen.update(cmd=cmd, dir_entries=sorted(os.listdir(outdir)), t=time.time())
+    wid = int(a["--workerid"])
+    if "--discard" not in cmd:
+        open(os.path.join(outdir, f"g-div-8-{wid}.cpd"), "wb").write(b"x" * 1000)
+    rec = {"worker": wid, "maxworker": int(a["--maxworker"]), "rows": 100 + wid, "runs": 1000,
+           "export_bytes": 5000, "export_span_s": 0.5, "total_s": 1.0 + 0.25 * wid}
+    return types.SimpleNamespace(returncode=0, stdout="make_cpd_auto-json: " + json.dumps(rec),
+                                 stderr="")
+
+fb, rec = bench.full_build_leg(args, "/nonexistent.xy", world, rank, 0, comm,
+                               runner=fake_make_cpd_auto)
+allseen = [None] * world
+dist.all_gather_object(allseen, {"cmd": seen["cmd"], "entries": seen["dir_entries"]})
+if rank == 0:
+    print("RESULT " + json.dumps({"fb": fb, "seen": allseen}), flush=True)
+dist.destroy_process_group()
+'''
+
+
+def test_eight_rank_full_build_plumbing(tmp_path):
+    """The end-to-end worker leg at 8 ranks on gloo (the driver's N = 8
+    scaling run, rehearsed on CPU): every rank runs worker r of the div-8
+    partition only after rank 0 has replaced the stale output directory
+    (ADVICE r03: no rank may see the old plan cache), rank 0 writes files
+    and the others --discard, and the node's figures aggregate all ranks."""
+    script = tmp_path / "fb.py"
+    script.write_text(FB_WORKER)
+    env = dict(os.environ, ROOT=ROOT, CACHE=str(tmp_path / "cache"), MASTER_ADDR="127.0.0.1",
+               OMP_NUM_THREADS="1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=8", "--master-addr", "127.0.0.1", "--master-port",
+                        "29633", str(script)], capture_output=True, text=True, env=env,
+                       timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")][0]
+    out = json.loads(line[len("RESULT "):])
+    fb, seen = out["fb"], out["seen"]
+    for r, sv in enumerate(seen):
+        cmd = sv["cmd"]
+        a = dict(zip(cmd[1::2], cmd[2::2]))
+        assert a["--workerid"] == str(r) and a["--maxworker"] == "8"
+        assert a["--partmethod"] == "div" and a["--partkey"] == "8" and a["--format"] == "moves"
+        assert ("--discard" in cmd) == (r != 0)
+        assert "stale.plan" not in sv["entries"]  # the cold directory, never the stale one
+    assert fb["total_s"] == 1.0 + 0.25 * 7           # the slowest worker
+    assert fb["rows"] == sum(100 + r for r in range(8))
+    assert fb["export_GB"] == round(8 * 5000 / 1e9, 2)
+    assert fb["files_GB"] == round(1000 / 1e9, 2)    # rank 0's files
