@@ -1387,6 +1387,172 @@ __global__ __launch_bounds__(256) void rle_moves(const uint32_t* __restrict__ fm
     }
 }
 
+// rle_moves for 4-bit sets on the packed nibbles (CPD_MOVES_SWAR, default
+// on; =0 runs the per-column kernel above — identical tables).  Per lane:
+//   forward: only the running sets S_k (one nibble insert per column);
+//   breaks:  a run starts at column k iff S_{k-1} & f_k == 0 — the running
+//            sets shifted up a nibble (the entry set at nibble 0) AND the
+//            segment's sets, zero nibbles found with the carry trick; the
+//            shifted sets also hold, at each break, the closing set of the
+//            run it ends;
+//   fill:    every column takes its run's closing set: run ends (a break at
+//            k + 1; column 31 with the tail run's set) keep theirs, the rest
+//            copy from the right in five doubling steps;
+//   moves:   the lowest set bit of every nibble at once.
+// The carry and the lanes' entry values are closing SETS here, not moves.
+struct Seg4 {
+    uint32_t S[4];  // nibble k: running set after column k
+    uint32_t P[4];  // nibble k: running set before column k (the entry set at 0)
+    uint32_t Z[4];  // bit 3 of nibble k: a run starts at column k
+};
+
+__device__ __forceinline__ Seg4 seg4_scan(const uint32_t (&v)[4], uint32_t Sin) {
+    Seg4 r;
+    r.S[0] = r.S[1] = r.S[2] = r.S[3] = 0u;
+    uint32_t S = Sin;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t f = (v[k >> 3] >> (4 * (k & 7))) & 0xFu;
+        const uint32_t T = S & f;
+        S = T ? T : f;
+        r.S[k >> 3] |= S << (4 * (k & 7));
+    }
+    r.P[0] = (r.S[0] << 4) | Sin;
+    r.P[1] = __builtin_amdgcn_alignbit(r.S[1], r.S[0], 28);
+    r.P[2] = __builtin_amdgcn_alignbit(r.S[2], r.S[1], 28);
+    r.P[3] = __builtin_amdgcn_alignbit(r.S[3], r.S[2], 28);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t a = r.P[i] & v[i];
+        r.Z[i] = ~(((a & 0x77777777u) + 0x77777777u) | a) & 0x88888888u;
+    }
+    return r;
+}
+
+// closing set of the run entering the segment (it closes at the first break);
+// only meaningful when the segment has a break
+__device__ __forceinline__ uint32_t seg4_entry_set(const Seg4& r) {
+    const uint32_t b0 = r.Z[0] ? ((uint32_t)__builtin_ctz(r.Z[0]) >> 2)
+                      : r.Z[1] ? 8u + ((uint32_t)__builtin_ctz(r.Z[1]) >> 2)
+                      : r.Z[2] ? 16u + ((uint32_t)__builtin_ctz(r.Z[2]) >> 2)
+                               : 24u + ((uint32_t)__builtin_ctz(r.Z[3] | 0x80000000u) >> 2);
+    return nib_at(r.P[0], r.P[1], r.P[2], r.P[3], b0);
+}
+
+__global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ fm, uint32_t npad,
+                                                  uint32_t nrows, const uint32_t* __restrict__ st,
+                                                  const uint8_t* __restrict__ rc,
+                                                  const uint32_t* __restrict__ out_row,
+                                                  uint32_t* __restrict__ dense) {
+    const uint32_t brow = blockIdx.y * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (brow >= nrows) return;  // wave-uniform
+    const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
+    const uint32_t t0 = blockIdx.x * kMoveTiles;
+    if (t0 >= ntiles) return;
+    const uint32_t t1 = min(ntiles, t0 + kMoveTiles);
+    const uint32_t* __restrict__ strow = st + (size_t)brow * nseg;
+    const uint8_t* __restrict__ rcrow = rc + (size_t)brow * nseg;
+    const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
+    auto load = [&](uint32_t seg, uint32_t (&v)[4]) {
+        const uint4 q = f4[fm4_piece(brow, nseg, seg)];
+        v[0] = q.x;
+        v[1] = q.y;
+        v[2] = q.z;
+        v[3] = q.w;
+    };
+    // carry: the closing set of the run open at the right edge of the tile
+    uint32_t carry = 0;
+    bool have = false;  // wave-uniform
+    for (uint32_t s0 = t1 * 64u; s0 < nseg && !have; s0 += 64u) {
+        const uint64_t m = __ballot(s0 + lane < nseg && rcrow[s0 + lane] != 0);
+        if (m) {
+            const uint32_t sj = s0 + (uint32_t)__builtin_ctzll(m);
+            uint32_t v[4];
+            load(sj, v);
+            carry = seg4_entry_set(seg4_scan(v, strow[sj] & 0xFu));
+            have = true;
+        }
+    }
+    if (!have) {  // no run closes right of the chunk: the row's final run
+        uint32_t v[4];
+        load(nseg - 1u, v);
+        carry = seg4_scan(v, strow[nseg - 1u] & 0xFu).S[3] >> 28;
+    }
+    uint4* __restrict__ orow = reinterpret_cast<uint4*>(dense + (size_t)out_row[brow] * (npad / 8u));
+    for (uint32_t t = t1; t-- > t0;) {
+        const uint32_t seg = t * 64u + lane;
+        uint32_t v[4];
+        load(seg, v);
+        const Seg4 r = seg4_scan(v, strow[seg] & 0xFu);
+        const bool any = (r.Z[0] | r.Z[1] | r.Z[2] | r.Z[3]) != 0u;
+        const uint32_t fl = seg4_entry_set(r);
+        const uint64_t m = __ballot(any);
+        const uint64_t right = lane == 63u ? 0ull : (m >> (lane + 1u)) << (lane + 1u);
+        const uint32_t j = right ? (uint32_t)__builtin_ctzll(right) : lane;
+        const uint32_t fj = (uint32_t)__shfl((int)fl, (int)j, 64);
+        const uint32_t tail = right ? fj : carry;
+        // run ends: a break at the next column (nibble mask, shifted down one
+        // nibble), and column 31 carrying the tail run's set
+        uint32_t V[4], X[4];
+        {
+            uint32_t nz[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) nz[i] = r.Z[i] | (r.Z[i] - (r.Z[i] >> 3));
+            V[0] = __builtin_amdgcn_alignbit(nz[1], nz[0], 4);
+            V[1] = __builtin_amdgcn_alignbit(nz[2], nz[1], 4);
+            V[2] = __builtin_amdgcn_alignbit(nz[3], nz[2], 4);
+            V[3] = (nz[3] >> 4) | 0xF0000000u;
+            X[0] = r.S[0];
+            X[1] = r.S[1];
+            X[2] = r.S[2];
+            X[3] = (r.S[3] & 0x0FFFFFFFu) | (tail << 28);
+        }
+        // every other column copies the nearest run end to its right
+#pragma unroll
+        for (int sh = 4; sh <= 16; sh <<= 1) {
+            uint32_t xs[4], vs[4];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                xs[i] = __builtin_amdgcn_alignbit(X[i + 1], X[i], sh);
+                vs[i] = __builtin_amdgcn_alignbit(V[i + 1], V[i], sh);
+            }
+            xs[3] = X[3] >> sh;
+            vs[3] = V[3] >> sh;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
+                V[i] |= vs[i];
+            }
+        }
+#pragma unroll
+        for (int w = 1; w <= 2; w <<= 1) {  // 32- and 64-bit steps: whole words
+            uint32_t xs[4], vs[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xs[i] = i + w < 4 ? X[i + w] : 0u;
+                vs[i] = i + w < 4 ? V[i + w] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
+                V[i] |= vs[i];
+            }
+        }
+        // lowest set bit of every (non-empty) nibble
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t b0 = ~X[i] & 0x11111111u;
+            const uint32_t b1 = ~(X[i] >> 1) & b0;
+            const uint32_t b2 = ~(X[i] >> 2) & b1;
+            o[i] = b0 + b1 + b2;
+        }
+        orow[(size_t)t * 64u + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
+    }
+}
+
 // Move tables -> RLE words, the inverse of rle_moves: a row's runs start at
 // column 0 and at every column whose move differs from its left neighbour's,
 // word = column << 4 | move (warthog rle_run32 [U]); columns >= n are
@@ -2901,8 +3067,12 @@ void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
     const uint32_t ntiles = npad / kern::kTile;
     const dim3 grid((ntiles + kern::kMoveTiles - 1u) / kern::kMoveTiles, (nrows + 3u) / 4u),
         block(256);
+    static const bool swar = env_u32("CPD_MOVES_SWAR", 1) != 0;
     switch (fmb) {
-        case 4: launch(kern::rle_moves<4>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
+        case 4:
+            if (swar) launch(kern::rle_moves4, grid, block, s, fm, npad, nrows, st, rc, out_row, dense);
+            else launch(kern::rle_moves<4>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense);
+            break;
         case 8: launch(kern::rle_moves<8>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
         default: launch(kern::rle_moves<16>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
     }

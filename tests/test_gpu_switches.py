@@ -13,9 +13,10 @@ oracle, walk queries over them dense and RLE.  What each reaches:
   CPD_XCD=0       identity block mapping
   CPD_FM_N4=0     first_moves<4, 2, true> (generic narrow first moves)
   CPD_ASYNC=0     the emit in line (one buffer set)
-  CPD_RLE_CH=0    rle_scan<false, 4> counts (no chunked count / seam repair)
+  CPD_RLE_CH=0    rle_scan<4> counts (no chunked count / seam repair)
   CPD_LEAFFM=0    leaf first-move sets recomputed by first_moves
   CPD_OVERLAP=0   each batch's up-sweep after the previous batch's first moves
+  CPD_MOVES_SWAR=0  rle_moves<4> (per-column move-table emit) instead of rle_moves4
 """
 import json
 import os
@@ -62,7 +63,7 @@ print(json.dumps(out))
 """
 
 SWITCHES = ["CPD_LIVE", "CPD_SORT", "CPD_LANE_KEY", "CPD_XCD", "CPD_FM_N4", "CPD_ASYNC",
-            "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP"]
+            "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP", "CPD_MOVES_SWAR"]
 
 
 @pytest.mark.parametrize("switch", SWITCHES)
