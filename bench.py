@@ -329,12 +329,29 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
                       "build_s": round(pinfo["ch_seconds"], 2),
                       "builder": "GPU contraction (ch_gpu.cpp), identical to the host build"}
         if pinfo else None,
+        # the whole step's real HBM traffic (PMC, every build kernel of the
+        # child's one step, both streams) over the timed step
+        "step_pmc": step_pmc(traffic, elapsed_max / args.steps),
         "pmc_traffic_per_launch": {k: {"launches": v["launches"],
                                        "bytes": round(v["bytes_per_launch"], 1),
                                        "read": round(v["read_bytes_per_launch"], 1),
                                        "write": round(v["write_bytes_per_launch"], 1)}
                                    for k, v in (traffic or {}).items()},
     }
+
+
+BUILD_KERNELS = ("sweep_up", "sweep_down", "first_moves", "rle_count", "rle_fix", "rle_moves")
+
+
+def step_pmc(traffic, step_s):
+    """PMC bytes of one build step (the pmc child builds exactly one batch:
+    every launch of every build kernel, on all streams) and the rate over the
+    timed step."""
+    if not traffic:
+        return None
+    b = sum(v["bytes_per_launch"] * v["launches"] for k, v in traffic.items() if k in BUILD_KERNELS)
+    return {"GB": round(b / 1e9, 2), "TBps": round(b / step_s / 1e12, 3),
+            "note": "2*FETCH_SIZE + WRITE_SIZE summed over the build kernels of one step / ms_per_step"}
 
 
 # libcpd reports these counters through the timing table (launches = count)
