@@ -80,6 +80,8 @@ def parse(argv=None):
                     help="skip the end-to-end worker build (make_cpd_auto, cold plan)")
     ap.add_argument("--full-build-discard", action="store_true",
                     help="full-build leg without file writes (make_cpd_auto --discard)")
+    ap.add_argument("--full-build-only", action="store_true",
+                    help="run only the end-to-end worker leg (no GPU context in the ranks)")
     ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP events")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the rocprofv3 --pmc passes that fill roofline.traffic")
@@ -689,6 +691,48 @@ def glob_xy(args):
     return os.path.join(args.cache, f"fb-synth{args.width}-s{args.seed}{style}.xy")
 
 
+def full_build_only(args, world, rank, local):
+    """The end-to-end worker leg alone (--full-build-only): rank r runs
+    make_cpd_auto for worker r, rank 0 writes its files and serves them, the
+    ranks' figures are gathered over gloo — no GPU context in these
+    processes, so an 8-rank rehearsal on one GPU (CPD_BENCH_SHARE_GPU=1)
+    holds 8 GPU processes, not 16.  One JSON line on rank 0."""
+    import numpy as np  # noqa: F401
+    import torch.distributed as dist
+    sys.path.insert(0, PKG)
+    import cpd
+    share = os.environ.get("CPD_BENCH_SHARE_GPU") == "1"
+    gpu = 0 if share else local
+    if share and args.batch == 0:  # eight workers' batch buffers on one card
+        args.batch = 1024
+    os.makedirs(args.cache, exist_ok=True)
+    if world > 1:
+        dist.init_process_group("gloo")
+    comm = Comm(world, rank, local, device=None)
+    xy = full_build_xy(args) if local == 0 else None
+    comm.barrier()
+    xy = xy or glob_xy(args)
+    t0 = time.time()
+    fb, rec = full_build_leg(args, xy, world, rank, gpu, comm)
+    W = full_build_workers(args, world)
+    if rank == 0 and "files_bytes" in rec:
+        g = cpd.synth_road_graph(args.width, args.width, seed=args.seed, style=args.style)
+        try:
+            fb["serve"] = serve_probe(args, xy, full_build_dir(args, world), W, gpu, g,
+                                      cpd.dfs_preorder(g.row_ptr, g.dst), host_threads(args))
+        except Exception as e:  # reported
+            fb["serve"] = {"error": str(e)[-400:]}
+    comm.barrier()
+    if rank == 0:
+        import shutil
+        shutil.rmtree(full_build_dir(args, world), ignore_errors=True)
+        print(json.dumps({"what": "full-build leg only", "n_gpus": world,
+                          "shared_gpu_rehearsal": share, "batch": args.batch or "auto",
+                          "wall_s": round(time.time() - t0, 3), "full_build": fb}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.cpu_worker:
@@ -707,6 +751,9 @@ def main():
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.full_build_only:
+        full_build_only(args, world, rank, local)
+        return
 
     import numpy as np
     import torch  # first: libcpd then binds to the same HIP runtime
