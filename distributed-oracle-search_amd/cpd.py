@@ -51,7 +51,7 @@ EXPORTED = [
     "cpd_graph_set_coords", "cpd_host_alloc", "cpd_host_free",
     "cpd_rows_lanes", "cpd_graph_hint_next", "cpd_graph_set_hbm_reserve",
     "cpd_device_mem_info", "cpd_rows_move_words", "cpd_rows_export_moves",
-    "cpd_index_append_moves",
+    "cpd_index_append_moves", "cpd_device_arena", "cpd_device_arena_release", "cpd_batch_bytes",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is

@@ -31,6 +31,40 @@ using namespace cpd;
 
 namespace {
 
+// Per-device HBM arena (cpd_device_arena): one block committed up front —
+// e.g. on a host thread while the plan is being contracted — that device
+// buffers on that device are carved from (bump allocation; a buffer carved
+// from it is never returned to it, the whole block is freed by
+// cpd_device_arena_release).  What does not fit falls back to hipMalloc.
+struct Arena {
+    char* base = nullptr;
+    size_t cap = 0, top = 0;
+};
+std::mutex g_arena_mu;
+std::map<int, Arena> g_arena;
+
+void* arena_take(size_t bytes) {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> l(g_arena_mu);
+    auto it = g_arena.find(d);
+    if (it == g_arena.end() || !it->second.base) return nullptr;
+    Arena& a = it->second;
+    const size_t at = (a.top + 255u) & ~(size_t)255u;
+    if (at + bytes > a.cap) return nullptr;
+    a.top = at + bytes;
+    return a.base + at;
+}
+
+bool arena_owns(const void* p) {
+    std::lock_guard<std::mutex> l(g_arena_mu);
+    for (auto& kv : g_arena) {
+        const char* c = static_cast<const char*>(p);
+        if (kv.second.base && c >= kv.second.base && c < kv.second.base + kv.second.cap) return true;
+    }
+    return false;
+}
+
 // Owning device buffer.
 template <class T>
 struct DevBuf {
@@ -41,14 +75,16 @@ struct DevBuf {
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { release(); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p && !arena_owns(p)) (void)hipFree(p);
         p = nullptr;
         n = 0;
     }
     void alloc(size_t count) {
         if (count <= n && p) return;
         release();
-        HIP_CHECK(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)));
+        const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+        if (void* q = arena_take(bytes)) p = static_cast<T*>(q);
+        else HIP_CHECK(hipMalloc(&p, bytes));
         n = count;
     }
     void upload(const T* src, size_t count, hipStream_t s) {
@@ -98,6 +134,17 @@ struct Agg {
 };
 
 bool async_on();  // CPD_ASYNC (defined with the other switches)
+
+// HBM per row of batch width: dist 4n (+ 2n narrow) + two buffer sets of
+// first-move rows and RLE segment states (emit overlap) + the chunked count's
+// chunk states (8 B per chunk) + leaf sets + two rows of move tables (npad / 2
+// each: the row set being built and the one a caller such as make_cpd_auto
+// is exporting).
+double batch_bytes_per_row(uint32_t n, uint32_t npad, uint32_t fmb, bool narrow, bool leaf_fm) {
+    return (narrow ? 6.0 : 4.0) * n + 2.0 * (fmb / 8.0 * npad + 5.0 / 32.0 * npad) +
+           (fmb == 4 ? 8.0 * rle_count_chunks(npad) : 0.0) + (leaf_fm ? 0.5 * n : 0.0) +
+           2.0 * 0.5 * npad;
+}
 bool up_priority_on();
 bool lane_key_on();
 std::vector<uint32_t> hilbert_keys(const int32_t* x, const int32_t* y, uint32_t n);
@@ -376,18 +423,11 @@ struct cpd_graph {
         if (want == 0) {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-            // per target: dist 4n (+ 2n narrow) + two buffer sets of fm rows
-            // and RLE segment states (emit overlap) + the chunked count's
-            // chunk states (8 B per chunk) + leaf sets + two rows of move
-            // tables (npad / 2 each: the row set being built and the one a
-            // caller such as make_cpd_auto is exporting), in 85% of free HBM;
-            // at most 24 slabs.  Larger batches amortise the latency-bound
+            // per target (batch_bytes_per_row), in 85% of free HBM; at most
+            // 24 slabs.  Larger batches amortise the latency-bound
             // narrow levels: at 1M nodes 20480 rows per batch measured 310.5k
             // rows/s against 296.1k for 16384 (round 2).
-            const double per = (narrow ? 6.0 : 4.0) * n +
-                               2.0 * (fmb / 8.0 * npad + 5.0 / 32.0 * npad) +
-                               (fmb == 4 ? 8.0 * rle_count_chunks(npad) : 0.0) +
-                               (leaf_fm ? 0.5 * n : 0.0) + 2.0 * 0.5 * npad;
+            const double per = batch_bytes_per_row(n, npad, fmb, narrow, leaf_fm);
             const double avail = free_b > hbm_reserve ? (double)(free_b - hbm_reserve) : 0.0;
             const double fit = 0.85 * avail / per;
             CPD_REQUIRE(hbm_reserve == 0 || fit >= 1024.0, CPD_E_OOM,
@@ -702,6 +742,60 @@ int cpd_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes)
         HIP_CHECK(hipMemGetInfo(&f, &t));
         *free_bytes = f;
         *total_bytes = t;
+    });
+}
+
+int cpd_device_arena(int device, uint64_t bytes, int touch) {
+    return guarded([&] {
+        require_device();
+        int count = 0;
+        HIP_CHECK(hipGetDeviceCount(&count));
+        CPD_REQUIRE(device >= 0 && device < count, CPD_E_ARG, "no such device");
+        HIP_CHECK(hipSetDevice(device));
+        {
+            std::lock_guard<std::mutex> l(g_arena_mu);
+            CPD_REQUIRE(!g_arena[device].base, CPD_E_ARG, "device arena already committed");
+        }
+        void* p = nullptr;
+        HIP_CHECK(hipMalloc(&p, std::max<uint64_t>(bytes, 256)));
+        if (touch) {  // first-touch costs paid here, off the build's path
+            HIP_CHECK(hipMemset(p, 0, std::max<uint64_t>(bytes, 256)));
+            HIP_CHECK(hipDeviceSynchronize());
+        }
+        std::lock_guard<std::mutex> l(g_arena_mu);
+        g_arena[device] = Arena{static_cast<char*>(p), (size_t)std::max<uint64_t>(bytes, 256), 0};
+    });
+}
+
+int cpd_device_arena_release(int device) {
+    return guarded([&] {
+        char* p = nullptr;
+        {
+            std::lock_guard<std::mutex> l(g_arena_mu);
+            auto it = g_arena.find(device);
+            if (it == g_arena.end()) return;
+            p = it->second.base;
+            g_arena.erase(it);
+        }
+        if (p) {
+            HIP_CHECK(hipSetDevice(device));
+            HIP_CHECK(hipFree(p));
+        }
+    });
+}
+
+int cpd_batch_bytes(uint32_t n, uint32_t max_degree, uint32_t batch, uint64_t* bytes) {
+    return guarded([&] {
+        CPD_REQUIRE(bytes && batch % 1024u == 0 && batch > 0, CPD_E_ARG,
+                    "batch_bytes: batch must be a positive multiple of 1024");
+        uint32_t shift = 0;
+        while ((1u << shift) < std::max(1u, max_degree)) ++shift;
+        const uint32_t fmb = fm_bits(shift);
+        const uint32_t npad = (n + kFmTile - 1u) / kFmTile * kFmTile;
+        // narrow rows and leaf sets assumed (their upper bound), plus the
+        // per-column arrays and the lane tables
+        *bytes = (uint64_t)(batch_bytes_per_row(n, npad, fmb, true, fmb == 4) * batch) +
+                 (uint64_t)batch * (n / 256u + 1u) * 4u + 512ull * n + (64ull << 20);
     });
 }
 

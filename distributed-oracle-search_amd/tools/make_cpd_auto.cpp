@@ -6,6 +6,10 @@
 //                 [--partition M]      README.md:89 spelling of --partmethod
 //                 [--device G]         default: I % (visible GPUs)
 //                 [--batch B]          rows per GPU sweep (multiple of 1024)
+//                 [--no-arena]         allocate the batch buffers at graph setup
+//                                      instead of committing them on a host
+//                                      thread beside the plan (default)
+//                 [--arena-touch]      also write the arena once while committing
 //                 [--threads T]        host threads for the hierarchy build (--ch-host)
 //                 [--ch-host]          contract the hierarchy on host threads, not the GPU
 //                 [--plan P | --no-plan-cache]
@@ -34,6 +38,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdio>
 #include <deque>
@@ -379,6 +384,48 @@ int main(int argc, char** argv) {
         // as the host build's, in a fraction of its time); --ch-host: threads
         o.ch_gpu = ndev > 0 && !a.has("ch-host");
         o.ch_device = std::max(device, 0);
+        // The build's HBM (batch buffers and two move-table row sets) is
+        // committed on a host thread while the plan is contracted or loaded
+        // (cpd_device_arena): committing 100-200 GB takes seconds.  --batch
+        // 0 (default): what fits in 85% of the free HBM above --hbm-reserve
+        // and a margin for the GPU contraction; --no-arena: the library
+        // allocates at cpd_graph_set_batch, as before.
+        const double hbm_reserve = a.real("hbm-reserve", 0.0) * (double)(1ull << 30);
+        uint32_t batch = (uint32_t)a.num("batch", 0);
+        const bool use_arena = ndev > 0 && !a.has("plan-only") && !a.has("no-arena");
+        uint64_t arena_bytes = 0;
+        double t_arena = 0.0, t_arena_wait = 0.0;
+        int arena_rc = CPD_OK;
+        std::string arena_err;
+        std::thread arena_thr;
+        struct JoinGuard {
+            std::thread& t;
+            ~JoinGuard() {
+                if (t.joinable()) t.join();
+            }
+        } arena_guard{arena_thr};
+        if (use_arena) {
+            uint32_t maxdeg = 1;
+            for (uint32_t v = 0; v < g.n; ++v) maxdeg = std::max(maxdeg, g.row_ptr[v + 1] - g.row_ptr[v]);
+            if (batch == 0) {
+                uint64_t fr = 0, tot = 0, per1k = 0;
+                cli::check(cpd_device_mem_info(device, &fr, &tot), "device memory");
+                cli::check(cpd_batch_bytes(g.n, maxdeg, 1024, &per1k), "batch bytes");
+                const double margin = 24.0 * (double)(1ull << 30);  // the contraction's working set
+                const double avail = (double)fr - hbm_reserve - margin;
+                const double fit = avail > 0 ? 0.85 * avail / (double)per1k : 0.0;
+                if (fit < 1.0)
+                    throw std::runtime_error("HBM reserve leaves too little for a 1024-row batch");
+                batch = (uint32_t)std::min(24.0, std::floor(fit)) * 1024u;
+            }
+            cli::check(cpd_batch_bytes(g.n, maxdeg, batch, &arena_bytes), "batch bytes");
+            arena_thr = std::thread([&] {
+                const double ta = now();
+                arena_rc = cpd_device_arena(device, arena_bytes, a.has("arena-touch") ? 1 : 0);
+                if (arena_rc != CPD_OK) arena_err = cpd_last_error();
+                t_arena = now() - ta;
+            });
+        }
         if (use_cache) {
             // workers started together (make_cpds.py:58-60) share one cache:
             // one builds, the others wait for it and load its plan
@@ -395,6 +442,13 @@ int main(int argc, char** argv) {
                        "plan");
         }
         double t_plan = now() - t0;
+        if (arena_thr.joinable()) {
+            const double tw = now();
+            arena_thr.join();
+            t_arena_wait = now() - tw;
+            if (arena_rc != CPD_OK)  // the library allocates at set_batch instead
+                std::fprintf(stderr, "make_cpd_auto: HBM arena not committed (%s)\n", arena_err.c_str());
+        }
         if (a.has("plan-only")) {  // warm the cache (host only, no GPU needed)
             std::printf("make_cpd_auto: plan ready in %.3fs\n", t_plan);
             cpd_plan_free(plan);
@@ -450,7 +504,7 @@ int main(int argc, char** argv) {
         if (a.has("hbm-reserve"))
             cli::check(cpd_graph_set_hbm_reserve(dg, (uint64_t)(a.real("hbm-reserve", 0.0) * (1ull << 30))),
                        "hbm reserve");
-        cli::check(cpd_graph_set_batch(dg, (uint32_t)a.num("batch", 0)), "batch");
+        cli::check(cpd_graph_set_batch(dg, batch), "batch");
         const double t_batch = now() - t_g0 - t_graph;
         // the .xy coordinates order each batch's lanes (compact target groups)
         if (g.x.size() == g.n && g.y.size() == g.n)
@@ -577,6 +631,7 @@ int main(int argc, char** argv) {
         if (rows) cpd_rows_free(rows);
         cpd_graph_free(dg);
         cpd_plan_free(plan);
+        if (use_arena) cli::check(cpd_device_arena_release(device), "arena release");
         const double t_free = now() - t_f0;
         double rate = t_build > 0 ? rows_done / t_build : 0.0;
         std::printf(
@@ -598,11 +653,13 @@ int main(int argc, char** argv) {
             "\"plan_cached\": %s, \"graph_s\": %.3f, \"batch_alloc_s\": %.3f, \"setup_s\": %.3f, "
             "\"rows_s\": %.3f, \"build_calls_s\": %.3f, \"wait_s\": %.3f, \"free_s\": %.3f, "
             "\"export_bytes\": %llu, \"export_thread_s\": %.3f, \"export_span_s\": %.3f, "
-            "\"write_thread_s\": %.3f, \"format\": \"%s\", \"total_s\": %.3f}\n",
+            "\"write_thread_s\": %.3f, \"format\": \"%s\", \"arena_GB\": %.2f, "
+            "\"arena_s\": %.3f, \"arena_wait_s\": %.3f, \"total_s\": %.3f}\n",
             wid, W, (unsigned long long)rows_done, (unsigned long long)runs_done, B,
             discard ? "true" : "false", t_read, t_plan, plan_loaded ? "true" : "false", t_graph,
             t_batch, t_setup, t_rows, t_build, t_io, t_free, (unsigned long long)x_bytes, x_sum, x_span,
-            w_sum, format.c_str(), now() - t_start);
+            w_sum, format.c_str(), arena_rc == CPD_OK ? arena_bytes / 1e9 : 0.0, t_arena,
+            t_arena_wait, now() - t_start);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "make_cpd_auto: %s\n", e.what());
         return 1;

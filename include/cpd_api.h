@@ -180,6 +180,19 @@ int  cpd_device_count(int* count);
 /* Free and total HBM bytes of `device` (hipMemGetInfo there): what a caller
  * sizes cpd_graph_set_hbm_reserve against.                                 */
 int  cpd_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes);
+/* HBM arena: commit `bytes` on `device` up front (touch != 0: also write
+ * them once, paying first-touch costs now), for the library's device buffers
+ * on that device to be carved from — so that a caller can overlap the
+ * commit of a build's batch buffers (~200 GB: seconds) with other work, as
+ * make_cpd_auto does with the plan.  Buffers carved from it are never
+ * returned to it; cpd_device_arena_release frees the block, once the graphs,
+ * rows and indexes using it are freed.  What does not fit is allocated
+ * separately.  cpd_batch_bytes [host]: the HBM a build at `batch` rows needs
+ * on a graph of n nodes and that max out-degree (an upper bound; graph
+ * arrays excluded).                                                        */
+int  cpd_device_arena(int device, uint64_t bytes, int touch);
+int  cpd_device_arena_release(int device);
+int  cpd_batch_bytes(uint32_t n, uint32_t max_degree, uint32_t batch, uint64_t* bytes);
 /* Upload a plan to `device` (column-space CSR, CH arcs, levels). */
 int  cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out);
 /* Batch width (rows built per sweep, multiple of 1024; 0 = auto from HBM). */
