@@ -135,6 +135,16 @@ struct Agg {
 
 bool async_on();  // CPD_ASYNC (defined with the other switches)
 
+// Largest auto batch (CPD_BATCH_MAX, a multiple of 1024 <= 32768; A/B knob).
+uint32_t batch_max() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("CPD_BATCH_MAX");
+        const unsigned long b = e && *e ? std::strtoul(e, nullptr, 10) : 24576ul;
+        return (uint32_t)std::max(1024ul, std::min(32768ul, b / 1024ul * 1024ul));
+    }();
+    return v;
+}
+
 // HBM per row of batch width: dist 4n (+ 2n narrow) + two buffer sets of
 // first-move rows and RLE segment states (emit overlap) + the chunked count's
 // chunk states (8 B per chunk) + leaf sets + two rows of move tables (npad / 2
@@ -433,7 +443,7 @@ struct cpd_graph {
             CPD_REQUIRE(hbm_reserve == 0 || fit >= 1024.0, CPD_E_OOM,
                         "HBM reserve of " + std::to_string(hbm_reserve >> 20) + " MiB leaves " +
                             std::to_string((size_t)avail >> 20) + " MiB: too little for a 1024-row batch");
-            want = (uint32_t)std::min(24576.0, std::max(1024.0, std::floor(fit / 1024) * 1024));
+            want = (uint32_t)std::min((double)batch_max(), std::max(1024.0, std::floor(fit / 1024) * 1024));
         }
         want = (want + 1023u) / 1024u * 1024u;
         if (want == B && dist.p) return;

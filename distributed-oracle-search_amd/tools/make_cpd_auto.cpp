@@ -416,7 +416,9 @@ int main(int argc, char** argv) {
                 const double fit = avail > 0 ? 0.85 * avail / (double)per1k : 0.0;
                 if (fit < 1.0)
                     throw std::runtime_error("HBM reserve leaves too little for a 1024-row batch");
-                batch = (uint32_t)std::min(24.0, std::floor(fit)) * 1024u;
+                const char* bm = std::getenv("CPD_BATCH_MAX");  // the library's cap (A/B knob)
+                const double cap = bm && *bm ? std::max(1.0, std::min(32.0, std::floor(std::atof(bm) / 1024))) : 24.0;
+                batch = (uint32_t)std::min(cap, std::floor(fit)) * 1024u;
             }
             cli::check(cpd_batch_bytes(g.n, maxdeg, batch, &arena_bytes), "batch bytes");
             arena_thr = std::thread([&] {
