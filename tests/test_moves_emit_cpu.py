@@ -1,0 +1,210 @@
+"""The move-table emit's algorithm (csrc/cpd_kernels.hip rle_moves4 — packed
+nibbles — and rle_moves<FMB> — per column), restated step for step in Python
+(wave = 64 lanes x 32 columns, tiles walked right to left, look-ahead carry)
+and checked on CPU against the greedy RLE rule expanded per column, on random
+first-move rows with short runs, long runs and a single run.  The GPU suite
+then checks the kernels themselves bit-exact against the oracle."""
+import random
+
+
+
+def greedy_moves(fm):
+    n = len(fm); S = 0xF; runs = []; h = 0
+    for c in range(n):
+        f = fm[c]; T = S & f
+        if T == 0:
+            runs.append((h, (S & -S).bit_length() - 1)); h = c; S = f
+        else:
+            S = T
+    runs.append((h, (S & -S).bit_length() - 1))
+    mv = [0] * n; ri = 0
+    for c in range(n):
+        while ri + 1 < len(runs) and runs[ri + 1][0] <= c: ri += 1
+        mv[c] = runs[ri][1]
+    return mv, runs
+
+def states(fm):  # entry set per 32-col segment, runs ending (breaks) per segment
+    S = 0xF; st = []; rc = []
+    for s0 in range(0, len(fm), 32):
+        st.append(S); cnt = 0
+        for c in range(s0, s0 + 32):
+            T = S & fm[c]
+            if T == 0: cnt += 1; S = fm[c]
+            else: S = T
+        rc.append(cnt)
+    return st, rc
+
+M32 = 0xFFFFFFFF
+def alignbit(hi, lo, sh): return ((hi << 32 | lo) >> sh) & M32
+def ctz(x): return (x & -x).bit_length() - 1
+
+def seg4_scan(v, Sin):
+    Sw = [0, 0, 0, 0]; S = Sin
+    for k in range(32):
+        f = (v[k >> 3] >> (4 * (k & 7))) & 0xF; T = S & f; S = T if T else f
+        Sw[k >> 3] |= S << (4 * (k & 7))
+    P = [((Sw[0] << 4) | Sin) & M32, alignbit(Sw[1], Sw[0], 28), alignbit(Sw[2], Sw[1], 28), alignbit(Sw[3], Sw[2], 28)]
+    Z = []
+    for i in range(4):
+        a = P[i] & v[i]
+        Z.append((~((((a & 0x77777777) + 0x77777777) & M32) | a)) & 0x88888888 & M32)
+    return Sw, P, Z
+
+def nib(w, i): return (w[i >> 3] >> (4 * (i & 7))) & 0xF
+
+def entry_set(P, Z):
+    if Z[0]: b0 = ctz(Z[0]) >> 2
+    elif Z[1]: b0 = 8 + (ctz(Z[1]) >> 2)
+    elif Z[2]: b0 = 16 + (ctz(Z[2]) >> 2)
+    else: b0 = 24 + (ctz(Z[3] | 0x80000000) >> 2)
+    return nib(P, b0)
+
+def moves4(fm, st, rc, KT=16):
+    npad = len(fm); nseg = npad // 32; ntiles = npad // 2048
+    vseg = []
+    for s in range(nseg):
+        w = [0, 0, 0, 0]
+        for k in range(32): w[k >> 3] |= fm[s * 32 + k] << (4 * (k & 7))
+        vseg.append(w)
+    out = [0] * npad
+    for t0 in range(0, ntiles, KT):
+        t1 = min(ntiles, t0 + KT)
+        have = False; carry = 0; s0 = t1 * 64
+        while s0 < nseg and not have:
+            m = [l for l in range(64) if s0 + l < nseg and rc[s0 + l] != 0]
+            if m:
+                sj = s0 + m[0]; Sw, P, Z = seg4_scan(vseg[sj], st[sj]); carry = entry_set(P, Z); have = True
+            s0 += 64
+        if not have:
+            Sw, P, Z = seg4_scan(vseg[nseg - 1], st[nseg - 1]); carry = Sw[3] >> 28
+        for t in range(t1 - 1, t0 - 1, -1):
+            lanes = [seg4_scan(vseg[t * 64 + l], st[t * 64 + l]) for l in range(64)]
+            anyl = [any(z for z in L[2]) for L in lanes]
+            fl = [entry_set(L[1], L[2]) for L in lanes]
+            for l in range(64):
+                Sw, P, Z = lanes[l]
+                right = [j for j in range(l + 1, 64) if anyl[j]]
+                tail = fl[right[0]] if right else carry
+                nz = [(Z[i] | ((Z[i] - (Z[i] >> 3)) & M32)) & M32 for i in range(4)]
+                V = [alignbit(nz[1], nz[0], 4), alignbit(nz[2], nz[1], 4), alignbit(nz[3], nz[2], 4), ((nz[3] >> 4) | 0xF0000000)]
+                X = [Sw[0], Sw[1], Sw[2], (Sw[3] & 0x0FFFFFFF) | (tail << 28)]
+                for sh in (4, 8, 16):
+                    xs = [alignbit(X[i + 1], X[i], sh) for i in range(3)] + [X[3] >> sh]
+                    vs = [alignbit(V[i + 1], V[i], sh) for i in range(3)] + [V[3] >> sh]
+                    for i in range(4):
+                        X[i] = (V[i] & X[i]) | (~V[i] & xs[i] & M32); V[i] |= vs[i]
+                for w in (1, 2):
+                    xs = [X[i + w] if i + w < 4 else 0 for i in range(4)]
+                    vs = [V[i + w] if i + w < 4 else 0 for i in range(4)]
+                    for i in range(4):
+                        X[i] = (V[i] & X[i]) | (~V[i] & xs[i] & M32); V[i] |= vs[i]
+                for i in range(4):
+                    b0 = ~X[i] & 0x11111111; b1 = ~(X[i] >> 1) & b0; b2 = ~(X[i] >> 2) & b1
+                    o = (b0 + b1 + b2) & M32
+                    for k in range(8): out[(t * 64 + l) * 32 + i * 8 + k] = (o >> (4 * k)) & 0xF
+            if any(anyl): carry = fl[anyl.index(True)]
+    return out
+
+# generic (per-column) kernel emulation for wide sets
+def greedy_moves_w(fm, ALL):
+    n = len(fm); S = ALL; runs = []; h = 0
+    for c in range(n):
+        f = fm[c]; T = S & f
+        if T == 0:
+            runs.append((h, ctz(S))); h = c; S = f
+        else: S = T
+    runs.append((h, ctz(S)))
+    mv = [0] * n; ri = 0
+    for c in range(n):
+        while ri + 1 < len(runs) and runs[ri + 1][0] <= c: ri += 1
+        mv[c] = runs[ri][1]
+    return mv
+
+def states_w(fm, ALL):
+    S = ALL; st = []; rc = []
+    for s0 in range(0, len(fm), 32):
+        st.append(S); cnt = 0
+        for c in range(s0, s0 + 32):
+            T = S & fm[c]
+            if T == 0: cnt += 1; S = fm[c]
+            else: S = T
+        rc.append(cnt)
+    return st, rc
+
+def low_bit(S): return ctz(S | 0x8000)
+
+def seg_moves(f32, S):
+    brk = 0; L = [0, 0, 0, 0]
+    for k in range(32):
+        f = f32[k]; T = S & f; b = T == 0
+        brk |= (1 if b else 0) << k
+        S = f if b else T
+        L[k >> 3] |= low_bit(S) << (4 * (k & 7))
+    return brk, L, S
+
+def entry_move(brk, L, Sin):
+    b0 = ctz(brk | 0x80000000)
+    return low_bit(Sin) if b0 == 0 else nib(L, b0 - 1)
+
+def moves_generic(fm, st, rc, KT=16):
+    npad = len(fm); nseg = npad // 32; ntiles = npad // 2048
+    out = [0] * npad
+    for t0 in range(0, ntiles, KT):
+        t1 = min(ntiles, t0 + KT)
+        have = False; carry = 0; s0 = t1 * 64
+        while s0 < nseg and not have:
+            m = [l for l in range(64) if s0 + l < nseg and rc[s0 + l] != 0]
+            if m:
+                sj = s0 + m[0]; brk, L, _ = seg_moves(fm[sj*32:sj*32+32], st[sj]); carry = entry_move(brk, L, st[sj]); have = True
+            s0 += 64
+        if not have:
+            _, _, S = seg_moves(fm[(nseg-1)*32:nseg*32], st[nseg - 1]); carry = low_bit(S)
+        for t in range(t1 - 1, t0 - 1, -1):
+            R = [seg_moves(fm[(t*64+l)*32:(t*64+l)*32+32], st[t*64+l]) for l in range(64)]
+            fl = [entry_move(R[l][0], R[l][1], st[t*64+l]) for l in range(64)]
+            anyl = [R[l][0] != 0 for l in range(64)]
+            for l in range(64):
+                brk, L, _ = R[l]
+                right = [j for j in range(l + 1, 64) if anyl[j]]
+                mv = fl[right[0]] if right else carry
+                for k in range(31, -1, -1):
+                    out[(t*64+l)*32 + k] = mv
+                    if k > 0 and (brk >> k) & 1: mv = nib(L, k - 1)
+            if any(anyl): carry = fl[anyl.index(True)]
+    return out
+
+
+
+def _rows(FMB, kinds, npads, seed):
+    rnd = random.Random(seed)
+    ALL = (1 << FMB) - 1
+    for kind in kinds:
+        npad = rnd.choice(npads)
+        fm = []
+        for _ in range(npad):
+            if kind == 0:
+                f = rnd.choice([1, 2, 4, 8, 3, 5, 6, 0xF]) if FMB == 4 else 1 << rnd.randint(0, FMB - 2)
+            elif kind == 1:
+                f = rnd.choice([ALL] * 30 + [1, 2])
+            elif kind == 2:
+                f = ALL
+            else:
+                f = rnd.randint(1, ALL)
+            fm.append(f)
+        yield fm
+
+
+def test_swar_emit_matches_greedy():
+    for i, fm in enumerate(_rows(4, [0, 1, 2, 3, 0, 3], [2048, 4096, 6144], 1)):
+        mv, _ = greedy_moves(fm)
+        st, rc = states(fm)
+        assert moves4(fm, st, rc, KT=[1, 2, 16][i % 3]) == mv
+
+
+def test_generic_emit_matches_greedy():
+    for FMB in (4, 8, 16):
+        ALL = (1 << FMB) - 1
+        for i, fm in enumerate(_rows(FMB, [0, 1, 3], [2048, 4096], FMB)):
+            mv = greedy_moves_w(fm, ALL)
+            st, rc = states_w(fm, ALL)
+            assert moves_generic(fm, st, rc, KT=[1, 16][i % 2]) == mv
