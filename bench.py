@@ -447,12 +447,12 @@ def cpu_search_leg(sp, g, order):
     import cpd
     import oracle
     srows = np.load(sp["targets_npy"]).astype(np.uint32)
-    q = np.load(sp["queries_npy"]).astype(np.uint32)
-    s, t = q[0], q[1]
     w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
     off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, srows, threads=sp["threads"])
     out = {}
     for leg in sp["legs"]:
+        q = np.load(leg["queries_npy"]).astype(np.uint32)
+        s, t = q[0], q[1]
         done, secs, expanded = 0, 0.0, 0
         while done < leg["queries"] and secs < leg["budget_s"]:
             k = min(leg["chunk"], leg["queries"] - done)
@@ -1024,20 +1024,20 @@ def main():
             six, ss2, st2, srows, ss_all, st_all, zs, zt = search_sample
             # the same searches on the host (child process, every job thread)
             snpy = os.path.join(args.cache, f"cpu-search-{os.getpid()}.npy")
-            qnpy = os.path.join(args.cache, f"cpu-search-q-{os.getpid()}.npy")
+            qnpy = [os.path.join(args.cache, f"cpu-search-q{i}-{os.getpid()}.npy") for i in (0, 1)]
             np.save(snpy, srows)
             try:
-                legs = []
-                for name, qs_, qt_, fs, chunk, budget in (("fscale0.1", ss_all, st_all, 0.1, 500, 8.0),
-                                                          ("fscale0", zs, zt, 0.0, 2 * threads, 12.0)):
-                    np.save(qnpy, np.stack([qs_, qt_]))
-                    r = collect(run_cpu_worker({"kind": "search", "width": args.width,
-                                                "seed": args.seed, "style": args.style,
-                                                "targets_npy": snpy, "queries_npy": qnpy,
-                                                "legs": [{"name": name, "fscale": fs,
-                                                          "queries": len(qs_), "chunk": chunk,
-                                                          "budget_s": budget}]}, threads))
-                    legs.append(r[name])
+                spec_legs = []
+                for i, (name, qs_, qt_, fs, chunk, budget) in enumerate(
+                        (("fscale0.1", ss_all, st_all, 0.1, 500, 8.0),
+                         ("fscale0", zs, zt, 0.0, 2 * threads, 12.0))):
+                    np.save(qnpy[i], np.stack([qs_, qt_]))
+                    spec_legs.append({"name": name, "fscale": fs, "queries": len(qs_),
+                                      "chunk": chunk, "budget_s": budget, "queries_npy": qnpy[i]})
+                r = collect(run_cpu_worker({"kind": "search", "width": args.width,
+                                            "seed": args.seed, "style": args.style,
+                                            "targets_npy": snpy, "legs": spec_legs}, threads))
+                legs = [r["fscale0.1"], r["fscale0"]]
                 gpu_q = (search["queries_per_s"], search["fscale0"]["queries_per_s"])
                 search["cpu_baseline"] = {
                     "kind": "port", "cores": threads,
@@ -1050,7 +1050,7 @@ def main():
             except Exception as e:  # reported, never fatal to the GPU numbers
                 search["cpu_baseline"] = {"error": str(e)[-300:]}
             finally:
-                for f in (snpy, qnpy):
+                for f in [snpy] + qnpy:
                     if os.path.exists(f):
                         os.remove(f)
             sref = oracle.build_rows(g.row_ptr, g.dst, g.w, order, srows, threads=threads)
