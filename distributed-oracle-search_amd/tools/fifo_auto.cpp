@@ -233,18 +233,22 @@ int main(int argc, char** argv) {
         // compact buckets: pieces read into two page-locked buffers by a
         // reader thread while the previous piece is appended (uploaded)
         uint32_t* pin[2] = {nullptr, nullptr};
+        uint64_t pin_bytes = 0;
         for (size_t k = 0; k < paths.size(); ++k) {
             if (formats[k] == 2) {
                 const auto& mh = mheads[k];
                 const uint32_t nr = (uint32_t)mh.targets.size();
                 if (!nr) continue;
-                const uint32_t per = (uint32_t)std::max<uint64_t>(1, kPiece / mh.words);
-                for (auto& p : pin)
-                    if (!p) {
+                const uint32_t per = (uint32_t)std::min<uint64_t>(nr, std::max<uint64_t>(1, kPiece / mh.words));
+                if (4ull * mh.words * per > pin_bytes) {  // grown for this bucket's pieces
+                    for (auto& p : pin) {
+                        cpd_host_free(p);
                         void* q = nullptr;
                         cli::check(cpd_host_alloc(4ull * mh.words * per, &q), "pinned buffer");
                         p = static_cast<uint32_t*>(q);
                     }
+                    pin_bytes = 4ull * mh.words * per;
+                }
                 auto read = [&, k, per, nr](uint32_t r0, int slot) {
                     cpd::io::read_move_bucket_rows(paths[k], mheads[k], r0, std::min(per, nr - r0), pin[slot]);
                 };
