@@ -597,24 +597,30 @@ def full_build_leg(args, xy, world, rank, device, comm, runner=subprocess.run):
 
 
 def _read_ready(p, deadline):
-    """fifo_auto's load record and its "listening" line (select with a
-    deadline: a server that never comes up fails the leg, not the bench)."""
+    """fifo_auto's load record and its "listening" line (raw reads of the
+    pipe after select, with a deadline: a server that never comes up fails
+    the leg, not the bench)."""
     import select
-    rec, buf = None, ""
+    fd = p.stdout.fileno()
+    buf = b""
     while time.time() < deadline:
-        r, _, _ = select.select([p.stdout], [], [], 1.0)
+        r, _, _ = select.select([fd], [], [], 1.0)
         if r:
-            line = p.stdout.readline()
-            if not line:
+            chunk = os.read(fd, 65536)
+            if not chunk:
                 break
-            buf += line
-            if line.startswith("fifo_auto-json: "):
-                rec = json.loads(line.split(": ", 1)[1])
-            if "listening" in line:
+            buf += chunk
+            if b"listening" in buf:
+                rec = None
+                for line in buf.decode(errors="replace").splitlines():
+                    if line.startswith("fifo_auto-json: "):
+                        rec = json.loads(line.split(": ", 1)[1])
                 return rec
         if p.poll() is not None:
             break
-    raise RuntimeError(f"fifo_auto did not come up: {buf[-300:]} {p.stderr.read()[-300:]}")
+    p.kill()
+    raise RuntimeError(f"fifo_auto did not come up: {buf.decode(errors='replace')[-300:]} "
+                       f"{p.stderr.read()[-300:]}")
 
 
 def serve_probe(args, xy, outdir, W, device, g, order, threads, nq=4000, nprobe=4):

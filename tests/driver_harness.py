@@ -134,3 +134,28 @@ def run(conf, config=None, script_dir=None):
                     for h, w, part in zip(hosts, range(maxworker), parts) if len(part) > 0]
             stats.append([f.result() for f in futs])
     return parts, stats
+
+
+def wait_ready(proc, timeout=60):
+    """Block until a resident fifo_auto prints its "listening" line; returns
+    its stdout so far.  Reads the raw pipe (os.read after select): a buffered
+    readline can swallow several lines at once, after which select never
+    reports the ones left in Python's buffer."""
+    import select
+    fd = proc.stdout.fileno()
+    t0 = time.time()
+    buf = b""
+    while time.time() - t0 < timeout:
+        r, _, _ = select.select([fd], [], [], 1.0)
+        if r:
+            chunk = os.read(fd, 65536)
+            if not chunk:
+                break
+            buf += chunk
+            if b"listening" in buf:
+                return buf.decode(errors="replace")
+        if proc.poll() is not None:
+            break
+    proc.kill()
+    err = proc.stderr.read() if proc.stderr else ""
+    raise AssertionError(f"fifo_auto did not come up: {buf.decode(errors='replace')} {err}")

@@ -4,7 +4,6 @@ process_query.py:35-111), with `ssh host 'bash -s'` replaced by local bash
 (tests/driver_harness.py; bytes pinned by tests/golden/driver_fixtures.json).
 The answers and per-query side files are checked against the CPU oracle."""
 import os
-import select
 import subprocess
 import time
 
@@ -32,20 +31,6 @@ def _read_diff(path, g):
                 break
     return w
 
-
-def _wait_ready(proc, timeout=60):
-    t0 = time.time()
-    buf = ""
-    while time.time() - t0 < timeout:
-        r, _, _ = select.select([proc.stdout], [], [], 1.0)
-        if r:
-            line = proc.stdout.readline()
-            buf += line
-            if "listening" in line:
-                return buf
-        if proc.poll() is not None:
-            break
-    raise AssertionError(f"fifo_auto did not come up: {buf} {proc.stderr.read()}")
 
 
 @pytest.mark.parametrize("method,key,fmt", [("mod", 3, "moves"), ("div", 5, "moves"),
@@ -83,7 +68,7 @@ def test_drivers_end_to_end(tmp_path, method, key, fmt):
                  outdir, "--alg", "table-search", "--device", "0"],
                 stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
         for pr in procs:
-            _wait_ready(pr)
+            H.wait_ready(pr, timeout=60)
         nfs = str(tmp_path / "nfs")
         os.makedirs(nfs)
         conf = {"workers": ["localhost"] * W, "nfs": nfs, "partmethod": method, "partkey": key,

@@ -19,7 +19,6 @@ configs[2] — partition mod 8: eight workers' indexes (one GPU, in turn), the
 """
 import gc
 import os
-import select
 import subprocess
 import time
 
@@ -101,20 +100,6 @@ def _make_cpds(m, outdir, concurrent):
     return [o for o, _ in outs]
 
 
-def _wait_ready(proc, timeout=300):
-    t0 = time.time()
-    buf = ""
-    while time.time() - t0 < timeout:
-        r, _, _ = select.select([proc.stdout], [], [], 1.0)
-        if r:
-            line = proc.stdout.readline()
-            buf += line
-            if "listening" in line:
-                return buf
-        if proc.poll() is not None:
-            break
-    raise AssertionError(f"fifo_auto did not come up: {buf} {proc.stderr.read()}")
-
 
 def test_melb_mod3_concurrent_build_and_driver_flow(melb):
     m = melb
@@ -141,7 +126,7 @@ def test_melb_mod3_concurrent_build_and_driver_flow(melb):
                  "--outdir", a, "--alg", "table-search", "--device", "0"],
                 stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
         for pr in procs:
-            _wait_ready(pr)
+            H.wait_ready(pr, timeout=300)
         nfs = str(m["dir"] / "nfs")
         os.makedirs(nfs, exist_ok=True)
         conf = {"workers": ["localhost"] * W, "nfs": nfs, "partmethod": "mod", "partkey": 3,
