@@ -134,6 +134,7 @@ struct Agg {
 };
 
 bool async_on();  // CPD_ASYNC (defined with the other switches)
+hipStream_t thread_stream(int device);
 
 // Largest auto batch (CPD_BATCH_MAX, a multiple of 1024 <= 32768; A/B knob).
 uint32_t batch_max() {
@@ -222,8 +223,6 @@ struct cpd_graph {
     // the same stream before the next batch: one set)
     DevBuf<uint32_t> rle_xs, rle_cc, rle_hard;
     HostBuf<uint32_t> rle_hard_h;          // [1]
-    HostBuf<uint32_t> lane_row_h[2];       // host source of lane_rowx[x]
-    HostBuf<uint32_t> counts_h;            // [B] runs per lane
     // the buffer set the next batch uses, once the emit that last read it is done
     uint32_t acquire_set() {
         const uint32_t x = async ? cur : 0u;
@@ -493,8 +492,6 @@ struct cpd_graph {
             b.tgt_h.alloc(B);
         }
         counts.alloc(B);
-        counts_h.alloc(B);
-        for (auto& l : lane_row_h) l.alloc(B);
         rle_hard_h.alloc(1);
         ovf_hb.alloc(1);
         ovf_hb.p[0] = 0;
@@ -504,8 +501,8 @@ struct cpd_graph {
 struct cpd_rows {
     int device = 0;
     uint32_t nrows = 0;
-    uint64_t total = 0;         // runs of all rows
-    hipEvent_t done = nullptr;  // after the last emit into `moves` (emit overlap)
+    mutable uint64_t total = 0;  // runs of all rows (valid after settle())
+    hipEvent_t done = nullptr;   // after the last batch's count + emit (emit stream)
     void wait() const {
         if (done) HIP_CHECK(hipEventSynchronize(done));
     }
@@ -515,16 +512,60 @@ struct cpd_rows {
             (void)hipEventDestroy(done);
         }
     }
+    // A batch's run counts arrive after its rows are queued: the count pass
+    // runs on the emit stream, beside the next batch's sweeps.  Per batch:
+    // its rows' lanes and two page-locked buffers — the lane -> table row map
+    // the emit reads and the per-lane run counts it lands — turned into run
+    // offsets by settle() once `done` has passed.  A rebuild into these rows
+    // retires the unsettled batches (their copies may still be in flight).
+    struct Batch {
+        uint32_t k = 0;
+        std::vector<uint32_t> pos_of;
+        HostBuf<uint32_t> lane_rows, counts;
+        hipEvent_t ev = nullptr;  // after the batch's last copy (emit stream)
+        ~Batch() {
+            if (ev) (void)hipEventDestroy(ev);
+        }
+    };
+    mutable std::mutex settle_mu;
+    mutable std::vector<std::unique_ptr<Batch>> pending, retired, spare;
+    Batch* new_batch(uint32_t B) {
+        for (size_t i = 0; i < retired.size();) {  // recycle what the device is done with
+            if (hipEventQuery(retired[i]->ev) == hipSuccess) {
+                spare.push_back(std::move(retired[i]));
+                retired.erase(retired.begin() + (long)i);
+            } else {
+                ++i;
+            }
+        }
+        std::unique_ptr<Batch> b;
+        if (!spare.empty()) {
+            b = std::move(spare.back());
+            spare.pop_back();
+        } else {
+            b = std::make_unique<Batch>();
+        }
+        b->lane_rows.alloc(B);
+        b->counts.alloc(B);
+        if (!b->ev) HIP_CHECK(hipEventCreateWithFlags(&b->ev, hipEventDisableTiming));
+        pending.push_back(std::move(b));
+        return pending.back().get();
+    }
+    void retire() {
+        for (auto& b : pending) retired.push_back(std::move(b));
+        pending.clear();
+    }
+    void settle() const;
     std::vector<uint32_t> targets;   // node ids, row order
     std::vector<uint32_t> lanes;     // batch lane of each row
-    std::vector<uint64_t> offsets;   // run offsets (host), nrows+1
+    mutable std::vector<uint64_t> offsets;  // run offsets (host), nrows+1 (after settle())
     // The rows in their compact form: 4-bit move tables, wpr = npad / 8 words
     // per row (rle_moves) — the RLE row expanded, 5x smaller than its runs on
     // the bench graphs.  Run words are decoded from them on demand
     // (moves_runs, at `off`).
     uint32_t n = 0, wpr = 0;
     DevBuf<uint32_t> moves;
-    DevBuf<uint64_t> off;
+    mutable DevBuf<uint64_t> off;
     // device staging for decoded runs, one buffer per concurrent exporter
     // (make_cpd_auto's writer threads), kept until the rows are freed
     mutable std::mutex stage_mu;
@@ -606,6 +647,25 @@ struct cpd_index {
     DevBuf<uint8_t> fin;
     DevBuf<unsigned long long> agg;
 };
+
+void cpd_rows::settle() const {
+    std::lock_guard<std::mutex> l(settle_mu);
+    HIP_CHECK(hipSetDevice(device));
+    wait();
+    for (auto& b : retired) spare.push_back(std::move(b));
+    retired.clear();
+    if (pending.empty()) return;
+    for (auto& b : pending) {
+        for (uint32_t i = 0; i < b->k; ++i)
+            offsets.push_back(offsets.back() + b->counts.p[b->pos_of[i]]);
+        spare.push_back(std::move(b));
+    }
+    pending.clear();
+    total = offsets.back();
+    hipStream_t st = thread_stream(device);
+    off.upload(offsets.data(), offsets.size(), st);
+    HIP_CHECK(hipStreamSynchronize(st));
+}
 
 namespace {
 
@@ -1373,38 +1433,14 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         g->prep_slot = ns;
         g->prep_targets.assign(next, next + next_k);
     };
-    const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
-    if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
-        HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), g->stream));
-        g->timed("rle_count", (fm_row + st_row + 8.0 * nch) * k, [&] {
-            launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->stream);
-        });
-        g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
-            launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
-                           g->rle_hard.p, g->stream);
-        });
-        HIP_CHECK(hipMemcpyAsync(g->rle_hard_h.p, g->rle_hard.p, sizeof(uint32_t),
-                                 hipMemcpyDeviceToHost, g->stream));
-        prep_next();  // everything of this batch is queued: start the next up-sweep
-        HIP_CHECK(hipStreamSynchronize(g->stream));
-        if (g->rle_hard_h.p[0]) {  // runs too long for the seam repair: the bounded pass
-            g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
-                launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);
-            });
-            if (trace_on()) std::fprintf(stderr, "[cpd] batch re-counted by rle_scan\n");
-        }
-    } else {
-        g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
-            launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, g->stream);
-        });
-        prep_next();
-    }
-    const uint32_t* counts = g->counts_h.p;
-    HIP_CHECK(hipMemcpyAsync(g->counts_h.p, g->counts.p, k * sizeof(uint32_t),
-                             hipMemcpyDeviceToHost, g->stream));
+    // The count, the seam repair and the move-table emit of this batch go to
+    // the emit stream (estream; `stream` when the overlap is off), after its
+    // first moves (ev_fm): they run beside the next batch's sweeps, and the
+    // run counts land in a page-locked buffer the rows settle from later
+    // (cpd_rows::settle) — the host waits for none of it here.
+    prep_next();  // this batch's sweeps and first moves are queued: start the next up-sweep
+    if (!g->prepped) HIP_CHECK(hipEventSynchronize(g->ev_down));  // ovf_h (prep_next did it otherwise)
     const bool probe = narrow && g->narrow_probe && k == g->B;
-    g->sync();
-    add_up_late_bytes(g, slot);
     const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
     if (narrow && g->timing) {  // group rows kept wide / all group rows
         g->agg["wide_rows"].launches += g->ovf_h();
@@ -1415,30 +1451,41 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         narrow_decide(g);
     }
     const double t2 = now_seconds();
-    // run offsets in the caller's order, appended after r->total (counts[]
-    // are per lane); the batch's rows become table rows r->nrows + i, written
-    // by lane pos_of[i]
-    std::vector<uint64_t> off(k + 1);
-    off[0] = r->total;
+    hipStream_t es = g->async ? g->estream : g->stream;
+    if (es != g->stream) HIP_CHECK(hipStreamWaitEvent(es, g->ev_fm, 0));
+    // the batch's rows become table rows r->nrows + i, written by lane pos_of[i]
     const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
-    uint32_t* lrow = g->lane_row_h[x].p;
-    for (uint32_t i = 0; i < k; ++i) {
-        const uint32_t p = pos_of[i];
-        lrow[p] = r->nrows + i;
-        off[i + 1] = off[i] + counts[p];
-    }
-    const uint64_t new_total = off[k];
     CPD_REQUIRE(r->moves.n >= (size_t)(r->nrows + k) * g->wpr(), CPD_E_ARG,
                 "rows: move table capacity");
-    const double t3 = now_seconds();
-    // the emit: on estream (the next batch's sweeps start meanwhile on
-    // stream), or in line when overlap is off; everything it reads came from
-    // `stream`, which the count sync above has drained.  (Deferring it until
-    // the next batch's up-sweep is done, so that it overlaps the down-sweep
-    // instead, measured 288.5k rows/s against 293.6k: round 2, run-word emit.)
-    hipStream_t es = g->async ? g->estream : g->stream;
-    HIP_CHECK(hipMemcpyAsync(g->lane_rowx[x].p, lrow, k * sizeof(uint32_t), hipMemcpyHostToDevice,
+    cpd_rows::Batch* rb = r->new_batch(g->B);
+    rb->k = k;
+    rb->pos_of.assign(pos_of.begin(), pos_of.begin() + k);
+    for (uint32_t i = 0; i < k; ++i) rb->lane_rows.p[pos_of[i]] = r->nrows + i;
+    HIP_CHECK(hipMemcpyAsync(g->lane_rowx[x].p, rb->lane_rows.p, k * sizeof(uint32_t),
+                             hipMemcpyHostToDevice, es));
+    const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
+    if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
+        HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), es));
+        g->timed("rle_count", (fm_row + st_row + 8.0 * nch) * k, [&] {
+            launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, es);
+        });
+        g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
+            launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
+                           g->rle_hard.p, es);
+        });
+        // runs too long for the seam repair: the bounded pass, which does
+        // nothing unless rle_fix raised rle_hard
+        g->timed("rle_recount", 0.0, [&] {
+            launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es, g->rle_hard.p);
+        });
+    } else {
+        g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
+            launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es);
+        });
+    }
+    HIP_CHECK(hipMemcpyAsync(rb->counts.p, g->counts.p, k * sizeof(uint32_t), hipMemcpyDeviceToHost,
                              es));
+    HIP_CHECK(hipEventRecord(rb->ev, es));
     // per row: the sets (fm_row), the segment states (4 B per 32 columns;
     // the run counts are read only where the look-ahead needs them), the
     // table (npad / 2)
@@ -1452,18 +1499,17 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         HIP_CHECK(hipEventRecord(g->ev_emit[x], es));
         g->emit_pending[x] = true;
     }
-    g->sync();
+    if (g->timing) {  // the up levels' bytes need this batch's stats (after its first moves)
+        g->sync();
+        add_up_late_bytes(g, slot);
+    }
     if (trace_on())
-        std::fprintf(stderr,
-                     "[cpd] batch %u rows: launch sweeps+fm %.2f ms, to counts %.2f ms, offsets "
-                     "%.2f ms, emit %.2f ms, runs %llu\n",
-                     k, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3,
-                     (now_seconds() - t3) * 1e3, (unsigned long long)(new_total - r->total));
-    r->offsets.insert(r->offsets.end(), off.begin() + 1, off.end());
+        std::fprintf(stderr, "[cpd] batch %u rows: launch sweeps+fm %.2f ms, to down-sweep end %.2f "
+                             "ms, count+emit queued %.2f ms\n",
+                     k, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (now_seconds() - t2) * 1e3);
     r->targets.insert(r->targets.end(), targets, targets + k);
     r->lanes.insert(r->lanes.end(), pos_of.begin(), pos_of.begin() + k);
     r->nrows += k;
-    r->total = new_total;
 }
 
 }  // namespace
@@ -1480,6 +1526,7 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         cpd_rows* r = reuse ? reuse : new cpd_rows();
         std::unique_ptr<cpd_rows> owned(reuse ? nullptr : r);
         r->device = g->device;
+        r->retire();  // an earlier build's unsettled batches (copies may be in flight)
         r->nrows = 0;
         r->total = 0;
         r->targets.clear();
@@ -1505,8 +1552,6 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
             build_batch(g, targets + b, k, r, next, next_k);
         }
         g->hint.clear();
-        r->off.upload(r->offsets.data(), r->offsets.size(), g->stream);
-        HIP_CHECK(hipStreamSynchronize(g->stream));
         owned.release();
         *out = r;
     });
@@ -1524,6 +1569,7 @@ int cpd_graph_hint_next(cpd_graph* g, const uint32_t* targets, uint32_t ntargets
 int cpd_rows_count(const cpd_rows* r, uint32_t* nrows, uint64_t* total_runs) {
     return guarded([&] {
         CPD_REQUIRE(r, CPD_E_ARG, "null rows");
+        if (total_runs) r->settle();
         if (nrows) *nrows = r->nrows;
         if (total_runs) *total_runs = r->total;
     });
@@ -1532,8 +1578,7 @@ int cpd_rows_count(const cpd_rows* r, uint32_t* nrows, uint64_t* total_runs) {
 int cpd_rows_wait(const cpd_rows* r) {
     return guarded([&] {
         CPD_REQUIRE(r, CPD_E_ARG, "null rows");
-        HIP_CHECK(hipSetDevice(r->device));
-        r->wait();
+        r->settle();
     });
 }
 
@@ -1547,12 +1592,12 @@ int cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count, uin
         CPD_REQUIRE(r, CPD_E_ARG, "null rows");
         CPD_REQUIRE(first <= r->nrows && count <= r->nrows - first, CPD_E_ARG,
                     "export range: rows out of range");
+        r->settle();
         const uint64_t base = r->offsets[first], end = r->offsets[first + count];
         if (offsets)
             for (uint32_t i = 0; i <= count; ++i) offsets[i] = r->offsets[first + i] - base;
         if (!runs || end == base) return;
         HIP_CHECK(hipSetDevice(r->device));
-        r->wait();
         hipStream_t st = thread_stream(r->device);
         // decode piece by piece (<= kDecodeRuns runs, a longer row alone) into
         // a staging buffer of the rows' pool, then copy out
@@ -1865,7 +1910,8 @@ void append_host(cpd_index* ix, uint32_t count, const uint64_t* offsets, const u
 void append_built(cpd_index* ix, const cpd_rows* r) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(r->device == g->device, CPD_E_ARG, "index: rows live on another device");
-    r->wait();
+    r->settle();
+    g->select();
     CPD_REQUIRE(r->nrows <= ix->nrows - ix->added, CPD_E_ARG, "index: more rows than declared");
     if (!r->nrows) return;
     // the built rows must be the declared rows at these positions (row i of
@@ -1974,6 +2020,8 @@ int cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out) {
     return guarded([&] {
         CPD_REQUIRE(g && r && out, CPD_E_ARG, "index: null argument");
         *out = nullptr;
+        g->select();
+        r->settle();
         g->select();
         auto ix = index_init(g, r->targets.data(), r->nrows);
         ix->declared = r->total;

@@ -1136,16 +1136,19 @@ struct RleState {
 // chunked count rle_count_ch + rle_fix replaces this for 4-bit sets; this
 // pass serves wider sets and rows whose long runs the seam repair gives up
 // on.)
+// gate (may be null): run only if *gate != 0 — the re-count of a batch
+// whose seam repair gave up, queued unconditionally after rle_fix.
 template <int FMB>
 __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm, uint32_t npad,
                                                 uint32_t nrows, uint32_t* __restrict__ counts,
-                                                RleState rs) {
+                                                RleState rs, const uint32_t* __restrict__ gate) {
     using F = FmFmt<FMB>;
     constexpr int Q = F::kWords / 4;  // 16-B loads per lane per tile
     constexpr int LB = CPD_RLE_LOOKBACK;  // lookback columns
     const uint32_t row = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     if (row >= nrows) return;
+    if (gate && *gate == 0u) return;
     const uint32_t nseg = npad / kSeg;
     // this lane's 16-B pieces of the row: 4-bit rows are row-group interleaved
     // (fm4_piece), wider ones row-major; tile t is `step` pieces further on
@@ -3024,14 +3027,15 @@ bool first_moves_reads_own(uint32_t shift, bool narrow) {
 }
 
 void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                      uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s) {
+                      uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s,
+                      const uint32_t* gate) {
     if (!nrows) return;
     const dim3 grid((nrows + 3u) / 4u), block(256);
     const kern::RleState rs{st, rc};
     switch (fmb) {
-        case 4: launch(kern::rle_scan<4>, grid, block, s, fm, npad, nrows, counts, rs); break;
-        case 8: launch(kern::rle_scan<8>, grid, block, s, fm, npad, nrows, counts, rs); break;
-        default: launch(kern::rle_scan<16>, grid, block, s, fm, npad, nrows, counts, rs); break;
+        case 4: launch(kern::rle_scan<4>, grid, block, s, fm, npad, nrows, counts, rs, gate); break;
+        case 8: launch(kern::rle_scan<8>, grid, block, s, fm, npad, nrows, counts, rs, gate); break;
+        default: launch(kern::rle_scan<16>, grid, block, s, fm, npad, nrows, counts, rs, gate); break;
     }
 }
 

@@ -108,9 +108,11 @@ constexpr uint32_t kFmTile = 2048;
 
 // Greedy RLE count, one wave per row: counts[row] = runs per row, and per
 // 32-column segment the scan's entry state and the runs ending inside it
-// (st / rc, [nrows][npad/32] u32 / u8).  fmb = fm_bits(shift).
+// (st / rc, [nrows][npad/32] u32 / u8).  fmb = fm_bits(shift).  gate (may be
+// null): the launch does nothing unless *gate != 0 when it runs.
 void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
-                      uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s);
+                      uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s,
+                      const uint32_t* gate = nullptr);
 
 // The compact row form: each row's greedy RLE row as a 4-bit move table
 // (column c = nibble c % 8 of word c / 8, npad / 8 words per row — the dense
