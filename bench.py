@@ -510,7 +510,7 @@ def cpu_partitioned(threads, rows_per_worker=384, queries=20000):
 # end-to-end worker build: bin/make_cpd_auto
 # as the driver runs it (make_cpds.py:20), on a cold plan cache, every row the
 # rank owns built, copied out of HBM and written to its bucket files in the
-# compact layout (DOSCPD02: a 4-bit move per column, n/2 bytes per row); then
+# compact layout (DOSCPD02: a 1/2/4-bit move per column by max out-degree); then
 # bin/fifo_auto (make_fifos.py:21) loads those files and answers a request
 # through the reference's FIFO protocol, checked against the oracle
 

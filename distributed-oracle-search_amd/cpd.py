@@ -52,6 +52,7 @@ EXPORTED = [
     "cpd_rows_lanes", "cpd_graph_hint_next", "cpd_graph_set_hbm_reserve",
     "cpd_device_mem_info", "cpd_rows_move_words", "cpd_rows_export_moves",
     "cpd_index_append_moves", "cpd_device_arena", "cpd_device_arena_release", "cpd_batch_bytes",
+    "cpd_rows_move_bits", "cpd_graph_move_bits",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
@@ -373,14 +374,21 @@ class Rows:
         return off, runs
 
     def move_words(self) -> int:
-        """Words per row of the compact form (ceil(n / 8))."""
+        """Words per row of the compact form (ceil(n * bits / 32))."""
         w = C.c_uint32()
         _check(lib.cpd_rows_move_words(self._h, C.byref(w)))
         return w.value
 
+    def move_bits(self) -> int:
+        """Bits per move of the compact form (1, 2 or 4)."""
+        b = C.c_uint32()
+        _check(lib.cpd_rows_move_bits(self._h, C.byref(b)))
+        return b.value
+
     def export_moves(self, first: int = 0, count: int | None = None) -> np.ndarray:
-        """Rows [first, first+count) as 4-bit move tables: (count, ceil(n/8))
-        u32, column c in bits 4*(c%8) of word c//8 (cpd_rows_export_moves)."""
+        """Rows [first, first+count) in the compact form: (count, words) u32,
+        column c's move in bits [b*c, b*c + b) of the row, b = move_bits()
+        (cpd_rows_export_moves)."""
         if count is None:
             count = self.count()[0] - first
         out = np.empty((count, self.move_words()), np.uint32)
@@ -433,6 +441,12 @@ class Graph:
         """HBM the auto batch leaves free for what follows on this GPU
         (cpd_graph_set_hbm_reserve); applies at the next set_batch(0)."""
         _check(lib.cpd_graph_set_hbm_reserve(self._h, C.c_uint64(nbytes)))
+
+    def move_bits(self) -> int:
+        """Bits per move of the compact rows this graph builds."""
+        b = C.c_uint32()
+        _check(lib.cpd_graph_move_bits(self._h, C.byref(b)))
+        return b.value
 
     def set_coords(self, x, y) -> None:
         """Node coordinates (node-id space; None clears them): a batch's
@@ -523,13 +537,14 @@ class Index:
         _check(lib.cpd_index_append_rows(self._h, C.c_uint32(len(off) - 1), _ptr(off, u64p),
                                          _ptr(rn, u32p)))
 
-    def append_moves(self, moves) -> None:
-        """Host rows in the compact form: (count, ceil(n/8)) u32 move tables
+    def append_moves(self, moves, bits: int = 4) -> None:
+        """Host rows in the compact form: (count, ceil(n * bits / 32)) u32
         (cpd_index_append_moves)."""
         mv = np.ascontiguousarray(moves, np.uint32)
         if mv.ndim != 2:
             raise ValueError("moves must be (rows, words)")
-        _check(lib.cpd_index_append_moves(self._h, C.c_uint32(mv.shape[0]), _ptr(mv, u32p)))
+        _check(lib.cpd_index_append_moves(self._h, C.c_uint32(mv.shape[0]), C.c_uint32(bits),
+                                          _ptr(mv, u32p)))
 
     def append_rows(self, rows: Rows) -> None:
         _check(lib.cpd_index_append_built_rows(self._h, rows._h))

@@ -203,6 +203,9 @@ struct cpd_graph {
     // batch workspace
     uint32_t B = 0;
     uint32_t fmb = 16;  // bits per first-move set (fm_bits(adj_shift))
+    // bits per move in the packed compact form: every move indexes its
+    // column's out-list (wildcard runs take bit 0), so out-degrees <= 2^bits
+    uint32_t move_bits = 4;
     DevBuf<uint32_t> dist, counts;
     // Emit overlap (CPD_ASYNC, default on): a batch's move-table emit
     // (rle_moves) runs on `estream` while the next batch's sweeps start on
@@ -563,9 +566,10 @@ struct cpd_rows {
     // per row (rle_moves) — the RLE row expanded, 5x smaller than its runs on
     // the bench graphs.  Run words are decoded from them on demand
     // (moves_runs, at `off`).
-    uint32_t n = 0, wpr = 0;
+    uint32_t n = 0, wpr = 0, bits = 4;  // bits: per move in the packed compact form
     DevBuf<uint32_t> moves;
     mutable DevBuf<uint64_t> off;
+    uint32_t packed_words() const { return (uint32_t)(((uint64_t)n * bits + 31u) / 32u); }
     // device staging for decoded runs, one buffer per concurrent exporter
     // (make_cpd_auto's writer threads), kept until the rows are freed
     mutable std::mutex stage_mu;
@@ -613,7 +617,7 @@ struct cpd_index {
     DevBuf<uint32_t> dense;
     bool dense_ready = false;
     // staging of host-appended chunks (stream_dense), format flag
-    DevBuf<uint32_t> stage;
+    DevBuf<uint32_t> stage, pstage;  // pstage: packed compact rows before unpacking
     DevBuf<uint64_t> stage_off;
     DevBuf<uint32_t> flag;
     // expand_rows work split: first run-chunk of each row being expanded
@@ -923,6 +927,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         }
         while ((1u << g->adj_shift) < maxdeg) ++g->adj_shift;
         g->fmb = fm_bits(g->adj_shift);
+        g->move_bits = maxdeg <= 2 ? 1u : maxdeg <= 4 ? 2u : 4u;
         hipStream_t s = g->stream;
         g->order_d.upload(g->order.data(), n, s);
         g->row_ptr.upload(g->rowc_host.data(), n + 1, s);
@@ -1071,6 +1076,13 @@ int cpd_graph_set_coords(cpd_graph* g, const int32_t* x, const int32_t* y) {
             return;
         }
         g->lane_key = hilbert_keys(x, y, g->n);
+    });
+}
+
+int cpd_graph_move_bits(const cpd_graph* g, uint32_t* bits) {
+    return guarded([&] {
+        CPD_REQUIRE(g && bits, CPD_E_ARG, "null argument");
+        *bits = g->move_bits;
     });
 }
 
@@ -1546,6 +1558,7 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         r->offsets.assign(1, 0);
         r->n = g->n;
         r->wpr = g->wpr();
+        r->bits = g->move_bits;
         if (r->moves.n < (size_t)ntargets * r->wpr) {
             r->wait();  // an earlier build's emit may still write the old table
             r->moves.alloc((size_t)ntargets * r->wpr);
@@ -1634,7 +1647,14 @@ int cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count, uin
 int cpd_rows_move_words(const cpd_rows* r, uint32_t* words) {
     return guarded([&] {
         CPD_REQUIRE(r && words, CPD_E_ARG, "null argument");
-        *words = (r->n + 7u) / 8u;
+        *words = r->packed_words();
+    });
+}
+
+int cpd_rows_move_bits(const cpd_rows* r, uint32_t* bits) {
+    return guarded([&] {
+        CPD_REQUIRE(r && bits, CPD_E_ARG, "null argument");
+        *bits = r->bits;
     });
 }
 
@@ -1647,10 +1667,24 @@ int cpd_rows_export_moves(const cpd_rows* r, uint32_t first, uint32_t count, uin
         HIP_CHECK(hipSetDevice(r->device));
         r->wait();
         hipStream_t st = thread_stream(r->device);
-        const size_t w = (r->n + 7u) / 8u;  // the compact row: ceil(n / 8) words
-        HIP_CHECK(hipMemcpy2DAsync(moves, w * sizeof(uint32_t), r->moves.p + (size_t)first * r->wpr,
-                                   (size_t)r->wpr * sizeof(uint32_t), w * sizeof(uint32_t), count,
-                                   hipMemcpyDeviceToHost, st));
+        const size_t w = r->packed_words();
+        if (r->bits == 4) {  // the nibble tables as they are, at the packed row width
+            HIP_CHECK(hipMemcpy2DAsync(moves, w * sizeof(uint32_t),
+                                       r->moves.p + (size_t)first * r->wpr,
+                                       (size_t)r->wpr * sizeof(uint32_t), w * sizeof(uint32_t),
+                                       count, hipMemcpyDeviceToHost, st));
+        } else {  // packed on the GPU, then one contiguous copy
+            auto stage = r->acquire_stage();
+            stage->alloc((size_t)count * w);
+            launch_pack_moves(r->moves.p + (size_t)first * r->wpr, r->wpr, count, r->bits,
+                              (uint32_t)w, stage->p, st);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipMemcpyAsync(moves, stage->p, (size_t)count * w * sizeof(uint32_t),
+                                     hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            r->release_stage(std::move(stage));
+            return;
+        }
         HIP_CHECK(hipStreamSynchronize(st));
     });
 }
@@ -1964,31 +1998,45 @@ void append_built(cpd_index* ix, const cpd_rows* r) {
 // RLE index decodes them on the GPU, counting first.  No format check is
 // needed: every nibble is some move, and a move naming no out-edge of its
 // column stops the walk (unfinished) like the oracle's.
-void append_moves(cpd_index* ix, uint32_t count, const uint32_t* moves) {
+void append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* moves) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(count <= ix->nrows - ix->added, CPD_E_ARG, "index: more rows than declared");
     if (!count) return;
     CPD_REQUIRE(moves, CPD_E_ARG, "index: null move rows");
-    const size_t w = (g->n + 7u) / 8u, wpr = g->wpr();
+    CPD_REQUIRE(bits == 1 || bits == 2 || bits == 4, CPD_E_ARG, "index: bits per move must be 1, 2 or 4");
+    const size_t w = ((uint64_t)g->n * bits + 31u) / 32u, wpr = g->wpr();
     hipStream_t s = g->stream;
-    if (!ix->keep_rle) {
-        HIP_CHECK(hipMemcpy2DAsync(ix->dense.p + (size_t)ix->added * wpr, wpr * sizeof(uint32_t),
-                                   moves, w * sizeof(uint32_t), w * sizeof(uint32_t), count,
-                                   hipMemcpyHostToDevice, s));
-        HIP_CHECK(hipStreamSynchronize(s));
-        ix->added += count;
-        return;
-    }
-    // RLE: pieces of <= 1 GiB of tables staged at the table stride
+    // pieces of <= 1 GiB of nibble tables: the packed rows are staged and
+    // unpacked into the dense index (or, for an RLE index, into a stage the
+    // runs are decoded from)
     const uint32_t piece = (uint32_t)std::max<size_t>(1, ((size_t)1 << 28) / wpr);
     for (uint32_t r0 = 0; r0 < count; r0 += piece) {
         const uint32_t nr = std::min(piece, count - r0);
-        ix->stage.alloc((size_t)std::min(piece, count) * wpr);
+        uint32_t* tables = nullptr;
+        if (!ix->keep_rle) {
+            tables = ix->dense.p + (size_t)ix->added * wpr;
+        } else {
+            ix->stage.alloc((size_t)std::min(piece, count) * wpr);
+            tables = ix->stage.p;
+        }
+        if (bits == 4) {
+            HIP_CHECK(hipMemcpy2DAsync(tables, wpr * sizeof(uint32_t), moves + (size_t)r0 * w,
+                                       w * sizeof(uint32_t), w * sizeof(uint32_t), nr,
+                                       hipMemcpyHostToDevice, s));
+        } else {
+            ix->pstage.alloc((size_t)std::min(piece, count) * w);
+            HIP_CHECK(hipMemcpyAsync(ix->pstage.p, moves + (size_t)r0 * w, (size_t)nr * w * sizeof(uint32_t),
+                                     hipMemcpyHostToDevice, s));
+            launch_unpack_moves(ix->pstage.p, (uint32_t)w, nr, bits, (uint32_t)wpr, tables, s);
+            HIP_CHECK(hipGetLastError());
+        }
+        if (!ix->keep_rle) {
+            HIP_CHECK(hipStreamSynchronize(s));
+            ix->added += nr;
+            continue;
+        }
         ix->flag.alloc(std::max<size_t>(ix->flag.n, (size_t)std::min(piece, count)));
-        HIP_CHECK(hipMemcpy2DAsync(ix->stage.p, wpr * sizeof(uint32_t), moves + (size_t)r0 * w,
-                                   w * sizeof(uint32_t), w * sizeof(uint32_t), nr,
-                                   hipMemcpyHostToDevice, s));
-        launch_moves_count(ix->stage.p, (uint32_t)wpr, g->n, nr, ix->flag.p, s);
+        launch_moves_count(tables, (uint32_t)wpr, g->n, nr, ix->flag.p, s);
         HIP_CHECK(hipGetLastError());
         std::vector<uint32_t> cnt(nr);
         HIP_CHECK(hipMemcpyAsync(cnt.data(), ix->flag.p, nr * sizeof(uint32_t),
@@ -2000,8 +2048,7 @@ void append_moves(cpd_index* ix, uint32_t count, const uint32_t* moves) {
         CPD_REQUIRE(o[nr] <= ix->cap, CPD_E_ARG, "index: more runs than the index was created for");
         HIP_CHECK(hipMemcpyAsync(ix->off.p + ix->added, o.data(), o.size() * sizeof(uint64_t),
                                  hipMemcpyHostToDevice, s));
-        launch_moves_runs(ix->stage.p, (uint32_t)wpr, g->n, nr, ix->off.p + ix->added, 0,
-                          ix->runs.p, s);
+        launch_moves_runs(tables, (uint32_t)wpr, g->n, nr, ix->off.p + ix->added, 0, ix->runs.p, s);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipStreamSynchronize(s));
         ix->offsets.insert(ix->offsets.end(), o.begin() + 1, o.end());
@@ -2075,11 +2122,11 @@ int cpd_index_append_rows(cpd_index* ix, uint32_t count, const uint64_t* offsets
     });
 }
 
-int cpd_index_append_moves(cpd_index* ix, uint32_t count, const uint32_t* moves) {
+int cpd_index_append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* moves) {
     return guarded([&] {
         CPD_REQUIRE(ix, CPD_E_ARG, "index: null argument");
         ix->g->select();
-        append_moves(ix, count, moves);
+        append_moves(ix, count, bits, moves);
     });
 }
 

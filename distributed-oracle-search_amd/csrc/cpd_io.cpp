@@ -449,12 +449,14 @@ uint64_t MoveBucket::rows_offset() const {
 MoveBucketFile::MoveBucketFile(const std::string& path, const MoveBucket& b)
     : path_(path), tmp_(path + ".tmp"), nrows_((uint32_t)b.targets.size()), words_(b.words),
       rows_off_(b.rows_offset()) {
-    if (b.words != (b.n + 7u) / 8u) throw Error(CPD_E_ARG, "move bucket: words != ceil(n / 8)");
+    if (!(b.bits == 1 || b.bits == 2 || b.bits == 4) ||
+        b.words != ((uint64_t)b.n * b.bits + 31u) / 32u)
+        throw Error(CPD_E_ARG, "move bucket: words != ceil(n * bits / 32)");
     fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (fd_ < 0) throw Error(CPD_E_IO, "cannot write " + tmp_);
     std::vector<char> h(rows_off_, 0);  // header, targets, zero counts, pad
     std::memcpy(h.data(), kMoveBucketMagic, 8);
-    const uint32_t h32[8] = {b.n, nrows_, b.bid, b.method, b.key, b.maxworker, b.words, 0u};
+    const uint32_t h32[8] = {b.n, nrows_, b.bid, b.method, b.key, b.maxworker, b.words, b.bits};
     std::memcpy(h.data() + 8, h32, sizeof h32);
     std::memcpy(h.data() + 48, &b.fingerprint, 8);  // total (h + 40) is written by close()
     std::memcpy(h.data() + kMoveHeader, b.targets.data(), 4ull * nrows_);
@@ -521,7 +523,10 @@ MoveBucket read_move_bucket_head(const std::string& path) {
     b.key = h32[4];
     b.maxworker = h32[5];
     b.words = h32[6];
-    if (b.words != (b.n + 7u) / 8u) throw Error(CPD_E_IO, path + ": row width does not match n");
+    b.bits = h32[7];
+    if (!(b.bits == 1 || b.bits == 2 || b.bits == 4) ||
+        b.words != ((uint64_t)b.n * b.bits + 31u) / 32u)
+        throw Error(CPD_E_IO, path + ": row width does not match n and bits per move");
     b.targets.resize(nrows);
     b.counts.resize(nrows);
     if (size != b.rows_offset() + 4ull * b.words * nrows)

@@ -10,8 +10,9 @@
 //   query  "{n}\n" then n lines "s t" (process_query.send_queries, :93-96).
 //   .cpd   one file per partition bucket (README.md:86-93 "one or more CPDs"),
 //          our own layout == the HBM layout, so a load is one read + one copy.
-//          DOSCPD02 (default): the rows in their compact form, a 4-bit move
-//          per column (cpd_rows_export_moves), n/2 bytes per row; DOSCPD01
+//          DOSCPD02 (default): the rows in their compact form, a move per
+//          column (cpd_rows_export_moves) in `bits` = 1, 2 or 4 bits by the
+//          graph's max out-degree (header word 7), n*bits/8 bytes per row; DOSCPD01
 //          (make_cpd_auto --format rle): RLE run words, 4 B per run.
 //   .order the DFS column order shared by every bucket of a graph.
 #pragma once
@@ -95,14 +96,15 @@ void read_bucket_runs(const std::string& path, const CpdBucket& head, uint64_t f
 // move tables); throws CPD_E_IO for anything else.
 int bucket_format(const std::string& path);
 
-// DOSCPD02 — compact bucket: the rows as 4-bit move tables (bijective with
-// the greedy RLE rows; cpd_api.h cpd_rows_export_moves):
-//   magic "DOSCPD02" | n nrows bid method key maxworker words pad (8 x u32) |
+// DOSCPD02 — compact bucket: the rows as move tables, `bits` (1, 2 or 4)
+// per column (bijective with the greedy RLE rows; cpd_api.h
+// cpd_rows_export_moves):
+//   magic "DOSCPD02" | n nrows bid method key maxworker words bits (8 x u32) |
 //   total_runs u64 | fingerprint u64 | targets u32[nrows] |
 //   runs u32[nrows] (run count of each row) | zero pad to a 4-KiB boundary |
-//   rows u32[nrows][words], words = ceil(n / 8)
+//   rows u32[nrows][words], words = ceil(n * bits / 32)
 struct MoveBucket {
-    uint32_t n = 0, bid = 0, method = 0, key = 0, maxworker = 0, words = 0;
+    uint32_t n = 0, bid = 0, method = 0, key = 0, maxworker = 0, words = 0, bits = 4;
     uint64_t fingerprint = 0, total_runs = 0;
     std::vector<uint32_t> targets, counts;
     uint64_t rows_offset() const;

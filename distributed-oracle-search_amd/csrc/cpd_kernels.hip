@@ -1556,6 +1556,49 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
     }
 }
 
+// The compact form on the wire and on disk: a move per column in `bits` =
+// 1, 2 or 4 bits (every move of a graph whose out-degrees are <= 2^bits fits:
+// a move indexes its column's out-list, and a wildcard run's lowest set bit
+// is 0), ceil(n * bits / 32) words per row, rows back to back.  pack: one
+// thread per packed word, from the nibble tables (stride words per row);
+// unpack: one thread per nibble word.  Columns >= n carry whatever the
+// nibble table holds there (the last run's move).
+__global__ __launch_bounds__(256) void pack_moves(const uint32_t* __restrict__ dense,
+                                                  uint32_t stride, uint32_t rows, uint32_t bits,
+                                                  uint32_t words, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)rows * words) return;
+    const uint32_t r = (uint32_t)(i / words), w = (uint32_t)(i % words);
+    const uint32_t per = 32u / bits;  // columns per packed word
+    const uint32_t* __restrict__ src = dense + (size_t)r * stride + (size_t)w * per / 8u;
+    const uint32_t mask = (1u << bits) - 1u;
+    uint32_t o = 0;
+    for (uint32_t j = 0; j < per / 8u; ++j) {
+        const uint32_t x = (size_t)w * per / 8u + j < stride ? src[j] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k) o |= ((x >> (4u * k)) & mask) << (bits * (8u * j + k));
+    }
+    out[i] = o;
+}
+
+__global__ __launch_bounds__(256) void unpack_moves(const uint32_t* __restrict__ packed,
+                                                    uint32_t words, uint32_t rows, uint32_t bits,
+                                                    uint32_t stride, uint32_t* __restrict__ dense) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)rows * stride) return;
+    const uint32_t r = (uint32_t)(i / stride), d = (uint32_t)(i % stride);
+    const uint32_t bit0 = d * 8u * bits;  // first bit of column 8d in the packed row
+    const uint32_t w = bit0 / 32u;
+    uint32_t o = 0;
+    if (w < words) {
+        const uint32_t x = packed[(size_t)r * words + w] >> (bit0 % 32u);
+        const uint32_t mask = (1u << bits) - 1u;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k) o |= ((x >> (bits * k)) & mask) << (4u * k);
+    }
+    dense[i] = o;
+}
+
 // Move tables -> RLE words, the inverse of rle_moves: a row's runs start at
 // column 0 and at every column whose move differs from its left neighbour's,
 // word = column << 4 | move (warthog rle_run32 [U]); columns >= n are
@@ -3080,6 +3123,22 @@ void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
         case 8: launch(kern::rle_moves<8>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
         default: launch(kern::rle_moves<16>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
     }
+}
+
+void launch_pack_moves(const uint32_t* dense, uint32_t stride, uint32_t rows, uint32_t bits,
+                       uint32_t words, uint32_t* out, hipStream_t s) {
+    const uint64_t items = (uint64_t)rows * words;
+    if (!items) return;
+    launch(kern::pack_moves, dim3((uint32_t)((items + 255u) / 256u)), dim3(256), s, dense, stride,
+           rows, bits, words, out);
+}
+
+void launch_unpack_moves(const uint32_t* packed, uint32_t words, uint32_t rows, uint32_t bits,
+                         uint32_t stride, uint32_t* dense, hipStream_t s) {
+    const uint64_t items = (uint64_t)rows * stride;
+    if (!items) return;
+    launch(kern::unpack_moves, dim3((uint32_t)((items + 255u) / 256u)), dim3(256), s, packed, words,
+           rows, bits, stride, dense);
 }
 
 void launch_moves_count(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,

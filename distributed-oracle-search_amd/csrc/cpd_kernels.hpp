@@ -121,6 +121,14 @@ void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
 void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
                       const uint32_t* st, const uint8_t* rc, const uint32_t* out_row,
                       uint32_t* dense, hipStream_t s);
+// The compact form's packed width: `bits` (1, 2 or 4) per column,
+// ceil(n * bits / 32) = words per row, rows back to back.  pack: nibble
+// tables (stride words per row) -> packed rows; unpack: the reverse (the
+// nibble words past a packed row's end are written as 0).
+void launch_pack_moves(const uint32_t* dense, uint32_t stride, uint32_t rows, uint32_t bits,
+                       uint32_t words, uint32_t* out, hipStream_t s);
+void launch_unpack_moves(const uint32_t* packed, uint32_t words, uint32_t rows, uint32_t bits,
+                         uint32_t stride, uint32_t* dense, hipStream_t s);
 // Move tables (row r at dense + r * stride words, stride % 4 == 0) back to
 // RLE words: runs start at column 0 and wherever the move changes (columns
 // >= n ignored).  count: counts[r] = runs of row r; runs: row r's words at

@@ -256,7 +256,7 @@ int main(int argc, char** argv) {
                 for (uint32_t r0 = 0, i = 0; r0 < nr; r0 += per, ++i) {
                     rd.get();  // piece i is in pin[i & 1] (a read error is rethrown here)
                     if (r0 + per < nr) rd = std::async(std::launch::async, read, r0 + per, (int)((i + 1) & 1u));
-                    const int rc = cpd_index_append_moves(ix, std::min(per, nr - r0), pin[i & 1u]);
+                    const int rc = cpd_index_append_moves(ix, std::min(per, nr - r0), mh.bits, pin[i & 1u]);
                     if (rc != CPD_OK) {
                         if (rd.valid()) rd.wait();
                         cli::check(rc, "index rows");

@@ -18,8 +18,9 @@
 //                 [--plan-only]        build / load the cached plan and exit
 //                 [--targets-from S]   only rows of targets of scenario S (q s t)
 //                 [--format moves|rle] bucket file layout: moves (default) =
-//                                      DOSCPD02, the rows as 4-bit move tables
-//                                      (n/2 bytes per row); rle = DOSCPD01,
+//                                      DOSCPD02, the rows as move tables of
+//                                      1/2/4 bits per column (by max out-degree,
+//                                      n*bits/8 bytes per row); rle = DOSCPD01,
 //                                      the run words (4 B per run)
 //                 [--discard]          null sink: every row is still built and
 //                                      copied out of HBM (D2H), but no file is
@@ -200,14 +201,17 @@ public:
     uint64_t x_bytes = 0;
 
 private:
-    static cpd::io::MoveBucket move_head(const CpdBucket& h) {
+    cpd::io::MoveBucket move_head(const CpdBucket& h) const {
         cpd::io::MoveBucket m;
         m.n = h.n;
         m.bid = h.bid;
         m.method = h.method;
         m.key = h.key;
         m.maxworker = h.maxworker;
-        m.words = (h.n + 7u) / 8u;
+        uint32_t bits = 4;
+        ok(cpd_graph_move_bits(g_, &bits), "move bits");
+        m.bits = bits;
+        m.words = (uint32_t)(((uint64_t)h.n * bits + 31u) / 32u);
         m.fingerprint = h.fingerprint;
         m.targets = h.targets;
         return m;
@@ -416,8 +420,13 @@ int main(int argc, char** argv) {
                 const double fit = avail > 0 ? 0.85 * avail / (double)per1k : 0.0;
                 if (fit < 1.0)
                     throw std::runtime_error("HBM reserve leaves too little for a 1024-row batch");
-                const char* bm = std::getenv("CPD_BATCH_MAX");  // the library's cap (A/B knob)
-                const double cap = bm && *bm ? std::max(1.0, std::min(32.0, std::floor(std::atof(bm) / 1024))) : 24.0;
+                // the library's cap (A/B knob).  Writing files, the sink bounds
+                // the worker (the GPU builds rows ~30x faster than a disk takes
+                // them), so a batch past 4096 rows only adds HBM to
+                // commit beside the plan; --discard keeps the build-bound cap
+                const char* bm = std::getenv("CPD_BATCH_MAX");
+                const double dflt = a.has("discard") ? 24.0 : 4.0;
+                const double cap = bm && *bm ? std::max(1.0, std::min(32.0, std::floor(std::atof(bm) / 1024))) : dflt;
                 batch = (uint32_t)std::min(cap, std::floor(fit)) * 1024u;
             }
             cli::check(cpd_batch_bytes(g.n, maxdeg, batch, &arena_bytes), "batch bytes");
@@ -542,10 +551,11 @@ int main(int argc, char** argv) {
                 first.push_back(targets.size());
                 double tb = now();
                 cli::check(cpd_build_rows(dg, targets.data(), (uint32_t)targets.size(), rows, &rows), "build");
-                uint32_t nr = 0, words = 0;
+                uint32_t nr = 0, words = 0, bits = 4;
                 uint64_t tot = 0;
                 cli::check(cpd_rows_count(rows, &nr, &tot), "rows");
                 cli::check(cpd_rows_move_words(rows, &words), "move words");
+                cli::check(cpd_rows_move_bits(rows, &bits), "move bits");
                 std::vector<uint64_t> off(nr + 1);
                 std::vector<uint32_t> runs(moves ? 0 : tot), mv(moves ? (size_t)nr * words : 0);
                 if (moves) {
@@ -567,6 +577,7 @@ int main(int argc, char** argv) {
                         b.key = (uint32_t)key;
                         b.maxworker = (uint32_t)W;
                         b.words = words;
+                        b.bits = bits;
                         b.fingerprint = fp;
                         b.targets.assign(targets.begin() + first[k], targets.begin() + first[k + 1]);
                         const uint32_t nb = (uint32_t)b.targets.size();

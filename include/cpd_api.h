@@ -198,6 +198,9 @@ int  cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out);
 /* Batch width (rows built per sweep, multiple of 1024; 0 = auto from HBM). */
 int  cpd_graph_set_batch(cpd_graph* g, uint32_t batch);
 int  cpd_graph_get_batch(const cpd_graph* g, uint32_t* batch);
+/* Bits per move of the graph's packed compact rows (cpd_rows_move_bits of
+ * every cpd_rows it builds): 1, 2 or 4 for max out-degree <= 2, <= 4, else. */
+int  cpd_graph_move_bits(const cpd_graph* g, uint32_t* bits);
 /* HBM bytes the auto batch (batch 0) leaves free for what follows on this
  * GPU: an index built from the rows on the same handle, or a fifo_auto
  * serving beside a make_cpd_auto.  The auto batch takes 85% of the free HBM
@@ -225,7 +228,8 @@ void cpd_graph_free(cpd_graph* g);
  * (t itself and unreachable nodes: wildcard), and the greedy run-length row
  * over the DFS column order with the lowest-set-bit tie-break
  * (warthog graph_oracle::add_row [U]).  Rows stay in HBM in their compact
- * form — the RLE row expanded into a 4-bit move per column, which under the
+ * form — the RLE row expanded into a move per column (1, 2 or 4 bits by the
+ * graph's max out-degree: cpd_graph_move_bits), which under the
  * greedy rule is a bijection (consecutive runs always carry different moves,
  * so the runs are column 0 and every column whose move differs from its left
  * neighbour's) — and are exported either as run words or in that form.
@@ -251,11 +255,15 @@ int  cpd_rows_export(const cpd_rows* r, uint64_t* offsets /* nrows+1 */,
  * (the overlapped writer of bin/make_cpd_auto).  Either output may be NULL. */
 int  cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count,
                            uint64_t* offsets /* count+1 */, uint32_t* runs);
-/* The compact form (DOSCPD02 bucket files, cpd_index_append_moves): a row is
- * *words = ceil(n / 8) u32, column c's move in bits 4*(c%8)..+3 of word
- * c/8; the nibbles past column n-1 repeat the last run's move.  Rows
- * [first, first + count) back to back, on the calling thread's stream.      */
+/* The compact form (DOSCPD02 bucket files, cpd_index_append_moves): a move
+ * per column in *bits = 1, 2 or 4 bits — the fewest that hold every move of
+ * the graph (a move indexes its column's out-list: out-degrees <= 2, <= 4,
+ * else) — column c at bits bits*c .. bits*c + bits-1 of the row, a row being
+ * *words = ceil(n * bits / 32) u32; the fields past column n-1 repeat the
+ * last run's move.  Rows [first, first + count) back to back, on the calling
+ * thread's stream (packed on the GPU when bits < 4).                        */
 int  cpd_rows_move_words(const cpd_rows* r, uint32_t* words);
+int  cpd_rows_move_bits(const cpd_rows* r, uint32_t* bits);
 int  cpd_rows_export_moves(const cpd_rows* r, uint32_t first, uint32_t count,
                            uint32_t* moves /* count * words */);
 int  cpd_rows_targets(const cpd_rows* r, uint32_t* targets /* nrows */);
@@ -307,12 +315,13 @@ int  cpd_index_create_empty(cpd_graph* g, const uint32_t* row_targets, uint32_t 
 int  cpd_index_append_rows(cpd_index* ix, uint32_t count, const uint64_t* offsets,
                            const uint32_t* runs);
 int  cpd_index_append_built_rows(cpd_index* ix, const cpd_rows* r);
-/* Rows in the compact form (cpd_rows_export_moves layout, count rows of
- * ceil(n / 8) words): a DENSE index takes them as they are, an RLE index
- * decodes them into run words on the GPU (total_runs of the create call must
- * cover them).  No format check is needed: a nibble naming no out-edge of its
- * column stops a walk there, unfinished, as the oracle's walk does.          */
-int  cpd_index_append_moves(cpd_index* ix, uint32_t count, const uint32_t* moves);
+/* Rows in the compact form (cpd_rows_export_moves layout: count rows of
+ * ceil(n * bits / 32) words, bits = 1, 2 or 4): unpacked on the GPU into a
+ * DENSE index's 4-bit tables, or decoded into run words for an RLE index
+ * (total_runs of the create call must cover them).  No format check is
+ * needed: a move naming no out-edge of its column stops a walk there,
+ * unfinished, as the oracle's walk does.                                    */
+int  cpd_index_append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* moves);
 /* Rows declared / appended, runs resident in HBM, bytes of dense tables.     */
 int  cpd_index_info(const cpd_index* ix, uint32_t* nrows, uint32_t* added,
                     uint64_t* runs_resident, uint64_t* dense_bytes);

@@ -114,36 +114,39 @@ def build_rows(row_ptr, dst, w, order, targets, threads=0):
     return off, runs
 
 
-def moves_from_runs(offsets, runs, n):
+def moves_from_runs(offsets, runs, n, bits=4):
     """The compact form of RLE rows (the checker of cpd_rows_export_moves /
-    DOSCPD02): (nrows, ceil(n/8)) u32, column c's move — that of the last run
-    starting at or before c (get_move) — in bits 4*(c%8) of word c//8; the
-    nibbles past column n-1 repeat the last run's move."""
+    DOSCPD02): (nrows, ceil(n*bits/32)) u32, column c's move — that of the
+    last run starting at or before c (get_move) — in bits [bits*c, bits*c +
+    bits) of the row; the fields past column n-1 repeat the last run's move."""
     offsets = np.ascontiguousarray(offsets, np.uint64)
     runs = _u32(runs)
-    nrows, w = len(offsets) - 1, (n + 7) // 8
+    nrows, per = len(offsets) - 1, 32 // bits
+    w = (n * bits + 31) // 32
     out = np.zeros((nrows, w), np.uint32)
-    cols = np.arange(8 * w, dtype=np.int64)
+    cols = np.arange(per * w, dtype=np.int64)
+    shifts = (bits * np.arange(per, dtype=np.uint64)).astype(np.uint64)
     for r in range(nrows):
         rr = runs[int(offsets[r]):int(offsets[r + 1])]
         starts = (rr >> 4).astype(np.int64)
         idx = np.searchsorted(starts, cols, side="right") - 1  # last run starting <= c
-        nib = (rr[idx] & 0xF).astype(np.uint32).reshape(w, 8)
-        out[r] = (nib << (4 * np.arange(8, dtype=np.uint32))).sum(axis=1, dtype=np.uint64)
+        mv = (rr[idx] & 0xF).astype(np.uint64).reshape(w, per)
+        out[r] = (mv << shifts).sum(axis=1, dtype=np.uint64).astype(np.uint32)
     return out
 
 
-def runs_from_moves(moves, n):
+def runs_from_moves(moves, n, bits=4):
     """Inverse of moves_from_runs under the greedy rule: a run starts at
     column 0 and wherever the move differs from the left neighbour's."""
     moves = _u32(moves)
-    nrows = moves.shape[0]
+    nrows, per = moves.shape[0], 32 // bits
+    mask = (1 << bits) - 1
     off = np.zeros(nrows + 1, np.uint64)
     out = []
     for r in range(nrows):
-        nib = ((moves[r][:, None] >> (4 * np.arange(8, dtype=np.uint32))) & 0xF).ravel()[:n]
-        starts = np.flatnonzero(np.concatenate(([True], nib[1:] != nib[:-1])))
-        out.append(((starts.astype(np.uint32) << 4) | nib[starts]).astype(np.uint32))
+        mv = ((moves[r][:, None] >> (bits * np.arange(per, dtype=np.uint32))) & mask).ravel()[:n]
+        starts = np.flatnonzero(np.concatenate(([True], mv[1:] != mv[:-1])))
+        out.append(((starts.astype(np.uint32) << 4) | mv[starts]).astype(np.uint32))
         off[r + 1] = off[r] + len(starts)
     return off, (np.concatenate(out) if out else np.empty(0, np.uint32))
 

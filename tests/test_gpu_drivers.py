@@ -129,8 +129,8 @@ def _read_move_bucket(path):
     """The compact bucket layout of csrc/cpd_io.cpp (DOSCPD02, MoveBucketFile)."""
     raw = open(path, "rb").read()
     assert raw[:8] == b"DOSCPD02"
-    n, nrows, bid, method, key, maxworker, words, _ = (int(x) for x in np.frombuffer(raw, np.uint32, 8, 8))
-    assert words == (n + 7) // 8
+    n, nrows, bid, method, key, maxworker, words, bits = (int(x) for x in np.frombuffer(raw, np.uint32, 8, 8))
+    assert bits in (1, 2, 4) and words == (n * bits + 31) // 32
     total = int(np.frombuffer(raw, np.uint64, 1, 40)[0])
     p = 56
     targets = np.frombuffer(raw, np.uint32, nrows, p)
@@ -138,7 +138,7 @@ def _read_move_bucket(path):
     rows_at = -(-(p + 8 * nrows) // 4096) * 4096
     assert len(raw) == rows_at + 4 * words * nrows and int(counts.sum()) == total
     moves = np.frombuffer(raw, np.uint32, nrows * words, rows_at).reshape(nrows, words)
-    return targets, counts, moves
+    return targets, counts, moves, bits
 
 
 @pytest.mark.parametrize("fmt", ["moves", "rle"])
@@ -188,7 +188,8 @@ def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key, fmt):
         np.testing.assert_array_equal(off, o_off)
         np.testing.assert_array_equal(runs, o_runs)
     else:
-        targets, counts, moves = _read_move_bucket(os.path.join(dirs["pipe"], pipe[0]))
+        targets, counts, moves, bits = _read_move_bucket(os.path.join(dirs["pipe"], pipe[0]))
+        assert bits == 2  # out-degrees <= 4
         o_off, o_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, np.array(targets))
         np.testing.assert_array_equal(counts, np.diff(o_off))
-        np.testing.assert_array_equal(moves, oracle.moves_from_runs(o_off, o_runs, g.n))
+        np.testing.assert_array_equal(moves, oracle.moves_from_runs(o_off, o_runs, g.n, bits))

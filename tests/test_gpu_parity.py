@@ -83,8 +83,12 @@ def test_compact_rows_bit_exact(setup):
     targets = rng.permutation(g.n)[: min(g.n, 1500)].astype(np.uint32)
     rows = dev.build_rows(targets)
     ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    bits = rows.move_bits()
+    deg = int(np.diff(g.row_ptr.astype(np.int64)).max())
+    assert bits == (1 if deg <= 2 else 2 if deg <= 4 else 4) == dev.move_bits()
     mv = rows.export_moves()
-    np.testing.assert_array_equal(mv, oracle.moves_from_runs(ref_off, ref_runs, g.n), err_msg=name)
+    np.testing.assert_array_equal(mv, oracle.moves_from_runs(ref_off, ref_runs, g.n, bits),
+                                  err_msg=name)
     # a range, and the decoded runs of a range
     a = len(targets) // 3
     b = min(len(targets), a + 7)
@@ -96,11 +100,12 @@ def test_compact_rows_bit_exact(setup):
     t = targets[rng.integers(0, len(targets), 3000)]
     rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, plan.order(), targets, ref_off,
                                      ref_runs, s, t)
+    mv4 = oracle.moves_from_runs(ref_off, ref_runs, g.n, 4)
     for mode in ("dense", "rle"):
         ix = cpd.Index.streamed(dev, targets, int(ref_off[-1]), mode=mode)
         half = len(targets) // 2
-        ix.append_moves(mv[:half])
-        ix.append_moves(mv[half:])
+        ix.append_moves(mv[:half], bits)
+        ix.append_moves(mv4[half:], 4)  # any width holding the moves is accepted
         assert ix.mode == mode
         cost, hops, fin, _ = ix.query(s, t)
         np.testing.assert_array_equal(cost, rc, err_msg=f"{name} {mode}")

@@ -102,11 +102,15 @@ def test_compact_rows_are_the_rle_rows(graphs):
         for i in range(len(targets)):
             row = runs[off[i]:off[i + 1]]
             assert np.all(np.diff((row & 0xF).astype(np.int64)) != 0), name
-        mv = oracle.moves_from_runs(off, runs, g.n)
-        assert mv.shape == (len(targets), (g.n + 7) // 8)
-        off2, runs2 = oracle.runs_from_moves(mv, g.n)
-        np.testing.assert_array_equal(off2, off, err_msg=name)
-        np.testing.assert_array_equal(runs2, runs, err_msg=name)
+        deg = int(np.diff(g.row_ptr.astype(np.int64)).max())
+        for bits in (1, 2, 4):  # the packed widths: every move < 2^bits when deg <= 2^bits
+            if max(deg, 1) > (1 << bits):
+                continue
+            mv = oracle.moves_from_runs(off, runs, g.n, bits)
+            assert mv.shape == (len(targets), (g.n * bits + 31) // 32)
+            off2, runs2 = oracle.runs_from_moves(mv, g.n, bits)
+            np.testing.assert_array_equal(off2, off, err_msg=f"{name} {bits}")
+            np.testing.assert_array_equal(runs2, runs, err_msg=f"{name} {bits}")
 
 
 def _ka_graph(case):
