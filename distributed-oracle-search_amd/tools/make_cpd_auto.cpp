@@ -259,7 +259,10 @@ private:
             for (uint32_t u = r0; u < r1; ++u) c[u - r0] = (uint32_t)((*offs)[u + 1] - (*offs)[u]);
             f->write_counts(brow0, c.data(), r1 - r0);
         });
-        const uint32_t per = (uint32_t)std::max<uint64_t>(1, kPieceRuns / words);
+        // pieces of <= kPieceRuns words, and at least one per writer thread
+        // in a block so the whole pool copies and writes it
+        const uint64_t fair = (B_ + pool_.size() - 1) / pool_.size();
+        const uint32_t per = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(kPieceRuns / words, fair));
         for (uint32_t p0 = r0; p0 < r1; p0 += per) {
             const uint32_t p1 = std::min(r1, p0 + per);
             submit([=] {
@@ -422,10 +425,10 @@ int main(int argc, char** argv) {
                     throw std::runtime_error("HBM reserve leaves too little for a 1024-row batch");
                 // the library's cap (A/B knob).  Writing files, the sink bounds
                 // the worker (the GPU builds rows ~30x faster than a disk takes
-                // them), so a batch past 4096 rows only adds HBM to
+                // them), so a batch past 2048 rows only adds HBM to
                 // commit beside the plan; --discard keeps the build-bound cap
                 const char* bm = std::getenv("CPD_BATCH_MAX");
-                const double dflt = a.has("discard") ? 24.0 : 4.0;
+                const double dflt = a.has("discard") ? 24.0 : 2.0;
                 const double cap = bm && *bm ? std::max(1.0, std::min(32.0, std::floor(std::atof(bm) / 1024))) : dflt;
                 batch = (uint32_t)std::min(cap, std::floor(fit)) * 1024u;
             }

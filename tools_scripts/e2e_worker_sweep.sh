@@ -13,7 +13,7 @@ mkdir -p $W gpurun_out
 for c in $CFGS; do
   B=${c%%:*}; T=${c#*:}
   rm -rf $W/out; mkdir -p $W/out
-  timeout -k 10 300 $R/bin/make_cpd_auto --input $W/g.xy --partmethod div --partkey 8 --workerid 0 \
+  timeout -k 10 300 env ${ENVS:-} $R/bin/make_cpd_auto --input $W/g.xy --partmethod div --partkey 8 --workerid 0 \
       --maxworker 8 --outdir $W/out --device 0 --batch $B --write-threads $T > $W/log 2>&1 \
       || { echo "make_cpd_auto B=$B T=$T failed"; tail -5 $W/log; exit 1; }
   echo "B=$B T=$T $(grep make_cpd_auto-json $W/log)" | tee -a $R/gpurun_out/${TAG}_e2e.log
