@@ -542,7 +542,7 @@ def full_build(args, xy, world, rank, device, comm, runner=subprocess.run):
     fresh (cold) plan cache shared by the node's ranks; returns its JSON phase
     line.  Rank 0 writes its bucket files (DOSCPD02) into the cache directory
     on the box's disk; the other ranks run the same worker path with
-    --discard (D2H export, no file writes): eight 62.5-GB workers would
+    --discard (D2H export, no file writes): eight 31-GB workers would
     outgrow one node's disk."""
     import glob
     import shutil

@@ -373,6 +373,16 @@ class Rows:
                                          None, _ptr(runs, u32p)))
         return off, runs
 
+    def offsets(self, first: int = 0, count: int | None = None) -> np.ndarray:
+        """Run offsets of rows [first, first+count) relative to row `first`
+        (count + 1 values), without the runs."""
+        if count is None:
+            count = self.count()[0] - first
+        off = np.empty(count + 1, np.uint64)
+        _check(lib.cpd_rows_export_range(self._h, C.c_uint32(first), C.c_uint32(count),
+                                         _ptr(off, u64p), None))
+        return off
+
     def move_words(self) -> int:
         """Words per row of the compact form (ceil(n * bits / 32))."""
         w = C.c_uint32()

@@ -53,6 +53,32 @@ def check_row_format(off, runs, n):
     assert cols.max() < n
 
 
+def move_run_counts(mv, n, bits, chunk=1024):
+    """Runs per row of compact rows (cpd_rows_export_moves layout), counted
+    on the whole array in numpy: 1 (column 0) + the columns 1..n-1 whose move
+    differs from the left neighbour's — the greedy RLE row's run count
+    (DESIGN §2), so it must equal the row's offsets difference."""
+    mv = np.ascontiguousarray(mv, np.uint32)
+    per, W = 32 // bits, mv.shape[1]
+    low = np.uint32(sum(1 << (bits * i) for i in range(per)))
+    # per word: the fields of columns 1..n-1 (column 0 and pad never count)
+    cols = np.arange(W * per, dtype=np.int64).reshape(W, per)
+    ok = (cols >= 1) & (cols < n)
+    valid = (ok.astype(np.uint64) << (bits * np.arange(per, dtype=np.uint64))).sum(axis=1)
+    valid = valid.astype(np.uint32) & low
+    out = np.empty(len(mv), np.int64)
+    for a in range(0, len(mv), chunk):
+        x = mv[a:a + chunk]
+        carry = np.zeros_like(x)
+        carry[:, 1:] = x[:, :-1] >> np.uint32(32 - bits)
+        d = x ^ ((x << np.uint32(bits)) | carry)  # field c: move(c) ^ move(c-1)
+        f = d
+        for k in range(1, bits):
+            f = f | (d >> np.uint32(k))
+        out[a:a + chunk] = 1 + np.bitwise_count(f & valid).sum(axis=1, dtype=np.int64)
+    return out
+
+
 def hilbert_keys(x, y):
     """libcpd's lane key (cpd_gpu.cpp hilbert_keys): the Hilbert index of each
     node's coordinates on a 2^16 x 2^16 grid over the bounding box."""

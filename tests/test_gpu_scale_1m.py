@@ -6,9 +6,12 @@ idle MI355X) — the bench's own workload and shape.
   - 128 rows spread over the worker's targets: bit-exact against the oracle;
   - the bench's first full batch (worker 0's first B targets, Hilbert lane
     order): every row well formed, and in EVERY 1024-lane slab the rows at
-    its first, last and one interior lane bit-exact against the oracle; then
-    the batch streamed into a dense index and walked: free-flow cost ==
-    Dijkstra distance for every query of 16 targets;
+    its first, last and one interior lane bit-exact against the oracle; the
+    whole batch in its compact form (what DOSCPD02 files hold): the sampled
+    rows bit-exact against the oracle's runs expanded, and every row's move
+    changes == its run count; then those compact rows streamed into a dense
+    index (the fifo_auto load) and walked: free-flow cost == Dijkstra
+    distance for every query of 16 targets;
   - congested (.diff stand-in, SURVEY.md §8d: 10% of edges x U[1, 3], seed 3)
     and free-flow queries over the oracle's 128 rows, dense and RLE: cost,
     moves and finished flags bit-exact.
@@ -20,7 +23,7 @@ import pytest
 
 import cpd
 import oracle
-from scale_common import check_row_format, lane_of, owned, plan_for, spread
+from scale_common import check_row_format, lane_of, move_run_counts, owned, plan_for, spread
 
 pytestmark = pytest.mark.gpu
 
@@ -79,10 +82,22 @@ def test_1m_full_batch(w1m):
         off, runs = rows.export_range(int(i), 1)
         np.testing.assert_array_equal(runs, ref_runs[int(ref_off[k]):int(ref_off[k + 1])],
                                       err_msg=f"row {i} lane {want[k]} (target {targets[i]})")
-    # the whole batch as a streamed dense index (what fifo_auto holds), walked
+    # the whole batch in its compact form: the sampled
+    # rows against the oracle's runs, every row's run count from its moves
+    bits = rows.move_bits()
+    assert bits == 2  # out-degree <= 4
+    mv = rows.export_moves()
+    assert mv.shape == (B, (g.n * bits + 31) // 32)
+    np.testing.assert_array_equal(mv[sample], oracle.moves_from_runs(ref_off, ref_runs, g.n, bits))
+    counts = np.diff(rows.offsets().astype(np.int64))
+    np.testing.assert_array_equal(move_run_counts(mv, g.n, bits), counts)
+    assert int(counts.sum()) == total
+    del rows  # the compact rows streamed into a dense index, as fifo_auto loads a file
+    gc.collect()
     ix = cpd.Index.streamed(dev, targets, total, mode="dense")
-    ix.append_rows(rows)
-    del rows  # the dense index alone stays in HBM
+    for a in range(0, B, 6000):
+        ix.append_moves(mv[a:a + 6000], bits)
+    del mv
     gc.collect()
     rng = np.random.default_rng(7)
     probe = rng.choice(targets, 16, replace=False)

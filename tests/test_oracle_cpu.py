@@ -17,6 +17,7 @@ from scipy.sparse.csgraph import dijkstra
 
 import cpd
 import oracle
+from scale_common import move_run_counts
 
 KA = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "known_answers.json")))
 
@@ -111,6 +112,9 @@ def test_compact_rows_are_the_rle_rows(graphs):
             off2, runs2 = oracle.runs_from_moves(mv, g.n, bits)
             np.testing.assert_array_equal(off2, off, err_msg=f"{name} {bits}")
             np.testing.assert_array_equal(runs2, runs, err_msg=f"{name} {bits}")
+            # the bulk run counter the 1M full-batch GPU test applies
+            np.testing.assert_array_equal(move_run_counts(mv, g.n, bits, chunk=5),
+                                          np.diff(off.astype(np.int64)), err_msg=f"{name} {bits}")
 
 
 def _ka_graph(case):
