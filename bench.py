@@ -947,21 +947,23 @@ def main():
                   "form": {1: "per-row tables", 2: "memoised walks"}[sst["tables"]],
                   "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
         # fscale 0 (optimal under the .diff weights): a 1M-node search expands
-        # ~48k nodes into a 2^19-column workspace (36 MB per lane with
-        # tables); as many searches as lanes fit in 60% of the free HBM run at
-        # once (round 3 ran 512)
-        cap0 = 1 << 19
-        free_b, _ = cpd.device_mem_info(gpu)
-        zq = int(max(512, min(8192, (0.6 * free_b / (68 * cap0)) // 256 * 256)))
+        # ~48k nodes.  16384 searches start at once in 2^17-column workspaces
+        # (8.9 MB per lane with tables, 60% of the free HBM); the few that
+        # outgrow them rerun in 2^19-column ones (capacity escalation; round
+        # 3 ran 512 searches, round 4's first runs 4096, all at 2^19)
+        cap0, capmax = 1 << 17, 1 << 19
+        zq = 16384
         zs = rng.integers(0, g.n, zq).astype(np.uint32)
         zt = srows[rng.integers(0, len(srows), zq)]
-        six.search(zs[:64], zt[:64], capacity=cap0)  # warm
-        _, _, zfin, zcnt, zst = six.search(zs, zt, capacity=cap0, workspace_frac=0.6)
+        six.search(zs[:64], zt[:64], capacity=capmax)  # warm
+        _, _, zfin, zcnt, zst = six.search(zs, zt, capacity=cap0, capacity_max=capmax,
+                                           workspace_frac=0.6)
         ztot = comm.reduce([float(zq), zst["kernel_ms"]], "SUM")
         (zmax,) = comm.reduce([zst["kernel_ms"]], "MAX")
         search["fscale0"] = {
             "queries_per_s": round(ztot[0] / (zmax / 1e3), 1) if zmax else 0.0,
-            "queries": zq, "capacity": cap0, "lanes": int(zst["lanes"]),
+            "queries": zq, "capacity": cap0, "capacity_max": capmax,
+            "reruns": int(zst["reruns"]), "lanes": int(zst["lanes"]),
             "mean_expanded": round(float(zcnt[:, 0].mean()), 1),
             "finished": int(zfin.sum()), "overflow": int(zst["overflow"]),
             "kernel_ms": round(zst["kernel_ms"], 3),

@@ -89,14 +89,14 @@ class SearchOpts(C.Structure):
     _fields_ = [("hscale", C.c_double), ("fscale", C.c_double), ("k_moves", C.c_int32),
                 ("itrs", C.c_int64), ("time_ns", C.c_uint64), ("capacity", C.c_uint32),
                 ("virtual_tick_ns", C.c_uint64), ("tables", C.c_int32),
-                ("workspace_frac", C.c_double)]
+                ("workspace_frac", C.c_double), ("capacity_max", C.c_uint32)]
 
 
 class SearchStats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("queries", "finished", "expanded", "inserted",
                                           "touched", "updated", "surplus", "plen", "overflow")] + \
                [("kernel_ms", C.c_double), ("lanes", C.c_uint64), ("tables_ms", C.c_double),
-                ("tables", C.c_int32)]
+                ("tables", C.c_int32), ("reruns", C.c_uint64)]
 
 
 class KernelTime(C.Structure):
@@ -604,13 +604,15 @@ class Index:
         return {k: getattr(st, k) for k, _ in QueryStats._fields_}
 
     def search(self, s, t, hscale=1.0, fscale=0.0, k_moves=-1, itrs=-1, time_ns=0,
-               capacity=0, virtual_tick_ns=0, tables="auto", workspace_frac=0.0):
+               capacity=0, virtual_tick_ns=0, tables="auto", workspace_frac=0.0,
+               capacity_max=0):
         """CPD-heuristic search (cpd_query_search) for queries (s, t):
-        (cost, plen, finished, counters[nq, 5], stats)."""
+        (cost, plen, finished, counters[nq, 5], stats); finished = 2: the
+        search outgrew its workspace (after the capacity_max reruns)."""
         self.prepare(s, t)
         o = SearchOpts(float(hscale), float(fscale), int(k_moves), int(itrs), int(time_ns),
                        int(capacity), int(virtual_tick_ns), SEARCH_FORMS[tables],
-                       float(workspace_frac))
+                       float(workspace_frac), int(capacity_max))
         st = SearchStats()
         _check(lib.cpd_query_search(self._h, C.byref(o), C.byref(st)))
         nq = len(s)

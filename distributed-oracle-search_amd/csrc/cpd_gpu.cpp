@@ -2371,12 +2371,16 @@ void cpd_index_free(cpd_index* ix) {
 int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st) {
     return guarded([&] {
         CPD_REQUIRE(ix, CPD_E_ARG, "null index");
-        cpd_search_opts o{1.0, 0.0, -1, -1, 0, 0, 0, CPD_SEARCH_AUTO, 0.0};
+        cpd_search_opts o{1.0, 0.0, -1, -1, 0, 0, 0, CPD_SEARCH_AUTO, 0.0, 0};
         if (opts) o = *opts;
         if (!o.capacity) o.capacity = 32768;
         CPD_REQUIRE((o.capacity & (o.capacity - 1)) == 0 && o.capacity >= 64 &&
                         o.capacity <= (1u << 24),
                     CPD_E_ARG, "search capacity must be a power of 2 in [64, 2^24]");
+        CPD_REQUIRE(o.capacity_max == 0 ||
+                        ((o.capacity_max & (o.capacity_max - 1)) == 0 &&
+                         o.capacity_max >= o.capacity && o.capacity_max <= (1u << 24)),
+                    CPD_E_ARG, "search capacity_max must be 0 or a power of 2 in [capacity, 2^24]");
         CPD_REQUIRE(o.hscale >= 0.0 && o.fscale >= 0.0, CPD_E_ARG,
                     "hscale and fscale must be >= 0");
         CPD_REQUIRE(o.workspace_frac >= 0.0 && o.workspace_frac <= 0.9, CPD_E_ARG,
@@ -2468,6 +2472,83 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
         HIP_CHECK(hipStreamSynchronize(g->stream));
         float ms = 0.f;
         HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+        // Capacity escalation: the searches that outgrew the workspace
+        // (fin = 2) run again from scratch, alone, with 4x the columns per
+        // lane (fewer lanes fit) until none overflows or capacity_max is
+        // reached — so a batch runs most searches at a small capacity, many
+        // lanes at once, and pays the large workspace only for the few long
+        // ones.  Their first-pass counters leave the sums; the rerun's
+        // results and counters are scattered over theirs.
+        uint64_t reruns = 0;
+        for (uint32_t cap = o.capacity; h[7] && cap < o.capacity_max;) {
+            cap = std::min(cap * 4u, o.capacity_max);
+            std::vector<uint8_t> f(nq);
+            std::vector<uint32_t> qst(5ull * nq), hq(3ull * nq);
+            HIP_CHECK(hipMemcpyAsync(f.data(), ix->fin.p, nq, hipMemcpyDeviceToHost, g->stream));
+            HIP_CHECK(hipMemcpyAsync(qst.data(), ix->qstats.p, 20ull * nq, hipMemcpyDeviceToHost, g->stream));
+            HIP_CHECK(hipMemcpyAsync(hq.data(), ix->qs.p, 4ull * nq, hipMemcpyDeviceToHost, g->stream));
+            HIP_CHECK(hipMemcpyAsync(hq.data() + nq, ix->qt.p, 4ull * nq, hipMemcpyDeviceToHost, g->stream));
+            HIP_CHECK(hipMemcpyAsync(hq.data() + 2ull * nq, ix->qrow.p, 4ull * nq, hipMemcpyDeviceToHost,
+                                     g->stream));
+            HIP_CHECK(hipStreamSynchronize(g->stream));
+            std::vector<uint32_t> idx, sub(0);
+            for (uint32_t i = 0; i < nq; ++i)
+                if (f[i] == 2u) idx.push_back(i);
+            const uint32_t m = (uint32_t)idx.size();
+            if (!m) break;
+            sub.resize(3ull * m);
+            for (uint32_t j = 0; j < m; ++j) {
+                const uint32_t i = idx[j];  // target-sorted order is kept
+                sub[j] = hq[i];
+                sub[m + j] = hq[nq + i];
+                sub[2ull * m + j] = hq[2ull * nq + i];
+                for (int k = 0; k < 5; ++k) h[k] -= qst[5ull * i + k];
+            }
+            reruns += m;
+            DevBuf<uint32_t> d_idx, d_q, d_hops, d_st;
+            DevBuf<uint64_t> d_cost;
+            DevBuf<uint8_t> d_fin;
+            DevBuf<unsigned long long> d_agg;
+            d_idx.upload(idx.data(), m, g->stream);
+            d_q.upload(sub.data(), 3ull * m, g->stream);
+            d_hops.alloc(m);
+            d_st.alloc(5ull * m);
+            d_cost.alloc(m);
+            d_fin.alloc(m);
+            d_agg.alloc(8);
+            HIP_CHECK(hipMemsetAsync(d_agg.p, 0, 8 * sizeof(unsigned long long), g->stream));
+            const size_t per2 = search_ws_bytes_per_slot(cap, tables);
+            size_t free_b = 0, total_b = 0;
+            HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            const size_t per_block = 256ull * per2;
+            CPD_REQUIRE((free_b + ix->sws.n) / 2 >= per_block, CPD_E_OOM,
+                        "search workspace of 256 lanes x capacity " + std::to_string(cap) +
+                            " does not fit in HBM");
+            const size_t fit2 =
+                std::max<size_t>(1, (size_t)(wfrac * (double)(free_b + ix->sws.n)) / per_block);
+            const uint32_t slots2 = (uint32_t)std::min<size_t>(search_slots(m), fit2 * 256u);
+            ix->sws.alloc((size_t)slots2 * per2);
+            HIP_CHECK(hipEventRecord(a, g->stream));
+            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad,
+                              tables ? ix->hrow.p : nullptr, ix->crow.p, ix->lrow.p, n, d_q.p,
+                              d_q.p + m, d_q.p + 2ull * m, m, o.hscale, o.fscale, o.k_moves,
+                              o.itrs, o.time_ns, o.virtual_tick_ns, ix->sws.p, cap, slots2,
+                              d_cost.p, d_hops.p, d_fin.p, d_st.p, d_agg.p, g->stream);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipEventRecord(b, g->stream));
+            launch_scatter_u64(d_cost.p, d_idx.p, m, ix->cost.p, g->stream);
+            launch_scatter_u32(d_hops.p, d_idx.p, m, 1u, ix->hops.p, g->stream);
+            launch_scatter_u8(d_fin.p, d_idx.p, m, ix->fin.p, g->stream);
+            launch_scatter_u32(d_st.p, d_idx.p, m, 5u, ix->qstats.p, g->stream);
+            unsigned long long h2[8];
+            HIP_CHECK(hipMemcpyAsync(h2, d_agg.p, sizeof h2, hipMemcpyDeviceToHost, g->stream));
+            HIP_CHECK(hipStreamSynchronize(g->stream));
+            float ms2 = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms2, a, b));
+            ms += ms2;
+            for (int k = 0; k < 7; ++k) h[k] += h2[k];
+            h[7] = h2[7];
+        }
         g->ev_pool.push_back(a);
         g->ev_pool.push_back(b);
         if (g->timing) {
@@ -2490,6 +2571,7 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             st->lanes = slots;
             st->tables_ms = tables_ms;
             st->tables = tables ? CPD_SEARCH_TABLES : CPD_SEARCH_WALKS;
+            st->reruns = reruns;
         }
     });
 }

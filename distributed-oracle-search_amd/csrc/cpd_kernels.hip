@@ -2743,7 +2743,7 @@ __global__ __launch_bounds__(256) void cpd_search(
                 const bool found = L.ub != kInf64 && !L.overflow;
                 cost_out[L.q] = found ? L.ub : 0ull;
                 plen_out[L.q] = found ? L.best_len : 0u;
-                fin_out[L.q] = (uint8_t)found;
+                fin_out[L.q] = found ? 1u : L.overflow ? 2u : 0u;
                 uint32_t* st = qstats + 5ull * L.q;
                 st[0] = L.expanded;
                 st[1] = L.inserted;

@@ -320,7 +320,12 @@ int main(int argc, char** argv) {
         bool debug = json_field(conf, "debug") == "true";
         // cpd-search knobs (process_query.py:149-160): hscale, fscale, time
         // (ns; args.get_time_ns may send a float), itrs
-        cpd_search_opts so{1.0, 0.0, k_moves, -1, 0, 0, 0, CPD_SEARCH_AUTO, 0.0};  // wall-clock time limit
+        // wall-clock time limit; a search that outgrows the default workspace
+        // reruns with up to every column of the graph, so none stops on it
+        uint32_t cap_all = 64;
+        while (cap_all < g.n && cap_all < (1u << 24)) cap_all <<= 1;
+        cpd_search_opts so{1.0, 0.0, k_moves, -1, 0, 0, 0, CPD_SEARCH_AUTO, 0.0,
+                           std::max<uint32_t>(cap_all, 32768u)};
         if (!json_field(conf, "hscale").empty()) so.hscale = std::atof(json_field(conf, "hscale").c_str());
         if (!json_field(conf, "fscale").empty()) so.fscale = std::atof(json_field(conf, "fscale").c_str());
         if (!json_field(conf, "itrs").empty()) so.itrs = std::atoll(json_field(conf, "itrs").c_str());
@@ -372,7 +377,7 @@ int main(int argc, char** argv) {
                 if (std::FILE* f = std::fopen(res.c_str(), "w")) {
                     for (size_t i = 0; i < q.size(); ++i)
                         std::fprintf(f, "%u %u %llu %u %u\n", s[i], t[i], (unsigned long long)cost[i],
-                                     hops[i], fin[i]);
+                                     hops[i], fin[i] == 1 ? 1u : 0u);
                     std::fclose(f);
                 }
             }

@@ -388,7 +388,8 @@ void cpd_index_free(cpd_index* ix);
  * in each search's workspace, so an index of any size can be searched.  The
  * results and counters are the same either way.  A search's workspace holds
  * `capacity` columns (searched ones; with walks also the walked ones; 68 /
- * 116 B each): one that needs more stops unfinished and is counted in
+ * 116 B each): one that needs more (after capacity_max's reruns) stops
+ * unfinished, with finished = 2 in cpd_query_fetch, and is counted in
  * `overflow`.  The time limit is wall clock (as fifo_auto runs it);
  * virtual_tick_ns > 0 replaces it by a deterministic clock that advances
  * virtual_tick_ns per expansion and per edge touched (the oracle's
@@ -407,6 +408,11 @@ typedef struct cpd_search_opts {
     int32_t  tables;       /* CPD_SEARCH_AUTO / _TABLES / _WALKS             */
     double   workspace_frac; /* share of the free HBM the lanes' workspaces may
                                 take (0 = 0.25); more lanes search at once   */
+    uint32_t capacity_max; /* 0: none; else searches that overflow `capacity`
+                              run again, alone, at 4x the capacity (fewer
+                              lanes) up to capacity_max: many lanes for the
+                              common short searches, the big workspace only
+                              for the long ones                             */
 } cpd_search_opts;
 
 typedef struct cpd_search_stats {
@@ -415,6 +421,7 @@ typedef struct cpd_search_stats {
     uint64_t lanes;        /* concurrent searches (workspace slots)         */
     double   tables_ms;    /* device time spent (re)building the tables     */
     int32_t  tables;       /* the form used: CPD_SEARCH_TABLES or _WALKS    */
+    uint64_t reruns;       /* searches run again at a larger capacity       */
 } cpd_search_stats;
 
 int  cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st);

@@ -110,7 +110,8 @@ def test_search_overflow_is_counted_tables(env):
     assert small.sum() > 100
     np.testing.assert_array_equal(cost[small], rc[small])
     np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small])
-    assert not fin[rs[:, 1] > cap].any()
+    assert (fin[rs[:, 1] > cap] == 2).all()  # stopped on the workspace, not unfinished
+    assert int((fin == 2).sum()) == st["overflow"]
 
 
 def test_search_overflow_is_counted_walks(env):
@@ -129,7 +130,31 @@ def test_search_overflow_is_counted_walks(env):
     assert small.sum() > 100
     np.testing.assert_array_equal(cost[small], rc[small])
     np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small, :5])
-    assert not fin[rs[:, 5] > cap].any()
+    assert (fin[rs[:, 5] > cap] == 2).all()
+    assert int((fin == 2).sum()) == st["overflow"]
+
+
+@pytest.mark.parametrize("form", ["tables", "walks"])
+def test_search_capacity_escalation(env, form):
+    """Searches that overflow a small workspace rerun at 4x capacity until
+    none does: every result and counter (and the sums) the oracle's."""
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    rc, rp, rf, rs = _oracle(env, wc)
+    _, _, fin1, _, st1 = ix.search(s, t, capacity=64, tables=form)
+    assert st1["overflow"] > 0 and st1["reruns"] == 0
+    cost, plen, fin, cnt, st = ix.search(s, t, capacity=64, capacity_max=4096, tables=form)
+    assert st["overflow"] == 0 and st["reruns"] >= st1["overflow"]
+    np.testing.assert_array_equal(cost, rc)
+    np.testing.assert_array_equal(plen, rp)
+    np.testing.assert_array_equal(fin, rf)
+    np.testing.assert_array_equal(cnt.astype(np.uint64), rs)
+    assert st["expanded"] == int(rs[:, 0].sum()) and st["inserted"] == int(rs[:, 1].sum())
+    assert st["finished"] == int(rf.sum()) and st["plen"] == int(rp[rf == 1].sum())
+    # a capacity_max that still leaves some overflowing: those report 2
+    _, _, fin3, _, st3 = ix.search(s, t, capacity=64, capacity_max=256, tables=form)
+    assert int((fin3 == 2).sum()) == st3["overflow"] <= st1["overflow"]
 
 
 @pytest.mark.parametrize("form", ["tables", "walks"])
