@@ -13,7 +13,7 @@
 //                 [--threads T]        host threads for the hierarchy build (--ch-host)
 //                 [--ch-host]          contract the hierarchy on host threads, not the GPU
 //                 [--plan P | --no-plan-cache]
-//                 [--write-threads T]  host threads copying + writing rows (8)
+//                 [--write-threads T]  host threads copying + writing rows (16)
 //                 [--no-pipeline]      build, then export, then write, per group
 //                 [--plan-only]        build / load the cached plan and exit
 //                 [--targets-from S]   only rows of targets of scenario S (q s t)
@@ -611,7 +611,7 @@ int main(int argc, char** argv) {
                 runs_done += tot;
             }
         } else {
-            Pipeline pl(dg, B, (int)a.num("write-threads", 8), discard, moves);
+            Pipeline pl(dg, B, (int)a.num("write-threads", 16), discard, moves);
             std::vector<uint32_t> targets;
             std::vector<CpdBucket> heads(owned.size());
             std::vector<uint64_t> first(owned.size() + 1, 0);
