@@ -230,6 +230,44 @@ class Comm:
         return t.tolist()
 
 
+class FileComm:
+    """Barrier / reductions through small files in a directory the node's
+    ranks share — for --full-build-only, whose ranks then load neither torch
+    nor HIP: on one shared GPU the workers' make_cpd_auto processes (and the
+    launcher) are then the only processes holding the card."""
+
+    def __init__(self, world, rank, local, path, timeout=1800.0):
+        self.world, self.rank, self.local, self.device = world, rank, local, None
+        self.path, self.timeout, self.gen = path, timeout, 0
+        os.makedirs(path, exist_ok=True)
+
+    def _exchange(self, vals):
+        self.gen += 1
+        mine = os.path.join(self.path, f"g{self.gen}.r{self.rank}")
+        with open(mine + ".tmp", "w") as f:
+            json.dump(vals, f)
+        os.rename(mine + ".tmp", mine + ".json")
+        names = [os.path.join(self.path, f"g{self.gen}.r{r}.json") for r in range(self.world)]
+        deadline = time.time() + self.timeout
+        while not all(os.path.exists(n) for n in names):
+            if time.time() > deadline:
+                raise RuntimeError(f"FileComm: ranks missing at step {self.gen} in {self.path}")
+            time.sleep(0.05)
+        out = []
+        for n in names:
+            with open(n) as f:
+                out.append(json.load(f))
+        return out
+
+    def barrier(self):
+        self._exchange(None)
+
+    def reduce(self, vals, op):
+        allv = self._exchange(list(vals))
+        fn = {"SUM": sum, "MAX": max, "MIN": min}[op]
+        return [fn(v[i] for v in allv) for i in range(len(vals))]
+
+
 def shard_targets(nodenum, world, method, key, rank):
     """The rank's targets: distribution_controller partition, worker = rank."""
     sys.path.insert(0, PKG)
@@ -700,28 +738,27 @@ def glob_xy(args):
 def full_build_only(args, world, rank, local):
     """The end-to-end worker leg alone (--full-build-only): rank r runs
     make_cpd_auto for worker r, rank 0 writes its files and serves them, the
-    ranks' figures are gathered over gloo — no GPU context in these
-    processes, so an 8-rank rehearsal on one GPU (CPD_BENCH_SHARE_GPU=1)
-    holds 8 GPU processes, not 16.  One JSON line on rank 0."""
-    import numpy as np  # noqa: F401
-    import torch.distributed as dist
-    sys.path.insert(0, PKG)
-    import cpd
+    ranks' figures are gathered through files (FileComm) — these processes
+    load neither torch nor HIP until every worker is done, so an 8-rank
+    rehearsal on one GPU (CPD_BENCH_SHARE_GPU=1) holds the 8 workers and the
+    launcher, within the box's 16 GPU processes.  One JSON line on rank 0."""
     share = os.environ.get("CPD_BENCH_SHARE_GPU") == "1"
     gpu = 0 if share else local
     if share and args.batch == 0:  # eight workers' batch buffers on one card
         args.batch = 1024
     os.makedirs(args.cache, exist_ok=True)
-    if world > 1:
-        dist.init_process_group("gloo")
-    comm = Comm(world, rank, local, device=None)
+    # a directory per launch (the launcher's run id and port) for FileComm
+    run_id = f"{os.environ.get('TORCHELASTIC_RUN_ID', 'solo')}-{os.environ.get('MASTER_PORT', '0')}"
+    comm = FileComm(world, rank, local, os.path.join(args.cache, f"fb-comm-{world}-{run_id}"))
     xy = full_build_xy(args) if local == 0 else None
     comm.barrier()
     xy = xy or glob_xy(args)
     t0 = time.time()
     fb, rec = full_build_leg(args, xy, world, rank, gpu, comm)
     W = full_build_workers(args, world)
-    if rank == 0 and "files_bytes" in rec:
+    if rank == 0 and "files_bytes" in rec:  # every worker is done: rank 0 alone on the GPU
+        sys.path.insert(0, PKG)
+        import cpd
         g = cpd.synth_road_graph(args.width, args.width, seed=args.seed, style=args.style)
         try:
             fb["serve"] = serve_probe(args, xy, full_build_dir(args, world), W, gpu, g,
@@ -735,8 +772,6 @@ def full_build_only(args, world, rank, local):
         print(json.dumps({"what": "full-build leg only", "n_gpus": world,
                           "shared_gpu_rehearsal": share, "batch": args.batch or "auto",
                           "wall_s": round(time.time() - t0, 3), "full_build": fb}), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def main():

@@ -72,14 +72,18 @@ def test_two_rank_gloo_aggregation(tmp_path):
 FB_WORKER = r'''
 import json, os, sys, time, types
 sys.path.insert(0, os.environ["ROOT"])
-import torch.distributed as dist
 import bench
 
-dist.init_process_group("gloo")
-rank, world = dist.get_rank(), dist.get_world_size()
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 cache = os.environ["CACHE"]
 args = bench.parse(["--width", "40", "--cache", cache])
-comm = bench.Comm(world, rank, rank, device=None)
+filecomm = os.environ.get("FILECOMM") == "1"
+if filecomm:  # what --full-build-only runs: no torch in the ranks
+    comm = bench.FileComm(world, rank, rank, os.path.join(cache, "comm"))
+else:
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    comm = bench.Comm(world, rank, rank, device=None)
 if rank == 0:  # a stale directory from an earlier run, with a stale plan cache
     stale = bench.full_build_dir(args, world)
     os.makedirs(stale, exist_ok=True)
@@ -101,15 +105,22 @@ def fake_make_cpd_auto(cmd, **kw):
 
 fb, rec = bench.full_build_leg(args, "/nonexistent.xy", world, rank, 0, comm,
                                runner=fake_make_cpd_auto)
-allseen = [None] * world
-dist.all_gather_object(allseen, {"cmd": seen["cmd"], "entries": seen["dir_entries"]})
+mine = {"cmd": seen["cmd"], "entries": seen["dir_entries"]}
+if filecomm:
+    allseen = comm._exchange(mine)
+    assert "torch" not in sys.modules  # the ranks never load torch (nor HIP)
+else:
+    allseen = [None] * world
+    dist.all_gather_object(allseen, mine)
 if rank == 0:
     print("RESULT " + json.dumps({"fb": fb, "seen": allseen}), flush=True)
-dist.destroy_process_group()
+if not filecomm:
+    dist.destroy_process_group()
 '''
 
 
-def test_eight_rank_full_build_plumbing(tmp_path):
+@pytest.mark.parametrize("filecomm", [False, True], ids=["gloo", "filecomm"])
+def test_eight_rank_full_build_plumbing(tmp_path, filecomm):
     """The end-to-end worker leg at 8 ranks on gloo (the driver's N = 8
     scaling run, rehearsed on CPU): every rank runs worker r of the div-8
     partition only after rank 0 has replaced the stale output directory
@@ -118,10 +129,11 @@ def test_eight_rank_full_build_plumbing(tmp_path):
     script = tmp_path / "fb.py"
     script.write_text(FB_WORKER)
     env = dict(os.environ, ROOT=ROOT, CACHE=str(tmp_path / "cache"), MASTER_ADDR="127.0.0.1",
-               OMP_NUM_THREADS="1")
+               OMP_NUM_THREADS="1", FILECOMM="1" if filecomm else "0")
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node=8", "--master-addr", "127.0.0.1", "--master-port",
-                        "29633", str(script)], capture_output=True, text=True, env=env,
+                        "29634" if filecomm else "29633", str(script)], capture_output=True,
+                       text=True, env=env,
                        timeout=400)
     assert p.returncode == 0, p.stderr[-3000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")][0]
