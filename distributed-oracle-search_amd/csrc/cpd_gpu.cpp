@@ -206,6 +206,10 @@ struct cpd_graph {
     // bits per move in the packed compact form: every move indexes its
     // column's out-list (wildcard runs take bit 0), so out-degrees <= 2^bits
     uint32_t move_bits = 4;
+    // the move tables in HBM (built rows, dense indexes) at the same width:
+    // 2^tlb bits per column (CPD_TABLE_BITS=4: nibble tables whatever the
+    // degree, the round-4 layout, for A/B)
+    uint32_t tlb = 2;
     DevBuf<uint32_t> dist, counts;
     // Emit overlap (CPD_ASYNC, default on): a batch's move-table emit
     // (rle_moves) runs on `estream` while the next batch's sweeps start on
@@ -428,7 +432,7 @@ struct cpd_graph {
         pending.swap(keep);
     }
     void select() const { HIP_CHECK(hipSetDevice(device)); }
-    uint32_t wpr() const { return npad / 8u; }  // words per move-table row
+    uint32_t wpr() const { return npad >> (5u - tlb); }  // words per move-table row
 
     uint64_t hbm_reserve = 0;  // cpd_graph_set_hbm_reserve
     void reserve_batch(uint32_t want) {
@@ -562,11 +566,11 @@ struct cpd_rows {
     std::vector<uint32_t> targets;   // node ids, row order
     std::vector<uint32_t> lanes;     // batch lane of each row
     mutable std::vector<uint64_t> offsets;  // run offsets (host), nrows+1 (after settle())
-    // The rows in their compact form: 4-bit move tables, wpr = npad / 8 words
-    // per row (rle_moves) — the RLE row expanded, 5x smaller than its runs on
-    // the bench graphs.  Run words are decoded from them on demand
-    // (moves_runs, at `off`).
-    uint32_t n = 0, wpr = 0, bits = 4;  // bits: per move in the packed compact form
+    // The rows in their compact form: move tables at 2^tlb bits per column,
+    // wpr = npad * 2^tlb / 32 words per row (rle_moves) — the RLE row
+    // expanded, 10x smaller than its runs on the bench graph (2 bits).  Run
+    // words are decoded from them on demand (moves_runs, at `off`).
+    uint32_t n = 0, wpr = 0, bits = 4, tlb = 2;  // bits: per move in the exported form
     DevBuf<uint32_t> moves;
     mutable DevBuf<uint64_t> off;
     uint32_t packed_words() const { return (uint32_t)(((uint64_t)n * bits + 31u) / 32u); }
@@ -618,6 +622,7 @@ struct cpd_index {
     bool dense_ready = false;
     // staging of host-appended chunks (stream_dense), format flag
     DevBuf<uint32_t> stage, pstage;  // pstage: packed compact rows before unpacking
+    DevBuf<uint32_t> xstage, lost;   // nibble rows before narrowing; repack's flag
     DevBuf<uint64_t> stage_off;
     DevBuf<uint32_t> flag;
     // expand_rows work split: first run-chunk of each row being expanded
@@ -628,8 +633,9 @@ struct cpd_index {
         if (stream_dense) return true;
         if (mode == CPD_INDEX_DENSE) return true;
         if (mode == CPD_INDEX_RLE) return false;
-        // auto: the table whose bytes are fewer (4 B per run vs n/2 B per row)
-        return nrows > 0 && 4.0 * (double)declared > (double)g->npad / 2.0 * nrows;
+        // auto: the table whose bytes are fewer (4 B per run vs npad * bits / 8
+        // B per row)
+        return nrows > 0 && 4.0 * (double)declared > 4.0 * (double)g->wpr() * nrows;
     }
     // CPD-search: per-row tables when they fit (hrow free-flow heuristic,
     // crow / lrow incumbent cost and moves under the current weights; rebuilt
@@ -928,6 +934,11 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         while ((1u << g->adj_shift) < maxdeg) ++g->adj_shift;
         g->fmb = fm_bits(g->adj_shift);
         g->move_bits = maxdeg <= 2 ? 1u : maxdeg <= 4 ? 2u : 4u;
+        {
+            const char* tb = std::getenv("CPD_TABLE_BITS");  // 4: nibble tables (A/B)
+            const bool nib = tb && std::strcmp(tb, "4") == 0;
+            g->tlb = nib ? 2u : g->move_bits == 1u ? 0u : g->move_bits == 2u ? 1u : 2u;
+        }
         hipStream_t s = g->stream;
         g->order_d.upload(g->order.data(), n, s);
         g->row_ptr.upload(g->rowc_host.data(), n + 1, s);
@@ -1512,10 +1523,10 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     HIP_CHECK(hipEventRecord(rb->ev, es));
     // per row: the sets (fm_row), the segment states (4 B per 32 columns;
     // the run counts are read only where the look-ahead needs them), the
-    // table (npad / 2)
-    const double ebytes = (fm_row + 4.0 * npad / 32.0 + 0.5 * npad) * k + 4.0 * k;
+    // table (npad * bits / 8)
+    const double ebytes = (fm_row + 4.0 * npad / 32.0 + 4.0 * g->wpr()) * k + 4.0 * k;
     g->timed("rle_moves", ebytes, [&] {
-        launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, r->moves.p, es);
+        launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, g->tlb, r->moves.p, es);
     });
     if (!r->done) HIP_CHECK(hipEventCreateWithFlags(&r->done, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(r->done, es));
@@ -1559,6 +1570,7 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         r->n = g->n;
         r->wpr = g->wpr();
         r->bits = g->move_bits;
+        r->tlb = g->tlb;
         if (r->moves.n < (size_t)ntargets * r->wpr) {
             r->wait();  // an earlier build's emit may still write the old table
             r->moves.alloc((size_t)ntargets * r->wpr);
@@ -1632,7 +1644,7 @@ int cpd_rows_export_range(const cpd_rows* r, uint32_t first, uint32_t count, uin
             while (p1 < first + count && r->offsets[p1 + 1] - r->offsets[p0] <= kDecodeRuns) ++p1;
             const uint64_t nr = r->offsets[p1] - r->offsets[p0];
             stage->alloc(std::max<uint64_t>(nr, std::min<uint64_t>(end - base, kDecodeRuns)));
-            launch_moves_runs(r->moves.p + (size_t)p0 * r->wpr, r->wpr, r->n, p1 - p0,
+            launch_moves_runs(r->moves.p + (size_t)p0 * r->wpr, r->wpr, r->tlb, r->n, p1 - p0,
                               r->off.p + p0, r->offsets[p0], stage->p, st);
             HIP_CHECK(hipGetLastError());
             HIP_CHECK(hipMemcpyAsync(runs + (r->offsets[p0] - base), stage->p, nr * sizeof(uint32_t),
@@ -1668,24 +1680,29 @@ int cpd_rows_export_moves(const cpd_rows* r, uint32_t first, uint32_t count, uin
         r->wait();
         hipStream_t st = thread_stream(r->device);
         const size_t w = r->packed_words();
-        if (r->bits == 4) {  // the nibble tables as they are, at the packed row width
-            HIP_CHECK(hipMemcpy2DAsync(moves, w * sizeof(uint32_t),
-                                       r->moves.p + (size_t)first * r->wpr,
-                                       (size_t)r->wpr * sizeof(uint32_t), w * sizeof(uint32_t),
-                                       count, hipMemcpyDeviceToHost, st));
-        } else {  // packed on the GPU, then one contiguous copy
-            auto stage = r->acquire_stage();
-            stage->alloc((size_t)count * w);
-            launch_pack_moves(r->moves.p + (size_t)first * r->wpr, r->wpr, count, r->bits,
-                              (uint32_t)w, stage->p, st);
-            HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipMemcpyAsync(moves, stage->p, (size_t)count * w * sizeof(uint32_t),
+        const uint32_t* src = r->moves.p + (size_t)first * r->wpr;
+        if (w == r->wpr && r->bits == (1u << r->tlb)) {  // the tables as they are
+            HIP_CHECK(hipMemcpyAsync(moves, src, (size_t)count * w * sizeof(uint32_t),
                                      hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
-            r->release_stage(std::move(stage));
             return;
         }
+        // rows made contiguous at the exported width on the GPU (a pitched
+        // device copy when the widths agree, else repacked), then one copy out
+        auto stage = r->acquire_stage();
+        stage->alloc((size_t)count * w);
+        if (r->bits == (1u << r->tlb))
+            HIP_CHECK(hipMemcpy2DAsync(stage->p, w * sizeof(uint32_t), src,
+                                       (size_t)r->wpr * sizeof(uint32_t), w * sizeof(uint32_t),
+                                       count, hipMemcpyDeviceToDevice, st));
+        else
+            launch_repack_moves(src, r->wpr, r->wpr, 1u << r->tlb, count, stage->p, (uint32_t)w,
+                                (uint32_t)w, r->bits, st);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(moves, stage->p, (size_t)count * w * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, st));
         HIP_CHECK(hipStreamSynchronize(st));
+        r->release_stage(std::move(stage));
     });
 }
 
@@ -1834,9 +1851,12 @@ void index_stream_dense(cpd_index* ix) {
     ix->keep_rle = false;
     ix->stream_dense = true;
     ix->mode = CPD_INDEX_DENSE;
-    ix->dense.alloc((size_t)ix->nrows * (g->npad / 8u));
+    ix->dense.alloc((size_t)ix->nrows * g->wpr());
     ix->dense_ready = true;
 }
+
+// Moves an index's tables can hold: 16 (any 4-bit word) or 2^bits.
+uint32_t table_move_limit(const cpd_graph* g) { return g->tlb == 2u ? 16u : 1u << (1u << g->tlb); }
 
 // Host-side checks of a chunk's offsets (relative, offsets[0] == 0).
 void check_chunk_offsets(const uint64_t* offsets, uint32_t count) {
@@ -1868,20 +1888,21 @@ uint32_t prepare_chunks(cpd_index* ix, const uint64_t* h_off, uint32_t count) {
 // Leaves the rows' chunk table in ix->chunk_first and returns its size, for
 // expand_into.
 uint32_t validate_device_rows(cpd_index* ix, const uint64_t* d_off, const uint32_t* d_runs,
-                              const uint64_t* h_off, uint32_t count) {
+                              const uint64_t* h_off, uint32_t count, uint32_t mlimit = 16u) {
     cpd_graph* g = ix->g;
     const uint32_t chunks = prepare_chunks(ix, h_off, count);
     HIP_CHECK(hipMemsetAsync(ix->flag.p, 0, sizeof(uint32_t), g->stream));
     g->timed("validate_rows", 4.0 * (double)(h_off[count] - h_off[0]), [&] {
-        launch_validate_rows(d_off, d_runs, ix->chunk_first.p, count, chunks, g->n, ix->flag.p,
-                             g->stream);
+        launch_validate_rows(d_off, d_runs, ix->chunk_first.p, count, chunks, g->n, mlimit,
+                             ix->flag.p, g->stream);
     });
     uint32_t bad = 0;
     HIP_CHECK(hipMemcpyAsync(&bad, ix->flag.p, sizeof bad, hipMemcpyDeviceToHost, g->stream));
     g->sync();
     CPD_REQUIRE(!bad, CPD_E_ARG,
                 "index: malformed row (must start at column 0, run columns strictly increasing "
-                "and < n)");
+                "and < n" + std::string(mlimit < 16u ? ", moves < " + std::to_string(mlimit) +
+                                                           " for this graph's move tables" : "") + ")");
     return chunks;
 }
 
@@ -1893,6 +1914,28 @@ void expand_into(cpd_index* ix, const uint64_t* d_off, const uint32_t* d_runs,
                  const uint64_t* h_off, uint32_t count, uint64_t runs_in_chunk, uint32_t first,
                  uint32_t chunks = 0) {
     cpd_graph* g = ix->g;
+    if (g->tlb != 2u) {
+        // narrower tables: nibble rows into a stage (<= 256 MiB), then
+        // narrowed into the index — rows checked to fit (validate_rows)
+        const size_t w4 = g->npad / 8u, wpr = g->wpr();
+        const uint32_t piece = (uint32_t)std::max<size_t>(1, ((size_t)1 << 26) / w4);
+        ix->xstage.alloc((size_t)std::min(piece, count) * w4);
+        for (uint32_t p0 = 0; p0 < count; p0 += piece) {
+            const uint32_t p1 = std::min(count, p0 + piece);
+            const uint32_t ch = prepare_chunks(ix, h_off + p0, p1 - p0);
+            g->timed("expand_rows", 4.0 * (double)(h_off[p1] - h_off[p0]) + 4.0 * (double)w4 * (p1 - p0),
+                     [&] {
+                         launch_expand_rows(d_off + p0, d_runs, ix->chunk_first.p, p1 - p0, ch,
+                                            g->npad, ix->xstage.p, g->stream);
+                     });
+            launch_repack_moves(ix->xstage.p, (uint32_t)w4, (uint32_t)w4, 4u, p1 - p0,
+                                ix->dense.p + (size_t)(first + p0) * wpr, (uint32_t)wpr,
+                                (uint32_t)wpr, 1u << g->tlb, g->stream);
+            HIP_CHECK(hipGetLastError());
+            g->sync();  // the chunk table and the stage are reused by the next piece
+        }
+        return;
+    }
     const size_t wpr = g->npad / 8u;
     if (!chunks) chunks = prepare_chunks(ix, h_off, count);
     g->timed("expand_rows", 4.0 * (double)runs_in_chunk + 4.0 * (double)wpr * count + 16.0 * count,
@@ -1941,7 +1984,8 @@ void append_host(cpd_index* ix, uint32_t count, const uint64_t* offsets, const u
                                  hipMemcpyHostToDevice, s));
         HIP_CHECK(hipMemcpyAsync(ix->stage_off.p, o.data(), o.size() * sizeof(uint64_t),
                                  hipMemcpyHostToDevice, s));
-        const uint32_t ch = validate_device_rows(ix, ix->stage_off.p, ix->stage.p, o.data(), r1 - r0);
+        const uint32_t ch = validate_device_rows(ix, ix->stage_off.p, ix->stage.p, o.data(), r1 - r0,
+                                                 table_move_limit(g));
         expand_into(ix, ix->stage_off.p, ix->stage.p, o.data(), r1 - r0, pr, ix->added, ch);
         g->sync();  // the stage is reused by the next piece
         ix->added += r1 - r0;
@@ -1979,8 +2023,8 @@ void append_built(cpd_index* ix, const cpd_rows* r) {
                     "index: more runs than the index was created for");
         std::vector<uint64_t> o(r->nrows + 1);
         for (uint32_t i = 0; i <= r->nrows; ++i) o[i] = ix->total + r->offsets[i];
-        g->timed("moves_runs", 0.5 * (double)g->npad * r->nrows + 4.0 * (double)r->total, [&] {
-            launch_moves_runs(r->moves.p, r->wpr, r->n, r->nrows, r->off.p, 0,
+        g->timed("moves_runs", 4.0 * (double)g->wpr() * r->nrows + 4.0 * (double)r->total, [&] {
+            launch_moves_runs(r->moves.p, r->wpr, r->tlb, r->n, r->nrows, r->off.p, 0,
                               ix->runs.p + ix->total, g->stream);
         });
         HIP_CHECK(hipMemcpyAsync(ix->off.p + ix->added, o.data(), o.size() * sizeof(uint64_t),
@@ -1993,11 +2037,13 @@ void append_built(cpd_index* ix, const cpd_rows* r) {
     ix->added += r->nrows;
 }
 
-// Append `count` host rows in the compact form (ceil(n / 8) words each).  A
-// dense index takes them as they are (one 2-D copy to the table stride); an
-// RLE index decodes them on the GPU, counting first.  No format check is
-// needed: every nibble is some move, and a move naming no out-edge of its
-// column stops the walk (unfinished) like the oracle's.
+// Append `count` host rows in the compact form (ceil(n * bits / 32) words
+// each).  They are staged and, at the tables' width, copied into a dense
+// index as they are (a pitched device copy to the table stride), else
+// repacked — narrowing checks every move fits; an RLE index decodes them on
+// the GPU, counting first.  No other format check is needed: every field is
+// some move, and a move naming no out-edge of its column stops the walk
+// (unfinished) like the oracle's.
 void append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* moves) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(count <= ix->nrows - ix->added, CPD_E_ARG, "index: more rows than declared");
@@ -2005,11 +2051,11 @@ void append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* 
     CPD_REQUIRE(moves, CPD_E_ARG, "index: null move rows");
     CPD_REQUIRE(bits == 1 || bits == 2 || bits == 4, CPD_E_ARG, "index: bits per move must be 1, 2 or 4");
     const size_t w = ((uint64_t)g->n * bits + 31u) / 32u, wpr = g->wpr();
+    const uint32_t tb = 1u << g->tlb;
     hipStream_t s = g->stream;
-    // pieces of <= 1 GiB of nibble tables: the packed rows are staged and
-    // unpacked into the dense index (or, for an RLE index, into a stage the
-    // runs are decoded from)
-    const uint32_t piece = (uint32_t)std::max<size_t>(1, ((size_t)1 << 28) / wpr);
+    // pieces of <= 1 GiB of tables or packed rows
+    const uint32_t piece = (uint32_t)std::max<size_t>(1, ((size_t)1 << 28) / std::max(w, wpr));
+    ix->lost.alloc(1);
     for (uint32_t r0 = 0; r0 < count; r0 += piece) {
         const uint32_t nr = std::min(piece, count - r0);
         uint32_t* tables = nullptr;
@@ -2019,16 +2065,27 @@ void append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* 
             ix->stage.alloc((size_t)std::min(piece, count) * wpr);
             tables = ix->stage.p;
         }
-        if (bits == 4) {
-            HIP_CHECK(hipMemcpy2DAsync(tables, wpr * sizeof(uint32_t), moves + (size_t)r0 * w,
+        ix->pstage.alloc((size_t)std::min(piece, count) * w);
+        HIP_CHECK(hipMemcpyAsync(ix->pstage.p, moves + (size_t)r0 * w, (size_t)nr * w * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, s));
+        const bool narrowing = bits > tb;
+        if (bits == tb) {
+            HIP_CHECK(hipMemcpy2DAsync(tables, wpr * sizeof(uint32_t), ix->pstage.p,
                                        w * sizeof(uint32_t), w * sizeof(uint32_t), nr,
-                                       hipMemcpyHostToDevice, s));
+                                       hipMemcpyDeviceToDevice, s));
         } else {
-            ix->pstage.alloc((size_t)std::min(piece, count) * w);
-            HIP_CHECK(hipMemcpyAsync(ix->pstage.p, moves + (size_t)r0 * w, (size_t)nr * w * sizeof(uint32_t),
-                                     hipMemcpyHostToDevice, s));
-            launch_unpack_moves(ix->pstage.p, (uint32_t)w, nr, bits, (uint32_t)wpr, tables, s);
+            if (narrowing) HIP_CHECK(hipMemsetAsync(ix->lost.p, 0, sizeof(uint32_t), s));
+            launch_repack_moves(ix->pstage.p, (uint32_t)w, (uint32_t)w, bits, nr, tables,
+                                (uint32_t)wpr, (uint32_t)wpr, tb, s, narrowing ? ix->lost.p : nullptr);
             HIP_CHECK(hipGetLastError());
+        }
+        if (narrowing) {
+            uint32_t lost = 0;
+            HIP_CHECK(hipMemcpyAsync(&lost, ix->lost.p, sizeof lost, hipMemcpyDeviceToHost, s));
+            HIP_CHECK(hipStreamSynchronize(s));
+            CPD_REQUIRE(!lost, CPD_E_ARG,
+                        "index: a move does not fit this graph's " + std::to_string(tb) +
+                            "-bit move tables (malformed rows)");
         }
         if (!ix->keep_rle) {
             HIP_CHECK(hipStreamSynchronize(s));
@@ -2036,7 +2093,7 @@ void append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* 
             continue;
         }
         ix->flag.alloc(std::max<size_t>(ix->flag.n, (size_t)std::min(piece, count)));
-        launch_moves_count(tables, (uint32_t)wpr, g->n, nr, ix->flag.p, s);
+        launch_moves_count(tables, (uint32_t)wpr, g->tlb, g->n, nr, ix->flag.p, s);
         HIP_CHECK(hipGetLastError());
         std::vector<uint32_t> cnt(nr);
         HIP_CHECK(hipMemcpyAsync(cnt.data(), ix->flag.p, nr * sizeof(uint32_t),
@@ -2048,7 +2105,8 @@ void append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* 
         CPD_REQUIRE(o[nr] <= ix->cap, CPD_E_ARG, "index: more runs than the index was created for");
         HIP_CHECK(hipMemcpyAsync(ix->off.p + ix->added, o.data(), o.size() * sizeof(uint64_t),
                                  hipMemcpyHostToDevice, s));
-        launch_moves_runs(tables, (uint32_t)wpr, g->n, nr, ix->off.p + ix->added, 0, ix->runs.p, s);
+        launch_moves_runs(tables, (uint32_t)wpr, g->tlb, g->n, nr, ix->off.p + ix->added, 0,
+                          ix->runs.p, s);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipStreamSynchronize(s));
         ix->offsets.insert(ix->offsets.end(), o.begin() + 1, o.end());
@@ -2230,7 +2288,10 @@ namespace {
 void ensure_dense(cpd_index* ix) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(g->npad / kFmTile < 65536u, CPD_E_RANGE, "graph too large for dense tables");
-    ix->dense.alloc((size_t)ix->nrows * (g->npad / 8u));
+    ix->dense.alloc((size_t)ix->nrows * g->wpr());
+    if (ix->nrows && g->tlb != 2u)  // the runs' moves must fit the narrower tables
+        validate_device_rows(ix, ix->off.p, ix->runs.p, ix->offsets.data(), ix->nrows,
+                             table_move_limit(g));
     if (ix->nrows)
         expand_into(ix, ix->off.p, ix->runs.p, ix->offsets.data(), ix->nrows, ix->total, 0);
     g->sync();
@@ -2273,7 +2334,7 @@ int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
         const uint32_t* adj = ix->custom_w ? ix->adj_sel.p : g->adj.p;
         (void)hipGetLastError();
         if (nq && dense)
-            launch_table_search_dense(adj, g->adj_shift, ix->d_row_of_col.p, ix->dense.p, g->npad,
+            launch_table_search_dense(adj, g->adj_shift, ix->d_row_of_col.p, ix->dense.p, g->npad, g->tlb,
                                       ix->qs.p, ix->qt.p, ix->qrow.p, nq, k_moves, g->n,
                                       ix->cost.p, ix->hops.p, ix->fin.p, ix->agg.p, g->stream);
         else if (nq)
@@ -2427,7 +2488,7 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             DevBuf<uint8_t> scratch;
             scratch.alloc((size_t)chunk * n * 48u);
             HIP_CHECK(hipEventRecord(a, g->stream));
-            launch_search_tables(ix->dense.p, g->npad, g->adj.p, adj_w, g->adj_shift, ix->tcol.p,
+            launch_search_tables(ix->dense.p, g->npad, g->tlb, g->adj.p, adj_w, g->adj_shift, ix->tcol.p,
                                  ix->nrows, n, scratch.p, chunk, ix->hrow.p, ix->crow.p,
                                  ix->lrow.p, ix->h_ready ? 0 : 1, g->stream);
             HIP_CHECK(hipEventRecord(b, g->stream));
@@ -2459,7 +2520,7 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
         HIP_CHECK(hipEventRecord(a, g->stream));
         (void)hipGetLastError();
         if (nq)
-            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad,
+            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad, g->tlb,
                               tables ? ix->hrow.p : nullptr, ix->crow.p, ix->lrow.p, n, ix->qs.p,
                               ix->qt.p, ix->qrow.p, nq, o.hscale, o.fscale, o.k_moves, o.itrs,
                               o.time_ns, o.virtual_tick_ns, ix->sws.p, o.capacity, slots,
@@ -2529,7 +2590,7 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             const uint32_t slots2 = (uint32_t)std::min<size_t>(search_slots(m), fit2 * 256u);
             ix->sws.alloc((size_t)slots2 * per2);
             HIP_CHECK(hipEventRecord(a, g->stream));
-            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad,
+            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad, g->tlb,
                               tables ? ix->hrow.p : nullptr, ix->crow.p, ix->lrow.p, n, d_q.p,
                               d_q.p + m, d_q.p + 2ull * m, m, o.hscale, o.fscale, o.k_moves,
                               o.itrs, o.time_ns, o.virtual_tick_ns, ix->sws.p, cap, slots2,

@@ -1260,6 +1260,81 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
 // tile: a wave writes 1 KiB contiguous.
 constexpr uint32_t kMoveTiles = 16;
 
+// Move tables at 2^lb bits per column (lb = 0, 1, 2: 1, 2 or 4 bits, by the
+// graph's max out-degree — a move indexes its column's out-list, so every
+// valid move fits), column c in bits [b·c, b·c + b) of its row, npad·b/32
+// words per row.  The emit computes 32 columns per lane as four nibble words
+// and narrows them on the store; readers of whole 32-column groups widen
+// them back; the walks read one column's field.
+struct Tbl {
+    uint32_t lb;
+    __device__ __forceinline__ uint32_t move(const uint32_t* __restrict__ row, uint32_t c) const {
+        return (row[c >> (5u - lb)] >> ((c & (31u >> lb)) << lb)) & ((1u << (1u << lb)) - 1u);
+    }
+};
+
+// 8 nibbles (each < 4) -> 16 bits of 2-bit fields; (each < 2) -> 8 bits
+__device__ __forceinline__ uint32_t nib_to2(uint32_t x) {
+    x &= 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    return (x | (x >> 8)) & 0x0000FFFFu;
+}
+__device__ __forceinline__ uint32_t nib_to1(uint32_t x) {
+    x &= 0x11111111u;
+    x = (x | (x >> 3)) & 0x03030303u;
+    x = (x | (x >> 6)) & 0x000F000Fu;
+    return (x | (x >> 12)) & 0x000000FFu;
+}
+__device__ __forceinline__ uint32_t nib_from2(uint32_t y) {  // 16 bits -> 8 nibbles
+    y &= 0xFFFFu;
+    y = (y | (y << 8)) & 0x00FF00FFu;
+    y = (y | (y << 4)) & 0x0F0F0F0Fu;
+    return (y | (y << 2)) & 0x33333333u;
+}
+__device__ __forceinline__ uint32_t nib_from1(uint32_t y) {  // 8 bits -> 8 nibbles
+    y &= 0xFFu;
+    y = (y | (y << 12)) & 0x000F000Fu;
+    y = (y | (y << 6)) & 0x03030303u;
+    return (y | (y << 3)) & 0x11111111u;
+}
+
+// Columns [32 g, 32 g + 32) of a table row, as four nibble words o[0..3]
+// (column 32 g + k in nibble k % 8 of o[k / 8]): one 16-, 8- or 4-B access.
+__device__ __forceinline__ void store_cols32(uint32_t* __restrict__ row, uint32_t g, uint32_t lb,
+                                             const uint32_t (&o)[4]) {
+    if (lb == 2u) {
+        reinterpret_cast<uint4*>(row)[g] = make_uint4(o[0], o[1], o[2], o[3]);
+    } else if (lb == 1u) {
+        reinterpret_cast<uint2*>(row)[g] =
+            make_uint2(nib_to2(o[0]) | (nib_to2(o[1]) << 16), nib_to2(o[2]) | (nib_to2(o[3]) << 16));
+    } else {
+        row[g] = nib_to1(o[0]) | (nib_to1(o[1]) << 8) | (nib_to1(o[2]) << 16) | (nib_to1(o[3]) << 24);
+    }
+}
+__device__ __forceinline__ void load_cols32(const uint32_t* __restrict__ row, uint32_t g, uint32_t lb,
+                                            uint32_t (&x)[4]) {
+    if (lb == 2u) {
+        const uint4 q = reinterpret_cast<const uint4*>(row)[g];
+        x[0] = q.x;
+        x[1] = q.y;
+        x[2] = q.z;
+        x[3] = q.w;
+    } else if (lb == 1u) {
+        const uint2 q = reinterpret_cast<const uint2*>(row)[g];
+        x[0] = nib_from2(q.x);
+        x[1] = nib_from2(q.x >> 16);
+        x[2] = nib_from2(q.y);
+        x[3] = nib_from2(q.y >> 16);
+    } else {
+        const uint32_t q = row[g];
+        x[0] = nib_from1(q);
+        x[1] = nib_from1(q >> 8);
+        x[2] = nib_from1(q >> 16);
+        x[3] = nib_from1(q >> 24);
+    }
+}
+
 __device__ __forceinline__ uint32_t low_bit(uint32_t S) {
     return (uint32_t)__builtin_ctz(S | 0x8000u);  // S != 0: every set is non-empty
 }
@@ -1335,7 +1410,7 @@ __global__ __launch_bounds__(256) void rle_moves(const uint32_t* __restrict__ fm
                                                  uint32_t nrows, const uint32_t* __restrict__ st,
                                                  const uint8_t* __restrict__ rc,
                                                  const uint32_t* __restrict__ out_row,
-                                                 uint32_t* __restrict__ dense) {
+                                                 uint32_t lb, uint32_t* __restrict__ dense) {
     using F = FmFmt<FMB>;
     const uint32_t brow = blockIdx.y * 4u + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -1366,7 +1441,7 @@ __global__ __launch_bounds__(256) void rle_moves(const uint32_t* __restrict__ fm
         load_seg<FMB>(fm, npad, brow, nseg - 1u, v);
         carry = low_bit(seg_moves<FMB>(v, strow[nseg - 1u] & smask).S);
     }
-    uint4* __restrict__ orow = reinterpret_cast<uint4*>(dense + (size_t)out_row[brow] * (npad / 8u));
+    uint32_t* __restrict__ orow = dense + (size_t)out_row[brow] * (npad >> (5u - lb));
     for (uint32_t t = t1; t-- > t0;) {
         const uint32_t seg = t * 64u + lane;
         uint32_t v[F::kWords];
@@ -1385,7 +1460,7 @@ __global__ __launch_bounds__(256) void rle_moves(const uint32_t* __restrict__ fm
             o[k >> 3] |= mv << (4 * (k & 7));
             if (k > 0 && ((r.brk >> k) & 1u)) mv = (r.L[(k - 1) >> 3] >> (4 * ((k - 1) & 7))) & 0xFu;
         }
-        orow[(size_t)t * 64u + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        store_cols32(orow, t * 64u + lane, lb, o);
         if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
     }
 }
@@ -1446,7 +1521,7 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
                                                   uint32_t nrows, const uint32_t* __restrict__ st,
                                                   const uint8_t* __restrict__ rc,
                                                   const uint32_t* __restrict__ out_row,
-                                                  uint32_t* __restrict__ dense) {
+                                                  uint32_t lb, uint32_t* __restrict__ dense) {
     const uint32_t brow = blockIdx.y * 4u + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     if (brow >= nrows) return;  // wave-uniform
@@ -1482,7 +1557,7 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
         load(nseg - 1u, v);
         carry = seg4_scan(v, strow[nseg - 1u] & 0xFu).S[3] >> 28;
     }
-    uint4* __restrict__ orow = reinterpret_cast<uint4*>(dense + (size_t)out_row[brow] * (npad / 8u));
+    uint32_t* __restrict__ orow = dense + (size_t)out_row[brow] * (npad >> (5u - lb));
     for (uint32_t t = t1; t-- > t0;) {
         const uint32_t seg = t * 64u + lane;
         uint32_t v[4];
@@ -1551,7 +1626,7 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
             const uint32_t b2 = ~(X[i] >> 2) & b1;
             o[i] = b0 + b1 + b2;
         }
-        orow[(size_t)t * 64u + lane] = make_uint4(o[0], o[1], o[2], o[3]);
+        store_cols32(orow, t * 64u + lane, lb, o);
         if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
     }
 }
@@ -1559,44 +1634,36 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
 // The compact form on the wire and on disk: a move per column in `bits` =
 // 1, 2 or 4 bits (every move of a graph whose out-degrees are <= 2^bits fits:
 // a move indexes its column's out-list, and a wildcard run's lowest set bit
-// is 0), ceil(n * bits / 32) words per row, rows back to back.  pack: one
-// thread per packed word, from the nibble tables (stride words per row);
-// unpack: one thread per nibble word.  Columns >= n carry whatever the
-// nibble table holds there (the last run's move).
-__global__ __launch_bounds__(256) void pack_moves(const uint32_t* __restrict__ dense,
-                                                  uint32_t stride, uint32_t rows, uint32_t bits,
-                                                  uint32_t words, uint32_t* __restrict__ out) {
+// is 0), ceil(n * bits / 32) words per row, rows back to back.  repack: any
+// width to any width — the tables (stride words per row) to a file's packed
+// rows on export, a file's rows to the tables on load when the widths differ
+// (4-bit rows into a narrower index: each move must fit, which valid rows of
+// the graph always do; *lost |= 1 when one does not).  One thread per output
+// word; input past a row's s_words reads as 0.
+__global__ __launch_bounds__(256) void repack_moves(const uint32_t* __restrict__ src,
+                                                    uint32_t s_stride, uint32_t s_words,
+                                                    uint32_t s_bits, uint32_t rows,
+                                                    uint32_t* __restrict__ dst, uint32_t d_stride,
+                                                    uint32_t d_words, uint32_t d_bits,
+                                                    uint32_t* __restrict__ lost) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)rows * words) return;
-    const uint32_t r = (uint32_t)(i / words), w = (uint32_t)(i % words);
-    const uint32_t per = 32u / bits;  // columns per packed word
-    const uint32_t* __restrict__ src = dense + (size_t)r * stride + (size_t)w * per / 8u;
-    const uint32_t mask = (1u << bits) - 1u;
-    uint32_t o = 0;
-    for (uint32_t j = 0; j < per / 8u; ++j) {
-        const uint32_t x = (size_t)w * per / 8u + j < stride ? src[j] : 0u;
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) o |= ((x >> (4u * k)) & mask) << (bits * (8u * j + k));
+    if (i >= (uint64_t)rows * d_words) return;
+    const uint32_t r = (uint32_t)(i / d_words), w = (uint32_t)(i % d_words);
+    const uint32_t per = 32u / d_bits;  // columns per output word
+    const uint32_t* __restrict__ in = src + (size_t)r * s_stride;
+    const uint32_t smask = (1u << s_bits) - 1u, dmask = (1u << d_bits) - 1u;
+    uint32_t o = 0, wide = 0;
+    for (uint32_t k = 0; k < per; ++k) {
+        const uint64_t bit = (uint64_t)(w * per + k) * s_bits;  // first bit in the input row
+        const uint32_t sw = (uint32_t)(bit >> 5);
+        const uint32_t v = sw < s_words ? (in[sw] >> (bit & 31u)) & smask : 0u;
+        o |= (v & dmask) << (d_bits * k);
+        wide |= v & ~dmask;
     }
-    out[i] = o;
-}
-
-__global__ __launch_bounds__(256) void unpack_moves(const uint32_t* __restrict__ packed,
-                                                    uint32_t words, uint32_t rows, uint32_t bits,
-                                                    uint32_t stride, uint32_t* __restrict__ dense) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)rows * stride) return;
-    const uint32_t r = (uint32_t)(i / stride), d = (uint32_t)(i % stride);
-    const uint32_t bit0 = d * 8u * bits;  // first bit of column 8d in the packed row
-    const uint32_t w = bit0 / 32u;
-    uint32_t o = 0;
-    if (w < words) {
-        const uint32_t x = packed[(size_t)r * words + w] >> (bit0 % 32u);
-        const uint32_t mask = (1u << bits) - 1u;
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) o |= ((x >> (bits * k)) & mask) << (4u * k);
-    }
-    dense[i] = o;
+    dst[(size_t)r * d_stride + w] = o;
+    // a move that does not fit the output width (only rows from outside the
+    // library can carry one): flagged, never silently truncated
+    if (lost && __any(wide != 0u) && (threadIdx.x & 63u) == 0u) atomicOr(lost, 1u);
 }
 
 // Move tables -> RLE words, the inverse of rle_moves: a row's runs start at
@@ -1605,10 +1672,11 @@ __global__ __launch_bounds__(256) void unpack_moves(const uint32_t* __restrict__
 // ignored.  EMIT = false: counts[r] = the row's runs; EMIT = true: the runs at
 // runs[off[r] - base].  A wave per row, 2048-column tiles left to right, runs
 // staged per tile in LDS and stored coalesced.  Row r's table at
-// dense + r * stride (stride: words, a multiple of 4).
+// dense + r * stride, 2^lb bits per column (Tbl).
 template <bool EMIT>
 __global__ __launch_bounds__(256) void moves_runs(const uint32_t* __restrict__ dense,
-                                                  uint32_t stride, uint32_t n, uint32_t nrows,
+                                                  uint32_t stride, uint32_t lb, uint32_t n,
+                                                  uint32_t nrows,
                                                   const uint64_t* __restrict__ off, uint64_t base,
                                                   uint32_t* __restrict__ runs,
                                                   uint32_t* __restrict__ counts) {
@@ -1617,16 +1685,15 @@ __global__ __launch_bounds__(256) void moves_runs(const uint32_t* __restrict__ d
     const uint32_t lane = threadIdx.x & 63u;
     if (row >= nrows) return;
     uint32_t* stage = stage_all + (EMIT ? (threadIdx.x >> 6) * kTile : 0u);
-    const uint4* __restrict__ rowp = reinterpret_cast<const uint4*>(dense + (size_t)row * stride);
+    const uint32_t* __restrict__ rowp = dense + (size_t)row * stride;
     uint32_t* __restrict__ out = EMIT ? runs + (off[row] - base) : nullptr;
     const uint32_t ntiles = (n + kTile - 1u) / kTile;
     uint32_t prev = 0x10u;  // no nibble: column 0 always starts a run
     uint32_t total = 0;
     for (uint32_t t = 0; t < ntiles; ++t) {
         const uint32_t c0 = t * kTile + lane * kSeg;
-        uint4 q = make_uint4(0u, 0u, 0u, 0u);
-        if (c0 < n) q = rowp[(size_t)t * 64u + lane];
-        const uint32_t x[4] = {q.x, q.y, q.z, q.w};
+        uint32_t x[4] = {0u, 0u, 0u, 0u};
+        if (c0 < n) load_cols32(rowp, t * 64u + lane, lb, x);
         uint32_t pl = (uint32_t)__shfl_up((int)(x[3] >> 28), 1, 64);
         if (lane == 0) pl = prev;
         uint32_t chg = 0;
@@ -1649,7 +1716,7 @@ __global__ __launch_bounds__(256) void moves_runs(const uint32_t* __restrict__ d
             uint32_t p = incl - cnt;
             for (uint32_t b = chg; b; b &= b - 1u) {
                 const uint32_t k = (uint32_t)__builtin_ctz(b);
-                stage[p++] = ((c0 + k) << 4) | nib_at(q.x, q.y, q.z, q.w, k);
+                stage[p++] = ((c0 + k) << 4) | nib_at(x[0], x[1], x[2], x[3], k);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -2012,7 +2079,8 @@ __global__ __launch_bounds__(256) void expand_rows(const uint64_t* __restrict__ 
 // Row format check for rows loaded from outside the library (bucket files,
 // host arrays), in expand_rows' run chunks: *bad |= 1 when a row does not
 // start at column 0, its run columns do not strictly increase, or a column
-// is >= n.  expand_rows and the binary searches rely on exactly these
+// is >= n, or (mlimit < 16: rows bound for tables narrower than 4 bits) a
+// move does not fit the table's field.  expand_rows and the binary searches rely on exactly these
 // properties (a run's move is checked by the walk itself: a move naming no
 // edge of its column stops the walk, so it is not checked here — a run that
 // starts on a wildcard column may legally carry a move that column does not
@@ -2021,7 +2089,8 @@ __global__ __launch_bounds__(256) void validate_rows(const uint64_t* __restrict_
                                                      const uint32_t* __restrict__ runs,
                                                      const uint32_t* __restrict__ chunk_first,
                                                      uint32_t nrows, uint32_t total_chunks,
-                                                     uint32_t n, uint32_t* __restrict__ bad) {
+                                                     uint32_t n, uint32_t mlimit,
+                                                     uint32_t* __restrict__ bad) {
     const uint32_t chunk = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     if (chunk >= total_chunks) return;
@@ -2039,6 +2108,7 @@ __global__ __launch_bounds__(256) void validate_rows(const uint64_t* __restrict_
     for (uint32_t i = r0 + lane; i < r1; i += 64u) {
         const uint32_t c = runs[o0 + i] >> 4;
         b |= c >= n;
+        b |= (runs[o0 + i] & 0xFu) >= mlimit;
         if (i == 0) b |= c != 0u;
         else b |= c <= (runs[o0 + i - 1] >> 4);
     }
@@ -2068,6 +2138,7 @@ constexpr uint32_t kIdleQ = 0xFFFFFFFFu;
 struct DenseRows {
     const uint32_t* __restrict__ dense;
     uint32_t wpr;  // words per row
+    Tbl tb;        // bits per column
 };
 
 struct RleRows {
@@ -2113,8 +2184,8 @@ __device__ __forceinline__ void walk_begin(WalkState& w, uint32_t q, const uint3
 __device__ __forceinline__ const uint32_t* rows_base(const DenseRows& d) { return d.dense; }
 __device__ __forceinline__ const uint32_t* rows_base(const RleRows& r) { return r.runs; }
 
-__device__ __forceinline__ uint32_t walk_move(WalkState& w, const DenseRows&) {
-    return (w.row[w.cur >> 3] >> (4u * (w.cur & 7u))) & 0xFu;
+__device__ __forceinline__ uint32_t walk_move(WalkState& w, const DenseRows& d) {
+    return d.tb.move(w.row, w.cur);
 }
 
 // The last run with start <= cur, galloping from the previous hop's run.
@@ -2201,13 +2272,14 @@ __device__ __forceinline__ void walk_hop(WalkState& w, const uint2* __restrict__
 // are in flight together instead of one branch region after another.
 template <int SHIFT, int ILP>
 __device__ __forceinline__ void walk_hops(WalkState (&w)[ILP], const uint2* __restrict__ adj,
-                                          const DenseRows&) {
+                                          const DenseRows& d) {
     constexpr int NQ = SHIFT == 2 ? 2 : 1;  // 16-B pieces of an adjacency row
+    const uint32_t wsh = 5u - d.tb.lb, cm = 31u >> d.tb.lb, mm = (1u << (1u << d.tb.lb)) - 1u;
     uint32_t word[ILP];
     uint4 p[ILP][NQ];
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
-        word[i] = w[i].row[w[i].cur >> 3];
+        word[i] = w[i].row[w[i].cur >> wsh];
         if (SHIFT <= 2) {
             if (SHIFT == 0) {
                 const uint2 e = adj[w[i].cur];
@@ -2222,7 +2294,7 @@ __device__ __forceinline__ void walk_hops(WalkState (&w)[ILP], const uint2* __re
 #pragma unroll
     for (int i = 0; i < ILP; ++i) {
         if (w[i].q == kIdleQ || w[i].cur == w[i].t) continue;
-        const uint32_t mv = (word[i] >> (4u * (w[i].cur & 7u))) & 0xFu;
+        const uint32_t mv = (word[i] >> ((w[i].cur & cm) << d.tb.lb)) & mm;
         uint32_t ex, ew;
         if (SHIFT <= 2) {
             const uint4 q = (NQ == 2 && (mv & 2u)) ? p[i][NQ - 1] : p[i][0];
@@ -2387,7 +2459,7 @@ struct JumpState {
 };
 
 __global__ __launch_bounds__(256) void jump_init(const uint32_t* __restrict__ dense,
-                                                 uint32_t wpr, const uint2* __restrict__ adj_f,
+                                                 uint32_t wpr, Tbl tbl, const uint2* __restrict__ adj_f,
                                                  const uint2* __restrict__ adj_w, uint32_t shift,
                                                  const uint32_t* __restrict__ tcol, uint32_t rows,
                                                  uint32_t n, JumpState js) {
@@ -2399,7 +2471,7 @@ __global__ __launch_bounds__(256) void jump_init(const uint32_t* __restrict__ de
     if (c == tcol[r]) {
         nx = c;
     } else {
-        const uint32_t mv = (dense[(size_t)r * wpr + (c >> 3)] >> (4u * (c & 7u))) & 0xFu;
+        const uint32_t mv = tbl.move(dense + (size_t)r * wpr, c);
         if (!(mv >> shift)) {
             const size_t e = ((size_t)c << shift) + mv;
             const uint2 ef = adj_f[e];
@@ -2574,6 +2646,7 @@ struct LaneWs {
     uint32_t* __restrict__ hc;
     uint4* __restrict__ stk;
     uint32_t C, mask;
+    Tbl tb;  // the move tables' bits per column
 };
 
 // Insert column c (absent: slot i from hprobe) as walked-only; false on
@@ -2611,7 +2684,7 @@ __device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj
             break;
         }
         W.aux[xi].y = (W.aux[xi].y & 0x3FFFFFFFu) | (kOnWalk << 30);
-        const uint32_t mv = (row[x >> 3] >> (4u * (x & 7u))) & 0xFu;
+        const uint32_t mv = W.tb.move(row, x);
         uint2 ef = make_uint2(kNoEdge, 0u), ew = make_uint2(kNoEdge, 0u);
         if (!(mv >> SHIFT)) {
             ef = adj_f[((size_t)x << SHIFT) + mv];
@@ -2662,7 +2735,7 @@ struct SearchTables {
 template <int SHIFT, bool TABLES>
 __global__ __launch_bounds__(256) void cpd_search(
     const uint2* __restrict__ adj_f, const uint2* __restrict__ adj_w,
-    const uint32_t* __restrict__ dense, uint32_t wpr, SearchTables tb,
+    const uint32_t* __restrict__ dense, uint32_t wpr, uint32_t lb, SearchTables tb,
     const uint32_t* __restrict__ qs,
     const uint32_t* __restrict__ qt, const uint32_t* __restrict__ qrow, uint32_t nq,
     uint32_t chunk, SearchOpt opt, SearchWs ws, uint64_t* __restrict__ cost_out,
@@ -2677,7 +2750,7 @@ __global__ __launch_bounds__(256) void cpd_search(
     const uint32_t C = ws.cap;
     const LaneWs W{ws.ent + slot * 2u * C, TABLES ? nullptr : ws.memo + slot * 2u * C,
                    ws.aux + slot * 2u * C, ws.he + slot * C, ws.hc + slot * C,
-                   TABLES ? nullptr : ws.stk + slot * C, C, 2u * C - 1u};
+                   TABLES ? nullptr : ws.stk + slot * C, C, 2u * C - 1u, Tbl{lb}};
     unsigned long long s_exp = 0, s_ins = 0, s_tou = 0, s_upd = 0, s_sur = 0, s_len = 0,
                        s_fin = 0, s_ovf = 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -3109,7 +3182,7 @@ void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t*
 
 void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
                       const uint32_t* st, const uint8_t* rc, const uint32_t* out_row,
-                      uint32_t* dense, hipStream_t s) {
+                      uint32_t lb, uint32_t* dense, hipStream_t s) {
     if (!nrows) return;
     const uint32_t ntiles = npad / kern::kTile;
     const dim3 grid((ntiles + kern::kMoveTiles - 1u) / kern::kMoveTiles, (nrows + 3u) / 4u),
@@ -3117,50 +3190,44 @@ void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
     static const bool swar = env_u32("CPD_MOVES_SWAR", 1) != 0;
     switch (fmb) {
         case 4:
-            if (swar) launch(kern::rle_moves4, grid, block, s, fm, npad, nrows, st, rc, out_row, dense);
-            else launch(kern::rle_moves<4>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense);
+            if (swar) launch(kern::rle_moves4, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense);
+            else launch(kern::rle_moves<4>, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense);
             break;
-        case 8: launch(kern::rle_moves<8>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
-        default: launch(kern::rle_moves<16>, grid, block, s, fm, npad, nrows, st, rc, out_row, dense); break;
+        case 8: launch(kern::rle_moves<8>, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense); break;
+        default: launch(kern::rle_moves<16>, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense); break;
     }
 }
 
-void launch_pack_moves(const uint32_t* dense, uint32_t stride, uint32_t rows, uint32_t bits,
-                       uint32_t words, uint32_t* out, hipStream_t s) {
-    const uint64_t items = (uint64_t)rows * words;
+void launch_repack_moves(const uint32_t* src, uint32_t s_stride, uint32_t s_words,
+                         uint32_t s_bits, uint32_t rows, uint32_t* dst, uint32_t d_stride,
+                         uint32_t d_words, uint32_t d_bits, hipStream_t s, uint32_t* lost) {
+    const uint64_t items = (uint64_t)rows * d_words;
     if (!items) return;
-    launch(kern::pack_moves, dim3((uint32_t)((items + 255u) / 256u)), dim3(256), s, dense, stride,
-           rows, bits, words, out);
+    launch(kern::repack_moves, dim3((uint32_t)((items + 255u) / 256u)), dim3(256), s, src,
+           s_stride, s_words, s_bits, rows, dst, d_stride, d_words, d_bits, lost);
 }
 
-void launch_unpack_moves(const uint32_t* packed, uint32_t words, uint32_t rows, uint32_t bits,
-                         uint32_t stride, uint32_t* dense, hipStream_t s) {
-    const uint64_t items = (uint64_t)rows * stride;
-    if (!items) return;
-    launch(kern::unpack_moves, dim3((uint32_t)((items + 255u) / 256u)), dim3(256), s, packed, words,
-           rows, bits, stride, dense);
-}
-
-void launch_moves_count(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,
-                        uint32_t* counts, hipStream_t s) {
+void launch_moves_count(const uint32_t* dense, uint32_t stride, uint32_t lb, uint32_t n,
+                        uint32_t nrows, uint32_t* counts, hipStream_t s) {
     if (!nrows) return;
-    launch(kern::moves_runs<false>, dim3((nrows + 3u) / 4u), dim3(256), s, dense, stride, n, nrows,
-           (const uint64_t*)nullptr, (uint64_t)0, (uint32_t*)nullptr, counts);
+    launch(kern::moves_runs<false>, dim3((nrows + 3u) / 4u), dim3(256), s, dense, stride, lb, n,
+           nrows, (const uint64_t*)nullptr, (uint64_t)0, (uint32_t*)nullptr, counts);
 }
 
-void launch_moves_runs(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,
-                       const uint64_t* off, uint64_t base, uint32_t* runs, hipStream_t s) {
+void launch_moves_runs(const uint32_t* dense, uint32_t stride, uint32_t lb, uint32_t n,
+                       uint32_t nrows, const uint64_t* off, uint64_t base, uint32_t* runs,
+                       hipStream_t s) {
     if (!nrows) return;
-    launch(kern::moves_runs<true>, dim3((nrows + 3u) / 4u), dim3(256), s, dense, stride, n, nrows,
-           off, base, runs, (uint32_t*)nullptr);
+    launch(kern::moves_runs<true>, dim3((nrows + 3u) / 4u), dim3(256), s, dense, stride, lb, n,
+           nrows, off, base, runs, (uint32_t*)nullptr);
 }
 
 void launch_validate_rows(const uint64_t* offsets, const uint32_t* runs,
                           const uint32_t* chunk_first, uint32_t nrows, uint32_t total_chunks,
-                          uint32_t n, uint32_t* bad, hipStream_t s) {
+                          uint32_t n, uint32_t mlimit, uint32_t* bad, hipStream_t s) {
     if (!nrows || !total_chunks) return;
     launch(kern::validate_rows, dim3((total_chunks + 3u) / 4u), dim3(256), s, offsets, runs,
-           chunk_first, nrows, total_chunks, n, bad);
+           chunk_first, nrows, total_chunks, n, mlimit, bad);
 }
 
 uint32_t expand_chunk_runs() { return kern::kExpandRuns; }
@@ -3224,11 +3291,13 @@ static uint32_t walk_limit(int32_t kmoves, uint32_t n) {
 }
 
 void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
-                               const uint32_t* dense, uint32_t npad, const uint32_t* qs,
-                               const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
-                               int32_t kmoves, uint32_t n, uint64_t* cost, uint32_t* hops,
-                               uint8_t* fin, unsigned long long* agg, hipStream_t s) {
-    launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::DenseRows{dense, npad / 8u}, qs,
+                               const uint32_t* dense, uint32_t npad, uint32_t lb,
+                               const uint32_t* qs, const uint32_t* qt, const uint32_t* qrow,
+                               uint32_t nq, int32_t kmoves, uint32_t n, uint64_t* cost,
+                               uint32_t* hops, uint8_t* fin, unsigned long long* agg,
+                               hipStream_t s) {
+    launch_walk(reinterpret_cast<const uint2*>(adj), shift,
+                kern::DenseRows{dense, npad >> (5u - lb), kern::Tbl{lb}}, qs,
                 qt, qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(1024),
                 ts_chunk_max(1024), s);
 }
@@ -3250,7 +3319,7 @@ uint32_t search_slots(uint32_t nq) {  // lanes with a workspace: whole blocks of
     return 64u * ((w + 3u) / 4u * 4u);
 }
 
-void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* adj_f,
+void launch_search_tables(const uint32_t* dense, uint32_t npad, uint32_t lb, const uint32_t* adj_f,
                           const uint32_t* adj_w, uint32_t shift, const uint32_t* tcol,
                           uint32_t rows, uint32_t n, void* scratch, uint32_t chunk_rows,
                           uint64_t* hrow, uint64_t* crow, uint32_t* lrow, int write_h,
@@ -3273,7 +3342,8 @@ void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* 
         const uint32_t R = std::min(chunk_rows, rows - r0);
         const uint64_t items = (uint64_t)R * n;
         const dim3 grid((uint32_t)((items + 255u) / 256u)), blk(256);
-        launch(kern::jump_init, grid, blk, s, dense + (size_t)r0 * (npad / 8u), npad / 8u, af, aw,
+        const uint32_t wpr = npad >> (5u - lb);
+        launch(kern::jump_init, grid, blk, s, dense + (size_t)r0 * wpr, wpr, kern::Tbl{lb}, af, aw,
                shift, tcol + r0, R, n, A);
         kern::JumpState a = A, b = Bs;
         for (uint32_t k = 0; k < rounds; ++k) {
@@ -3286,7 +3356,7 @@ void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* 
 }
 
 void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t shift,
-                       const uint32_t* dense, uint32_t npad, const uint64_t* hrow,
+                       const uint32_t* dense, uint32_t npad, uint32_t lb, const uint64_t* hrow,
                        const uint64_t* crow, const uint32_t* lrow, uint32_t n,
                        const uint32_t* qs, const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
                        double hscale, double fscale, int32_t kmoves, int64_t itrs,
@@ -3320,9 +3390,9 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     const uint32_t c2 = (uint32_t)(((uint64_t)nq + waves - 1u) / waves);
     const uint2* af = reinterpret_cast<const uint2*>(adj_f);
     const uint2* aw = reinterpret_cast<const uint2*>(adj_w);
-    const uint32_t wpr = npad / 8u;
+    const uint32_t wpr = npad >> (5u - lb);
 #define CPD_SEARCH(SH, T)                                                                    \
-    launch(kern::cpd_search<SH, T>, grid, blk, s, af, aw, dense, wpr, tb, qs, qt, qrow, nq, c2, \
+    launch(kern::cpd_search<SH, T>, grid, blk, s, af, aw, dense, wpr, lb, tb, qs, qt, qrow, nq, c2, \
            o, w, cost, plen, fin, qstats, agg)
 #define CPD_SEARCH_T(SH)          \
     if (tables) CPD_SEARCH(SH, true); \

@@ -114,29 +114,32 @@ void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
                       uint32_t* counts, uint32_t* st, uint8_t* rc, hipStream_t s,
                       const uint32_t* gate = nullptr);
 
-// The compact row form: each row's greedy RLE row as a 4-bit move table
-// (column c = nibble c % 8 of word c / 8, npad / 8 words per row — the dense
-// table the walks read), from the first-move sets and the count pass's
-// segment states st / rc; batch row r goes to dense row out_row[r].
+// The compact row form: each row's greedy RLE row as a move table at
+// 2^lb bits per column (lb = 0, 1, 2; column c in bits [b c, b c + b) of the
+// row, npad * b / 32 words per row — the dense table the walks read), from
+// the first-move sets and the count pass's segment states st / rc; batch row
+// r goes to dense row out_row[r].
 void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
                       const uint32_t* st, const uint8_t* rc, const uint32_t* out_row,
-                      uint32_t* dense, hipStream_t s);
-// The compact form's packed width: `bits` (1, 2 or 4) per column,
-// ceil(n * bits / 32) = words per row, rows back to back.  pack: nibble
-// tables (stride words per row) -> packed rows; unpack: the reverse (the
-// nibble words past a packed row's end are written as 0).
-void launch_pack_moves(const uint32_t* dense, uint32_t stride, uint32_t rows, uint32_t bits,
-                       uint32_t words, uint32_t* out, hipStream_t s);
-void launch_unpack_moves(const uint32_t* packed, uint32_t words, uint32_t rows, uint32_t bits,
-                         uint32_t stride, uint32_t* dense, hipStream_t s);
-// Move tables (row r at dense + r * stride words, stride % 4 == 0) back to
-// RLE words: runs start at column 0 and wherever the move changes (columns
+                      uint32_t lb, uint32_t* dense, hipStream_t s);
+// Rows of moves from one width to another: src rows of s_bits per column at
+// s_stride words per row (s_words of them valid), dst rows of d_bits at
+// d_stride, d_words written per row (input past s_words reads as 0).  The
+// file / wire form is d_words = d_stride = ceil(n * bits / 32).  lost (may be
+// null): |= 1 when some move does not fit d_bits.
+void launch_repack_moves(const uint32_t* src, uint32_t s_stride, uint32_t s_words,
+                         uint32_t s_bits, uint32_t rows, uint32_t* dst, uint32_t d_stride,
+                         uint32_t d_words, uint32_t d_bits, hipStream_t s,
+                         uint32_t* lost = nullptr);
+// Move tables (row r at dense + r * stride words, 2^lb bits per column) back
+// to RLE words: runs start at column 0 and wherever the move changes (columns
 // >= n ignored).  count: counts[r] = runs of row r; runs: row r's words at
 // runs[off[r] - base].
-void launch_moves_count(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,
-                        uint32_t* counts, hipStream_t s);
-void launch_moves_runs(const uint32_t* dense, uint32_t stride, uint32_t n, uint32_t nrows,
-                       const uint64_t* off, uint64_t base, uint32_t* runs, hipStream_t s);
+void launch_moves_count(const uint32_t* dense, uint32_t stride, uint32_t lb, uint32_t n,
+                        uint32_t nrows, uint32_t* counts, hipStream_t s);
+void launch_moves_runs(const uint32_t* dense, uint32_t stride, uint32_t lb, uint32_t n,
+                       uint32_t nrows, const uint64_t* off, uint64_t base, uint32_t* runs,
+                       hipStream_t s);
 
 // Chunked RLE count (4-bit sets; cpd_kernels.hip rle_count_ch): the same st /
 // rc as launch_rle_count, with each chunk of segments scanned by one lane
@@ -153,14 +156,16 @@ void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t*
                     hipStream_t s);
 
 // *bad |= 1 if some row [0, nrows) of (offsets, runs) does not start at column
-// 0, has non-increasing run columns or a column >= n (empty rows: refused by
-// the caller).  Rows from outside the library pass this before expand_rows /
-// the walks touch them.  chunk_first / total_chunks as for launch_expand_rows.
+// 0, has non-increasing run columns, a column >= n or a move >= mlimit (16:
+// any; a narrower table's 2^bits) (empty rows: refused by the caller).  Rows
+// from outside the library pass this before expand_rows / the walks touch
+// them.  chunk_first / total_chunks as for launch_expand_rows.
 void launch_validate_rows(const uint64_t* offsets, const uint32_t* runs,
                           const uint32_t* chunk_first, uint32_t nrows, uint32_t total_chunks,
-                          uint32_t n, uint32_t* bad, hipStream_t s);
+                          uint32_t n, uint32_t mlimit, uint32_t* bad, hipStream_t s);
 
-// RLE rows -> dense 4-bit move tables, npad/8 words per row.  Work is cut in
+// RLE rows -> dense 4-bit move tables, npad/8 words per row (narrower
+// tables: into a stage, then launch_repack_moves).  Work is cut in
 // chunks of expand_chunk_runs() runs: chunk_first[row] (nrows + 1 values) =
 // sum over earlier rows of ceil(R / expand_chunk_runs()), total_chunks its
 // last value.  Rows must be well formed (validate_rows).
@@ -194,10 +199,11 @@ void launch_scatter_u8(const uint8_t* in, const uint32_t* perm, uint32_t nq, uin
 // table-search over dense move tables.  qs / qt: query columns, sorted by
 // target row; qrow[q]: the row of query q's target (row_of_col is unused).
 void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
-                               const uint32_t* dense, uint32_t npad, const uint32_t* qs,
-                               const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
-                               int32_t kmoves, uint32_t n, uint64_t* cost, uint32_t* hops,
-                               uint8_t* fin, unsigned long long* agg, hipStream_t s);
+                               const uint32_t* dense, uint32_t npad, uint32_t lb,
+                               const uint32_t* qs, const uint32_t* qt, const uint32_t* qrow,
+                               uint32_t nq, int32_t kmoves, uint32_t n, uint64_t* cost,
+                               uint32_t* hops, uint8_t* fin, unsigned long long* agg,
+                               hipStream_t s);
 
 // adj: packed fixed-stride adjacency, (dst column, weight) pairs, 2^shift
 // slots per column, dst = 0xFFFFFFFF past the out-degree.
@@ -209,7 +215,7 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
 
 // CPD-heuristic search (cpd_kernels.hip "CPD-heuristic search"): one search
 // per query (sorted by target row, qrow as for table-search) over the dense
-// move rows (npad/8 words per row); adj_f / adj_w: packed adjacency with
+// move rows (2^lb bits per column); adj_f / adj_w: packed adjacency with
 // free-flow / selected weights.  The CPD path values come from the per-row
 // tables hrow / crow / lrow (n per row; launch_search_tables) when hrow is
 // non-null, else from CPD walks memoised in the workspace.  cost / plen / fin
@@ -219,7 +225,7 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
 // clock (tick_ns per expansion and per touched edge).
 // Tables for index rows [0, rows) by pointer jumping in chunks of chunk_rows
 // rows; scratch = 48 B x chunk_rows x n; tcol[r] = row r's target column.
-void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* adj_f,
+void launch_search_tables(const uint32_t* dense, uint32_t npad, uint32_t lb, const uint32_t* adj_f,
                           const uint32_t* adj_w, uint32_t shift, const uint32_t* tcol,
                           uint32_t rows, uint32_t n, void* scratch, uint32_t chunk_rows,
                           uint64_t* hrow, uint64_t* crow, uint32_t* lrow, int write_h,
@@ -229,7 +235,7 @@ void launch_search_tables(const uint32_t* dense, uint32_t npad, const uint32_t* 
 uint32_t search_slots(uint32_t nq);
 uint64_t search_ws_bytes_per_slot(uint32_t cap, bool tables);
 void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t shift,
-                       const uint32_t* dense, uint32_t npad, const uint64_t* hrow,
+                       const uint32_t* dense, uint32_t npad, uint32_t lb, const uint64_t* hrow,
                        const uint64_t* crow, const uint32_t* lrow, uint32_t n,
                        const uint32_t* qs, const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
                        double hscale, double fscale, int32_t kmoves, int64_t itrs,

@@ -2,6 +2,8 @@
 what fifo_auto loads a worker's buckets with (make_fifos.py:21 serves every
 CPD the worker owns) — against the CPU oracle, bit-exact, plus its error
 behaviour on malformed, incomplete or mismatched input."""
+import os
+
 import numpy as np
 import pytest
 
@@ -134,6 +136,13 @@ def test_move_naming_no_edge_stops_walk(env, mode):
     r = runs[: int(off[1])].copy()
     r = (r & ~np.uint32(0xF)) | np.uint32(15)   # every move = 15: no such edge
     ix = cpd.Index.streamed(dev, targets[:1], len(r), mode=mode)
+    if mode == "dense" and dev.move_bits() < 4 and os.environ.get("CPD_TABLE_BITS") != "4":
+        # this graph's tables hold 1- or 2-bit moves: such a row is refused,
+        # never truncated into a move that names a real edge
+        with pytest.raises(cpd.CpdError) as ei:
+            ix.append(np.array([0, len(r)], np.uint64), r)
+        assert ei.value.code == cpd.CPD_E_ARG and "moves <" in str(ei.value)
+        return
     ix.append(np.array([0, len(r)], np.uint64), r)
     s = np.where(deg > 0)[0][:50].astype(np.uint32)
     s = s[s != targets[0]]
@@ -173,3 +182,32 @@ def test_crafted_row_lengths(env, mode):
     np.testing.assert_array_equal(cost, rc)
     np.testing.assert_array_equal(hops, rh)
     np.testing.assert_array_equal(fin, rf)
+
+
+@pytest.mark.parametrize("mode", ["dense", "rle"])
+def test_compact_rows_wider_than_tables(env, mode):
+    """4-bit compact rows into an index whose tables are narrower (the graph's
+    out-degree <= 4): valid rows are repacked bit-exact; a row carrying a move
+    the tables cannot hold is refused (never truncated)."""
+    g, plan, dev, targets, off, runs = env[:6]
+    if dev.move_bits() == 4 or os.environ.get("CPD_TABLE_BITS") == "4":
+        pytest.skip("this graph's tables are 4-bit")
+    k = 5
+    mv4 = oracle.moves_from_runs(off[:k + 1], runs, g.n, 4)
+    ix = cpd.Index.streamed(dev, targets[:k], int(off[k]), mode=mode)
+    ix.append_moves(mv4, 4)
+    rng = np.random.default_rng(3)
+    s = rng.integers(0, g.n, 2000).astype(np.uint32)
+    t = targets[:k][rng.integers(0, k, 2000)]
+    rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, plan.order(), targets[:k],
+                                     off[:k + 1], runs[: int(off[k])], s, t)
+    c, h, f, _ = ix.query(s, t)
+    np.testing.assert_array_equal(c, rc)
+    np.testing.assert_array_equal(h, rh)
+    np.testing.assert_array_equal(f, rf)
+    bad = mv4.copy()
+    bad[0, 0] |= np.uint32(0xF)  # column 0 of row 0: move 15
+    ix2 = cpd.Index.streamed(dev, targets[:k], int(off[k]) + 2, mode=mode)
+    with pytest.raises(cpd.CpdError) as ei:
+        ix2.append_moves(bad, 4)
+    assert ei.value.code == cpd.CPD_E_ARG

@@ -17,6 +17,8 @@ oracle, walk queries over them dense and RLE.  What each reaches:
   CPD_LEAFFM=0    leaf first-move sets recomputed by first_moves
   CPD_OVERLAP=0   each batch's up-sweep after the previous batch's first moves
   CPD_MOVES_SWAR=0  rle_moves<4> (per-column move-table emit) instead of rle_moves4
+  CPD_TABLE_BITS=4  4-bit move tables whatever the degree (the rows' export
+                    and the index then repack to / from the packed width)
 """
 import json
 import os
@@ -49,6 +51,9 @@ for name in ("synth", "deg8"):
     off, runs = rows.export()
     ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
     ok = bool(np.array_equal(off, ref_off) and np.array_equal(runs, ref_runs))
+    bits = rows.move_bits()
+    mv = rows.export_moves(0, 300)
+    ok = ok and bool(np.array_equal(mv, oracle.moves_from_runs(ref_off[:301], ref_runs, g.n, bits)))
     s = rng.integers(0, g.n, 3000).astype(np.uint32)
     t = targets[rng.integers(0, len(targets), 3000)]
     rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, plan.order(), targets, ref_off,
@@ -63,14 +68,15 @@ print(json.dumps(out))
 """
 
 SWITCHES = ["CPD_LIVE", "CPD_SORT", "CPD_LANE_KEY", "CPD_XCD", "CPD_FM_N4", "CPD_ASYNC",
-            "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP", "CPD_MOVES_SWAR"]
+            "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP", "CPD_MOVES_SWAR", "CPD_TABLE_BITS"]
+OFF = {"CPD_TABLE_BITS": "4"}
 
 
 @pytest.mark.parametrize("switch", SWITCHES)
 def test_switch_off_bit_exact(switch):
     code = CHILD % (HERE, os.path.join(ROOT, "distributed-oracle-search_amd"),
                     os.path.join(ROOT, "oracle"))
-    env = dict(os.environ, **{switch: "0"})
+    env = dict(os.environ, **{switch: OFF.get(switch, "0")})
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
