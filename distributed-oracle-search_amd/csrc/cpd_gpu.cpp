@@ -1490,7 +1490,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         HIP_CHECK(hipStreamWaitEvent(es, g->ev_up, 0));
     // the batch's rows become table rows r->nrows + i, written by lane pos_of[i]
     const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
-    CPD_REQUIRE(r->moves.n >= (size_t)(r->nrows + k) * g->wpr(), CPD_E_ARG,
+    CPD_REQUIRE(r->moves.n >= (size_t)(r->nrows + k) * r->wpr, CPD_E_ARG,
                 "rows: move table capacity");
     cpd_rows::Batch* rb = r->new_batch(g->B);
     rb->k = k;
@@ -1524,9 +1524,9 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     // per row: the sets (fm_row), the segment states (4 B per 32 columns;
     // the run counts are read only where the look-ahead needs them), the
     // table (npad * bits / 8)
-    const double ebytes = (fm_row + 4.0 * npad / 32.0 + 4.0 * g->wpr()) * k + 4.0 * k;
+    const double ebytes = (fm_row + 4.0 * npad / 32.0 + 4.0 * r->wpr) * k + 4.0 * k;
     g->timed("rle_moves", ebytes, [&] {
-        launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, g->tlb, r->moves.p, es);
+        launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, r->tlb, r->moves.p, es);
     });
     if (!r->done) HIP_CHECK(hipEventCreateWithFlags(&r->done, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(r->done, es));
@@ -1568,9 +1568,12 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         r->lanes.clear();
         r->offsets.assign(1, 0);
         r->n = g->n;
-        r->wpr = g->wpr();
+        // built rows stay nibble tables: the emit narrowing its stores cost
+        // ~0.5 ms per 24576-row step (rle_moves 7.9 against 7.4 ms, the step
+        // 68.2 against 67.2); the export and an index narrow them instead
+        r->tlb = 2u;
+        r->wpr = g->npad / 8u;
         r->bits = g->move_bits;
-        r->tlb = g->tlb;
         if (r->moves.n < (size_t)ntargets * r->wpr) {
             r->wait();  // an earlier build's emit may still write the old table
             r->moves.alloc((size_t)ntargets * r->wpr);
@@ -2012,18 +2015,27 @@ void append_built(cpd_index* ix, const cpd_rows* r) {
                     "index: built row " + std::to_string(i) + " (target " +
                         std::to_string(r->targets[i]) + ") is not the declared row " +
                         std::to_string(ix->added + i));
-    CPD_REQUIRE(r->wpr == g->wpr(), CPD_E_ARG, "index: rows built for another graph");
+    CPD_REQUIRE(r->n == g->n && r->wpr == (g->npad >> (5u - r->tlb)), CPD_E_ARG,
+                "index: rows built for another graph");
     const size_t wpr = g->wpr();
-    if (ix->dense.p && (ix->stream_dense || !ix->keep_rle || ix->dense_ready))
-        HIP_CHECK(hipMemcpyAsync(ix->dense.p + (size_t)ix->added * wpr, r->moves.p,
-                                 (size_t)r->nrows * wpr * sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                                 g->stream));
+    if (ix->dense.p && (ix->stream_dense || !ix->keep_rle || ix->dense_ready)) {
+        if (r->tlb == g->tlb)
+            HIP_CHECK(hipMemcpyAsync(ix->dense.p + (size_t)ix->added * wpr, r->moves.p,
+                                     (size_t)r->nrows * wpr * sizeof(uint32_t),
+                                     hipMemcpyDeviceToDevice, g->stream));
+        else  // the rows' nibble tables narrowed to the index's width
+            g->timed("repack_moves", 4.0 * ((double)r->wpr + (double)wpr) * r->nrows, [&] {
+                launch_repack_moves(r->moves.p, r->wpr, r->wpr, 1u << r->tlb, r->nrows,
+                                    ix->dense.p + (size_t)ix->added * wpr, (uint32_t)wpr,
+                                    (uint32_t)wpr, 1u << g->tlb, g->stream);
+            });
+    }
     if (ix->keep_rle) {
         CPD_REQUIRE(ix->total + r->total <= ix->cap, CPD_E_ARG,
                     "index: more runs than the index was created for");
         std::vector<uint64_t> o(r->nrows + 1);
         for (uint32_t i = 0; i <= r->nrows; ++i) o[i] = ix->total + r->offsets[i];
-        g->timed("moves_runs", 4.0 * (double)g->wpr() * r->nrows + 4.0 * (double)r->total, [&] {
+        g->timed("moves_runs", 4.0 * (double)r->wpr * r->nrows + 4.0 * (double)r->total, [&] {
             launch_moves_runs(r->moves.p, r->wpr, r->tlb, r->n, r->nrows, r->off.p, 0,
                               ix->runs.p + ix->total, g->stream);
         });

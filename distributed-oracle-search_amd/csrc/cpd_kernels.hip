@@ -1651,6 +1651,24 @@ __global__ __launch_bounds__(256) void repack_moves(const uint32_t* __restrict__
     const uint32_t r = (uint32_t)(i / d_words), w = (uint32_t)(i % d_words);
     const uint32_t per = 32u / d_bits;  // columns per output word
     const uint32_t* __restrict__ in = src + (size_t)r * s_stride;
+    auto at = [&](uint32_t k) { return k < s_words ? in[k] : 0u; };
+    if (s_bits == 4u && d_bits == 2u && !lost) {  // nibble tables -> 2 bits (export, index)
+        dst[(size_t)r * d_stride + w] = nib_to2(at(2u * w)) | (nib_to2(at(2u * w + 1u)) << 16);
+        return;
+    }
+    if (s_bits == 4u && d_bits == 1u && !lost) {
+        dst[(size_t)r * d_stride + w] = nib_to1(at(4u * w)) | (nib_to1(at(4u * w + 1u)) << 8) |
+                                        (nib_to1(at(4u * w + 2u)) << 16) | (nib_to1(at(4u * w + 3u)) << 24);
+        return;
+    }
+    if (s_bits == 2u && d_bits == 4u) {  // 2-bit rows -> nibble tables
+        dst[(size_t)r * d_stride + w] = nib_from2(at(w >> 1) >> (16u * (w & 1u)));
+        return;
+    }
+    if (s_bits == 1u && d_bits == 4u) {
+        dst[(size_t)r * d_stride + w] = nib_from1(at(w >> 2) >> (8u * (w & 3u)));
+        return;
+    }
     const uint32_t smask = (1u << s_bits) - 1u, dmask = (1u << d_bits) - 1u;
     uint32_t o = 0, wide = 0;
     for (uint32_t k = 0; k < per; ++k) {
