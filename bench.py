@@ -209,19 +209,20 @@ class Comm:
     """Barrier / reductions over torch.distributed.  Only the bench harness
     uses them (timing and a handful of counters); nothing on the data path."""
 
-    def __init__(self, world, rank, local, device=None):
+    def __init__(self, world, rank, local, device=None, pg=None):
         self.world, self.rank, self.local, self.device = world, rank, local, device
+        self.pg = world > 1 if pg is None else pg  # collectives through the process group
 
     def barrier(self):
         import torch
         if self.device is not None:
             torch.cuda.synchronize()
-        if self.world > 1:
+        if self.pg:
             import torch.distributed as dist
             dist.barrier()
 
     def reduce(self, vals, op):
-        if self.world == 1:
+        if not self.pg:
             return list(vals)
         import torch
         import torch.distributed as dist
@@ -825,13 +826,16 @@ def main():
     gpu = 0 if share else local
     if share and args.batch == 0:  # ranks sized from one card's free HBM would overcommit it
         args.batch = 4096
-    if world > 1:
+    # CPD_BENCH_PG=1: the process group (RCCL) even at one rank, so the N>1
+    # collectives' code path runs on a 1-GPU box too
+    use_pg = world > 1 or os.environ.get("CPD_BENCH_PG") == "1"
+    if use_pg:
         if share:
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    comm = Comm(world, rank, local, device=None if share else f"cuda:{local}")
+    comm = Comm(world, rank, local, device=None if share else f"cuda:{local}", pg=use_pg)
     comm.barrier()
     while not os.path.exists(ppath):  # another local rank is still saving it
         time.sleep(0.5)
@@ -1171,7 +1175,7 @@ def main():
                                    "copied out")
         out.update(extra)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 
