@@ -231,6 +231,17 @@ class Comm:
         return t.tolist()
 
 
+# The result line's file descriptor: stdout, or (with RCCL) a copy of it —
+# RCCL prints its version banner on fd 1 when a communicator starts, so fd 1
+# is pointed at stderr first and the one JSON line goes to the real stdout.
+_RESULT_FD = None
+
+
+def emit_line(line):
+    sys.stdout.flush()
+    os.write(_RESULT_FD if _RESULT_FD is not None else 1, (line + "\n").encode())
+
+
 class FileComm:
     """Barrier / reductions through small files in a directory the node's
     ranks share — for --full-build-only, whose ranks then load neither torch
@@ -829,6 +840,11 @@ def main():
     # CPD_BENCH_PG=1: the process group (RCCL) even at one rank, so the N>1
     # collectives' code path runs on a 1-GPU box too
     use_pg = world > 1 or os.environ.get("CPD_BENCH_PG") == "1"
+    if use_pg and not share:
+        global _RESULT_FD
+        sys.stdout.flush()
+        _RESULT_FD = os.dup(1)
+        os.dup2(2, 1)
     if use_pg:
         if share:
             dist.init_process_group("gloo")
@@ -1174,7 +1190,7 @@ def main():
                                    "and gather on the GPU, walk, results scattered back and "
                                    "copied out")
         out.update(extra)
-        print(json.dumps(out), flush=True)
+        emit_line(json.dumps(out))
     if use_pg:
         dist.destroy_process_group()
 
