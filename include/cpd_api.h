@@ -306,9 +306,11 @@ int  cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out);
  * at creation: DENSE (or AUTO resolving to it: 4 * total_runs > n/2 * nrows)
  * expands each chunk into the 4-bit move tables as it arrives and keeps no
  * runs, so HBM holds nrows * n/2 bytes however large the runs are; RLE keeps
- * the runs (total_runs of capacity).  Appended host rows are format-checked
- * on the GPU (first run at column 0, columns increasing and < n), CPD_E_ARG
- * otherwise.                                                                 */
+ * the runs (total_runs of capacity).  Dense tables hold a move per column
+ * at the graph's packed width (cpd_graph_move_bits: 1, 2 or 4 bits; nrows *
+ * npad * bits / 8 bytes).  Appended host rows are format-checked on the GPU
+ * (first run at column 0, columns increasing and < n; for tables narrower
+ * than 4 bits also every move < 2^bits), CPD_E_ARG otherwise.                */
 int  cpd_index_create_empty(cpd_graph* g, const uint32_t* row_targets, uint32_t nrows,
                             int mode, uint64_t total_runs, cpd_index** out);
 /* offsets: count + 1 values relative to the chunk (offsets[0] = 0). */
@@ -316,11 +318,12 @@ int  cpd_index_append_rows(cpd_index* ix, uint32_t count, const uint64_t* offset
                            const uint32_t* runs);
 int  cpd_index_append_built_rows(cpd_index* ix, const cpd_rows* r);
 /* Rows in the compact form (cpd_rows_export_moves layout: count rows of
- * ceil(n * bits / 32) words, bits = 1, 2 or 4): unpacked on the GPU into a
- * DENSE index's 4-bit tables, or decoded into run words for an RLE index
- * (total_runs of the create call must cover them).  No format check is
- * needed: a move naming no out-edge of its column stops a walk there,
- * unfinished, as the oracle's walk does.                                    */
+ * ceil(n * bits / 32) words, bits = 1, 2 or 4): copied into a DENSE index's
+ * tables when bits is the graph's packed width, else repacked on the GPU
+ * (wider rows must carry moves that fit: CPD_E_ARG otherwise), or decoded
+ * into run words for an RLE index (total_runs of the create call must cover
+ * them).  No other check is needed: a move naming no out-edge of its column
+ * stops a walk there, unfinished, as the oracle's walk does.               */
 int  cpd_index_append_moves(cpd_index* ix, uint32_t count, uint32_t bits, const uint32_t* moves);
 /* Rows declared / appended, runs resident in HBM, bytes of dense tables.     */
 int  cpd_index_info(const cpd_index* ix, uint32_t* nrows, uint32_t* added,
