@@ -208,3 +208,50 @@ def test_generic_emit_matches_greedy():
             mv = greedy_moves_w(fm, ALL)
             st, rc = states_w(fm, ALL)
             assert moves_generic(fm, st, rc, KT=[1, 16][i % 2]) == mv
+
+
+# The table-width conversions of cpd_kernels.hip (nib_to2 / nib_to1 /
+# nib_from2 / nib_from1, store_cols32 / load_cols32), restated bit for bit.
+M32 = 0xFFFFFFFF
+
+
+def nib_to2(x):
+    x &= 0x33333333
+    x = (x | (x >> 2)) & 0x0F0F0F0F
+    x = (x | (x >> 4)) & 0x00FF00FF
+    return (x | (x >> 8)) & 0x0000FFFF
+
+
+def nib_to1(x):
+    x &= 0x11111111
+    x = (x | (x >> 3)) & 0x03030303
+    x = (x | (x >> 6)) & 0x000F000F
+    return (x | (x >> 12)) & 0x000000FF
+
+
+def nib_from2(y):
+    y &= 0xFFFF
+    y = (y | (y << 8)) & 0x00FF00FF
+    y = (y | (y << 4)) & 0x0F0F0F0F
+    return (y | (y << 2)) & 0x33333333
+
+
+def nib_from1(y):
+    y &= 0xFF
+    y = (y | (y << 12)) & 0x000F000F
+    y = (y | (y << 6)) & 0x03030303
+    return (y | (y << 3)) & 0x11111111
+
+
+def test_table_width_conversions():
+    """8 moves in nibbles <-> 2-bit / 1-bit fields: column k of the nibble
+    word lands in field k of the narrow value and back, for every move
+    pattern that fits (exhaustive for 1 bit, random for 2)."""
+    rnd = random.Random(5)
+    for bits, to, frm, cases in ((2, nib_to2, nib_from2, [rnd.getrandbits(16) for _ in range(4000)]),
+                                 (1, nib_to1, nib_from1, range(256))):
+        for narrow in cases:
+            mv = [(narrow >> (bits * k)) & ((1 << bits) - 1) for k in range(8)]
+            nib = sum(m << (4 * k) for k, m in enumerate(mv))
+            assert to(nib) == narrow, (bits, mv)
+            assert frm(narrow) == nib, (bits, mv)
