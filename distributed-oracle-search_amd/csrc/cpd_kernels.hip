@@ -2596,11 +2596,17 @@ __device__ __forceinline__ uint32_t hprobe(const uint4* __restrict__ ent, uint32
     }
 }
 
+// The search heap: 4-ary (children of i at 4i+1 .. 4i+4), so a pop
+// descends log4 of the size in levels whose four child loads go out
+// together — half the dependent round trips of a binary heap.  The keys
+// (f, column, g) are a total order over the entries a search can hold (a
+// column is pushed again only with a strictly smaller g), so the pop
+// sequence — and every counter — is the oracle's binary heap's.
 __device__ __forceinline__ void heap_push(uint4* __restrict__ he, uint32_t* __restrict__ hc,
                                           uint32_t& size, uint64_t f, uint32_t c, uint64_t g) {
     uint32_t i = size++;
     while (i) {
-        const uint32_t p = (i - 1u) >> 1;
+        const uint32_t p = (i - 1u) >> 2;
         const uint4 pe = he[p];
         const uint32_t pc = hc[p];
         if (!hkey_less(f, c, g, u64of(pe.x, pe.y), pc, u64of(pe.z, pe.w))) break;
@@ -2625,24 +2631,33 @@ __device__ __forceinline__ void heap_pop(uint4* __restrict__ he, uint32_t* __res
     const uint64_t lf = u64of(le.x, le.y), lg = u64of(le.z, le.w);
     uint32_t i = 0;
     for (;;) {
-        uint32_t k = 2u * i + 1u;
-        if (k >= size) break;
-        uint4 ke = he[k];
-        uint32_t kc = hc[k];
-        if (k + 1u < size) {
-            const uint4 k2 = he[k + 1u];
-            const uint32_t c2 = hc[k + 1u];
-            if (hkey_less(u64of(k2.x, k2.y), c2, u64of(k2.z, k2.w), u64of(ke.x, ke.y), kc,
-                          u64of(ke.z, ke.w))) {
-                ++k;
-                ke = k2;
-                kc = c2;
+        const uint32_t k0 = 4u * i + 1u;
+        if (k0 >= size) break;
+        const uint32_t nk = min(4u, size - k0);
+        uint4 e[4];
+        uint32_t ec[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4u; ++j) {  // the live children, loaded together
+            if (j < nk) {
+                e[j] = he[k0 + j];
+                ec[j] = hc[k0 + j];
             }
         }
-        if (!hkey_less(u64of(ke.x, ke.y), kc, u64of(ke.z, ke.w), lf, lc, lg)) break;
-        he[i] = ke;
-        hc[i] = kc;
-        i = k;
+        uint4 be = e[0];
+        uint32_t bc = ec[0], bk = k0;
+#pragma unroll
+        for (uint32_t j = 1; j < 4u; ++j) {
+            if (j < nk && hkey_less(u64of(e[j].x, e[j].y), ec[j], u64of(e[j].z, e[j].w),
+                                    u64of(be.x, be.y), bc, u64of(be.z, be.w))) {
+                be = e[j];
+                bc = ec[j];
+                bk = k0 + j;
+            }
+        }
+        if (!hkey_less(u64of(be.x, be.y), bc, u64of(be.z, be.w), lf, lc, lg)) break;
+        he[i] = be;
+        hc[i] = bc;
+        i = bk;
     }
     he[i] = le;
     hc[i] = lc;
