@@ -13,6 +13,7 @@
 #include <cstring>
 #include <fstream>
 #include <memory>
+#include <thread>
 
 #include "cpd_internal.hpp"
 
@@ -576,24 +577,45 @@ MoveBucket read_move_bucket_head(const std::string& path) {
 }
 
 void read_move_bucket_rows(const std::string& path, const MoveBucket& head, uint32_t first,
-                           uint32_t count, uint32_t* out) {
+                           uint32_t count, uint32_t* out, int threads) {
     if ((uint64_t)first + count > head.targets.size()) throw Error(CPD_E_ARG, path + ": rows out of range");
     const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
     if (fd < 0) throw Error(CPD_E_IO, "cannot open " + path);
-    uint64_t pos = head.rows_offset() + 4ull * head.words * first;
-    char* c = reinterpret_cast<char*>(out);
-    uint64_t left = 4ull * head.words * count;
-    while (left) {
-        const ssize_t k = ::pread(fd, c, std::min<uint64_t>(left, 1ull << 30), (off_t)pos);
-        if (k <= 0) {
-            ::close(fd);
-            throw Error(CPD_E_IO, path + ": truncated rows");
+    const uint64_t pos0 = head.rows_offset() + 4ull * head.words * first;
+    const uint64_t total = 4ull * head.words * count;
+    auto span = [&](uint64_t a, uint64_t b) {  // bytes [a, b) of the rows read
+        char* c = reinterpret_cast<char*>(out) + a;
+        uint64_t pos = pos0 + a, left = b - a;
+        while (left) {
+            const ssize_t k = ::pread(fd, c, std::min<uint64_t>(left, 1ull << 30), (off_t)pos);
+            if (k <= 0) return false;
+            c += k;
+            pos += (uint64_t)k;
+            left -= (uint64_t)k;
         }
-        c += k;
-        pos += (uint64_t)k;
-        left -= (uint64_t)k;
+        return true;
+    };
+    // a read from the page cache is a copy one thread does at ~10 GB/s:
+    // large pieces are split over threads (>= 16 MB each)
+    const uint64_t parts = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, threads),
+                                                                     total >> 24));
+    bool ok = true;
+    if (parts == 1) {
+        ok = span(0, total);
+    } else {
+        std::vector<std::thread> th;
+        std::vector<char> good(parts, 1);
+        const uint64_t step = (total / parts + 4095) / 4096 * 4096;
+        for (uint64_t p = 0; p < parts; ++p) {
+            const uint64_t a = std::min(total, p * step), b = std::min(total, a + step);
+            if (p + 1 == parts) th.emplace_back([&, p, a] { good[p] = span(a, total); });
+            else th.emplace_back([&, p, a, b] { good[p] = span(a, b); });
+        }
+        for (auto& t : th) t.join();
+        for (char g : good) ok = ok && g;
     }
     ::close(fd);
+    if (!ok) throw Error(CPD_E_IO, path + ": truncated rows");
 }
 
 void write_order(const std::string& path, uint64_t fp, const std::vector<uint32_t>& order) {

@@ -140,7 +140,7 @@ private:
 // rows [first, first + count) then read by position.
 MoveBucket read_move_bucket_head(const std::string& path);
 void read_move_bucket_rows(const std::string& path, const MoveBucket& head, uint32_t first,
-                           uint32_t count, uint32_t* out);
+                           uint32_t count, uint32_t* out, int threads = 1);
 
 void write_order(const std::string& path, uint64_t fingerprint, const std::vector<uint32_t>& order);
 std::vector<uint32_t> read_order(const std::string& path, uint64_t fingerprint);

@@ -4,11 +4,12 @@
 //   fifo_auto --input X.xy DIFF --partmethod {div|mod} --partkey K
 //             --workerid I --maxworker W --outdir D --alg {table-search|cpd-search}
 //             [--partition M] [--device G] [--fifo PATH] [--once]
-//             [--index auto|rle|dense]
+//             [--index auto|rle|dense] [--read-threads T]
 //
 // Creates its request FIFO, streams the CPD buckets this worker owns onto its
-// GPU (as 4-bit move tables when they are smaller than the runs, the runs
-// then never held whole in HBM or host memory), then serves requests on
+// GPU (as move tables at the graph's packed width when they are smaller
+// than the runs, the runs then never held whole in HBM or host memory;
+// compact-file pieces read by T threads, default 8), then serves requests on
 // /tmp/worker{I}.fifo (process_query.py:86).  A request is what
 // process_query.send_remote pipes in (process_query.py:66-79,89):
 //     {worker JSON config}\n<query file> <answer fifo> <diff file>\n
@@ -234,6 +235,7 @@ int main(int argc, char** argv) {
         // reader thread while the previous piece is appended (uploaded)
         uint32_t* pin[2] = {nullptr, nullptr};
         uint64_t pin_bytes = 0;
+        const int read_threads = (int)a.num("read-threads", 8);
         for (size_t k = 0; k < paths.size(); ++k) {
             if (formats[k] == 2) {
                 const auto& mh = mheads[k];
@@ -250,7 +252,8 @@ int main(int argc, char** argv) {
                     pin_bytes = 4ull * mh.words * per;
                 }
                 auto read = [&, k, per, nr](uint32_t r0, int slot) {
-                    cpd::io::read_move_bucket_rows(paths[k], mheads[k], r0, std::min(per, nr - r0), pin[slot]);
+                    cpd::io::read_move_bucket_rows(paths[k], mheads[k], r0, std::min(per, nr - r0), pin[slot],
+                                                   read_threads);
                 };
                 std::future<void> rd = std::async(std::launch::async, read, 0u, 0);
                 for (uint32_t r0 = 0, i = 0; r0 < nr; r0 += per, ++i) {
