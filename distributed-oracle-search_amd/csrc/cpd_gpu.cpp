@@ -292,11 +292,6 @@ struct cpd_graph {
     // it runs beside that batch's first moves and RLE count.  prep: the slot
     // and targets it was launched for, ev_up its end.
     hipStream_t ustream = nullptr;
-    // CU partition (CPD_UP_CUS = U > 0): ustream runs on U CUs of its own,
-    // the first moves (fstream) and the emit (estream) on the others, the
-    // down-sweep on all of them; else fstream = stream
-    hipStream_t fstream = nullptr;
-    bool split = false;
     hipEvent_t ev_up = nullptr, ev_down = nullptr, ev_fm = nullptr;
     bool prepped = false;
     uint32_t prep_slot = 0;
@@ -331,10 +326,6 @@ struct cpd_graph {
             for (auto e : {ev_up, ev_down, ev_fm})
                 if (e) (void)hipEventDestroy(e);
             if (ustream) (void)hipStreamDestroy(ustream);
-            if (split && fstream) {
-                (void)hipStreamSynchronize(fstream);
-                (void)hipStreamDestroy(fstream);
-            }
             if (stream) (void)hipStreamSynchronize(stream);
             for (auto& p : pending) {
                 (void)hipEventDestroy(p.a);
@@ -417,7 +408,6 @@ struct cpd_graph {
     // intervals that have completed into agg; intervals of an emit still
     // running on estream stay pending until a later sync.
     void sync(bool all = false) {
-        if (split) HIP_CHECK(hipStreamSynchronize(fstream));
         HIP_CHECK(hipStreamSynchronize(stream));
         if (all) {
             drain_emits();
@@ -701,11 +691,6 @@ bool env_on(const char* name) {
     return !(e && *e == '0');
 }
 
-uint32_t env_u32_host(const char* name, uint32_t dflt) {
-    const char* e = std::getenv(name);
-    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
-}
-
 // One non-blocking stream per (host thread, device), kept for the thread's
 // lifetime: exports from several host threads never queue behind a build's
 // stream or each other.
@@ -914,29 +899,6 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             HIP_CHECK(hipStreamCreateWithPriority(&g->ustream, hipStreamNonBlocking,
                                                   up_priority_on() ? greatest : least));
-        }
-        g->fstream = g->stream;
-        if (const uint32_t ucu = env_u32_host("CPD_UP_CUS", 0)) {
-            hipDeviceProp_t prop{};
-            HIP_CHECK(hipGetDeviceProperties(&prop, device));
-            const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
-            if (ucu < ncu) {
-                // the up-sweep's CUs spread over the mask (every ncu / U-th)
-                const uint32_t words = (ncu + 31u) / 32u, stride = ncu / ucu;
-                std::vector<uint32_t> um(words, 0u), om(words, 0u);
-                uint32_t taken = 0;
-                for (uint32_t c = 0; c < ncu; ++c) {
-                    const bool mine = c % stride == 0 && taken < ucu;
-                    taken += mine ? 1u : 0u;
-                    (mine ? um : om)[c / 32u] |= 1u << (c % 32u);
-                }
-                HIP_CHECK(hipStreamDestroy(g->ustream));
-                HIP_CHECK(hipStreamDestroy(g->estream));
-                HIP_CHECK(hipExtStreamCreateWithCUMask(&g->ustream, words, um.data()));
-                HIP_CHECK(hipExtStreamCreateWithCUMask(&g->fstream, words, om.data()));
-                HIP_CHECK(hipExtStreamCreateWithCUMask(&g->estream, words, om.data()));
-                g->split = true;
-            }
         }
         for (hipEvent_t* e : {&g->ev_up, &g->ev_down, &g->ev_fm})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -1357,17 +1319,15 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
         (own + drow * (g->m - ml) + 0.5 * nl + g->fmb / 8.0 * g->npad) *
             (fslabs * 1024.0) +
         8.0 * (double)(n - nl) * (double)(1u << g->adj_shift) * fslabs + 4.0 * g->npad / 32.0;
-    hipStream_t fs = g->fstream;  // = stream unless the CUs are partitioned
-    if (fs != g->stream) HIP_CHECK(hipStreamWaitEvent(fs, g->ev_down, 0));
     g->timed("first_moves", fbytes, [&] {
         launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, S.tgt.p, B, k, n, g->npad,
                            fm, g->leaf_fm ? g->leafbits.p : nullptr,
-                           g->leaf_fm ? g->fmleaf.p : nullptr, nr, fs);
+                           g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream);
     });
-    HIP_CHECK(hipEventRecord(g->ev_fm, fs));
+    HIP_CHECK(hipEventRecord(g->ev_fm, g->stream));
     if (stat)
         HIP_CHECK(hipMemcpyAsync(S.stat_h.p, stat, S.stat.n * sizeof(unsigned int),
-                                 hipMemcpyDeviceToHost, fs));
+                                 hipMemcpyDeviceToHost, g->stream));
 }
 
 // Upload a batch's targets as columns into `slot`, on stream st.  With
@@ -1463,9 +1423,6 @@ bool trace_on() {
 void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
                  const uint32_t* next, uint32_t next_k) {
     const double t0 = now_seconds();
-    // partitioned CUs: the previous batch's first moves (fstream) read the
-    // rows this batch's sweeps rewrite
-    if (g->split) HIP_CHECK(hipStreamWaitEvent(g->stream, g->ev_fm, 0));
     const uint32_t x = g->acquire_set();
     uint32_t* fm = g->fmx[x].p;
     uint32_t* rst = g->rle_stx[x].p;
