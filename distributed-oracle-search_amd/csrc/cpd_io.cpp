@@ -2,14 +2,11 @@
 #include "cpd_io.hpp"
 
 #include <fcntl.h>
-#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
-#include <cerrno>
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -456,18 +453,8 @@ MoveBucketFile::MoveBucketFile(const std::string& path, const MoveBucket& b)
     if (!(b.bits == 1 || b.bits == 2 || b.bits == 4) ||
         b.words != ((uint64_t)b.n * b.bits + 31u) / 32u)
         throw Error(CPD_E_ARG, "move bucket: words != ceil(n * bits / 32)");
-    const char* mm = std::getenv("CPD_BUCKET_MMAP");
-    const bool use_map = mm && std::strcmp(mm, "1") == 0 && nrows_ > 0;
-    fd_ = ::open(tmp_.c_str(), (use_map ? O_RDWR : O_WRONLY) | O_CREAT | O_TRUNC, 0644);
+    fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (fd_ < 0) throw Error(CPD_E_IO, "cannot write " + tmp_);
-    if (use_map) {
-        map_bytes_ = 4ull * words_ * nrows_;
-        if (::ftruncate(fd_, (off_t)(rows_off_ + map_bytes_)) != 0)
-            throw Error(CPD_E_IO, "cannot size " + tmp_);
-        void* m = ::mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, (off_t)rows_off_);
-        if (m == MAP_FAILED) throw Error(CPD_E_IO, "cannot map " + tmp_);
-        map_ = static_cast<char*>(m);
-    }
     std::vector<char> h(rows_off_, 0);  // header, targets, zero counts, pad
     std::memcpy(h.data(), kMoveBucketMagic, 8);
     const uint32_t h32[8] = {b.n, nrows_, b.bid, b.method, b.key, b.maxworker, b.words, b.bits};
@@ -477,13 +464,7 @@ MoveBucketFile::MoveBucketFile(const std::string& path, const MoveBucket& b)
     pwrite_all(h.data(), h.size(), 0);
 }
 
-void MoveBucketFile::unmap() {
-    if (map_) ::munmap(map_, map_bytes_);
-    map_ = nullptr;
-}
-
 MoveBucketFile::~MoveBucketFile() {
-    unmap();
     if (fd_ >= 0) {
         ::close(fd_);
         ::unlink(tmp_.c_str());
@@ -510,24 +491,11 @@ void MoveBucketFile::write_counts(uint32_t first_row, const uint32_t* counts, ui
 void MoveBucketFile::write_rows(uint32_t first_row, const uint32_t* rows, uint32_t count) {
     if (first_row > nrows_ || count > nrows_ - first_row)
         throw Error(CPD_E_ARG, "bucket rows out of range: " + tmp_);
-    const uint64_t at = 4ull * words_ * first_row, bytes = 4ull * words_ * count;
-    if (!map_) {
-        pwrite_all(rows, bytes, rows_off_ + at);
-        return;
-    }
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23
-#endif
-    // populate the piece's pages in one call (page-aligned span), then copy
-    const uint64_t pg = 4096, a0 = at / pg * pg, a1 = std::min<uint64_t>((at + bytes + pg - 1) / pg * pg, map_bytes_);
-    if (::madvise(map_ + a0, a1 - a0, MADV_POPULATE_WRITE) != 0 && errno != EINVAL)
-        throw Error(CPD_E_IO, "cannot write " + tmp_ + " (disk full?)");
-    std::memcpy(map_ + at, rows, bytes);
+    pwrite_all(rows, 4ull * words_ * count, rows_off_ + 4ull * words_ * first_row);
 }
 
 void MoveBucketFile::close(uint64_t total_runs) {
     pwrite_all(&total_runs, 8, 40);
-    unmap();  // the pages stay in the page cache, written back by the kernel
     const int fd = fd_;
     fd_ = -1;
     if (::close(fd) != 0) throw Error(CPD_E_IO, "close failed: " + tmp_);

@@ -124,17 +124,10 @@ public:
 
 private:
     void pwrite_all(const void* p, size_t bytes, uint64_t pos);
-    void unmap();
     std::string path_, tmp_;
     int fd_ = -1;
     uint32_t nrows_ = 0, words_ = 0;
     uint64_t rows_off_ = 0;
-    // CPD_BUCKET_MMAP=1: the rows region mapped shared (file sized up front),
-    // each piece's pages populated with MADV_POPULATE_WRITE (an error, not a
-    // SIGBUS, on a full disk) and copied in — writer threads then proceed in
-    // parallel where pwrites to one file serialise on its inode
-    char* map_ = nullptr;
-    uint64_t map_bytes_ = 0;
 };
 // Header, targets and counts (the file size checked against the header);
 // rows [first, first + count) then read by position.
