@@ -2596,6 +2596,25 @@ __device__ __forceinline__ uint32_t hprobe(const uint4* __restrict__ ent, uint32
     }
 }
 
+// hprobe with the first slot's entry already loaded (e = ent[hash(c)]); the
+// slot found is returned with its entry in e
+__device__ __forceinline__ uint32_t hprobe_from(const uint4* __restrict__ ent, uint32_t mask,
+                                                uint32_t tag, uint32_t c, bool& found, uint4& e) {
+    uint32_t i = (c * 0x9E3779B1u) & mask;
+    for (;;) {
+        if (e.x != tag) {
+            found = false;
+            return i;
+        }
+        if (e.y == c) {
+            found = true;
+            return i;
+        }
+        i = (i + 1u) & mask;
+        e = ent[i];
+    }
+}
+
 // The search heap: 4-ary (children of i at 4i+1 .. 4i+4), so a pop
 // descends log4 of the size in levels whose four child loads go out
 // together — half the dependent round trips of a binary heap.  The keys
@@ -2876,6 +2895,21 @@ __global__ __launch_bounds__(256) void cpd_search(
         uint64_t f, g;
         uint32_t v;
         heap_pop(W.he, W.hc, L.hsize, f, v, g);
+        // what the expansion reads and nothing in it writes — v's out-edges
+        // and, per-row tables, v's incumbent values — is loaded beside v's
+        // hash probe, one round trip for all of it
+        constexpr int ND = SHIFT <= 2 ? (1 << SHIFT) : 1;
+        uint2 ed[ND];
+        if (SHIFT <= 2) {
+#pragma unroll
+            for (int k = 0; k < ND; ++k) ed[k] = adj_w[((size_t)v << SHIFT) + k];
+        }
+        uint64_t cw_t = 0;
+        uint32_t lw_t = 0;
+        if (TABLES) {
+            cw_t = tb.crow[rb + v];
+            lw_t = tb.lrow[rb + v];
+        }
         bool found;
         const uint32_t hi = hprobe(W.ent, W.mask, L.tag, v, found);
         const uint4 ev = W.ent[hi];
@@ -2898,8 +2932,8 @@ __global__ __launch_bounds__(256) void cpd_search(
             uint64_t cw;
             uint32_t lw;
             if (TABLES) {
-                cw = tb.crow[rb + v];
-                lw = tb.lrow[rb + v];
+                cw = cw_t;
+                lw = lw_t;
             } else {
                 const uint4 mv = W.memo[hi];
                 cw = u64of(mv.z, mv.w);
@@ -2913,6 +2947,82 @@ __global__ __launch_bounds__(256) void cpd_search(
                 }
             }
         }
+if (SHIFT <= 2) {
+            // per-row tables: every head's heuristic and first hash slot,
+            // loaded together before the edges are taken in order
+            uint4 e0[ND];
+            uint64_t hr[ND];
+            uint32_t wr[ND];  // slot this expansion wrote for edge k
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                wr[k] = 0xFFFFFFFFu;
+                if (TABLES && ed[k].x != kNoEdge) {
+                    e0[k] = W.ent[(ed[k].x * 0x9E3779B1u) & W.mask];
+                    hr[k] = tb.hrow[rb + ed[k].x];
+                } else if (ed[k].x != kNoEdge) {
+                    e0[k] = W.ent[(ed[k].x * 0x9E3779B1u) & W.mask];
+                }
+            }
+#pragma unroll
+        for (int k = 0; k < ND; ++k) {
+            const uint2 e = ed[k];
+            if (e.x == kNoEdge) break;  // edges are packed first
+            ++L.touched;
+            const uint32_t u = e.x;
+            const uint64_t ng = g + e.y;
+            bool fu;
+            uint4 eu = e0[k];
+            // the first slot again if this expansion wrote it for an earlier
+            // edge (or a memoised walk may have written anything)
+            bool dirty = !TABLES && k > 0;
+#pragma unroll
+            for (int j = 0; j < k; ++j) dirty |= wr[j] == ((u * 0x9E3779B1u) & W.mask);
+            if (dirty) eu = W.ent[(u * 0x9E3779B1u) & W.mask];
+            uint32_t ui = hprobe_from(W.ent, W.mask, L.tag, u, fu, eu);
+            const bool seen = fu && !(eu.z == 0xFFFFFFFFu && eu.w == 0xFFFFFFFFu);
+            if (!seen) {
+                uint64_t hu;
+                if (TABLES) {
+                    hu = hr[k];
+                    if (hu == kInf64) continue;
+                    if (!ws_insert(L, W, ui, u, 0u)) {
+                        L.overflow = L.done = true;
+                        break;
+                    }
+                } else {
+                    if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, u, ui)) {
+                        L.overflow = L.done = true;
+                        break;
+                    }
+                    const uint4 mu = W.memo[ui];
+                    hu = u64of(mu.x, mu.y);
+                    if (hu == kInf64) continue;
+                }
+                if (L.hsize >= C) {
+                    L.overflow = L.done = true;
+                    break;
+                }
+                W.ent[ui].z = (uint32_t)ng;
+                W.ent[ui].w = (uint32_t)(ng >> 32);
+                W.aux[ui].x = dv + 1u;
+                wr[k] = ui;
+                ++L.inserted;
+                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
+            } else if (ng < u64of(eu.z, eu.w)) {
+                if (L.hsize >= C) {
+                    L.overflow = L.done = true;
+                    break;
+                }
+                W.ent[ui].z = (uint32_t)ng;
+                W.ent[ui].w = (uint32_t)(ng >> 32);
+                W.aux[ui].x = dv + 1u;
+                wr[k] = ui;
+                ++L.updated;
+                const uint64_t hu = TABLES ? hr[k] : u64of(W.memo[ui].x, W.memo[ui].y);
+                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
+            }
+        }
+        } else {
 #pragma unroll 1
         for (int k = 0; k < (1 << SHIFT); ++k) {
             const uint2 e = adj_w[((size_t)v << SHIFT) + k];
@@ -2963,6 +3073,7 @@ __global__ __launch_bounds__(256) void cpd_search(
                                            : u64of(W.memo[ui].x, W.memo[ui].y);
                 heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
             }
+        }
         }
     }
     // wave sums, one atomic per wave per counter
