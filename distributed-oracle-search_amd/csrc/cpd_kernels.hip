@@ -3530,7 +3530,10 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     w.hc = reinterpret_cast<uint32_t*>(p);
     const kern::SearchOpt o{hscale, fscale, kmoves, itrs, time_ns, tick_ns};
     const kern::SearchTables tb{hrow, crow, lrow, n};
-    const dim3 grid(waves / 4u), blk(256);  // every wave has a workspace slot
+    // a wave per workgroup: the searches are latency chains, and 256 waves
+    // as 64 four-wave workgroups sat on a quarter of the CUs (their L1s and
+    // address units shared four ways) while the rest idled
+    const dim3 grid(waves), blk(64);  // every wave has a workspace slot
     const uint32_t c2 = (uint32_t)(((uint64_t)nq + waves - 1u) / waves);
     const uint2* af = reinterpret_cast<const uint2*>(adj_f);
     const uint2* aw = reinterpret_cast<const uint2*>(adj_w);
