@@ -2728,19 +2728,41 @@ __device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj
     vslot = i;
     uint32_t sp = 0, x = v, xi = i;
     bool bad = false;
+    // per step, everything that depends only on the column x — its first
+    // hash slot (entry and aux), its move word and its adjacency rows — is
+    // loaded together: one round trip per step when the probe hits at once
+    uint32_t auy = W.aux[xi].y;
     for (;;) {
-        const uint32_t st = W.aux[xi].y >> 30;
+        const uint32_t st = auy >> 30;
         if (st == kWalked) break;
         if (st == kOnWalk) {  // a cycle: no path to t
             bad = true;
             break;
         }
-        W.aux[xi].y = (W.aux[xi].y & 0x3FFFFFFFu) | (kOnWalk << 30);
-        const uint32_t mv = W.tb.move(row, x);
+        W.aux[xi].y = (auy & 0x3FFFFFFFu) | (kOnWalk << 30);
         uint2 ef = make_uint2(kNoEdge, 0u), ew = make_uint2(kNoEdge, 0u);
-        if (!(mv >> SHIFT)) {
-            ef = adj_f[((size_t)x << SHIFT) + mv];
-            ew = adj_w[((size_t)x << SHIFT) + mv];
+        if (SHIFT <= 2) {
+            constexpr int ND = 1 << (SHIFT <= 2 ? SHIFT : 0);
+            uint2 af[ND], aw[ND];
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                af[k] = adj_f[((size_t)x << SHIFT) + k];
+                aw[k] = adj_w[((size_t)x << SHIFT) + k];
+            }
+            const uint32_t mv = W.tb.move(row, x);
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                if (mv == (uint32_t)k) {
+                    ef = af[k];
+                    ew = aw[k];
+                }
+            }
+        } else {
+            const uint32_t mv = W.tb.move(row, x);
+            if (!(mv >> SHIFT)) {
+                ef = adj_f[((size_t)x << SHIFT) + mv];
+                ew = adj_w[((size_t)x << SHIFT) + mv];
+            }
         }
         if (sp >= W.C) return false;
         W.stk[sp++] = make_uint4(xi, ef.y, ew.y, 0u);
@@ -2749,8 +2771,16 @@ __device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj
             break;
         }
         x = ef.x;
-        xi = hprobe(W.ent, W.mask, L.tag, x, found);
-        if (!found && !ws_insert(L, W, xi, x, 0u)) return false;
+        const uint32_t h = (x * 0x9E3779B1u) & W.mask;
+        uint4 e = W.ent[h];
+        const uint2 au = W.aux[h];
+        xi = hprobe_from(W.ent, W.mask, L.tag, x, found, e);
+        if (!found) {
+            if (!ws_insert(L, W, xi, x, 0u)) return false;
+            auy = 0u;  // what ws_insert wrote: not walked
+        } else {
+            auy = xi == h ? au.y : W.aux[xi].y;
+        }
     }
     uint64_t hf = kInf64, cw = kInf64;
     uint32_t lw = 0;
