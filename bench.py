@@ -1027,10 +1027,11 @@ def main():
                                                max(1.0, float(zcnt[:, 0].sum())), 2)}
         # the fscale-0.1 queries with the memoised-walk form (what a
         # worker-sized index, whose tables do not fit, runs)
-        _, _, _, _, wsst = six.search(ss[:4096], st_[:4096], fscale=0.1, tables="walks")
+        wq = 16384  # as many searches as lanes (round 4's first lines: 4096)
+        _, _, _, _, wsst = six.search(ss[:wq], st_[:wq], fscale=0.1, tables="walks")
         search["walks_form"] = {
-            "queries": 4096, "lanes": int(wsst["lanes"]), "fscale": 0.1,
-            "queries_per_s": round(4096 / (wsst["kernel_ms"] / 1e3), 1) if wsst["kernel_ms"]
+            "queries": wq, "lanes": int(wsst["lanes"]), "fscale": 0.1,
+            "queries_per_s": round(wq / (wsst["kernel_ms"] / 1e3), 1) if wsst["kernel_ms"]
             else 0.0}
         search_sample = (six, ss[:2000], st_[:2000], srows, ss, st_, zs, zt)
     # walk kernel vs its roofline: per query 8 (s, t) + 4 (row) + 13 (cost,
