@@ -618,8 +618,8 @@ def full_build(args, xy, world, rank, device, comm, runner=subprocess.run):
     line = next(l for l in p.stdout.splitlines() if l.startswith("make_cpd_auto-json: "))
     rec = json.loads(line.split(": ", 1)[1])
     if write:
-        rec["files_bytes"] = sum(os.path.getsize(os.path.join(outdir, f))
-                                 for f in os.listdir(outdir) if f.endswith(".cpd"))
+        rec["files_bytes"] = sum(os.path.getsize(os.path.join(outdir, f))  # with the part files
+                                 for f in os.listdir(outdir) if ".cpd" in f and not f.endswith(".tmp"))
     return rec
 
 

@@ -73,6 +73,7 @@ uint32_t to_u32(int64_t v, const std::string& what) {
 const char kBucketMagic[8] = {'D', 'O', 'S', 'C', 'P', 'D', '0', '1'};
 const char kOrderMagic[8] = {'D', 'O', 'S', 'O', 'R', 'D', '0', '1'};
 const char kMoveBucketMagic[8] = {'D', 'O', 'S', 'C', 'P', 'D', '0', '2'};
+const char kMoveStripedMagic[8] = {'D', 'O', 'S', 'C', 'P', 'D', '0', '3'};
 
 }  // namespace
 
@@ -433,13 +434,18 @@ int bucket_format(const std::string& path) {
     char magic[8];
     f.read(magic, 8);
     if (f && std::memcmp(magic, kBucketMagic, 8) == 0) return 1;
-    if (f && std::memcmp(magic, kMoveBucketMagic, 8) == 0) return 2;
+    if (f && (std::memcmp(magic, kMoveBucketMagic, 8) == 0 ||
+              std::memcmp(magic, kMoveStripedMagic, 8) == 0))
+        return 2;
     throw Error(CPD_E_IO, path + ": not a CPD bucket file");
 }
 
 // DOSCPD02 layout: magic 8 | 8 x u32 | total u64 | fingerprint u64 (= 56 B) |
-// targets | counts | pad | rows from rows_offset()
+// targets | counts | pad | rows from rows_offset().  DOSCPD03: the same 56 B
+// + stripes u32 + stripe_rows u32 | targets | counts, and the rows in part
+// files {path}.p{j}: unit u (rows [u S, u S + S)) is unit u / K of part u % K.
 static constexpr uint64_t kMoveHeader = 8 + 32 + 8 + 8;
+static constexpr uint64_t kStripedHeader = kMoveHeader + 8;
 static constexpr uint64_t kMoveRowsAlign = 4096;
 
 uint64_t MoveBucket::rows_offset() const {
@@ -447,34 +453,74 @@ uint64_t MoveBucket::rows_offset() const {
     return (end + kMoveRowsAlign - 1) / kMoveRowsAlign * kMoveRowsAlign;
 }
 
-MoveBucketFile::MoveBucketFile(const std::string& path, const MoveBucket& b)
+uint64_t MoveBucket::head_bytes() const { return kStripedHeader + 8ull * targets.size(); }
+
+uint64_t MoveBucket::part_rows(uint32_t j) const {
+    const uint64_t nr = targets.size(), S = stripe_rows, K = stripes;
+    if (!S || !K) return 0;
+    const uint64_t units = (nr + S - 1) / S;
+    uint64_t rows = 0;
+    if (j < units) {
+        const uint64_t mine = (units - 1 - j) / K + 1;  // units j, j + K, ...
+        rows = mine * S;
+        const uint64_t last = j + (mine - 1) * K;         // a short final unit
+        if (last == units - 1) rows -= units * S - nr;
+    }
+    return rows;
+}
+
+std::string move_part_path(const std::string& path, uint32_t j) { return path + ".p" + std::to_string(j); }
+
+MoveBucketFile::MoveBucketFile(const std::string& path, const MoveBucket& b, uint32_t stripes,
+                               uint32_t stripe_rows)
     : path_(path), tmp_(path + ".tmp"), nrows_((uint32_t)b.targets.size()), words_(b.words),
-      rows_off_(b.rows_offset()) {
+      stripes_(std::max(1u, stripes)), stripe_rows_(std::max(1u, stripe_rows)) {
     if (!(b.bits == 1 || b.bits == 2 || b.bits == 4) ||
         b.words != ((uint64_t)b.n * b.bits + 31u) / 32u)
         throw Error(CPD_E_ARG, "move bucket: words != ceil(n * bits / 32)");
+    const bool striped = stripes_ > 1;
+    rows_off_ = striped ? 0 : b.rows_offset();
     fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
     if (fd_ < 0) throw Error(CPD_E_IO, "cannot write " + tmp_);
-    std::vector<char> h(rows_off_, 0);  // header, targets, zero counts, pad
-    std::memcpy(h.data(), kMoveBucketMagic, 8);
+    // header, targets, zero counts (and pad)
+    const uint64_t head = striped ? kStripedHeader + 8ull * nrows_ : b.rows_offset();
+    std::vector<char> h(head, 0);
+    std::memcpy(h.data(), striped ? kMoveStripedMagic : kMoveBucketMagic, 8);
     const uint32_t h32[8] = {b.n, nrows_, b.bid, b.method, b.key, b.maxworker, b.words, b.bits};
     std::memcpy(h.data() + 8, h32, sizeof h32);
     std::memcpy(h.data() + 48, &b.fingerprint, 8);  // total (h + 40) is written by close()
-    std::memcpy(h.data() + kMoveHeader, b.targets.data(), 4ull * nrows_);
-    pwrite_all(h.data(), h.size(), 0);
+    const uint64_t tgt = striped ? kStripedHeader : kMoveHeader;
+    if (striped) {
+        const uint32_t st[2] = {stripes_, stripe_rows_};
+        std::memcpy(h.data() + kMoveHeader, st, sizeof st);
+    }
+    std::memcpy(h.data() + tgt, b.targets.data(), 4ull * nrows_);
+    pwrite_all(fd_, h.data(), h.size(), 0);
+    if (striped)
+        for (uint32_t j = 0; j < stripes_; ++j) {
+            const std::string pt = move_part_path(path_, j) + ".tmp";
+            const int pf = ::open(pt.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+            if (pf < 0) throw Error(CPD_E_IO, "cannot write " + pt);
+            part_fd_.push_back(pf);
+        }
 }
 
 MoveBucketFile::~MoveBucketFile() {
+    for (uint32_t j = 0; j < part_fd_.size(); ++j) {
+        if (part_fd_[j] < 0) continue;
+        ::close(part_fd_[j]);
+        ::unlink((move_part_path(path_, j) + ".tmp").c_str());
+    }
     if (fd_ >= 0) {
         ::close(fd_);
         ::unlink(tmp_.c_str());
     }
 }
 
-void MoveBucketFile::pwrite_all(const void* p, size_t bytes, uint64_t pos) {
+void MoveBucketFile::pwrite_all(int fd, const void* p, size_t bytes, uint64_t pos) {
     const char* c = static_cast<const char*>(p);
     while (bytes > 0) {
-        const ssize_t k = ::pwrite(fd_, c, std::min<size_t>(bytes, size_t(1) << 30), (off_t)pos);
+        const ssize_t k = ::pwrite(fd, c, std::min<size_t>(bytes, size_t(1) << 30), (off_t)pos);
         if (k <= 0) throw Error(CPD_E_IO, "write failed: " + tmp_);
         c += k;
         pos += (uint64_t)k;
@@ -485,21 +531,46 @@ void MoveBucketFile::pwrite_all(const void* p, size_t bytes, uint64_t pos) {
 void MoveBucketFile::write_counts(uint32_t first_row, const uint32_t* counts, uint32_t count) {
     if (first_row > nrows_ || count > nrows_ - first_row)
         throw Error(CPD_E_ARG, "bucket counts out of range: " + tmp_);
-    pwrite_all(counts, 4ull * count, kMoveHeader + 4ull * nrows_ + 4ull * first_row);
+    const uint64_t tgt = stripes_ > 1 ? kStripedHeader : kMoveHeader;
+    pwrite_all(fd_, counts, 4ull * count, tgt + 4ull * nrows_ + 4ull * first_row);
 }
 
 void MoveBucketFile::write_rows(uint32_t first_row, const uint32_t* rows, uint32_t count) {
     if (first_row > nrows_ || count > nrows_ - first_row)
         throw Error(CPD_E_ARG, "bucket rows out of range: " + tmp_);
-    pwrite_all(rows, 4ull * words_ * count, rows_off_ + 4ull * words_ * first_row);
+    const uint64_t rb = 4ull * words_;
+    if (stripes_ == 1) {
+        pwrite_all(fd_, rows, rb * count, rows_off_ + rb * first_row);
+        return;
+    }
+    const uint64_t S = stripe_rows_, K = stripes_;
+    for (uint64_t r = first_row, end = (uint64_t)first_row + count; r < end;) {
+        const uint64_t u = r / S, take = std::min(end - r, (u + 1) * S - r);
+        const uint64_t at = ((u / K) * S + r % S) * rb;
+        pwrite_all(part_fd_[u % K], rows + (r - first_row) * words_, take * rb, at);
+        r += take;
+    }
 }
 
 void MoveBucketFile::close(uint64_t total_runs) {
-    pwrite_all(&total_runs, 8, 40);
+    pwrite_all(fd_, &total_runs, 8, 40);
+    for (uint32_t j = 0; j < part_fd_.size(); ++j) {
+        const int pf = part_fd_[j];
+        part_fd_[j] = -1;
+        const std::string pp = move_part_path(path_, j);
+        if (::close(pf) != 0) throw Error(CPD_E_IO, "close failed: " + pp + ".tmp");
+        if (std::rename((pp + ".tmp").c_str(), pp.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + pp);
+    }
     const int fd = fd_;
     fd_ = -1;
     if (::close(fd) != 0) throw Error(CPD_E_IO, "close failed: " + tmp_);
     if (std::rename(tmp_.c_str(), path_.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path_);
+}
+
+static uint64_t file_size(const std::string& path) {
+    struct stat st {};
+    if (::stat(path.c_str(), &st) != 0) throw Error(CPD_E_IO, "cannot open " + path);
+    return (uint64_t)st.st_size;
 }
 
 MoveBucket read_move_bucket_head(const std::string& path) {
@@ -509,13 +580,20 @@ MoveBucket read_move_bucket_head(const std::string& path) {
     f.seekg(0);
     char magic[8];
     f.read(magic, 8);
-    if (!f || std::memcmp(magic, kMoveBucketMagic, 8) != 0)
-        throw Error(CPD_E_IO, path + ": not a compact (DOSCPD02) CPD bucket file");
+    const bool striped = f && std::memcmp(magic, kMoveStripedMagic, 8) == 0;
+    if (!f || !(striped || std::memcmp(magic, kMoveBucketMagic, 8) == 0))
+        throw Error(CPD_E_IO, path + ": not a compact (DOSCPD02/03) CPD bucket file");
     MoveBucket b;
     uint32_t h32[8];
     f.read(reinterpret_cast<char*>(h32), sizeof h32);
     f.read(reinterpret_cast<char*>(&b.total_runs), 8);
     f.read(reinterpret_cast<char*>(&b.fingerprint), 8);
+    if (striped) {
+        uint32_t st[2];
+        f.read(reinterpret_cast<char*>(st), sizeof st);
+        b.stripes = st[0];
+        b.stripe_rows = st[1];
+    }
     if (!f) throw Error(CPD_E_IO, path + ": truncated header");
     b.n = h32[0];
     const uint32_t nrows = h32[1];
@@ -528,10 +606,18 @@ MoveBucket read_move_bucket_head(const std::string& path) {
     if (!(b.bits == 1 || b.bits == 2 || b.bits == 4) ||
         b.words != ((uint64_t)b.n * b.bits + 31u) / 32u)
         throw Error(CPD_E_IO, path + ": row width does not match n and bits per move");
+    if (striped && (b.stripes < 2 || b.stripes > 4096 || b.stripe_rows == 0))
+        throw Error(CPD_E_IO, path + ": bad stripe layout");
     b.targets.resize(nrows);
     b.counts.resize(nrows);
-    if (size != b.rows_offset() + 4ull * b.words * nrows)
+    if (striped) {
+        if (size != b.head_bytes()) throw Error(CPD_E_IO, path + ": size does not match its header");
+        for (uint32_t j = 0; j < b.stripes; ++j)
+            if (file_size(move_part_path(path, j)) != b.part_rows(j) * 4ull * b.words)
+                throw Error(CPD_E_IO, move_part_path(path, j) + ": size does not match its bucket");
+    } else if (size != b.rows_offset() + 4ull * b.words * nrows) {
         throw Error(CPD_E_IO, path + ": size does not match its header");
+    }
     f.read(reinterpret_cast<char*>(b.targets.data()), nrows * 4ull);
     f.read(reinterpret_cast<char*>(b.counts.data()), nrows * 4ull);
     if (!f) throw Error(CPD_E_IO, path + ": truncated body");
@@ -547,15 +633,47 @@ MoveBucket read_move_bucket_head(const std::string& path) {
 void read_move_bucket_rows(const std::string& path, const MoveBucket& head, uint32_t first,
                            uint32_t count, uint32_t* out, int threads) {
     if ((uint64_t)first + count > head.targets.size()) throw Error(CPD_E_ARG, path + ": rows out of range");
-    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
-    if (fd < 0) throw Error(CPD_E_IO, "cannot open " + path);
-    const uint64_t pos0 = head.rows_offset() + 4ull * head.words * first;
-    const uint64_t total = 4ull * head.words * count;
-    auto span = [&](uint64_t a, uint64_t b) {  // bytes [a, b) of the rows read
-        char* c = reinterpret_cast<char*>(out) + a;
-        uint64_t pos = pos0 + a, left = b - a;
+    const uint64_t rb = 4ull * head.words;
+    // spans (file, file offset, bytes into out, bytes): one per stripe unit
+    // touched, or pieces of the one rows region
+    struct Span {
+        uint32_t file;
+        uint64_t pos, at, bytes;
+    };
+    std::vector<Span> spans;
+    std::vector<std::string> files;
+    if (head.stripes > 1) {
+        for (uint32_t j = 0; j < head.stripes; ++j) files.push_back(move_part_path(path, j));
+        const uint64_t S = head.stripe_rows, K = head.stripes;
+        for (uint64_t r = first, end = (uint64_t)first + count; r < end;) {
+            const uint64_t u = r / S, take = std::min(end - r, (u + 1) * S - r);
+            spans.push_back({(uint32_t)(u % K), ((u / K) * S + r % S) * rb, (r - first) * rb, take * rb});
+            r += take;
+        }
+    } else {
+        files.push_back(path);
+        // a read from the page cache is a copy one thread does at ~10 GB/s:
+        // large pieces are split over threads (>= 16 MB each)
+        const uint64_t total = rb * count, pos0 = head.rows_offset() + rb * first;
+        const uint64_t parts = std::max<uint64_t>(
+            1, std::min<uint64_t>((uint64_t)std::max(1, threads), total >> 24));
+        const uint64_t step = (total / parts + 4095) / 4096 * 4096;
+        for (uint64_t a = 0; a < total; a += step) spans.push_back({0, pos0 + a, a, std::min(step, total - a)});
+    }
+    std::vector<int> fds(files.size(), -1);
+    for (size_t i = 0; i < files.size(); ++i) {
+        fds[i] = ::open(files[i].c_str(), O_RDONLY | O_CLOEXEC);
+        if (fds[i] < 0) {
+            for (int fd : fds)
+                if (fd >= 0) ::close(fd);
+            throw Error(CPD_E_IO, "cannot open " + files[i]);
+        }
+    }
+    auto read_span = [&](const Span& sp) {
+        char* c = reinterpret_cast<char*>(out) + sp.at;
+        uint64_t pos = sp.pos, left = sp.bytes;
         while (left) {
-            const ssize_t k = ::pread(fd, c, std::min<uint64_t>(left, 1ull << 30), (off_t)pos);
+            const ssize_t k = ::pread(fds[sp.file], c, std::min<uint64_t>(left, 1ull << 30), (off_t)pos);
             if (k <= 0) return false;
             c += k;
             pos += (uint64_t)k;
@@ -563,26 +681,21 @@ void read_move_bucket_rows(const std::string& path, const MoveBucket& head, uint
         }
         return true;
     };
-    // a read from the page cache is a copy one thread does at ~10 GB/s:
-    // large pieces are split over threads (>= 16 MB each)
-    const uint64_t parts = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(1, threads),
-                                                                     total >> 24));
+    const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), spans.size()));
     bool ok = true;
-    if (parts == 1) {
-        ok = span(0, total);
+    if (T == 1) {
+        for (const Span& sp : spans) ok = ok && read_span(sp);
     } else {
         std::vector<std::thread> th;
-        std::vector<char> good(parts, 1);
-        const uint64_t step = (total / parts + 4095) / 4096 * 4096;
-        for (uint64_t p = 0; p < parts; ++p) {
-            const uint64_t a = std::min(total, p * step), b = std::min(total, a + step);
-            if (p + 1 == parts) th.emplace_back([&, p, a] { good[p] = span(a, total); });
-            else th.emplace_back([&, p, a, b] { good[p] = span(a, b); });
-        }
-        for (auto& t : th) t.join();
+        std::vector<char> good(T, 1);
+        for (size_t t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                for (size_t i = t; i < spans.size(); i += T) good[t] = good[t] && read_span(spans[i]);
+            });
+        for (auto& x : th) x.join();
         for (char g : good) ok = ok && g;
     }
-    ::close(fd);
+    for (int fd : fds) ::close(fd);
     if (!ok) throw Error(CPD_E_IO, path + ": truncated rows");
 }
 

@@ -106,15 +106,25 @@ int bucket_format(const std::string& path);
 struct MoveBucket {
     uint32_t n = 0, bid = 0, method = 0, key = 0, maxworker = 0, words = 0, bits = 4;
     uint64_t fingerprint = 0, total_runs = 0;
+    // striped (DOSCPD03): the rows in `stripes` part files {path}.p{j}, in
+    // units of stripe_rows rows dealt round robin (unit u in part u % stripes)
+    uint32_t stripes = 1, stripe_rows = 0;
     std::vector<uint32_t> targets, counts;
-    uint64_t rows_offset() const;
+    uint64_t rows_offset() const;  // DOSCPD02: where the rows start
+    uint64_t head_bytes() const;   // DOSCPD03: the main file's size
+    uint64_t part_rows(uint32_t j) const;
 };
+std::string move_part_path(const std::string& path, uint32_t j);
 // Written in pieces from several threads, in any order (positional writes);
-// close() writes the run total and renames the .tmp into place.
+// close() writes the run total and renames the .tmp files into place (the
+// parts first, the main file last).  stripes > 1: DOSCPD03, the rows in
+// part files — writes to one file serialise on its inode (~10 GB/s of
+// page-cache copies on the GPU box, 117 GB/s over 16 files).
 class MoveBucketFile {
 public:
     // `b` supplies the header fields and targets (counts / total unused)
-    MoveBucketFile(const std::string& path, const MoveBucket& b);
+    MoveBucketFile(const std::string& path, const MoveBucket& b, uint32_t stripes = 1,
+                   uint32_t stripe_rows = 64);
     ~MoveBucketFile();  // without close(): the .tmp is removed
     MoveBucketFile(const MoveBucketFile&) = delete;
     MoveBucketFile& operator=(const MoveBucketFile&) = delete;
@@ -123,11 +133,12 @@ public:
     void close(uint64_t total_runs);
 
 private:
-    void pwrite_all(const void* p, size_t bytes, uint64_t pos);
+    void pwrite_all(int fd, const void* p, size_t bytes, uint64_t pos);
     std::string path_, tmp_;
     int fd_ = -1;
-    uint32_t nrows_ = 0, words_ = 0;
+    uint32_t nrows_ = 0, words_ = 0, stripes_ = 1, stripe_rows_ = 0;
     uint64_t rows_off_ = 0;
+    std::vector<int> part_fd_;
 };
 // Header, targets and counts (the file size checked against the header);
 // rows [first, first + count) then read by position.

@@ -18,10 +18,14 @@
 //                 [--plan-only]        build / load the cached plan and exit
 //                 [--targets-from S]   only rows of targets of scenario S (q s t)
 //                 [--format moves|rle] bucket file layout: moves (default) =
-//                                      DOSCPD02, the rows as move tables of
-//                                      1/2/4 bits per column (by max out-degree,
-//                                      n*bits/8 bytes per row); rle = DOSCPD01,
-//                                      the run words (4 B per run)
+//                                      the rows as move tables of 1/2/4 bits
+//                                      per column (by max out-degree, n*bits/8
+//                                      bytes per row); rle = DOSCPD01, the run
+//                                      words (4 B per run)
+//                 [--stripes K]        moves: the rows striped over K part
+//                                      files per bucket (DOSCPD03, default 16:
+//                                      writes to one file serialise on its
+//                                      inode); 1 = one DOSCPD02 file
 //                 [--discard]          null sink: every row is still built and
 //                                      copied out of HBM (D2H), but no file is
 //                                      written (times the build + export path
@@ -103,8 +107,8 @@ struct PinnedBuf {
 
 class Pipeline {
 public:
-    Pipeline(cpd_graph* g, uint32_t B, int threads, bool discard, bool moves)
-        : g_(g), B_(B), discard_(discard), moves_(moves) {
+    Pipeline(cpd_graph* g, uint32_t B, int threads, bool discard, bool moves, uint32_t stripes)
+        : g_(g), B_(B), discard_(discard), moves_(moves), stripes_(stripes) {
         for (int i = 0; i < std::max(1, threads); ++i) pool_.emplace_back([this] { worker(); });
     }
     ~Pipeline() {
@@ -129,7 +133,8 @@ public:
         std::vector<size_t> to_close;        // buckets finished by the block in flight
         auto open_bucket = [&](size_t k) {
             if (discard_) return;
-            if (moves_) mfiles[k] = std::make_unique<MoveBucketFile>(paths[k], move_head(heads[k]));
+            if (moves_)
+                mfiles[k] = std::make_unique<MoveBucketFile>(paths[k], move_head(heads[k]), stripes_);
             else files[k] = std::make_unique<BucketFile>(paths[k], heads[k]);
         };
         auto close_bucket = [&](size_t k) {
@@ -334,6 +339,7 @@ private:
     cpd_graph* g_;
     uint32_t B_;
     bool discard_, moves_;
+    uint32_t stripes_;
     cpd_rows* rows_[2] = {nullptr, nullptr};
     std::vector<std::thread> pool_;
     std::mutex mu_;
@@ -355,7 +361,7 @@ int main(int argc, char** argv) {
                      "--workerid I --maxworker W [--outdir D] [--device G] [--batch B] "
                      "[--threads T] [--plan P | --no-plan-cache] [--write-threads T] "
                      "[--no-pipeline] [--plan-only] [--targets-from SCEN] [--discard] "
-                     "[--hbm-reserve GIB] [--format moves|rle]\n");
+                     "[--hbm-reserve GIB] [--format moves|rle] [--stripes K]\n");
         return 2;
     }
     int mcode = cli::method_code(method);
@@ -365,6 +371,8 @@ int main(int argc, char** argv) {
         return 2;
     }
     const bool moves = format == "moves";
+    // compact buckets striped over part files (DOSCPD03; 1 = one DOSCPD02 file)
+    const uint32_t stripes = (uint32_t)std::max<long long>(1, a.num("stripes", 16));
     std::string outdir = a.str("outdir", dir_of(input));
     ::mkdir(outdir.c_str(), 0755);
     double t_start = now();
@@ -587,7 +595,7 @@ int main(int argc, char** argv) {
                         std::vector<uint32_t> c(nb);
                         for (uint32_t r = 0; r < nb; ++r)
                             c[r] = (uint32_t)(off[first[k] + r + 1] - off[first[k] + r]);
-                        cpd::io::MoveBucketFile f(path, b);
+                        cpd::io::MoveBucketFile f(path, b, stripes);
                         f.write_counts(0, c.data(), nb);
                         f.write_rows(0, mv.data() + first[k] * (size_t)words, nb);
                         f.close(off[first[k + 1]] - off[first[k]]);
@@ -611,7 +619,7 @@ int main(int argc, char** argv) {
                 runs_done += tot;
             }
         } else {
-            Pipeline pl(dg, B, (int)a.num("write-threads", 16), discard, moves);
+            Pipeline pl(dg, B, (int)a.num("write-threads", 16), discard, moves, stripes);
             std::vector<uint32_t> targets;
             std::vector<CpdBucket> heads(owned.size());
             std::vector<uint64_t> first(owned.size() + 1, 0);

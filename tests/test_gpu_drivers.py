@@ -126,29 +126,47 @@ def _read_bucket(path):
 
 
 def _read_move_bucket(path):
-    """The compact bucket layout of csrc/cpd_io.cpp (DOSCPD02, MoveBucketFile)."""
+    """The compact bucket layouts of csrc/cpd_io.cpp (MoveBucketFile): DOSCPD02
+    (rows after the header) or DOSCPD03 (rows striped over part files
+    {path}.p{j}: unit u of stripe_rows rows is unit u // K of part u % K)."""
     raw = open(path, "rb").read()
-    assert raw[:8] == b"DOSCPD02"
+    assert raw[:8] in (b"DOSCPD02", b"DOSCPD03")
     n, nrows, bid, method, key, maxworker, words, bits = (int(x) for x in np.frombuffer(raw, np.uint32, 8, 8))
     assert bits in (1, 2, 4) and words == (n * bits + 31) // 32
     total = int(np.frombuffer(raw, np.uint64, 1, 40)[0])
-    p = 56
-    targets = np.frombuffer(raw, np.uint32, nrows, p)
-    counts = np.frombuffer(raw, np.uint32, nrows, p + 4 * nrows)
-    rows_at = -(-(p + 8 * nrows) // 4096) * 4096
-    assert len(raw) == rows_at + 4 * words * nrows and int(counts.sum()) == total
-    moves = np.frombuffer(raw, np.uint32, nrows * words, rows_at).reshape(nrows, words)
+    if raw[:8] == b"DOSCPD02":
+        p = 56
+        targets = np.frombuffer(raw, np.uint32, nrows, p)
+        counts = np.frombuffer(raw, np.uint32, nrows, p + 4 * nrows)
+        rows_at = -(-(p + 8 * nrows) // 4096) * 4096
+        assert len(raw) == rows_at + 4 * words * nrows
+        moves = np.frombuffer(raw, np.uint32, nrows * words, rows_at).reshape(nrows, words)
+    else:
+        K, S = (int(x) for x in np.frombuffer(raw, np.uint32, 2, 56))
+        p = 64
+        targets = np.frombuffer(raw, np.uint32, nrows, p)
+        counts = np.frombuffer(raw, np.uint32, nrows, p + 4 * nrows)
+        assert len(raw) == p + 8 * nrows
+        parts = [np.fromfile(f"{path}.p{j}", np.uint32).reshape(-1, words) for j in range(K)]
+        moves = np.empty((nrows, words), np.uint32)
+        for u in range(-(-nrows // S)):
+            r0, r1 = u * S, min(nrows, u * S + S)
+            q = (u // K) * S
+            moves[r0:r1] = parts[u % K][q:q + (r1 - r0)]
+        assert sum(len(x) for x in parts) == nrows
+    assert int(counts.sum()) == total
     return targets, counts, moves, bits
 
 
-@pytest.mark.parametrize("fmt", ["moves", "rle"])
+@pytest.mark.parametrize("fmt", ["moves", "moves1", "rle"])
 @pytest.mark.parametrize("method,key", [("mod", 5), ("div", 7)])
 def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key, fmt):
     """The overlapped writer (build block k+1 while a pool copies block k out
     of HBM and writes it in place) gives byte-identical bucket files to the
-    sequential path, in both layouts (DOSCPD02 move tables, the default, and
-    DOSCPD01 run words); with --batch 1024 the blocks straddle bucket
-    boundaries and --write-threads 3 interleaves pieces of several buckets."""
+    sequential path, in every layout (move tables striped over part files,
+    DOSCPD03, the default; in one file, DOSCPD02, --stripes 1; DOSCPD01 run
+    words); with --batch 1024 the blocks straddle bucket boundaries and
+    --write-threads 3 interleaves pieces of several buckets."""
     prefix = str(tmp_path / "g")
     subprocess.run([os.path.join(BIN, "gen_synth"), "--width", "64", "--height", "48", "--seed",
                     "5", "--out", prefix, "--queries", "10"], check=True, capture_output=True)
@@ -161,7 +179,9 @@ def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key, fmt):
         out = str(tmp_path / mode)
         p = subprocess.run([os.path.join(BIN, "make_cpd_auto"), "--input", xy, "--partmethod",
                             method, "--partkey", str(key), "--workerid", "1", "--maxworker", "2",
-                            "--outdir", out, "--device", "0", "--format", fmt,
+                            "--outdir", out, "--device", "0",
+                            "--format", "rle" if fmt == "rle" else "moves",
+                            "--stripes", "1" if fmt == "moves1" else "16",
                             "--plan", str(tmp_path / "g.plan")] + extra,
                            capture_output=True, text=True, timeout=300)
         if mode == "too_much":  # a reserve past the free HBM: refused, nothing built
@@ -174,7 +194,10 @@ def test_make_cpd_auto_pipeline_matches_sequential(tmp_path, method, key, fmt):
     assert seq == pipe and len(seq) == key // 2
     assert not [f for f in os.listdir(dirs["pipe"]) if f.endswith(".tmp")]
     assert sorted(f for f in os.listdir(dirs["reserve"]) if f.endswith(".cpd")) == seq
-    for f in seq:
+    files = sorted(f for f in os.listdir(dirs["seq"]) if ".cpd" in f)  # with the parts
+    assert files == sorted(f for f in os.listdir(dirs["pipe"]) if ".cpd" in f)
+    assert (len(files) > len(seq)) == (fmt == "moves")
+    for f in files:
         a = open(os.path.join(dirs["seq"], f), "rb").read()
         b = open(os.path.join(dirs["pipe"], f), "rb").read()
         assert a == b, f

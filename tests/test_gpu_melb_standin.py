@@ -111,6 +111,8 @@ def test_melb_mod3_concurrent_build_and_driver_flow(melb):
     files = sorted(f for f in os.listdir(a) if f.endswith(".cpd"))
     assert files == sorted(f for f in os.listdir(b) if f.endswith(".cpd")) and len(files) == 3
     assert not [f for f in os.listdir(a) if ".tmp" in f]
+    files = sorted(f for f in os.listdir(a) if ".cpd" in f)  # the buckets' part files too
+    assert files == sorted(f for f in os.listdir(b) if ".cpd" in f)
     for f in files:
         assert open(os.path.join(a, f), "rb").read() == open(os.path.join(b, f), "rb").read(), f
     W = 3
