@@ -10,9 +10,10 @@
 //   query  "{n}\n" then n lines "s t" (process_query.send_queries, :93-96).
 //   .cpd   one file per partition bucket (README.md:86-93 "one or more CPDs"),
 //          our own layout == the HBM layout, so a load is one read + one copy.
-//          DOSCPD02 (default): the rows in their compact form, a move per
-//          column (cpd_rows_export_moves) in `bits` = 1, 2 or 4 bits by the
-//          graph's max out-degree (header word 7), n*bits/8 bytes per row; DOSCPD01
+//          DOSCPD02: the rows in their compact form, a move per column
+//          (cpd_rows_export_moves) in `bits` = 1, 2 or 4 bits by the
+//          graph's max out-degree (header word 7), n*bits/8 bytes per row;
+//          DOSCPD03 (default): the same rows striped over part files; DOSCPD01
 //          (make_cpd_auto --format rle): RLE run words, 4 B per run.
 //   .order the DFS column order shared by every bucket of a graph.
 #pragma once
