@@ -137,13 +137,10 @@ bool async_on();  // CPD_ASYNC (defined with the other switches)
 hipStream_t thread_stream(int device);
 
 // Largest auto batch (CPD_BATCH_MAX, a multiple of 1024 <= 32768; A/B knob).
-// 28672: free HBM, not this cap, sets the 1M-node batch (27648 rows since the
-// dense indexes hold packed tables: 366.2k against 361.2k rows/s at 24576,
-// profiles/batch_ab/r04af_*).
 uint32_t batch_max() {
     static const uint32_t v = [] {
         const char* e = std::getenv("CPD_BATCH_MAX");
-        const unsigned long b = e && *e ? std::strtoul(e, nullptr, 10) : 28672ul;
+        const unsigned long b = e && *e ? std::strtoul(e, nullptr, 10) : 24576ul;
         return (uint32_t)std::max(1024ul, std::min(32768ul, b / 1024ul * 1024ul));
     }();
     return v;
