@@ -7,6 +7,7 @@
 #include <array>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <functional>
 #include <map>
 #include <memory>
@@ -879,11 +880,16 @@ int cpd_batch_bytes(uint32_t n, uint32_t max_degree, uint32_t batch, uint64_t* b
     });
 }
 
+namespace {
+bool trace_on();
+}  // namespace
+
 int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
     return guarded([&] {
         CPD_REQUIRE(p && out, CPD_E_ARG, "graph: null argument");
         *out = nullptr;
         require_device();
+        const double tg0 = now_seconds();
         auto g = std::make_unique<cpd_graph>();
         g->device = device;
         g->select();
@@ -903,6 +909,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         for (hipEvent_t* e : {&g->ev_up, &g->ev_down, &g->ev_fm})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         for (auto& e : g->ev_emit) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (trace_on()) std::fprintf(stderr, "[cpd] graph streams %.3f s\n", now_seconds() - tg0);
         const uint32_t n = p->n, m = p->m;
         g->n = n;
         g->m = m;
@@ -947,6 +954,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         std::vector<uint32_t> adj = g->packed_adjacency(g->w_free_col);
         g->adj.upload(adj.data(), adj.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
+        if (trace_on()) std::fprintf(stderr, "[cpd] graph csr+adjacency %.3f s\n", now_seconds() - tg0);
         g->has_ch = !p->ch.rank.empty();
         if (!g->has_ch) {  // query-only graph (fifo_auto)
             *out = g.release();
@@ -960,6 +968,25 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 level_order(*p, p->ch.level_up, p->ch.nlev_up, lvl);
             for (uint32_t s2 = 0; s2 < n; ++s2) asc_slot[node_of_slot[s2]] = s2;
         }
+        // the two sweeps' lists are independent host work (~0.1 s each at 1M
+        // nodes): the down-sweep's is built on a second thread meanwhile
+        g->leaf_fm = g->fmb == 4 && env_on("CPD_LEAFFM");
+        std::vector<uint32_t> dnodes, doff, darcs;
+        std::exception_ptr derr;
+        std::thread dthr([&] {
+            try {
+                build_sweep(*p, false, asc_slot, dnodes, doff, darcs, g->dsc_lvl, g->dsc_lvl_arcs,
+                            g->dsc_lvl_reads, g->leaf_fm);
+            } catch (...) {
+                derr = std::current_exception();
+            }
+        });
+        struct Join {
+            std::thread& t;
+            ~Join() {
+                if (t.joinable()) t.join();
+            }
+        } djoin{dthr};
         build_sweep(*p, true, asc_slot, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs, unused);
         g->asc_off_host = off;
         const std::vector<uint32_t> nodes_asc_host = nodes, asc_arcs_host = arcs;
@@ -967,11 +994,14 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->asc_off.upload(off.data(), off.size(), s);
         g->asc_arcs.upload(arcs.data(), arcs.size(), s);
         HIP_CHECK(hipStreamSynchronize(s));
+        if (trace_on()) std::fprintf(stderr, "[cpd] graph up lists %.3f s\n", now_seconds() - tg0);
         g->ch_arcs = arcs.size() / 2;
         // leaf first moves in the down-sweep: 4-bit sets only (<= 4 slots)
-        g->leaf_fm = g->fmb == 4 && env_on("CPD_LEAFFM");
-        build_sweep(*p, false, asc_slot, nodes, off, arcs, g->dsc_lvl, g->dsc_lvl_arcs,
-                    g->dsc_lvl_reads, g->leaf_fm);
+        dthr.join();
+        if (derr) std::rethrow_exception(derr);
+        nodes.swap(dnodes);
+        off.swap(doff);
+        arcs.swap(darcs);
         g->dsc_nodes.upload(nodes.data(), nodes.size(), s);
         g->dsc_off.upload(off.data(), off.size(), s);
         g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
@@ -979,7 +1009,9 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             const uint32_t na = down_desc_arcs();
             std::vector<uint32_t> desc((size_t)n * 32u, 0u);
             const std::vector<uint32_t>& aoff = g->asc_off_host;
-            for (uint32_t x = 0; x < n; ++x) {
+            // 128 B per node written by 8 host threads (each node's own slots)
+            auto fill = [&](uint32_t x0, uint32_t x1) {
+            for (uint32_t x = x0; x < x1; ++x) {
                 uint32_t* d = desc.data() + (size_t)x * 32u;
                 d[0] = nodes[x];
                 d[1] = off[x];
@@ -999,9 +1031,19 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                     }
                 }
             }
+            };
+            {
+                constexpr uint32_t kFillThreads = 8;
+                const uint32_t per = (n + kFillThreads - 1u) / kFillThreads;
+                std::vector<std::thread> ft;
+                for (uint32_t t = 0; t < kFillThreads; ++t)
+                    ft.emplace_back(fill, std::min(n, t * per), std::min(n, (t + 1u) * per));
+                for (auto& t : ft) t.join();
+            }
             g->dsc_desc.upload(desc.data(), desc.size(), s);
         }
         HIP_CHECK(hipStreamSynchronize(s));
+        if (trace_on()) std::fprintf(stderr, "[cpd] graph down lists+desc %.3f s\n", now_seconds() - tg0);
         g->ch_arcs += arcs.size() / 2;
         g->narrow = env_on("CPD_NARROW") && p->dist_bound < 0xFFFFFFFEull;
         {
@@ -1057,6 +1099,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->asc_lvl_of.upload(la.data(), n, s);
         g->dsc_lvl_of.upload(ld.data(), n, s);
         HIP_CHECK(hipStreamSynchronize(s));
+        if (trace_on()) std::fprintf(stderr, "[cpd] graph levels %.3f s\n", now_seconds() - tg0);
         *out = g.release();
     });
 }
