@@ -766,36 +766,59 @@ void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& as
         uint32_t v = node_of_slot[s];
         nodes[s] = ascend ? p.order[v] : ref(v);  // descending: closed-form init
     }
+    const bool leaf_rows = !ascend && leaf_edges;  // a leaf's arcs: its out-edges
     off.assign(n + 1, 0);
-    arcs.clear();
-    arcs.reserve(2 * aoff[n]);
+    for (uint32_t s = 0; s < n; ++s) {
+        const uint32_t v = node_of_slot[s];
+        off[s + 1] = off[s] + (leaf_rows && lup[v] == 0 ? p.row_ptr[v + 1] - p.row_ptr[v]
+                                                        : (uint32_t)(aoff[v + 1] - aoff[v]));
+    }
+    arcs.assign(2ull * off[n], 0u);
+    // slots filled by 8 host threads (each writes its slots' arcs; level
+    // counts per thread, summed after)
+    constexpr uint32_t kThreads = 8;
+    std::vector<std::vector<double>> la(kThreads, std::vector<double>(nlev, 0.0)),
+        lr(kThreads, std::vector<double>(nlev, 0.0));
+    auto fill = [&](uint32_t t, uint32_t s0, uint32_t s1) {
+        std::vector<std::pair<uint32_t, uint32_t>> tmp;
+        for (uint32_t s = s0; s < s1; ++s) {
+            const uint32_t v = node_of_slot[s];
+            uint32_t* out = arcs.data() + 2ull * off[s];
+            if (leaf_rows && lup[v] == 0) {
+                for (uint32_t e = p.row_ptr[v]; e < p.row_ptr[v + 1]; ++e) {
+                    *out++ = p.order[p.dst[e]];
+                    *out++ = p.w[e];
+                    if (p.dst[e] != v) la[t][level[v]] += 1.0;
+                }
+                continue;
+            }
+            tmp.clear();
+            for (uint64_t e = aoff[v]; e < aoff[v + 1]; ++e) tmp.push_back({p.order[adst[e]], aw[e]});
+            std::sort(tmp.begin(), tmp.end());
+            for (auto& a : tmp) {
+                // ascending arcs into upward levels 0/1 use the closed forms
+                const uint32_t r = ascend ? ref(p.inv[a.first]) : a.first;
+                *out++ = r;
+                *out++ = a.second;
+                if (!(r & (kLeafBit | kL1Bit))) la[t][level[v]] += 1.0;
+            }
+            if (!ascend && !(nodes[s] & (kLeafBit | kL1Bit))) lr[t][level[v]] += 1.0;
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        const uint32_t per = (n + kThreads - 1u) / kThreads;
+        for (uint32_t t = 0; t < kThreads; ++t)
+            th.emplace_back(fill, t, std::min(n, t * per), std::min(n, (t + 1u) * per));
+        for (auto& x : th) x.join();
+    }
     lvl_arcs.assign(nlev, 0.0);
     lvl_reads.assign(nlev, 0.0);
-    std::vector<std::pair<uint32_t, uint32_t>> tmp;
-    for (uint32_t s = 0; s < n; ++s) {
-        uint32_t v = node_of_slot[s];
-        tmp.clear();
-        if (!ascend && leaf_edges && lup[v] == 0) {
-            for (uint32_t e = p.row_ptr[v]; e < p.row_ptr[v + 1]; ++e) {
-                arcs.push_back(p.order[p.dst[e]]);
-                arcs.push_back(p.w[e]);
-                if (p.dst[e] != v) lvl_arcs[level[v]] += 1.0;
-            }
-            off[s + 1] = off[s] + (p.row_ptr[v + 1] - p.row_ptr[v]);
-            continue;
+    for (uint32_t t = 0; t < kThreads; ++t)
+        for (uint32_t l = 0; l < nlev; ++l) {
+            lvl_arcs[l] += la[t][l];
+            lvl_reads[l] += lr[t][l];
         }
-        for (uint64_t e = aoff[v]; e < aoff[v + 1]; ++e) tmp.push_back({p.order[adst[e]], aw[e]});
-        std::sort(tmp.begin(), tmp.end());
-        for (auto& a : tmp) {
-            // ascending arcs into upward levels 0/1 use the closed forms
-            uint32_t r = ascend ? ref(p.inv[a.first]) : a.first;
-            arcs.push_back(r);
-            arcs.push_back(a.second);
-            if (!(r & (kLeafBit | kL1Bit))) lvl_arcs[level[v]] += 1.0;
-        }
-        off[s + 1] = off[s] + (uint32_t)tmp.size();
-        if (!ascend && !(nodes[s] & (kLeafBit | kL1Bit))) lvl_reads[level[v]] += 1.0;
-    }
 }
 
 
