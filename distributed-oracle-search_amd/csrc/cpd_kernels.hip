@@ -3445,7 +3445,9 @@ static void launch_walk(const uint2* adj, uint32_t shift, const Rows& rows, cons
     chunk = std::min<uint64_t>(chunk, std::max(unit, chunk_max));
     chunk = std::max<uint64_t>(unit, (chunk + unit - 1u) / unit * unit);
     const uint64_t waves = ((uint64_t)nq + chunk - 1u) / chunk;
-    const dim3 grid((uint32_t)std::max<uint64_t>(1u, (waves + 3u) / 4u)), blk(256);
+    // CPD_TS_WPB: waves per workgroup (A/B; 4 = the round-2..4 shape)
+    static const uint32_t wpb = std::min(4u, std::max(1u, env_u32("CPD_TS_WPB", 4)));
+    const dim3 grid((uint32_t)std::max<uint64_t>(1u, (waves + wpb - 1u) / wpb)), blk(64u * wpb);
     const uint32_t c = (uint32_t)chunk;
 #define CPD_WALK(SH, IL)                                                                       \
     launch(kern::table_walk<SH, IL, Rows>, grid, blk, s, adj, rows, qs, qt, qrow, nq, c, limit, \
