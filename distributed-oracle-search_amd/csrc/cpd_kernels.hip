@@ -3439,14 +3439,19 @@ template <class Rows>
 static void launch_walk(const uint2* adj, uint32_t shift, const Rows& rows, const uint32_t* qs,
                         const uint32_t* qt, const uint32_t* qrow, uint32_t nq, uint32_t limit,
                         uint64_t* cost, uint32_t* hops, uint8_t* fin, unsigned long long* agg,
-                        uint32_t waves_target, uint32_t chunk_max, hipStream_t s) {
+                        uint32_t waves_target, uint32_t chunk_max, hipStream_t s,
+                        uint32_t wpb_default) {
     constexpr uint32_t unit = 64u;
     uint64_t chunk = ((uint64_t)nq + waves_target - 1u) / waves_target;
     chunk = std::min<uint64_t>(chunk, std::max(unit, chunk_max));
     chunk = std::max<uint64_t>(unit, (chunk + unit - 1u) / unit * unit);
     const uint64_t waves = ((uint64_t)nq + chunk - 1u) / chunk;
-    // CPD_TS_WPB: waves per workgroup (A/B; 4 = the round-2..4 shape)
-    static const uint32_t wpb = std::min(4u, std::max(1u, env_u32("CPD_TS_WPB", 4)));
+    // waves per workgroup: dense walks 1 (their ~1000 waves spread over every
+    // CU: 92.3M against 90.3M q/s with 4), RLE walks 4 (8192 one-wave
+    // workgroups ran out of workgroup slots: 8.2M against 11.4M);
+    // CPD_TS_WPB overrides both (A/B, profiles/walk_wpb_ab/)
+    static const uint32_t wpb_env = env_u32("CPD_TS_WPB", 0);
+    const uint32_t wpb = std::min(4u, std::max(1u, wpb_env ? wpb_env : wpb_default));
     const dim3 grid((uint32_t)std::max<uint64_t>(1u, (waves + wpb - 1u) / wpb)), blk(64u * wpb);
     const uint32_t c = (uint32_t)chunk;
 #define CPD_WALK(SH, IL)                                                                       \
@@ -3475,7 +3480,7 @@ void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32
     launch_walk(reinterpret_cast<const uint2*>(adj), shift,
                 kern::DenseRows{dense, npad >> (5u - lb), kern::Tbl{lb}}, qs,
                 qt, qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(1024),
-                ts_chunk_max(1024), s);
+                ts_chunk_max(1024), s, 1u);
 }
 
 void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
@@ -3485,7 +3490,7 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
                          unsigned long long* agg, hipStream_t s) {
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::RleRows{offsets, runs}, qs, qt,
                 qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(8192),
-                ts_chunk_max(1u << 30), s);
+                ts_chunk_max(1u << 30), s, 4u);
 }
 
 uint32_t search_slots(uint32_t nq) {  // lanes with a workspace: whole blocks of 4 waves
