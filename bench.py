@@ -560,7 +560,8 @@ def cpu_partitioned(threads, rows_per_worker=384, queries=20000):
 # end-to-end worker build: bin/make_cpd_auto
 # as the driver runs it (make_cpds.py:20), on a cold plan cache, every row the
 # rank owns built, copied out of HBM and written to its bucket files in the
-# compact layout (DOSCPD02: a 1/2/4-bit move per column by max out-degree); then
+# compact layout (DOSCPD03: a 1/2/4-bit move per column by max out-degree,
+# striped over part files); then
 # bin/fifo_auto (make_fifos.py:21) loads those files and answers a request
 # through the reference's FIFO protocol, checked against the oracle
 
@@ -590,7 +591,7 @@ def full_build_dir(args, world):
 def full_build(args, xy, world, rank, device, comm, runner=subprocess.run):
     """Run make_cpd_auto for worker `rank` of full_build_workers() with a
     fresh (cold) plan cache shared by the node's ranks; returns its JSON phase
-    line.  Rank 0 writes its bucket files (DOSCPD02) into the cache directory
+    line.  Rank 0 writes its bucket files (DOSCPD03) into the cache directory
     on the box's disk; the other ranks run the same worker path with
     --discard (D2H export, no file writes): eight 31-GB workers would
     outgrow one node's disk."""
@@ -633,7 +634,7 @@ def full_build_leg(args, xy, world, rank, device, comm, runner=subprocess.run):
     W = full_build_workers(args, world)
     fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of {W} ({args.partmethod} "
                   f"{args.partkey}), one worker per rank: all its rows, cold plan cache, "
-                  "compact bucket files (DOSCPD02) written by rank 0, --discard (D2H export "
+                  "compact bucket files (DOSCPD03, striped) written by rank 0, --discard (D2H export "
                   "only) on the other ranks",
           "total_s": round(tmax, 3), "rows": int(tot[0]), "runs": int(tot[1]),
           "rows_per_s_end_to_end": round(tot[0] / tmax, 1) if tmax else 0.0,
