@@ -1007,7 +1007,8 @@ def main():
         # (8.9 MB per lane with tables, 60% of the free HBM); the few that
         # outgrow them rerun in 2^19-column ones (capacity escalation; round
         # 3 ran 512 searches, round 4's first runs 4096, all at 2^19)
-        cap0, capmax = 1 << 17, 1 << 19
+        cap0 = 1 << int(os.environ.get("CPD_BENCH_CAP0_LOG2", "17"))  # A/B
+        capmax = 1 << 19
         zq = 16384
         zs = rng.integers(0, g.n, zq).astype(np.uint32)
         zt = srows[rng.integers(0, len(srows), zq)]
