@@ -1009,7 +1009,7 @@ def main():
         # 3 ran 512 searches, round 4's first runs 4096, all at 2^19)
         cap0 = 1 << int(os.environ.get("CPD_BENCH_CAP0_LOG2", "17"))  # A/B
         capmax = 1 << 19
-        zq = 16384
+        zq = int(os.environ.get("CPD_BENCH_ZQ", "16384"))  # searches in the leg (A/B)
         zs = rng.integers(0, g.n, zq).astype(np.uint32)
         zt = srows[rng.integers(0, len(srows), zq)]
         six.search(zs[:64], zt[:64], capacity=capmax)  # warm
