@@ -1003,13 +1003,15 @@ def main():
                   "form": {1: "per-row tables", 2: "memoised walks"}[sst["tables"]],
                   "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
         # fscale 0 (optimal under the .diff weights): a 1M-node search expands
-        # ~48k nodes.  16384 searches start at once in 2^17-column workspaces
-        # (8.9 MB per lane with tables, 60% of the free HBM); the few that
-        # outgrow them rerun in 2^19-column ones (capacity escalation; round
-        # 3 ran 512 searches, round 4's first runs 4096, all at 2^19)
-        cap0 = 1 << int(os.environ.get("CPD_BENCH_CAP0_LOG2", "17"))  # A/B
+        # ~48k nodes.  65536 searches start at once in 2^15-column workspaces
+        # (2.2 MB per lane with tables); the ~60% that outgrow them rerun at
+        # 2^17, then 2^19 (capacity escalation): each search is a latency
+        # chain, so lanes buy throughput (16384 lanes at 2^17: 1,657 q/s,
+        # 65536 at 2^15: 3,389, 131072 at 2^14: 3,371 in twice the time;
+        # profiles/search_lanes_ab/).  Round 3 ran 512 searches.
+        cap0 = 1 << int(os.environ.get("CPD_BENCH_CAP0_LOG2", "15"))  # A/B
         capmax = 1 << 19
-        zq = int(os.environ.get("CPD_BENCH_ZQ", "16384"))  # searches in the leg (A/B)
+        zq = int(os.environ.get("CPD_BENCH_ZQ", "65536"))  # searches in the leg (A/B)
         zs = rng.integers(0, g.n, zq).astype(np.uint32)
         zt = srows[rng.integers(0, len(srows), zq)]
         six.search(zs[:64], zt[:64], capacity=capmax)  # warm

@@ -3493,8 +3493,11 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
                 ts_chunk_max(1u << 30), s, 4u);
 }
 
-uint32_t search_slots(uint32_t nq) {  // lanes with a workspace: whole blocks of 4 waves
-    static const uint32_t waves = std::max(4u, env_u32("CPD_SEARCH_WAVES", 256));
+// Lane slots for nq searches: at most CPD_SEARCH_WAVES (1024) one-wave
+// workgroups, in multiples of 4 waves (64k lanes: 3,389 q/s at fscale 0 on
+// the 1M graph against 1,657 with 256 waves, profiles/search_lanes_ab/)
+uint32_t search_slots(uint32_t nq) {
+    static const uint32_t waves = std::max(4u, env_u32("CPD_SEARCH_WAVES", 1024));
     const uint32_t want = (nq + 63u) / 64u;
     const uint32_t w = std::max(1u, std::min(waves, want));
     return 64u * ((w + 3u) / 4u * 4u);
