@@ -1458,14 +1458,6 @@ bool up_priority_on() {
     return on;
 }
 
-bool emit_after_up() {
-    static const bool on = [] {
-        const char* e = std::getenv("CPD_EMIT_AFTER_UP");
-        return e && *e == '1';
-    }();
-    return on;
-}
-
 // CPD_OVERLAP=0: no early up-sweep of the next batch (A/B; identical rows).
 bool overlap_on() {
     static const bool on = env_on("CPD_OVERLAP");
@@ -1550,10 +1542,6 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     const double t2 = now_seconds();
     hipStream_t es = g->async ? g->estream : g->stream;
     if (es != g->stream) HIP_CHECK(hipStreamWaitEvent(es, g->ev_fm, 0));
-    // CPD_EMIT_AFTER_UP=1: the count and emit also wait for the next batch's
-    // early up-sweep, so that they run beside its down-sweep instead (A/B)
-    if (es != g->stream && g->prepped && emit_after_up())
-        HIP_CHECK(hipStreamWaitEvent(es, g->ev_up, 0));
     // the batch's rows become table rows r->nrows + i, written by lane pos_of[i]
     const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
     CPD_REQUIRE(r->moves.n >= (size_t)(r->nrows + k) * r->wpr, CPD_E_ARG,
