@@ -988,7 +988,7 @@ def main():
         six.append_rows(sr)
         del sr
         six.set_weights(w_cong)
-        sq = 20000
+        sq = int(os.environ.get("CPD_BENCH_SQ", "20000"))  # fscale-0.1 searches (A/B)
         ss = rng.integers(0, g.n, sq).astype(np.uint32)
         st_ = srows[rng.integers(0, len(srows), sq)]
         wst = six.search(ss[:256], st_[:256], fscale=0.1)[4]  # warm: tables built here
@@ -1031,7 +1031,7 @@ def main():
                                                max(1.0, float(zcnt[:, 0].sum())), 2)}
         # the fscale-0.1 queries with the memoised-walk form (what a
         # worker-sized index, whose tables do not fit, runs)
-        wq = 16384  # as many searches as lanes (round 4's first lines: 4096)
+        wq = min(sq, int(os.environ.get("CPD_BENCH_WQ", "16384")))  # walks-form searches (A/B)
         _, _, _, _, wsst = six.search(ss[:wq], st_[:wq], fscale=0.1, tables="walks")
         search["walks_form"] = {
             "queries": wq, "lanes": int(wsst["lanes"]), "fscale": 0.1,
