@@ -979,7 +979,8 @@ def main():
     # CPD-heuristic search leg: 256 rows of the index, the
     # .diff stand-in weights, hscale 1 / fscale 0.1 (10%-bounded: at fscale 0
     # a 1M-node search inserts up to ~235k nodes, a lane-serial search's
-    # worst case), 20k queries
+    # worst case), 65536 queries (20k in round 3-4: 329k q/s; 65536 fill the
+    # 1024 search waves: 820k, profiles/r04ar_bench_sq64k.json)
     search = None
     if args.sample is None and not args.no_search:
         srows = last_targets[:256]
@@ -988,7 +989,7 @@ def main():
         six.append_rows(sr)
         del sr
         six.set_weights(w_cong)
-        sq = int(os.environ.get("CPD_BENCH_SQ", "20000"))  # fscale-0.1 searches (A/B)
+        sq = int(os.environ.get("CPD_BENCH_SQ", "65536"))  # fscale-0.1 searches (A/B)
         ss = rng.integers(0, g.n, sq).astype(np.uint32)
         st_ = srows[rng.integers(0, len(srows), sq)]
         wst = six.search(ss[:256], st_[:256], fscale=0.1)[4]  # warm: tables built here
@@ -1031,7 +1032,7 @@ def main():
                                                max(1.0, float(zcnt[:, 0].sum())), 2)}
         # the fscale-0.1 queries with the memoised-walk form (what a
         # worker-sized index, whose tables do not fit, runs)
-        wq = min(sq, int(os.environ.get("CPD_BENCH_WQ", "16384")))  # walks-form searches (A/B)
+        wq = min(sq, int(os.environ.get("CPD_BENCH_WQ", "65536")))  # walks-form searches (A/B)
         _, _, _, _, wsst = six.search(ss[:wq], st_[:wq], fscale=0.1, tables="walks")
         search["walks_form"] = {
             "queries": wq, "lanes": int(wsst["lanes"]), "fscale": 0.1,
