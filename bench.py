@@ -993,7 +993,14 @@ def main():
         ss = rng.integers(0, g.n, sq).astype(np.uint32)
         st_ = srows[rng.integers(0, len(srows), sq)]
         wst = six.search(ss[:256], st_[:256], fscale=0.1)[4]  # warm: tables built here
-        _, _, sfin, scnt, sst = six.search(ss, st_, fscale=0.1)
+        # first-pass columns per lane of the fscale-0.1 and walks legs (A/B);
+        # the searches that outgrow it rerun up to 2^19 (capacity escalation).
+        # 2^13: every search gets a lane (2^15 fit 33024 tables-form lanes in
+        # the workspace share); 2^12 leaves a rerun tail that halves the rate
+        # (profiles/search_cap_ab/)
+        scap = 1 << int(os.environ.get("CPD_BENCH_SCAP_LOG2", "13"))
+        _, _, sfin, scnt, sst = six.search(ss, st_, fscale=0.1, capacity=scap,
+                                           capacity_max=1 << 19)
         tot = comm.reduce([float(sq), sst["kernel_ms"]], "SUM")
         (smax,) = comm.reduce([sst["kernel_ms"]], "MAX")
         search = {"queries_per_s": round(tot[0] / (smax / 1e3), 1) if smax else 0.0,
@@ -1001,6 +1008,7 @@ def main():
                   "mean_expanded": round(float(scnt[:, 0].mean()), 1),
                   "finished": int(sfin.sum()), "overflow": int(sst["overflow"]),
                   "kernel_ms": round(sst["kernel_ms"], 3), "lanes": int(sst["lanes"]),
+                  "capacity": scap, "reruns": int(sst["reruns"]),
                   "form": {1: "per-row tables", 2: "memoised walks"}[sst["tables"]],
                   "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
         # fscale 0 (optimal under the .diff weights): a 1M-node search expands
@@ -1033,9 +1041,11 @@ def main():
         # the fscale-0.1 queries with the memoised-walk form (what a
         # worker-sized index, whose tables do not fit, runs)
         wq = min(sq, int(os.environ.get("CPD_BENCH_WQ", "65536")))  # walks-form searches (A/B)
-        _, _, _, _, wsst = six.search(ss[:wq], st_[:wq], fscale=0.1, tables="walks")
+        _, _, _, _, wsst = six.search(ss[:wq], st_[:wq], fscale=0.1, tables="walks",
+                                      capacity=scap, capacity_max=1 << 19)
         search["walks_form"] = {
             "queries": wq, "lanes": int(wsst["lanes"]), "fscale": 0.1,
+            "reruns": int(wsst["reruns"]),
             "queries_per_s": round(wq / (wsst["kernel_ms"] / 1e3), 1) if wsst["kernel_ms"]
             else 0.0}
         search_sample = (six, ss[:2000], st_[:2000], srows, ss, st_, zs, zt)
