@@ -219,26 +219,86 @@ void write_scen(const std::string& path, const Pairs& q) {
 }
 
 Pairs read_query_file(const std::string& path) {
-    std::string s = slurp(path);
-    Pairs q;
-    int64_t expect = -1;
-    for_lines(s, [&](Line ln, size_t lineno) {
-        int64_t a, b;
-        if (expect < 0) {
-            if (!ln.i64(a)) throw Error(CPD_E_IO, path + ": missing query count");
-            expect = a;
-            q.reserve((size_t)a);
-            return;
-        }
-        if (!ln.i64(a)) return;  // blank
-        if (!ln.i64(b)) throw Error(CPD_E_IO, path + ": bad query line " + std::to_string(lineno + 1));
-        q.push_back({to_u32(a, "query source"), to_u32(b, "query target")});
-    });
-    if (expect < 0) expect = 0;
-    if ((int64_t)q.size() != expect)
-        throw Error(CPD_E_IO, path + ": header says " + std::to_string(expect) + " queries, file has " +
-                                  std::to_string(q.size()));
+    std::vector<uint32_t> s, t;
+    read_query_file(path, 1, s, t);
+    Pairs q(s.size());
+    for (size_t i = 0; i < s.size(); ++i) q[i] = {s[i], t[i]};
     return q;
+}
+
+void read_query_file(const std::string& path, int threads, std::vector<uint32_t>& s,
+                     std::vector<uint32_t>& t) {
+    const std::string text = slurp(path);
+    const char* const b = text.data();
+    const char* const e = b + text.size();
+    // header: the query count (process_query.py:95); a file without one is empty
+    const char* body = static_cast<const char*>(std::memchr(b, '\n', text.size()));
+    body = body ? body + 1 : e;
+    int64_t expect = 0;
+    {
+        Line h{b, body};
+        if (!text.empty() && !h.i64(expect)) throw Error(CPD_E_IO, path + ": missing query count");
+    }
+    // the body cut into pieces at line starts, each parsed by a thread into
+    // its own arrays, then copied into place: a 1M-query file (~14 MB) is a
+    // ~30-ms scan for one thread (process_query.py:93-96 writes one per worker
+    // per batch)
+    const size_t len = (size_t)(e - body);
+    const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), len >> 20));
+    std::vector<const char*> cut(T + 1, e);
+    cut[0] = body;
+    for (size_t k = 1; k < T; ++k) {
+        const char* p = body + len * k / T;
+        if (p < cut[k - 1]) p = cut[k - 1];
+        const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
+        cut[k] = nl ? nl + 1 : e;
+    }
+    std::vector<std::vector<uint32_t>> ps(T), pt(T);
+    std::vector<const char*> bad(T, nullptr);
+    auto parse = [&](size_t k) {
+        const char* p = cut[k];
+        const char* end = cut[k + 1];
+        ps[k].reserve((size_t)(end - p) / 12 + 1);
+        pt[k].reserve((size_t)(end - p) / 12 + 1);
+        while (p < end) {
+            const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(end - p)));
+            const char* le = nl ? nl : end;
+            Line ln{p, le};
+            int64_t x, y;
+            if (ln.i64(x)) {  // else blank
+                if (!ln.i64(y) || x < 0 || y < 0 || x > 0xFFFFFFFFll || y > 0xFFFFFFFFll) {
+                    bad[k] = p;
+                    return;
+                }
+                ps[k].push_back((uint32_t)x);
+                pt[k].push_back((uint32_t)y);
+            }
+            p = le + 1;
+        }
+    };
+    if (T == 1) {
+        parse(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t k = 0; k < T; ++k) th.emplace_back(parse, k);
+        for (auto& x : th) x.join();
+    }
+    for (size_t k = 0; k < T; ++k)
+        if (bad[k]) {
+            const size_t lineno = 1 + (size_t)std::count(b, bad[k], '\n');
+            throw Error(CPD_E_IO, path + ": bad query line " + std::to_string(lineno));
+        }
+    std::vector<size_t> at(T + 1, 0);
+    for (size_t k = 0; k < T; ++k) at[k + 1] = at[k] + ps[k].size();
+    if ((int64_t)at[T] != expect)
+        throw Error(CPD_E_IO, path + ": header says " + std::to_string(expect) + " queries, file has " +
+                                  std::to_string(at[T]));
+    s.resize(at[T]);
+    t.resize(at[T]);
+    for (size_t k = 0; k < T; ++k) {
+        std::copy(ps[k].begin(), ps[k].end(), s.begin() + (std::ptrdiff_t)at[k]);
+        std::copy(pt[k].begin(), pt[k].end(), t.begin() + (std::ptrdiff_t)at[k]);
+    }
 }
 
 uint64_t graph_fingerprint(uint32_t n, const uint32_t* row_ptr, const uint32_t* dst,

@@ -43,6 +43,10 @@ using Pairs = std::vector<std::pair<uint32_t, uint32_t>>;
 Pairs read_scen(const std::string& path);
 void write_scen(const std::string& path, const Pairs& q);
 Pairs read_query_file(const std::string& path);
+// The same file as two arrays (sources, targets), its lines parsed by up to
+// `threads` threads (pieces of >= 1 MB).
+void read_query_file(const std::string& path, int threads, std::vector<uint32_t>& s,
+                     std::vector<uint32_t>& t);
 
 uint64_t graph_fingerprint(uint32_t n, const uint32_t* row_ptr, const uint32_t* dst,
                            const uint32_t* w);
