@@ -230,6 +230,17 @@ class Comm:
         dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
         return t.tolist()
 
+    def gather(self, vals):
+        """Every rank's `vals` (floats), in rank order."""
+        if not self.pg:
+            return [list(vals)]
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor(vals, dtype=torch.float64, device=self.device or "cpu")
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t)
+        return [x.tolist() for x in out]
+
 
 # The result line's file descriptor: stdout, or (with RCCL) a copy of it —
 # RCCL prints its version banner on fd 1 when a communicator starts, so fd 1
@@ -278,6 +289,19 @@ class FileComm:
         allv = self._exchange(list(vals))
         fn = {"SUM": sum, "MAX": max, "MIN": min}[op]
         return [fn(v[i] for v in allv) for i in range(len(vals))]
+
+    def gather(self, vals):
+        return [list(v) for v in self._exchange(list(vals))]
+
+
+def rank_table(B, steps, elapsed):
+    """The N > 1 line's per-rank view: each rank's step
+    time and rows/s, and the spread — which rank limits the curve."""
+    per = [{"rank": r, "ms_per_step": round(e / steps * 1e3, 3),
+            "rows_per_s": round(B * steps / e, 1) if e else 0.0} for r, e in enumerate(elapsed)]
+    lo, hi = min(elapsed), max(elapsed)
+    return {"per_rank": per, "slowest_rank": max(range(len(elapsed)), key=lambda r: elapsed[r]),
+            "imbalance_max_over_min": round(hi / lo, 4) if lo else None}
 
 
 def shard_targets(nodenum, world, method, key, rank):
@@ -631,6 +655,9 @@ def full_build_leg(args, xy, world, rank, device, comm, runner=subprocess.run):
     rec = full_build(args, xy, world, rank, device, comm, runner)
     (tmax,) = comm.reduce([rec["total_s"]], "MAX")
     tot = comm.reduce([float(rec["rows"]), float(rec["runs"]), float(rec["export_bytes"])], "SUM")
+    # every worker's own figures: which one limits the node
+    allr = comm.gather([float(rec["worker"]), rec["total_s"], float(rec["rows"]),
+                        float(rec.get("rows_s", 0.0))])
     W = full_build_workers(args, world)
     fb = {"what": f"bin/make_cpd_auto worker(s) 0..{world - 1} of {W} ({args.partmethod} "
                   f"{args.partkey}), one worker per rank: all its rows, cold plan cache, "
@@ -641,7 +668,13 @@ def full_build_leg(args, xy, world, rank, device, comm, runner=subprocess.run):
           "export_GB": round(tot[2] / 1e9, 2),
           "rank0": rec,
           "rank0_export_GBps": round(rec["export_bytes"] / rec["export_span_s"] / 1e9, 2)
-          if rec.get("export_span_s") else None}
+          if rec.get("export_span_s") else None,
+          "per_rank": [{"rank": r, "worker": int(v[0]), "total_s": round(v[1], 3), "rows": int(v[2]),
+                        "rows_per_s": round(v[2] / v[1], 1) if v[1] else 0.0,
+                        "rows_phase_s": round(v[3], 3)} for r, v in enumerate(allr)],
+          "slowest_rank": max(range(len(allr)), key=lambda r: allr[r][1]),
+          "imbalance_max_over_min": round(max(v[1] for v in allr) / min(v[1] for v in allr), 4)
+          if min(v[1] for v in allr) > 0 else None}
     if "files_bytes" in rec:
         fb["files_GB"] = round(rec["files_bytes"] / 1e9, 2)
     return fb, rec
@@ -674,61 +707,159 @@ def _read_ready(p, deadline):
                        f"{p.stderr.read()[-300:]}")
 
 
-def serve_probe(args, xy, outdir, W, device, g, order, threads, nq=4000, nprobe=4):
-    """bin/fifo_auto (make_fifos.py:21) on the bucket files worker 0 just
-    wrote, one request through the reference's protocol (process_query.py:
-    66-111: query file, answer FIFO, JSON config with debug on for the
-    per-query side file), answers checked against the oracle's rows of
-    `nprobe` of the worker's targets."""
-    import numpy as np
-    sys.path.insert(0, PKG)
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import cpd
-    import oracle
-    fifo = os.path.join(outdir, "worker0.fifo")
-    cmd = [os.path.join(ROOT, "bin", "fifo_auto"), "--input", xy, "--partmethod",
+CONF_DEFAULT = {"hscale": 1.0, "fscale": 0.0, "time": 0, "itrs": -1, "k_moves": -1, "threads": 0,
+                "verbose": False, "debug": False, "thread_alloc": False, "no_cache": False}
+
+
+def _serve_start(args, xy, outdir, W, device, alg, fifo):
+    """bin/fifo_auto as make_fifos.py:21 starts it (resident; its FIFO at
+    `fifo`): (process, its load record, seconds until it listens)."""
+    cmd = [os.path.join(ROOT, "bin", "fifo_auto"), "--input", xy, xy + ".diff", "--partmethod",
            args.partmethod, "--partkey", str(args.partkey), "--workerid", "0", "--maxworker",
-           str(W), "--outdir", outdir, "--alg", "table-search", "--device", str(device),
-           "--fifo", fifo, "--once"]
+           str(W), "--outdir", outdir, "--alg", alg, "--device", str(device), "--fifo", fifo]
     t0 = time.time()
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    rec = _read_ready(p, t0 + 300)
+    return p, rec, time.time() - t0
+
+
+def _write_queries(path, s, t):
+    """The query file process_query.send_queries writes (process_query.py:
+    93-96): "{n}\n" then "s t" lines."""
+    import numpy as np
+    body = np.char.add(np.char.add(s.astype(str), " "), t.astype(str))
+    with open(path, "w") as f:
+        f.write(f"{len(s)}\n")
+        if len(s):
+            f.write("\n".join(body.tolist()) + "\n")
+
+
+def _serve_request(fifo, outdir, name, s, t, diff="-", **conf):
+    """One request through the reference's protocol (process_query.py:66-111:
+    query file on the shared directory, answer FIFO made first, the JSON
+    config + "qfile answer diff" line written to the worker's FIFO, the one
+    stats line read back).  Returns (stats line, wall seconds from writing
+    the request to reading the answer, query file)."""
+    qfile = os.path.join(outdir, f"query.{name}")
+    _write_queries(qfile, s, t)
+    answer = os.path.join(outdir, f"answer.{name}")
+    if os.path.exists(answer):
+        os.remove(answer)
+    os.mkfifo(answer)
+    t1 = time.time()
+    with open(fifo, "w") as f:  # process_query.py:89
+        f.write(json.dumps(dict(CONF_DEFAULT, **conf)) + "\n" + f"{qfile} {answer} {diff}\n")
+    with open(answer) as f:
+        line = f.read().strip()
+    wall = time.time() - t1
+    os.remove(answer)
+    return line, wall, qfile
+
+
+def _serve_stop(p, fifo):
     try:
-        rec = _read_ready(p, t0 + 300)
-        ready = time.time() - t0
-        rng = np.random.default_rng(7)
-        mine = cpd.owned_nodes(g.n, W, args.partmethod, args.partkey, 0)
-        probes = np.sort(rng.choice(mine, nprobe, replace=False)).astype(np.uint32)
-        s = rng.integers(0, g.n, nq).astype(np.uint32)
-        t = probes[rng.integers(0, nprobe, nq)]
-        qfile = os.path.join(outdir, "query.localhost0")
-        with open(qfile, "w") as f:  # process_query.py:93-96
-            f.write(f"{nq}\n" + "".join(f"{a} {b}\n" for a, b in zip(s, t)))
-        answer = os.path.join(outdir, "answer.localhost0")
-        os.mkfifo(answer)
-        conf = {"hscale": 1.0, "fscale": 0.0, "time": 0, "itrs": -1, "k_moves": -1, "threads": 0,
-                "verbose": False, "debug": True, "thread_alloc": False, "no_cache": False}
-        t1 = time.time()
-        with open(fifo, "w") as f:  # process_query.py:89
-            f.write(json.dumps(conf) + "\n" + f"{qfile} {answer} -\n")
-        with open(answer) as f:
-            line = f.read().strip()
-        answered = time.time() - t1
+        with open(fifo, "w") as f:
+            f.write("quit\n")
         p.wait(timeout=60)
     finally:
         if p.poll() is None:
             p.kill()
             p.wait()
-    res = np.loadtxt(qfile + ".res", dtype=np.uint64, ndmin=2)
+
+
+def _stats(line):
+    """The worker's 10-field line (process_query.py:199-208), times in s."""
+    v = [int(x) for x in line.split(",")]
+    return {"n_expanded": v[0], "n_inserted": v[1], "n_touched": v[2], "n_updated": v[3],
+            "n_surplus": v[4], "plen": v[5], "finished": v[6], "t_receive_s": v[7] / 1e9,
+            "t_astar_s": v[8] / 1e9, "t_search_s": v[9] / 1e9}
+
+
+def serve_leg(args, xy, outdir, W, device, g, order, threads, nprobe=4, big=1_000_000,
+              probe_q=4000, search_q=65536, search_probe_q=1000):
+    """The drop-in server on the bucket files worker 0 just wrote (VERDICT
+    r04 item 1): bin/fifo_auto --alg table-search (make_fifos.py:21) with a
+    probe request (debug side file, `nprobe` of the worker's targets) checked
+    against the oracle, then one timed request of `big` queries (s uniform, t
+    uniform over all the worker's targets; debug off) — q/s through the
+    protocol and the worker's own t_receive / t_search split; then bin/
+    fifo_auto --alg cpd-search on the same files, congested weights (the
+    .diff gen_synth wrote beside the .xy), fscale 0.1: a probe request checked
+    against the oracle's ora_cpd_search and a timed request of `search_q`."""
+    import numpy as np
+    sys.path.insert(0, PKG)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpd
+    import oracle
+    rng = np.random.default_rng(7)
+    mine = cpd.owned_nodes(g.n, W, args.partmethod, args.partkey, 0)
+    probes = np.sort(rng.choice(mine, nprobe, replace=False)).astype(np.uint32)
     off, runs = oracle.build_rows(g.row_ptr, g.dst, g.w, order, probes, threads=threads)
-    rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, order, probes, off, runs, s, t,
-                                     threads=threads)
-    exact = bool(len(res) == nq and np.array_equal(res[:, 0], s) and np.array_equal(res[:, 2], rc)
-                 and np.array_equal(res[:, 3], rh) and np.array_equal(res[:, 4], rf))
-    return {"what": "bin/fifo_auto on worker 0's bucket files, one request through the "
-                    "reference FIFO protocol (debug side file), vs the oracle",
-            "ready_s": round(ready, 3), "load": rec, "request_s": round(answered, 3),
-            "queries": nq, "probe_targets": nprobe, "answer": line,
-            "bit_exact": exact}
+    out = {"what": "bin/fifo_auto on worker 0's bucket files through the reference FIFO protocol "
+                   "(query file, answer FIFO, JSON config line): probe requests vs the oracle, "
+                   "timed requests with debug off"}
+    fifo = os.path.join(outdir, "worker0.fifo")
+    # ---- table-search
+    p, rec, ready = _serve_start(args, xy, outdir, W, device, "table-search", fifo)
+    try:
+        s = rng.integers(0, g.n, probe_q).astype(np.uint32)
+        t = probes[rng.integers(0, nprobe, probe_q)]
+        line, wall, qfile = _serve_request(fifo, outdir, "probe", s, t, debug=True)
+        res = np.loadtxt(qfile + ".res", dtype=np.uint64, ndmin=2)
+        rc, rh, rf = oracle.table_search(g.row_ptr, g.dst, g.w, order, probes, off, runs, s, t,
+                                         threads=threads)
+        exact = bool(len(res) == probe_q and np.array_equal(res[:, 0], s)
+                     and np.array_equal(res[:, 2], rc) and np.array_equal(res[:, 3], rh)
+                     and np.array_equal(res[:, 4], rf))
+        bs = rng.integers(0, g.n, big).astype(np.uint32)
+        bt = mine[rng.integers(0, len(mine), big)].astype(np.uint32)
+        _serve_request(fifo, outdir, "warm", bs, bt)  # first request of this size: buffers
+        bline, bwall, _ = _serve_request(fifo, outdir, "big", bs, bt)
+    finally:
+        _serve_stop(p, fifo)
+    st = _stats(bline)
+    out.update({"ready_s": round(ready, 3), "load": rec, "probe_queries": probe_q,
+                "probe_targets": nprobe, "answer": line, "bit_exact": exact,
+                "request_s": round(wall, 3),
+                "table_search": {"queries": big, "wall_s": round(bwall, 4),
+                                 "queries_per_s": round(big / bwall, 1),
+                                 "t_receive_s": st["t_receive_s"], "t_search_s": st["t_search_s"],
+                                 "finished": st["finished"], "answer": bline,
+                                 "note": "wall = request written to answer read (the head's "
+                                         "t_partition without ssh); the query file is written "
+                                         "before, as process_query's t_prepare"}})
+    # ---- cpd-search (walks form: the worker's 125k rows have no room for
+    # per-row tables), congested weights, fscale 0.1
+    w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)  # == gen_synth's .diff
+    p, rec2, ready2 = _serve_start(args, xy, outdir, W, device, "cpd-search", fifo)
+    try:
+        s = rng.integers(0, g.n, search_probe_q).astype(np.uint32)
+        t = probes[rng.integers(0, nprobe, search_probe_q)]
+        line2, _, qfile = _serve_request(fifo, outdir, "sprobe", s, t, diff=xy + ".diff",
+                                         fscale=0.1, debug=True)
+        res = np.loadtxt(qfile + ".res", dtype=np.uint64, ndmin=2)
+        rc, rp, rf, _ = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, order, probes, off, runs,
+                                          s, t, fscale=0.1, threads=threads)
+        sexact = bool(len(res) == search_probe_q and np.array_equal(res[:, 2], rc)
+                      and np.array_equal(res[:, 3], rp) and np.array_equal(res[:, 4], rf))
+        ss = rng.integers(0, g.n, search_q).astype(np.uint32)
+        stt = mine[rng.integers(0, len(mine), search_q)].astype(np.uint32)
+        sline, swall, _ = _serve_request(fifo, outdir, "sbig", ss, stt, diff=xy + ".diff",
+                                         fscale=0.1)
+    finally:
+        _serve_stop(p, fifo)
+    st2 = _stats(sline)
+    out["cpd_search"] = {"ready_s": round(ready2, 3), "probe_queries": search_probe_q,
+                         "probe_answer": line2, "bit_exact": sexact, "fscale": 0.1,
+                         "queries": search_q, "wall_s": round(swall, 4),
+                         "queries_per_s": round(search_q / swall, 1),
+                         "t_receive_s": st2["t_receive_s"], "t_astar_s": st2["t_astar_s"],
+                         "t_search_s": st2["t_search_s"],
+                         "queries_per_s_search": round(search_q / st2["t_search_s"], 1)
+                         if st2["t_search_s"] else None,
+                         "finished": st2["finished"], "mean_expanded": round(st2["n_expanded"] / search_q, 1),
+                         "answer": sline}
+    return out
 
 
 def build_plan_child(args, ppath, device):
@@ -774,8 +905,8 @@ def full_build_only(args, world, rank, local):
         import cpd
         g = cpd.synth_road_graph(args.width, args.width, seed=args.seed, style=args.style)
         try:
-            fb["serve"] = serve_probe(args, xy, full_build_dir(args, world), W, gpu, g,
-                                      cpd.dfs_preorder(g.row_ptr, g.dst), host_threads(args))
+            fb["serve"] = serve_leg(args, xy, full_build_dir(args, world), W, gpu, g,
+                                    cpd.dfs_preorder(g.row_ptr, g.dst), host_threads(args))
         except Exception as e:  # reported
             fb["serve"] = {"error": str(e)[-400:]}
     comm.barrier()
@@ -895,6 +1026,7 @@ def main():
     comm.barrier()
     elapsed = time.perf_counter() - t0
     (elapsed_max,) = comm.reduce([elapsed], "MAX")
+    ranks = rank_table(B, args.steps, [v[0] for v in comm.gather([elapsed])])
     kt = dev.timing_get()
     dev.timing(False)
     nrows, nruns = rows.count()
@@ -904,9 +1036,26 @@ def main():
     rng = np.random.default_rng(100 + rank)
     extra = {}
     w_cong = cpd.synth_congestion(g.w, frac=0.1, lo=1.0, hi=3.0, seed=3)
+    runs_form = None
     if args.sample is None:
-        # the rank's last batch of rows, kept as RLE too (both forms timed)
+        # the rank's last batch of rows, kept as RLE too (both forms timed).
+        # Making this index decodes the batch's run words into HBM
+        # (moves_runs): the reference's own row form (warthog's RLE words,
+        # README.md:92-93), timed here so the line states its cost (VERDICT
+        # r04 item 8)
+        dev.timing(True)
+        dev.timing_reset()
         ix = cpd.Index(dev, rows=rows)
+        dkt = dev.timing_get()
+        dev.timing(False)
+        dec = dkt.get("moves_runs")
+        if dec and dec["ms"] > 0:
+            step_s = elapsed_max / args.steps
+            runs_form = {"decode_ms_per_batch": round(dec["ms"], 3),
+                         "decode_GBps": round(dec["bytes"] / (dec["ms"] / 1e3) / 1e9, 1),
+                         "rows_per_s_runs": round(world * B / (step_s + dec["ms"] / 1e3), 1),
+                         "note": "a step that also decodes its batch's run words into HBM "
+                                 "(moves_runs after the build, not overlapped)"}
         nq = args.queries
         qs = rng.integers(0, g.n, nq).astype(np.uint32)
         qt = last_targets[rng.integers(0, len(last_targets), nq)]
@@ -989,53 +1138,47 @@ def main():
         six.append_rows(sr)
         del sr
         six.set_weights(w_cong)
-        sq = int(os.environ.get("CPD_BENCH_SQ", "65536"))  # fscale-0.1 searches (A/B)
+        # every leg runs the library's workspace policy (capacity 0: the
+        # first pass's columns per lane, the passes at 4x that resume the
+        # searches that outgrew it, the share of HBM) — what fifo_auto runs
+        sq = 65536  # as many searches as the 1024 search waves have lanes
         ss = rng.integers(0, g.n, sq).astype(np.uint32)
         st_ = srows[rng.integers(0, len(srows), sq)]
         wst = six.search(ss[:256], st_[:256], fscale=0.1)[4]  # warm: tables built here
-        # first-pass columns per lane of the fscale-0.1 and walks legs (A/B);
-        # the searches that outgrow it rerun up to 2^19 (capacity escalation).
-        # 2^13: every search gets a lane (2^15 fit 33024 tables-form lanes in
-        # the workspace share); 2^12 leaves a rerun tail that halves the rate
-        # (profiles/search_cap_ab/)
-        scap = 1 << int(os.environ.get("CPD_BENCH_SCAP_LOG2", "13"))
-        _, _, sfin, scnt, sst = six.search(ss, st_, fscale=0.1, capacity=scap,
-                                           capacity_max=1 << 19)
+        _, _, sfin, scnt, sst = six.search(ss, st_, fscale=0.1)
         tot = comm.reduce([float(sq), sst["kernel_ms"]], "SUM")
         (smax,) = comm.reduce([sst["kernel_ms"]], "MAX")
+
+        def passes(stt):
+            return {"capacity": int(stt["capacity"]), "capacity_last": int(stt["capacity_last"]),
+                    "passes": int(stt["passes"]), "reruns": int(stt["reruns"]),
+                    "resumed": int(stt["resumed"]), "restarted": int(stt["restarted"]),
+                    "wasted_expanded": int(stt["wasted_expanded"])}
         search = {"queries_per_s": round(tot[0] / (smax / 1e3), 1) if smax else 0.0,
-                  "config": "256-row dense index, .diff stand-in weights, hscale 1, fscale 0.1",
-                  "mean_expanded": round(float(scnt[:, 0].mean()), 1),
+                  "config": "256-row dense index, .diff stand-in weights, hscale 1, fscale 0.1, "
+                            "library workspace policy",
+                  "queries": sq, "mean_expanded": round(float(scnt[:, 0].mean()), 1),
                   "finished": int(sfin.sum()), "overflow": int(sst["overflow"]),
                   "kernel_ms": round(sst["kernel_ms"], 3), "lanes": int(sst["lanes"]),
-                  "capacity": scap, "reruns": int(sst["reruns"]),
+                  **passes(sst),
                   "form": {1: "per-row tables", 2: "memoised walks"}[sst["tables"]],
                   "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
         # fscale 0 (optimal under the .diff weights): a 1M-node search expands
-        # ~48k nodes.  65536 searches start at once in 2^15-column workspaces
-        # (2.2 MB per lane with tables); the ~60% that outgrow them rerun at
-        # 2^17, then 2^19 (capacity escalation): each search is a latency
-        # chain, so lanes buy throughput (16384 lanes at 2^17: 1,657 q/s,
-        # 65536 at 2^15: 3,389, 131072 at 2^14: 3,371 in twice the time;
-        # profiles/search_lanes_ab/).  Round 3 ran 512 searches.
-        cap0 = 1 << int(os.environ.get("CPD_BENCH_CAP0_LOG2", "15"))  # A/B
-        capmax = 1 << 19
-        zq = int(os.environ.get("CPD_BENCH_ZQ", "65536"))  # searches in the leg (A/B)
+        # ~49k nodes; 65536 searches start at once in 2^15-column workspaces
+        # and the ~60% that outgrow them spill their state and resume at 2^17
+        # (then 2^19): each search is a latency chain, so lanes buy throughput
+        # (profiles/search_lanes_ab/).  Ranks sharing one card in a rehearsal
+        # split its HBM.
+        zq = 65536
         zs = rng.integers(0, g.n, zq).astype(np.uint32)
         zt = srows[rng.integers(0, len(srows), zq)]
-        six.search(zs[:64], zt[:64], capacity=capmax)  # warm
-        # workspace share of the free HBM: 0.85 gives the 2^17 reruns ~26k
-        # lanes (0.6: ~18k; 3,655 against 3,375 q/s, profiles/search_lanes_ab/)
-        # (ranks sharing one card in a rehearsal split it)
-        zwf = float(os.environ.get("CPD_BENCH_ZWF", str(0.6 / world if share else 0.85)))
-        _, _, zfin, zcnt, zst = six.search(zs, zt, capacity=cap0, capacity_max=capmax,
-                                           workspace_frac=zwf)
+        six.search(zs[:64], zt[:64])  # warm
+        _, _, zfin, zcnt, zst = six.search(zs, zt, workspace_frac=0.6 / world if share else 0.0)
         ztot = comm.reduce([float(zq), zst["kernel_ms"]], "SUM")
         (zmax,) = comm.reduce([zst["kernel_ms"]], "MAX")
         search["fscale0"] = {
             "queries_per_s": round(ztot[0] / (zmax / 1e3), 1) if zmax else 0.0,
-            "queries": zq, "capacity": cap0, "capacity_max": capmax,
-            "reruns": int(zst["reruns"]), "lanes": int(zst["lanes"]),
+            "queries": zq, **passes(zst), "lanes": int(zst["lanes"]),
             "mean_expanded": round(float(zcnt[:, 0].mean()), 1),
             "finished": int(zfin.sum()), "overflow": int(zst["overflow"]),
             "kernel_ms": round(zst["kernel_ms"], 3),
@@ -1044,13 +1187,10 @@ def main():
                                                max(1.0, float(zcnt[:, 0].sum())), 2)}
         # the fscale-0.1 queries with the memoised-walk form (what a
         # worker-sized index, whose tables do not fit, runs)
-        wq = min(sq, int(os.environ.get("CPD_BENCH_WQ", "65536")))  # walks-form searches (A/B)
-        _, _, _, _, wsst = six.search(ss[:wq], st_[:wq], fscale=0.1, tables="walks",
-                                      capacity=scap, capacity_max=1 << 19)
+        _, _, _, _, wsst = six.search(ss, st_, fscale=0.1, tables="walks")
         search["walks_form"] = {
-            "queries": wq, "lanes": int(wsst["lanes"]), "fscale": 0.1,
-            "reruns": int(wsst["reruns"]),
-            "queries_per_s": round(wq / (wsst["kernel_ms"] / 1e3), 1) if wsst["kernel_ms"]
+            "queries": sq, "lanes": int(wsst["lanes"]), "fscale": 0.1, **passes(wsst),
+            "queries_per_s": round(sq / (wsst["kernel_ms"] / 1e3), 1) if wsst["kernel_ms"]
             else 0.0}
         search_sample = (six, ss[:2000], st_[:2000], srows, ss, st_, zs, zt)
     # walk kernel vs its roofline: per query 8 (s, t) + 4 (row) + 13 (cost,
@@ -1149,7 +1289,7 @@ def main():
             rc, rp, rf, rs = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, order, srows,
                                                sref[0], sref[1], ss2[:64], st2[:64],
                                                threads=threads)
-            gcs, gps, gfs, gcnt, _ = six.search(ss2[:64], st2[:64], capacity=1 << 19)
+            gcs, gps, gfs, gcnt, _ = six.search(ss2[:64], st2[:64])
             search["fscale0"]["parity_64_bit_exact"] = bool(
                 np.array_equal(gcs, rc) and np.array_equal(gps, rp) and np.array_equal(gfs, rf)
                 and np.array_equal(gcnt.astype(np.uint64), rs))
@@ -1181,8 +1321,8 @@ def main():
         W = full_build_workers(args, world)
         if rank == 0 and "files_bytes" in rec:
             try:
-                fb["serve"] = serve_probe(args, fb_xy, full_build_dir(args, world), W, gpu, g,
-                                          plan.order(), host_threads(args))
+                fb["serve"] = serve_leg(args, fb_xy, full_build_dir(args, world), W, gpu, g,
+                                        plan.order(), host_threads(args))
             except Exception as e:  # reported, never fatal to the GPU numbers
                 fb["serve"] = {"error": str(e)[-400:]}
         comm.barrier()
@@ -1209,6 +1349,9 @@ def main():
         out["queries_e2e_note"] = ("cpd_query_batch by the host clock: (s, t) upload, target sort "
                                    "and gather on the GPU, walk, results scattered back and "
                                    "copied out")
+        out["ranks"] = ranks
+        out["runs_form"] = runs_form
+        out["rows_per_s_runs"] = runs_form["rows_per_s_runs"] if runs_form else None
         out.update(extra)
         emit_line(json.dumps(out))
     if use_pg:

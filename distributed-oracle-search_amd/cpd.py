@@ -96,7 +96,9 @@ class SearchStats(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("queries", "finished", "expanded", "inserted",
                                           "touched", "updated", "surplus", "plen", "overflow")] + \
                [("kernel_ms", C.c_double), ("lanes", C.c_uint64), ("tables_ms", C.c_double),
-                ("tables", C.c_int32), ("reruns", C.c_uint64)]
+                ("tables", C.c_int32), ("reruns", C.c_uint64), ("resumed", C.c_uint64),
+                ("restarted", C.c_uint64), ("wasted_expanded", C.c_uint64),
+                ("passes", C.c_uint32), ("capacity", C.c_uint32), ("capacity_last", C.c_uint32)]
 
 
 class KernelTime(C.Structure):

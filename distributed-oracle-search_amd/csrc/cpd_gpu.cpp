@@ -33,18 +33,32 @@ using namespace cpd;
 namespace {
 
 // Per-device HBM arena (cpd_device_arena): one block committed up front —
-// e.g. on a host thread while the plan is being contracted — that device
-// buffers on that device are carved from (bump allocation; a buffer carved
-// from it is never returned to it, the whole block is freed by
-// cpd_device_arena_release).  What does not fit falls back to hipMalloc.
+// e.g. on a host thread while the plan is being contracted — that the
+// long-lived bulk buffers on that device are carved from (bump allocation:
+// a carved buffer is never returned to it, the whole block is freed by
+// cpd_device_arena_release).  Only allocations inside an ArenaScope are
+// carved — a build's batch buffers, its row sets, an index's move tables —
+// so short-lived scratch never fills it; what does not fit
+// falls back to hipMalloc.  `live` counts the carved buffers still held:
+// the release refuses while any is.
 struct Arena {
     char* base = nullptr;
     size_t cap = 0, top = 0;
+    size_t live = 0;
 };
 std::mutex g_arena_mu;
 std::map<int, Arena> g_arena;
+thread_local int t_arena_scope = 0;
+
+struct ArenaScope {
+    ArenaScope() { ++t_arena_scope; }
+    ~ArenaScope() { --t_arena_scope; }
+    ArenaScope(const ArenaScope&) = delete;
+    ArenaScope& operator=(const ArenaScope&) = delete;
+};
 
 void* arena_take(size_t bytes) {
+    if (t_arena_scope <= 0) return nullptr;
     int d = 0;
     if (hipGetDevice(&d) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> l(g_arena_mu);
@@ -54,14 +68,19 @@ void* arena_take(size_t bytes) {
     const size_t at = (a.top + 255u) & ~(size_t)255u;
     if (at + bytes > a.cap) return nullptr;
     a.top = at + bytes;
+    ++a.live;
     return a.base + at;
 }
 
-bool arena_owns(const void* p) {
+// true (and one live buffer fewer) when p was carved from an arena
+bool arena_drop(const void* p) {
     std::lock_guard<std::mutex> l(g_arena_mu);
     for (auto& kv : g_arena) {
         const char* c = static_cast<const char*>(p);
-        if (kv.second.base && c >= kv.second.base && c < kv.second.base + kv.second.cap) return true;
+        if (kv.second.base && c >= kv.second.base && c < kv.second.base + kv.second.cap) {
+            if (kv.second.live) --kv.second.live;
+            return true;
+        }
     }
     return false;
 }
@@ -76,7 +95,7 @@ struct DevBuf {
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { release(); }
     void release() {
-        if (p && !arena_owns(p)) (void)hipFree(p);
+        if (p && !arena_drop(p)) (void)hipFree(p);
         p = nullptr;
         n = 0;
     }
@@ -149,16 +168,17 @@ uint32_t batch_max() {
 
 // HBM per row of batch width: dist 4n (+ 2n narrow) + two buffer sets of
 // first-move rows and RLE segment states (emit overlap) + the chunked count's
-// chunk states (8 B per chunk) + leaf sets + two rows of move tables (npad / 2
+// chunk states (12 B per chunk: exit, count, entry) + leaf sets + two rows of move tables (npad / 2
 // each: the row set being built and the one a caller such as make_cpd_auto
 // is exporting).
 double batch_bytes_per_row(uint32_t n, uint32_t npad, uint32_t fmb, bool narrow, bool leaf_fm) {
     return (narrow ? 6.0 : 4.0) * n + 2.0 * (fmb / 8.0 * npad + 5.0 / 32.0 * npad) +
-           (fmb == 4 ? 8.0 * rle_count_chunks(npad) : 0.0) + (leaf_fm ? 0.5 * n : 0.0) +
+           (fmb == 4 ? 12.0 * rle_count_chunks(npad) : 0.0) + (leaf_fm ? 0.5 * n : 0.0) +
            2.0 * 0.5 * npad;
 }
 bool up_priority_on();
 bool lane_key_on();
+bool seg_order_on();
 std::vector<uint32_t> hilbert_keys(const int32_t* x, const int32_t* y, uint32_t n);
 
 }  // namespace
@@ -311,6 +331,9 @@ struct cpd_graph {
     // lane position of each caller target in the current batch (sorted by
     // lane_key when the caller gave coordinates, else by column)
     std::vector<uint32_t> lane_key;  // node -> Hilbert key of its coordinates (may be empty)
+    // first_moves' segment order: the 32-column segments by the Hilbert key
+    // of their middle column's node (empty: column order)
+    DevBuf<uint32_t> seg_order;
     // timing
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
@@ -437,6 +460,7 @@ struct cpd_graph {
 
     uint64_t hbm_reserve = 0;  // cpd_graph_set_hbm_reserve
     void reserve_batch(uint32_t want) {
+        ArenaScope carve;  // the batch's buffers: what an arena is committed for
         if (want == 0) {
             size_t free_b = 0, total_b = 0;
             HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -483,7 +507,7 @@ struct cpd_graph {
         }
         cur = 0;
         if (fmb == 4 && rle_count_chunks(npad)) {
-            rle_xs.alloc((size_t)B * rle_count_chunks(npad));
+            rle_xs.alloc(2ull * B * rle_count_chunks(npad));
             rle_cc.alloc((size_t)B * rle_count_chunks(npad));
             rle_hard.alloc(1);
         }
@@ -646,6 +670,10 @@ struct cpd_index {
     DevBuf<uint32_t> lrow, tcol, qstats;
     DevBuf<uint8_t> sws;
     DevBuf<unsigned long long> sagg;
+    // resumable overflow: the two spill pools (records of the pass that just
+    // ran / of the one running), their bump counters, record offsets
+    DevBuf<uint32_t> spool[2];
+    DevBuf<unsigned long long> stop, sat;
     bool h_ready = false, c_ready = false;
     bool searched = false;  // qstats hold the counters of the prepared queries
     // query workspace; queries run sorted by target row (qperm[i] = caller
@@ -878,6 +906,9 @@ int cpd_device_arena_release(int device) {
             std::lock_guard<std::mutex> l(g_arena_mu);
             auto it = g_arena.find(device);
             if (it == g_arena.end()) return;
+            CPD_REQUIRE(it->second.live == 0, CPD_E_ARG,
+                        "device arena still holds " + std::to_string(it->second.live) +
+                            " live buffers: free the graphs, row sets and indexes first");
             p = it->second.base;
             g_arena.erase(it);
         }
@@ -1150,9 +1181,30 @@ int cpd_graph_set_coords(cpd_graph* g, const int32_t* x, const int32_t* y) {
         CPD_REQUIRE(g, CPD_E_ARG, "null graph");
         if (!x || !y) {
             g->lane_key.clear();
+            g->seg_order.release();
             return;
         }
         g->lane_key = hilbert_keys(x, y, g->n);
+        if (seg_order_on()) {
+            // first_moves gathers each column's out-neighbours' rows: with the
+            // segments handed out in Hilbert order, the blocks one XCD runs at
+            // once cover a compact patch of the graph and gather overlapping
+            // rows (in DFS order a lattice node's cross neighbours are far)
+            const uint32_t nseg = g->npad / 32u;
+            std::vector<uint32_t> node_of(g->n);
+            for (uint32_t v = 0; v < g->n; ++v) node_of[g->order[v]] = v;
+            std::vector<uint64_t> kv(nseg);
+            for (uint32_t sg = 0; sg < nseg; ++sg) {
+                const uint32_t c = std::min(g->n - 1u, sg * 32u + 16u);
+                kv[sg] = ((uint64_t)g->lane_key[node_of[c]] << 32) | sg;
+            }
+            std::sort(kv.begin(), kv.end());
+            std::vector<uint32_t> so(nseg);
+            for (uint32_t i = 0; i < nseg; ++i) so[i] = (uint32_t)kv[i];
+            g->select();
+            g->seg_order.upload(so.data(), nseg, g->stream);
+            HIP_CHECK(hipStreamSynchronize(g->stream));
+        }
     });
 }
 
@@ -1184,6 +1236,10 @@ bool live_on() {
 }
 bool lane_key_on() {  // CPD_LANE_KEY=0: ignore cpd_graph_set_coords (A/B)
     static const bool on = env_on("CPD_LANE_KEY");
+    return on;
+}
+bool seg_order_on() {  // CPD_FM_ORDER=0: first_moves takes segments in column order (A/B)
+    static const bool on = env_on("CPD_FM_ORDER");
     return on;
 }
 
@@ -1388,7 +1444,7 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
     g->timed("first_moves", fbytes, [&] {
         launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, S.tgt.p, B, k, n, g->npad,
                            fm, g->leaf_fm ? g->leafbits.p : nullptr,
-                           g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream);
+                           g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream, g->seg_order.p);
     });
     HIP_CHECK(hipEventRecord(g->ev_fm, g->stream));
     if (stat)
@@ -1555,7 +1611,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
     if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
         HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), es));
-        g->timed("rle_count", (fm_row + st_row + 8.0 * nch) * k, [&] {
+        g->timed("rle_count", (fm_row + st_row + 12.0 * nch) * k, [&] {
             launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, es);
         });
         g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
@@ -1630,6 +1686,7 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         r->bits = g->move_bits;
         if (r->moves.n < (size_t)ntargets * r->wpr) {
             r->wait();  // an earlier build's emit may still write the old table
+            ArenaScope carve;
             r->moves.alloc((size_t)ntargets * r->wpr);
         }
         for (uint32_t b = 0; b < ntargets; b += g->B) {
@@ -1908,7 +1965,10 @@ void index_stream_dense(cpd_index* ix) {
     ix->keep_rle = false;
     ix->stream_dense = true;
     ix->mode = CPD_INDEX_DENSE;
-    ix->dense.alloc((size_t)ix->nrows * g->wpr());
+    {
+        ArenaScope carve;  // an index's move tables (fifo_auto commits them early)
+        ix->dense.alloc((size_t)ix->nrows * g->wpr());
+    }
     ix->dense_ready = true;
 }
 
@@ -2211,7 +2271,10 @@ int cpd_index_from_rows(cpd_graph* g, const cpd_rows* r, cpd_index** out) {
         index_keep_rle(ix.get(), r->total);
         if (ix->use_dense()) {  // AUTO resolves dense: the rows' tables, copied
             CPD_REQUIRE(g->npad / kFmTile < 65536u, CPD_E_RANGE, "graph too large for dense tables");
-            ix->dense.alloc((size_t)ix->nrows * g->wpr());
+            {
+                ArenaScope carve;  // an index's move tables
+                ix->dense.alloc((size_t)ix->nrows * g->wpr());
+            }
             ix->dense_ready = true;
         }
         append_built(ix.get(), r);
@@ -2354,7 +2417,10 @@ namespace {
 void ensure_dense(cpd_index* ix) {
     cpd_graph* g = ix->g;
     CPD_REQUIRE(g->npad / kFmTile < 65536u, CPD_E_RANGE, "graph too large for dense tables");
-    ix->dense.alloc((size_t)ix->nrows * g->wpr());
+    {
+        ArenaScope carve;  // an index's move tables (fifo_auto commits them early)
+        ix->dense.alloc((size_t)ix->nrows * g->wpr());
+    }
     if (ix->nrows && g->tlb != 2u)  // the runs' moves must fit the narrower tables
         validate_device_rows(ix, ix->off.p, ix->runs.p, ix->offsets.data(), ix->nrows,
                              table_move_limit(g));
@@ -2495,24 +2561,57 @@ void cpd_index_free(cpd_index* ix) {
 // ---------------------------------------------------------------------------
 // CPD-heuristic search
 
+}  // extern "C"
+
+namespace {
+
+// The search workspace policy (fifo_auto and the bench
+// run the same one).  capacity 0 = automatic: the first pass's columns per
+// lane are 2^13 when fscale > 0 (a bounded-suboptimal search expands ~140
+// nodes on the 1M bench graph) and 2^15 at fscale 0 (~49k expansions: a
+// larger first pass spills fewer searches), lowered to 2^10 at most until
+// every search of the request gets a lane (profiles/search_cap_ab/,
+// search_lanes_ab/); capacity_max 0 = 4x the graph's columns rounded up to
+// a power of 2 (a search holds each column once, its heap some stale
+// entries more), at most 2^24; workspace_frac 0 = 0.85 of the free HBM.
+// An explicit capacity keeps the old defaults (no escalation, 0.25).
+uint32_t pow2_at_least(uint64_t x) {
+    uint32_t c = 64;
+    while (c < x && c < (1u << 24)) c <<= 1;
+    return c;
+}
+
+bool search_trace() {
+    static const bool on = [] {
+        const char* e = std::getenv("CPD_SEARCH_TRACE");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
+}  // namespace
+
+extern "C" {
+
 int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st) {
     return guarded([&] {
         CPD_REQUIRE(ix, CPD_E_ARG, "null index");
         cpd_search_opts o{1.0, 0.0, -1, -1, 0, 0, 0, CPD_SEARCH_AUTO, 0.0, 0};
         if (opts) o = *opts;
-        if (!o.capacity) o.capacity = 32768;
-        CPD_REQUIRE((o.capacity & (o.capacity - 1)) == 0 && o.capacity >= 64 &&
-                        o.capacity <= (1u << 24),
-                    CPD_E_ARG, "search capacity must be a power of 2 in [64, 2^24]");
+        const bool auto_cap = o.capacity == 0;
+        CPD_REQUIRE(auto_cap || ((o.capacity & (o.capacity - 1)) == 0 && o.capacity >= 64 &&
+                                 o.capacity <= (1u << 24)),
+                    CPD_E_ARG, "search capacity must be 0 (automatic) or a power of 2 in [64, 2^24]");
         CPD_REQUIRE(o.capacity_max == 0 ||
                         ((o.capacity_max & (o.capacity_max - 1)) == 0 &&
-                         o.capacity_max >= o.capacity && o.capacity_max <= (1u << 24)),
+                         o.capacity_max >= std::max<uint32_t>(o.capacity, 64u) &&
+                         o.capacity_max <= (1u << 24)),
                     CPD_E_ARG, "search capacity_max must be 0 or a power of 2 in [capacity, 2^24]");
         CPD_REQUIRE(o.hscale >= 0.0 && o.fscale >= 0.0, CPD_E_ARG,
                     "hscale and fscale must be >= 0");
         CPD_REQUIRE(o.workspace_frac >= 0.0 && o.workspace_frac <= 0.9, CPD_E_ARG,
                     "workspace_frac must be in [0, 0.9]");
-        const double wfrac = o.workspace_frac > 0.0 ? o.workspace_frac : 0.25;
+        const double wfrac = o.workspace_frac > 0.0 ? o.workspace_frac : auto_cap ? 0.85 : 0.25;
         CPD_REQUIRE(ix->added == ix->nrows, CPD_E_ARG, "search: index incomplete");
         CPD_REQUIRE(o.tables == CPD_SEARCH_AUTO || o.tables == CPD_SEARCH_TABLES ||
                         o.tables == CPD_SEARCH_WALKS,
@@ -2564,123 +2663,239 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             tables_ms = ms;
             ix->h_ready = ix->c_ready = true;
         }
-        // workspace per lane slot: search_ws_bytes_per_slot(capacity, tables)
-        // (68 B per column of capacity with tables, 116 B with walks); as many
-        // slots (whole blocks of 4 waves) as wfrac of the free HBM holds
-        uint32_t slots = nq ? search_slots(nq) : 0u;
-        const size_t per_slot = search_ws_bytes_per_slot(o.capacity, tables);
-        if (nq) {
-            size_t free_b = 0, total_b = 0;
-            HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-            const size_t per_block = 256ull * per_slot;
-            const size_t fit =
-                std::max<size_t>(1, (size_t)(wfrac * (double)(free_b + ix->sws.n)) / per_block);
-            CPD_REQUIRE((free_b + ix->sws.n) / 2 >= per_block, CPD_E_OOM,
-                        "search workspace of 256 lanes x capacity does not fit in HBM");
-            slots = (uint32_t)std::min<size_t>(slots, fit * 256u);
-        }
-        if (nq) ix->sws.alloc((size_t)slots * per_slot);
-        ix->qstats.alloc(5ull * std::max(1u, nq));
-        ix->sagg.alloc(8);
-        HIP_CHECK(hipMemsetAsync(ix->sagg.p, 0, 8 * sizeof(unsigned long long), g->stream));
-        HIP_CHECK(hipEventRecord(a, g->stream));
-        (void)hipGetLastError();
-        if (nq)
-            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad, g->tlb,
-                              tables ? ix->hrow.p : nullptr, ix->crow.p, ix->lrow.p, n, ix->qs.p,
-                              ix->qt.p, ix->qrow.p, nq, o.hscale, o.fscale, o.k_moves, o.itrs,
-                              o.time_ns, o.virtual_tick_ns, ix->sws.p, o.capacity, slots,
-                              ix->cost.p, ix->hops.p, ix->fin.p, ix->qstats.p, ix->sagg.p,
-                              g->stream);
-        HIP_CHECK(hipGetLastError());
-        HIP_CHECK(hipEventRecord(b, g->stream));
-        unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        HIP_CHECK(hipMemcpyAsync(h, ix->sagg.p, sizeof h, hipMemcpyDeviceToHost, g->stream));
-        HIP_CHECK(hipStreamSynchronize(g->stream));
-        float ms = 0.f;
-        HIP_CHECK(hipEventElapsedTime(&ms, a, b));
-        // Capacity escalation: the searches that outgrew the workspace
-        // (fin = 2) run again from scratch, alone, with 4x the columns per
-        // lane (fewer lanes fit) until none overflows or capacity_max is
-        // reached — so a batch runs most searches at a small capacity, many
-        // lanes at once, and pays the large workspace only for the few long
-        // ones.  Their first-pass counters leave the sums; the rerun's
-        // results and counters are scattered over theirs.
-        uint64_t reruns = 0;
-        for (uint32_t cap = o.capacity; h[7] && cap < o.capacity_max;) {
-            cap = std::min(cap * 4u, o.capacity_max);
-            std::vector<uint8_t> f(nq);
-            std::vector<uint32_t> qst(5ull * nq), hq(3ull * nq);
-            HIP_CHECK(hipMemcpyAsync(f.data(), ix->fin.p, nq, hipMemcpyDeviceToHost, g->stream));
-            HIP_CHECK(hipMemcpyAsync(qst.data(), ix->qstats.p, 20ull * nq, hipMemcpyDeviceToHost, g->stream));
-            HIP_CHECK(hipMemcpyAsync(hq.data(), ix->qs.p, 4ull * nq, hipMemcpyDeviceToHost, g->stream));
-            HIP_CHECK(hipMemcpyAsync(hq.data() + nq, ix->qt.p, 4ull * nq, hipMemcpyDeviceToHost, g->stream));
-            HIP_CHECK(hipMemcpyAsync(hq.data() + 2ull * nq, ix->qrow.p, 4ull * nq, hipMemcpyDeviceToHost,
-                                     g->stream));
-            HIP_CHECK(hipStreamSynchronize(g->stream));
-            std::vector<uint32_t> idx, sub(0);
-            for (uint32_t i = 0; i < nq; ++i)
-                if (f[i] == 2u) idx.push_back(i);
-            const uint32_t m = (uint32_t)idx.size();
-            if (!m) break;
-            sub.resize(3ull * m);
-            for (uint32_t j = 0; j < m; ++j) {
-                const uint32_t i = idx[j];  // target-sorted order is kept
-                sub[j] = hq[i];
-                sub[m + j] = hq[nq + i];
-                sub[2ull * m + j] = hq[2ull * nq + i];
-                for (int k = 0; k < 5; ++k) h[k] -= qst[5ull * i + k];
-            }
-            reruns += m;
-            DevBuf<uint32_t> d_idx, d_q, d_hops, d_st;
-            DevBuf<uint64_t> d_cost;
-            DevBuf<uint8_t> d_fin;
-            DevBuf<unsigned long long> d_agg;
-            d_idx.upload(idx.data(), m, g->stream);
-            d_q.upload(sub.data(), 3ull * m, g->stream);
-            d_hops.alloc(m);
-            d_st.alloc(5ull * m);
-            d_cost.alloc(m);
-            d_fin.alloc(m);
-            d_agg.alloc(8);
-            HIP_CHECK(hipMemsetAsync(d_agg.p, 0, 8 * sizeof(unsigned long long), g->stream));
-            const size_t per2 = search_ws_bytes_per_slot(cap, tables);
-            size_t free_b = 0, total_b = 0;
-            HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-            const size_t per_block = 256ull * per2;
-            CPD_REQUIRE((free_b + ix->sws.n) / 2 >= per_block, CPD_E_OOM,
-                        "search workspace of 256 lanes x capacity " + std::to_string(cap) +
-                            " does not fit in HBM");
-            const size_t fit2 =
-                std::max<size_t>(1, (size_t)(wfrac * (double)(free_b + ix->sws.n)) / per_block);
-            const uint32_t slots2 = (uint32_t)std::min<size_t>(search_slots(m), fit2 * 256u);
-            ix->sws.alloc((size_t)slots2 * per2);
-            HIP_CHECK(hipEventRecord(a, g->stream));
-            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad, g->tlb,
-                              tables ? ix->hrow.p : nullptr, ix->crow.p, ix->lrow.p, n, d_q.p,
-                              d_q.p + m, d_q.p + 2ull * m, m, o.hscale, o.fscale, o.k_moves,
-                              o.itrs, o.time_ns, o.virtual_tick_ns, ix->sws.p, cap, slots2,
-                              d_cost.p, d_hops.p, d_fin.p, d_st.p, d_agg.p, g->stream);
-            HIP_CHECK(hipGetLastError());
-            HIP_CHECK(hipEventRecord(b, g->stream));
-            launch_scatter_u64(d_cost.p, d_idx.p, m, ix->cost.p, g->stream);
-            launch_scatter_u32(d_hops.p, d_idx.p, m, 1u, ix->hops.p, g->stream);
-            launch_scatter_u8(d_fin.p, d_idx.p, m, ix->fin.p, g->stream);
-            launch_scatter_u32(d_st.p, d_idx.p, m, 5u, ix->qstats.p, g->stream);
-            unsigned long long h2[8];
-            HIP_CHECK(hipMemcpyAsync(h2, d_agg.p, sizeof h2, hipMemcpyDeviceToHost, g->stream));
-            HIP_CHECK(hipStreamSynchronize(g->stream));
-            float ms2 = 0.f;
-            HIP_CHECK(hipEventElapsedTime(&ms2, a, b));
-            ms += ms2;
-            for (int k = 0; k < 7; ++k) h[k] += h2[k];
-            h[7] = h2[7];
-        }
         g->ev_pool.push_back(a);
         g->ev_pool.push_back(b);
+        hipStream_t sm = g->stream;
+        const uint32_t cap_max = o.capacity_max ? o.capacity_max
+                                 : auto_cap     ? pow2_at_least(4ull * std::max(n, 16u))
+                                                : o.capacity;
+        // HBM the passes may use: what is free plus what this index's search
+        // buffers already hold (reused)
+        auto avail = [&](size_t live) {
+            size_t free_b = 0, total_b = 0;
+            HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+            return free_b + ix->sws.n + ix->spool[0].n * 4u + ix->spool[1].n * 4u - live;
+        };
+        uint32_t cap = o.capacity;
+        if (auto_cap) {
+            cap = std::min(o.fscale > 0.0 ? (1u << 13) : (1u << 15), cap_max);
+            const size_t budget = (size_t)(wfrac * (double)avail(0) * (cap < cap_max ? 0.75 : 1.0));
+            const uint64_t lanes = nq ? search_slots(nq) : 64u;
+            while (cap > (1u << 10) && lanes * search_ws_bytes_per_slot(cap, tables) > budget) cap >>= 1;
+        }
+        const uint32_t cap0 = cap;
+        uint64_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double ms = 0.0;
+        uint64_t reruns = 0, resumed = 0, restarted = 0, wasted = 0, lanes1 = 0;
+        uint32_t passes = 0, cap_last = cap;
+        ix->qstats.alloc(5ull * std::max(1u, nq));
+        ix->sagg.alloc(8);
+        ix->stop.alloc(1);
+        // The passes: pass 1 runs every query at `cap` columns per lane; a
+        // search that would outgrow it stops whole and spills its state
+        // (fin 3) or, with the pool full, stops to restart (fin 2); each
+        // later pass runs those at 4x the capacity — spilled ones resumed
+        // from their records — until none is left or capacity_max (or the
+        // HBM) is reached; what is left then reports finished = 2.
+        // Pass-local arrays (m queries; pass 1: the index's own, m = nq).
+        uint32_t m = nq;
+        std::vector<uint32_t> gidx;               // pass query -> caller-sorted query (pass >= 2)
+        DevBuf<uint32_t> d_idx, d_q, d_hops, d_st;
+        DevBuf<uint64_t> d_cost;
+        DevBuf<uint8_t> d_fin;
+        DevBuf<unsigned long long> d_agg, d_res;
+        int pin = 0;                              // spool[pin]: the records the pass resumes from
+        bool have_resume = false;
+        while (m) {
+            ++passes;
+            const bool first = passes == 1;
+            const bool more = cap < cap_max;      // a later pass can take what overflows
+            const uint32_t* pq_s = first ? ix->qs.p : d_q.p;
+            const uint32_t* pq_t = first ? ix->qt.p : d_q.p + m;
+            const uint32_t* pq_r = first ? ix->qrow.p : d_q.p + 2ull * m;
+            uint64_t* p_cost = first ? ix->cost.p : d_cost.p;
+            uint32_t* p_hops = first ? ix->hops.p : d_hops.p;
+            uint8_t* p_fin = first ? ix->fin.p : d_fin.p;
+            uint32_t* p_st = first ? ix->qstats.p : d_st.p;
+            unsigned long long* p_agg = first ? ix->sagg.p : d_agg.p;
+            // lanes: as many as the workspace share holds (whole waves),
+            // leaving a quarter of it to the spill pool when a later pass
+            // can resume; the pool takes the rest of the share
+            const size_t live_in = have_resume ? ix->spool[pin].n * 4u : 0u;
+            const size_t av = avail(live_in);
+            const size_t share = (size_t)(wfrac * (double)av);
+            const size_t per_slot = search_ws_bytes_per_slot(cap, tables);
+            // (a quarter in pass 1, a tenth later: fewer searches spill again)
+            const size_t ws_budget = more ? (first ? share / 4u * 3u : share / 10u * 9u) : share;
+            const uint64_t fit = ws_budget / (64ull * per_slot);
+            CPD_REQUIRE(fit > 0 || av / 2 >= 64ull * per_slot, CPD_E_OOM,
+                        "search workspace of 64 lanes x capacity " + std::to_string(cap) +
+                            " does not fit in HBM");
+            const uint32_t slots = (uint32_t)std::min<uint64_t>(search_slots(m), std::max<uint64_t>(1, fit) * 64u);
+            if (first) lanes1 = slots;
+            ix->sws.release();
+            ix->sws.alloc((size_t)slots * per_slot);
+            SearchSpillArgs sa;
+            if (have_resume) {
+                sa.resume = d_res.p;
+                sa.rin = ix->spool[pin].p;
+            }
+            if (more) {
+                const uint64_t want = (uint64_t)m * search_spill_words(cap, tables);
+                const uint64_t left = share > (size_t)slots * per_slot ? share - (size_t)slots * per_slot : 0;
+                uint64_t words = std::min<uint64_t>(want, left / 4u);
+                // CPD_SEARCH_POOL_WORDS (tests): a smaller pool, so that some
+                // records find it full and their searches restart instead
+                if (const char* e = std::getenv("CPD_SEARCH_POOL_WORDS"))
+                    if (*e) words = std::min<uint64_t>(words, std::strtoull(e, nullptr, 10));
+                if (words >= search_spill_words(cap, tables)) {
+                    DevBuf<uint32_t>& out = ix->spool[pin ^ 1];
+                    out.release();
+                    out.alloc(words);
+                    ix->sat.alloc(m);
+                    sa.rout = out.p;
+                    sa.at = ix->sat.p;
+                    sa.top = ix->stop.p;
+                    sa.cap_words = words;
+                    HIP_CHECK(hipMemsetAsync(ix->stop.p, 0, sizeof(unsigned long long), sm));
+                }
+            }
+            HIP_CHECK(hipMemsetAsync(p_agg, 0, 8 * sizeof(unsigned long long), sm));
+            hipEvent_t ea = g->get_event(), eb = g->get_event();
+            HIP_CHECK(hipEventRecord(ea, sm));
+            (void)hipGetLastError();
+            launch_cpd_search(g->adj.p, adj_w, g->adj_shift, ix->dense.p, g->npad, g->tlb,
+                              tables ? ix->hrow.p : nullptr, ix->crow.p, ix->lrow.p, n, pq_s, pq_t,
+                              pq_r, m, o.hscale, o.fscale, o.k_moves, o.itrs, o.time_ns,
+                              o.virtual_tick_ns, ix->sws.p, cap, slots, sa, p_cost, p_hops, p_fin,
+                              p_st, p_agg, sm);
+            HIP_CHECK(hipGetLastError());
+            HIP_CHECK(hipEventRecord(eb, sm));
+            if (!first) {  // this pass's results over the first pass's
+                launch_scatter_u64(d_cost.p, d_idx.p, m, ix->cost.p, sm);
+                launch_scatter_u32(d_hops.p, d_idx.p, m, 1u, ix->hops.p, sm);
+                launch_scatter_u8(d_fin.p, d_idx.p, m, ix->fin.p, sm);
+                launch_scatter_u32(d_st.p, d_idx.p, m, 5u, ix->qstats.p, sm);
+            }
+            unsigned long long hp[8];
+            HIP_CHECK(hipMemcpyAsync(hp, p_agg, sizeof hp, hipMemcpyDeviceToHost, sm));
+            HIP_CHECK(hipStreamSynchronize(sm));
+            float pms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&pms, ea, eb));
+            g->ev_pool.push_back(ea);
+            g->ev_pool.push_back(eb);
+            ms += pms;
+            for (int k = 0; k < 7; ++k) h[k] += hp[k];
+            h[7] = hp[7];
+            cap_last = cap;
+            if (search_trace())
+                std::fprintf(stderr, "[cpd_search] pass %u: %u queries, capacity %u, %u lanes, "
+                             "%.3f ms, %llu expanded, %llu overflowed, pool %llu words\n",
+                             passes, m, cap, slots, pms, (unsigned long long)hp[0],
+                             (unsigned long long)hp[7], (unsigned long long)sa.cap_words);
+            if (!hp[7]) break;
+            // the searches that overflowed: spilled (fin 3) resume, the others
+            // (fin 2) restart from scratch — their counters leave the sums
+            std::vector<uint8_t> f(m);
+            std::vector<uint32_t> qst(5ull * m), hq(3ull * m);
+            std::vector<unsigned long long> at(m, ~0ull);
+            HIP_CHECK(hipMemcpyAsync(f.data(), p_fin, m, hipMemcpyDeviceToHost, sm));
+            HIP_CHECK(hipMemcpyAsync(qst.data(), p_st, 20ull * m, hipMemcpyDeviceToHost, sm));
+            HIP_CHECK(hipMemcpyAsync(hq.data(), pq_s, 4ull * m, hipMemcpyDeviceToHost, sm));
+            HIP_CHECK(hipMemcpyAsync(hq.data() + m, pq_t, 4ull * m, hipMemcpyDeviceToHost, sm));
+            HIP_CHECK(hipMemcpyAsync(hq.data() + 2ull * m, pq_r, 4ull * m, hipMemcpyDeviceToHost, sm));
+            if (sa.rout) HIP_CHECK(hipMemcpyAsync(at.data(), ix->sat.p, 8ull * m, hipMemcpyDeviceToHost, sm));
+            HIP_CHECK(hipStreamSynchronize(sm));
+            // the next capacity: 4x, or less when that does not fit 64 lanes
+            // in the share (never throw there — what cannot grow
+            // reports finished = 2)
+            uint32_t next = 0;
+            if (more) {
+                const size_t av2 = avail(sa.rout ? ix->spool[pin ^ 1].n * 4u : 0u);
+                for (uint32_t c = std::min(cap * 4u, cap_max); c > cap; c >>= 1)
+                    if (64ull * search_ws_bytes_per_slot(c, tables) <= (size_t)(wfrac * (double)av2)) {
+                        next = c;
+                        break;
+                    }
+            }
+            std::vector<uint32_t> idx, sub;
+            std::vector<unsigned long long> res;
+            bool any_res = false;
+            for (uint32_t i = 0; i < m; ++i) {
+                if (f[i] != 2u && f[i] != 3u) continue;
+                const bool spilled = f[i] == 3u;
+                if (!spilled) {  // restarted: its first pass leaves the sums
+                    for (int k = 0; k < 5; ++k) h[k] -= qst[5ull * i + k];
+                    if (next) wasted += qst[5ull * i];
+                }
+                idx.push_back(i);
+                res.push_back(spilled ? at[i] : ~0ull);
+                any_res |= spilled;
+            }
+            const uint32_t m2 = (uint32_t)idx.size();
+            if (!next) {
+                // no larger workspace fits: spilled searches are final
+                // overflows too (finished = 2, their counters in the sums)
+                if (any_res) {
+                    for (uint32_t i = 0; i < m; ++i)
+                        if (f[i] == 3u) {
+                            f[i] = 2u;
+                            for (int k = 0; k < 5; ++k) h[k] += qst[5ull * i + k];
+                        }
+                    HIP_CHECK(hipMemcpyAsync(p_fin, f.data(), m, hipMemcpyHostToDevice, sm));
+                    if (!first) launch_scatter_u8(d_fin.p, d_idx.p, m, ix->fin.p, sm);
+                    HIP_CHECK(hipStreamSynchronize(sm));
+                }
+                break;
+            }
+            reruns += m2;
+            for (unsigned long long r : res) (r == ~0ull ? restarted : resumed)++;
+            sub.resize(3ull * m2);
+            std::vector<uint32_t> g2(m2);
+            for (uint32_t j = 0; j < m2; ++j) {
+                const uint32_t i = idx[j];  // target-sorted order is kept
+                sub[j] = hq[i];
+                sub[m2 + j] = hq[m + i];
+                sub[2ull * m2 + j] = hq[2ull * m + i];
+                g2[j] = first ? i : gidx[i];
+            }
+            gidx.swap(g2);
+            d_idx.upload(gidx.data(), m2, sm);
+            d_q.upload(sub.data(), 3ull * m2, sm);
+            d_res.upload(res.data(), m2, sm);
+            d_hops.alloc(m2);
+            d_st.alloc(5ull * m2);
+            d_cost.alloc(m2);
+            d_fin.alloc(m2);
+            d_agg.alloc(8);
+            have_resume = any_res;
+            ix->spool[pin].release();            // the records this pass resumed from
+            if (any_res) {                       // the records just written, kept at their size
+                unsigned long long used = 0;
+                HIP_CHECK(hipMemcpy(&used, ix->stop.p, sizeof used, hipMemcpyDeviceToHost));
+                DevBuf<uint32_t>& full = ix->spool[pin ^ 1];
+                used = std::min<unsigned long long>(used, full.n);
+                if (used < full.n / 10 * 9) {
+                    DevBuf<uint32_t>& fit = ix->spool[pin];
+                    fit.alloc(std::max<unsigned long long>(used, 1));
+                    HIP_CHECK(hipMemcpyAsync(fit.p, full.p, 4ull * used, hipMemcpyDeviceToDevice, sm));
+                    HIP_CHECK(hipStreamSynchronize(sm));
+                    full.release();
+                } else {
+                    pin ^= 1;
+                }
+            } else {
+                ix->spool[pin ^ 1].release();
+            }
+            m = m2;
+            cap = next;
+        }
+        // the spill pools are scratch: freed with the pass that used them
+        ix->spool[0].release();
+        ix->spool[1].release();
         if (g->timing) {
             Agg& ag = g->agg["cpd_search"];
-            ag.launches++;
+            ag.launches += passes;
             ag.ms += ms;
         }
         ix->searched = true;
@@ -2695,10 +2910,16 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             st->finished = h[6];
             st->overflow = h[7];
             st->kernel_ms = ms;
-            st->lanes = slots;
+            st->lanes = lanes1;
             st->tables_ms = tables_ms;
             st->tables = tables ? CPD_SEARCH_TABLES : CPD_SEARCH_WALKS;
             st->reruns = reruns;
+            st->resumed = resumed;
+            st->restarted = restarted;
+            st->wasted_expanded = wasted;
+            st->passes = passes;
+            st->capacity = cap0;
+            st->capacity_last = cap_last;
         }
     });
 }

@@ -503,7 +503,11 @@ int bucket_format(const std::string& path) {
 // DOSCPD02 layout: magic 8 | 8 x u32 | total u64 | fingerprint u64 (= 56 B) |
 // targets | counts | pad | rows from rows_offset().  DOSCPD03: the same 56 B
 // + stripes u32 + stripe_rows u32 | targets | counts, and the rows in part
-// files {path}.p{j}: unit u (rows [u S, u S + S)) is unit u / K of part u % K.
+// files {path}.{fingerprint}.p{j}: unit u (rows [u S, u S + S)) is unit u / K
+// of part u % K.  The parts carry the graph's fingerprint in their names, so a
+// main file only ever pairs with parts built for its graph (a rebuild that
+// stops between renaming its parts and its main file leaves the old main file
+// with the old parts).
 static constexpr uint64_t kMoveHeader = 8 + 32 + 8 + 8;
 static constexpr uint64_t kStripedHeader = kMoveHeader + 8;
 static constexpr uint64_t kMoveRowsAlign = 4096;
@@ -529,15 +533,23 @@ uint64_t MoveBucket::part_rows(uint32_t j) const {
     return rows;
 }
 
-std::string move_part_path(const std::string& path, uint32_t j) { return path + ".p" + std::to_string(j); }
+std::string move_part_path(const std::string& path, uint64_t fingerprint, uint32_t j) {
+    char fp[17];
+    std::snprintf(fp, sizeof fp, "%016llx", (unsigned long long)fingerprint);
+    return path + "." + fp + ".p" + std::to_string(j);
+}
+
+constexpr uint32_t kMaxStripes = 4096;
 
 MoveBucketFile::MoveBucketFile(const std::string& path, const MoveBucket& b, uint32_t stripes,
                                uint32_t stripe_rows)
     : path_(path), tmp_(path + ".tmp"), nrows_((uint32_t)b.targets.size()), words_(b.words),
-      stripes_(std::max(1u, stripes)), stripe_rows_(std::max(1u, stripe_rows)) {
+      stripes_(std::max(1u, stripes)), stripe_rows_(std::max(1u, stripe_rows)), fp_(b.fingerprint) {
     if (!(b.bits == 1 || b.bits == 2 || b.bits == 4) ||
         b.words != ((uint64_t)b.n * b.bits + 31u) / 32u)
         throw Error(CPD_E_ARG, "move bucket: words != ceil(n * bits / 32)");
+    if (stripes_ > kMaxStripes)  // what read_move_bucket_head accepts
+        throw Error(CPD_E_ARG, "move bucket: at most " + std::to_string(kMaxStripes) + " stripes");
     const bool striped = stripes_ > 1;
     rows_off_ = striped ? 0 : b.rows_offset();
     fd_ = ::open(tmp_.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
@@ -555,27 +567,35 @@ MoveBucketFile::MoveBucketFile(const std::string& path, const MoveBucket& b, uin
         std::memcpy(h.data() + kMoveHeader, st, sizeof st);
     }
     std::memcpy(h.data() + tgt, b.targets.data(), 4ull * nrows_);
-    pwrite_all(fd_, h.data(), h.size(), 0);
-    if (striped)
-        for (uint32_t j = 0; j < stripes_; ++j) {
-            const std::string pt = move_part_path(path_, j) + ".tmp";
+    try {
+        pwrite_all(fd_, h.data(), h.size(), 0);
+        for (uint32_t j = 0; striped && j < stripes_; ++j) {
+            const std::string pt = move_part_path(path_, fp_, j) + ".tmp";
             const int pf = ::open(pt.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
             if (pf < 0) throw Error(CPD_E_IO, "cannot write " + pt);
             part_fd_.push_back(pf);
         }
+    } catch (...) {  // the destructor does not run: close and remove what was opened
+        discard();
+        throw;
+    }
 }
 
-MoveBucketFile::~MoveBucketFile() {
+void MoveBucketFile::discard() {
     for (uint32_t j = 0; j < part_fd_.size(); ++j) {
         if (part_fd_[j] < 0) continue;
         ::close(part_fd_[j]);
-        ::unlink((move_part_path(path_, j) + ".tmp").c_str());
+        ::unlink((move_part_path(path_, fp_, j) + ".tmp").c_str());
+        part_fd_[j] = -1;
     }
     if (fd_ >= 0) {
         ::close(fd_);
         ::unlink(tmp_.c_str());
+        fd_ = -1;
     }
 }
+
+MoveBucketFile::~MoveBucketFile() { discard(); }
 
 void MoveBucketFile::pwrite_all(int fd, const void* p, size_t bytes, uint64_t pos) {
     const char* c = static_cast<const char*>(p);
@@ -614,10 +634,20 @@ void MoveBucketFile::write_rows(uint32_t first_row, const uint32_t* rows, uint32
 
 void MoveBucketFile::close(uint64_t total_runs) {
     pwrite_all(fd_, &total_runs, 8, 40);
+    // a bucket file already here from an earlier build: its parts go once the
+    // new main file is in place (when they are not the ones just written)
+    uint64_t old_fp = 0;
+    uint32_t old_k = 0;
+    try {
+        const MoveBucket old = read_move_bucket_head(path_, false);
+        old_fp = old.fingerprint;
+        old_k = old.stripes > 1 ? old.stripes : 0;
+    } catch (const Error&) {
+    }
     for (uint32_t j = 0; j < part_fd_.size(); ++j) {
         const int pf = part_fd_[j];
         part_fd_[j] = -1;
-        const std::string pp = move_part_path(path_, j);
+        const std::string pp = move_part_path(path_, fp_, j);
         if (::close(pf) != 0) throw Error(CPD_E_IO, "close failed: " + pp + ".tmp");
         if (std::rename((pp + ".tmp").c_str(), pp.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + pp);
     }
@@ -625,6 +655,8 @@ void MoveBucketFile::close(uint64_t total_runs) {
     fd_ = -1;
     if (::close(fd) != 0) throw Error(CPD_E_IO, "close failed: " + tmp_);
     if (std::rename(tmp_.c_str(), path_.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path_);
+    for (uint32_t j = 0; j < old_k; ++j)
+        if (old_fp != fp_ || j >= part_fd_.size()) ::unlink(move_part_path(path_, old_fp, j).c_str());
 }
 
 static uint64_t file_size(const std::string& path) {
@@ -633,7 +665,7 @@ static uint64_t file_size(const std::string& path) {
     return (uint64_t)st.st_size;
 }
 
-MoveBucket read_move_bucket_head(const std::string& path) {
+MoveBucket read_move_bucket_head(const std::string& path, bool check_parts) {
     std::ifstream f(path, std::ios::binary | std::ios::ate);
     if (!f) throw Error(CPD_E_IO, "cannot open " + path);
     const uint64_t size = (uint64_t)f.tellg();
@@ -666,15 +698,15 @@ MoveBucket read_move_bucket_head(const std::string& path) {
     if (!(b.bits == 1 || b.bits == 2 || b.bits == 4) ||
         b.words != ((uint64_t)b.n * b.bits + 31u) / 32u)
         throw Error(CPD_E_IO, path + ": row width does not match n and bits per move");
-    if (striped && (b.stripes < 2 || b.stripes > 4096 || b.stripe_rows == 0))
+    if (striped && (b.stripes < 2 || b.stripes > kMaxStripes || b.stripe_rows == 0))
         throw Error(CPD_E_IO, path + ": bad stripe layout");
     b.targets.resize(nrows);
     b.counts.resize(nrows);
     if (striped) {
         if (size != b.head_bytes()) throw Error(CPD_E_IO, path + ": size does not match its header");
-        for (uint32_t j = 0; j < b.stripes; ++j)
-            if (file_size(move_part_path(path, j)) != b.part_rows(j) * 4ull * b.words)
-                throw Error(CPD_E_IO, move_part_path(path, j) + ": size does not match its bucket");
+        for (uint32_t j = 0; check_parts && j < b.stripes; ++j)
+            if (file_size(move_part_path(path, b.fingerprint, j)) != b.part_rows(j) * 4ull * b.words)
+                throw Error(CPD_E_IO, move_part_path(path, b.fingerprint, j) + ": size does not match its bucket");
     } else if (size != b.rows_offset() + 4ull * b.words * nrows) {
         throw Error(CPD_E_IO, path + ": size does not match its header");
     }
@@ -703,7 +735,7 @@ void read_move_bucket_rows(const std::string& path, const MoveBucket& head, uint
     std::vector<Span> spans;
     std::vector<std::string> files;
     if (head.stripes > 1) {
-        for (uint32_t j = 0; j < head.stripes; ++j) files.push_back(move_part_path(path, j));
+        for (uint32_t j = 0; j < head.stripes; ++j) files.push_back(move_part_path(path, head.fingerprint, j));
         const uint64_t S = head.stripe_rows, K = head.stripes;
         for (uint64_t r = first, end = (uint64_t)first + count; r < end;) {
             const uint64_t u = r / S, take = std::min(end - r, (u + 1) * S - r);
@@ -772,6 +804,17 @@ void write_order(const std::string& path, uint64_t fp, const std::vector<uint32_
         if (!f) throw Error(CPD_E_IO, "write failed: " + tmp);
     }
     if (std::rename(tmp.c_str(), path.c_str()) != 0) throw Error(CPD_E_IO, "rename failed: " + path);
+}
+
+uint32_t read_order_n(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw Error(CPD_E_IO, "cannot open " + path);
+    char magic[8];
+    uint32_t n = 0;
+    f.read(magic, 8);
+    f.read(reinterpret_cast<char*>(&n), 4);
+    if (!f || std::memcmp(magic, kOrderMagic, 8) != 0) throw Error(CPD_E_IO, path + ": not an order file");
+    return n;
 }
 
 std::vector<uint32_t> read_order(const std::string& path, uint64_t fp) {

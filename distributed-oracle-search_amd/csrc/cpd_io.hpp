@@ -111,15 +111,16 @@ int bucket_format(const std::string& path);
 struct MoveBucket {
     uint32_t n = 0, bid = 0, method = 0, key = 0, maxworker = 0, words = 0, bits = 4;
     uint64_t fingerprint = 0, total_runs = 0;
-    // striped (DOSCPD03): the rows in `stripes` part files {path}.p{j}, in
-    // units of stripe_rows rows dealt round robin (unit u in part u % stripes)
+    // striped (DOSCPD03): the rows in `stripes` (<= 4096) part files
+    // {path}.{fingerprint as 16 hex digits}.p{j}, in units of stripe_rows
+    // rows dealt round robin (unit u in part u % stripes)
     uint32_t stripes = 1, stripe_rows = 0;
     std::vector<uint32_t> targets, counts;
     uint64_t rows_offset() const;  // DOSCPD02: where the rows start
     uint64_t head_bytes() const;   // DOSCPD03: the main file's size
     uint64_t part_rows(uint32_t j) const;
 };
-std::string move_part_path(const std::string& path, uint32_t j);
+std::string move_part_path(const std::string& path, uint64_t fingerprint, uint32_t j);
 // Written in pieces from several threads, in any order (positional writes);
 // close() writes the run total and renames the .tmp files into place (the
 // parts first, the main file last).  stripes > 1: DOSCPD03, the rows in
@@ -130,7 +131,7 @@ public:
     // `b` supplies the header fields and targets (counts / total unused)
     MoveBucketFile(const std::string& path, const MoveBucket& b, uint32_t stripes = 1,
                    uint32_t stripe_rows = 64);
-    ~MoveBucketFile();  // without close(): the .tmp is removed
+    ~MoveBucketFile();  // without close(): the .tmp files are removed
     MoveBucketFile(const MoveBucketFile&) = delete;
     MoveBucketFile& operator=(const MoveBucketFile&) = delete;
     void write_counts(uint32_t first_row, const uint32_t* counts, uint32_t count);
@@ -139,20 +140,23 @@ public:
 
 private:
     void pwrite_all(int fd, const void* p, size_t bytes, uint64_t pos);
+    void discard();  // close and remove every .tmp still open
     std::string path_, tmp_;
     int fd_ = -1;
     uint32_t nrows_ = 0, words_ = 0, stripes_ = 1, stripe_rows_ = 0;
-    uint64_t rows_off_ = 0;
+    uint64_t rows_off_ = 0, fp_ = 0;
     std::vector<int> part_fd_;
 };
-// Header, targets and counts (the file size checked against the header);
-// rows [first, first + count) then read by position.
-MoveBucket read_move_bucket_head(const std::string& path);
+// Header, targets and counts (the file size checked against the header, and
+// with check_parts the part files' sizes); rows [first, first + count) then
+// read by position.
+MoveBucket read_move_bucket_head(const std::string& path, bool check_parts = true);
 void read_move_bucket_rows(const std::string& path, const MoveBucket& head, uint32_t first,
                            uint32_t count, uint32_t* out, int threads = 1);
 
 void write_order(const std::string& path, uint64_t fingerprint, const std::vector<uint32_t>& order);
 std::vector<uint32_t> read_order(const std::string& path, uint64_t fingerprint);
+uint32_t read_order_n(const std::string& path);  // its node count (header only)
 
 }  // namespace io
 }  // namespace cpd

@@ -985,14 +985,19 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                                                       uint32_t* __restrict__ fm,
                                                       const uint32_t* __restrict__ leafbits,
                                                       const uint16_t* __restrict__ fmleaf,
-                                                      NarrowRows nr) {
+                                                      NarrowRows nr,
+                                                      const uint32_t* __restrict__ seg_order) {
     static_assert(kSeg % G == 0, "group size");
     const uint32_t nseg = npad / kSeg;
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t slab = L / nseg;
     const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t B4 = B / 4u;
-    const uint32_t cb = (L - slab * nseg) * kSeg;
+    // segments in the order seg_order gives (spatially compact runs: the
+    // neighbour rows one XCD's blocks gather at once overlap in its L2), else
+    // in column order
+    const uint32_t sl = L - slab * nseg;
+    const uint32_t cb = (seg_order ? seg_order[sl] : sl) * kSeg;
     const uint32_t lane = threadIdx.x & 63u;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
@@ -1769,6 +1774,10 @@ __global__ __launch_bounds__(256) void moves_runs(const uint32_t* __restrict__ d
 struct RleChunks {
     uint32_t* xs;  // [nrows][nch] exit state (h << 4 | S) of the chunk
     uint32_t* cc;  // [nrows][nch] runs ending inside the chunk
+    uint32_t* xe;  // [nrows][nch] its guessed entry state (= its first segment's st):
+                   // rle_fix reads the seams from here, 4 B per chunk, instead of
+                   // one 4-B state per 128-B line of st (3.4 GB per 24576-row
+                   // launch)
 };
 
 // the greedy scan over one 32-column segment (word v[c / 8], nibble c % 8)
@@ -1822,6 +1831,7 @@ __global__ __launch_bounds__(256) void rle_count_ch(const uint32_t* __restrict__
         }
     }
     uint32_t* __restrict__ stp = st + (size_t)row * nseg + s0;
+    rk.xe[(size_t)row * nch + ch] = (h << 4) | S;
     uint32_t total = 0;
     uint4 nq = f4[fm4_piece(row, nseg, s0)];
     uint2 r0 = {}, r1 = {}, r2 = {};  // counts of segments 0-7, 8-15, 16-23 of 32
@@ -1892,7 +1902,7 @@ __global__ __launch_bounds__(64) void rle_fix(const uint32_t* __restrict__ fm, u
     for (uint32_t b = 0; b < nch; b += 64u) {
         const uint32_t c = b + lane;
         const bool valid = c < nch;
-        uint32_t in = valid ? str[(size_t)c * CH] : 0u;
+        uint32_t in = valid ? rk.xe[(size_t)row * nch + c] : 0u;
         uint32_t ex = valid ? xs[c] : 0u;
         uint32_t cnt = valid ? cc[c] : 0u;
         for (;;) {
@@ -2686,8 +2696,33 @@ struct Lane {
     uint32_t q, s, t, tag, hsize, used, best_len;
     uint64_t ub, t0;
     uint32_t expanded, inserted, touched, updated, surplus;
-    bool done, overflow;
+    bool done, overflow, spilled;
 };
+
+// Resumable overflow.  A search checks, before each
+// pop, that the expansion cannot outgrow its workspace: at most 2^SHIFT new
+// columns and heap entries (the tables form), or — the walks form, whose
+// walks add any number — the heads' walks done first and the heap's room.
+// When it could, the search stops there with its state whole and, given a
+// spill pool, copies it out as a record: the heap verbatim, then every
+// column it holds (column, g, depth, moves | state, and with walks the memo)
+// — ~20-36 B per column, not the 68-116 B per column of capacity a
+// workspace costs.  The next pass (4x the capacity) rebuilds the hash from
+// the record and continues from the same pop: the heap keys (f, column, g)
+// are a total order, so pops, counters and results are those of one
+// uninterrupted search.  Record (u32 words): hsize, used, ub lo/hi,
+// best_len, the five counters, elapsed ticks lo/hi, entries, 0 | heap
+// hsize x (f lo, f hi, g lo, g hi, column) | entries x (column, g lo, g hi,
+// depth, moves | state [, memo x4]).
+struct SearchSpill {
+    const unsigned long long* resume;  // [nq] record of query q in rin, ~0 = fresh (null: all)
+    const uint32_t* rin;
+    unsigned long long* at;            // [nq] record written for a spilled query (fin 3)
+    uint32_t* rout;                    // the pool records go to (null: no spilling)
+    unsigned long long* top;           // its bump counter, words
+    unsigned long long cap;            // its size, words
+};
+constexpr uint32_t kSpillHead = 14;
 
 // The lane's workspace (one slot's arrays).
 struct LaneWs {
@@ -2712,8 +2747,16 @@ __device__ __forceinline__ bool ws_insert(Lane& L, const LaneWs& W, uint32_t i, 
     return true;
 }
 
+// A walk that overflowed: the columns it marked "on the walk" (the stack and
+// the column in hand) go back to "not walked", so the search's state stays
+// whole — it is spilled and resumed, or restarted, from there.
+__device__ __forceinline__ void walk_abandon(const LaneWs& W, uint32_t sp, uint32_t xi) {
+    W.aux[xi].y &= 0x3FFFFFFFu;
+    for (uint32_t j = 0; j < sp; ++j) W.aux[W.stk[j].x].y &= 0x3FFFFFFFu;
+}
+
 // Memoised CPD walk from column v (ora_walk): afterwards v's entry (returned
-// slot) is walked; false on overflow.
+// slot) is walked; false on overflow (walk_abandon: nothing half-walked).
 template <int SHIFT>
 __device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj_f,
                          const uint2* __restrict__ adj_w, const uint32_t* __restrict__ row,
@@ -2764,7 +2807,10 @@ __device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj
                 ew = adj_w[((size_t)x << SHIFT) + mv];
             }
         }
-        if (sp >= W.C) return false;
+        if (sp >= W.C) {
+            walk_abandon(W, sp, xi);
+            return false;
+        }
         W.stk[sp++] = make_uint4(xi, ef.y, ew.y, 0u);
         if (ef.x == kNoEdge) {  // names no edge of x
             bad = true;
@@ -2776,7 +2822,10 @@ __device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj
         const uint2 au = W.aux[h];
         xi = hprobe_from(W.ent, W.mask, L.tag, x, found, e);
         if (!found) {
-            if (!ws_insert(L, W, xi, x, 0u)) return false;
+            if (!ws_insert(L, W, xi, x, 0u)) {
+                walk_abandon(W, sp, W.stk[sp - 1u].x);  // sp >= 1: the column just left
+                return false;
+            }
             auy = 0u;  // what ws_insert wrote: not walked
         } else {
             auy = xi == h ? au.y : W.aux[xi].y;
@@ -2820,9 +2869,10 @@ __global__ __launch_bounds__(256) void cpd_search(
     const uint32_t* __restrict__ dense, uint32_t wpr, uint32_t lb, SearchTables tb,
     const uint32_t* __restrict__ qs,
     const uint32_t* __restrict__ qt, const uint32_t* __restrict__ qrow, uint32_t nq,
-    uint32_t chunk, SearchOpt opt, SearchWs ws, uint64_t* __restrict__ cost_out,
+    uint32_t chunk, SearchOpt opt, SearchWs ws, SearchSpill sp, uint64_t* __restrict__ cost_out,
     uint32_t* __restrict__ plen_out, uint8_t* __restrict__ fin_out,
     uint32_t* __restrict__ qstats, unsigned long long* __restrict__ agg) {
+    constexpr uint32_t KD = 1u << SHIFT;  // most new columns / heap entries of one expansion
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t slot = wave * 64u + lane;  // this lane's workspace
@@ -2857,9 +2907,40 @@ __global__ __launch_bounds__(256) void cpd_search(
         L.expanded = L.inserted = L.touched = L.updated = L.surplus = 0;
         L.done = false;
         L.overflow = false;
+        L.spilled = false;
         L.t0 = __builtin_amdgcn_s_memrealtime();
         row = dense + (size_t)qrow[q] * wpr;
         rb = (size_t)qrow[q] * tb.n;
+        if (sp.resume && sp.resume[q] != ~0ull) {  // a spilled search: its state back
+            const uint32_t* __restrict__ r = sp.rin + sp.resume[q];
+            L.hsize = r[0];
+            L.used = r[1];
+            L.ub = u64of(r[2], r[3]);
+            L.best_len = r[4];
+            L.expanded = r[5];
+            L.inserted = r[6];
+            L.touched = r[7];
+            L.updated = r[8];
+            L.surplus = r[9];
+            L.t0 -= u64of(r[10], r[11]);
+            const uint32_t ne = r[12];
+            const uint32_t* __restrict__ h = r + kSpillHead;
+            for (uint32_t i = 0; i < L.hsize; ++i) {
+                W.he[i] = make_uint4(h[5u * i], h[5u * i + 1u], h[5u * i + 2u], h[5u * i + 3u]);
+                W.hc[i] = h[5u * i + 4u];
+            }
+            constexpr uint32_t per = TABLES ? 5u : 9u;
+            const uint32_t* __restrict__ en = h + 5ull * L.hsize;
+            for (uint32_t k = 0; k < ne; ++k) {
+                const uint32_t* __restrict__ o = en + (size_t)per * k;
+                bool f;
+                const uint32_t i = hprobe(W.ent, W.mask, L.tag, o[0], f);
+                W.ent[i] = make_uint4(L.tag, o[0], o[1], o[2]);
+                W.aux[i] = make_uint2(o[3], o[4]);
+                if (!TABLES) W.memo[i] = make_uint4(o[5], o[6], o[7], o[8]);
+            }
+            return;
+        }
         bool found;
         uint32_t si;
         uint64_t hs;
@@ -2886,6 +2967,64 @@ __global__ __launch_bounds__(256) void cpd_search(
             heap_push(W.he, W.hc, L.hsize, (uint64_t)(opt.hscale * (double)hs), L.s, 0ull);
         }
     };
+    // a search stopped before a pop that could outgrow the workspace: its
+    // record into the spill pool (false: no pool, or the pool is full — the
+    // search then restarts from scratch at the next capacity)
+    auto spill = [&]() -> bool {
+        if (!sp.rout) return false;
+        constexpr uint32_t per = TABLES ? 5u : 9u;
+        const unsigned long long words =
+            kSpillHead + 5ull * L.hsize + (unsigned long long)per * L.used;
+        const unsigned long long off = atomicAdd(sp.top, words);
+        if (off + words > sp.cap) return false;
+        uint32_t* __restrict__ r = sp.rout + off;
+        uint32_t* __restrict__ h = r + kSpillHead;
+        for (uint32_t i = 0; i < L.hsize; ++i) {
+            const uint4 e = W.he[i];
+            h[5u * i] = e.x;
+            h[5u * i + 1u] = e.y;
+            h[5u * i + 2u] = e.z;
+            h[5u * i + 3u] = e.w;
+            h[5u * i + 4u] = W.hc[i];
+        }
+        uint32_t* __restrict__ en = h + 5ull * L.hsize;
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < 2u * C && k < L.used; ++i) {
+            const uint4 e = W.ent[i];
+            if (e.x != L.tag) continue;
+            const uint2 a = W.aux[i];
+            uint32_t* __restrict__ o = en + (size_t)per * k++;
+            o[0] = e.y;
+            o[1] = e.z;
+            o[2] = e.w;
+            o[3] = a.x;
+            o[4] = a.y;
+            if (!TABLES) {
+                const uint4 mm = W.memo[i];
+                o[5] = mm.x;
+                o[6] = mm.y;
+                o[7] = mm.z;
+                o[8] = mm.w;
+            }
+        }
+        const uint64_t el = __builtin_amdgcn_s_memrealtime() - L.t0;
+        r[0] = L.hsize;
+        r[1] = L.used;
+        r[2] = (uint32_t)L.ub;
+        r[3] = (uint32_t)(L.ub >> 32);
+        r[4] = L.best_len;
+        r[5] = L.expanded;
+        r[6] = L.inserted;
+        r[7] = L.touched;
+        r[8] = L.updated;
+        r[9] = L.surplus;
+        r[10] = (uint32_t)el;
+        r[11] = (uint32_t)(el >> 32);
+        r[12] = k;
+        r[13] = 0u;
+        sp.at[L.q] = off;
+        return true;
+    };
     uint32_t next = q0;
     if (q0 + lane < q1) begin(q0 + lane);
     next = min(q1, q0 + 64u);
@@ -2898,18 +3037,21 @@ __global__ __launch_bounds__(256) void cpd_search(
                 const bool found = L.ub != kInf64 && !L.overflow;
                 cost_out[L.q] = found ? L.ub : 0ull;
                 plen_out[L.q] = found ? L.best_len : 0u;
-                fin_out[L.q] = found ? 1u : L.overflow ? 2u : 0u;
+                // 2: stopped on the workspace (restarts), 3: spilled (resumes)
+                fin_out[L.q] = found ? 1u : L.overflow ? (L.spilled ? 3u : 2u) : 0u;
                 uint32_t* st = qstats + 5ull * L.q;
                 st[0] = L.expanded;
                 st[1] = L.inserted;
                 st[2] = L.touched;
                 st[3] = L.updated;
                 st[4] = L.surplus;
-                s_exp += L.expanded;
-                s_ins += L.inserted;
-                s_tou += L.touched;
-                s_upd += L.updated;
-                s_sur += L.surplus;
+                // a spilled search's counters are summed when it completes
+                const uint32_t keep = L.spilled ? 0u : 1u;
+                s_exp += keep * L.expanded;
+                s_ins += keep * L.inserted;
+                s_tou += keep * L.touched;
+                s_upd += keep * L.updated;
+                s_sur += keep * L.surplus;
                 s_len += found ? L.best_len : 0u;
                 s_fin += found ? 1u : 0u;
                 s_ovf += L.overflow ? 1u : 0u;
@@ -2921,10 +3063,16 @@ __global__ __launch_bounds__(256) void cpd_search(
         }
         if (!__any(L.q != kIdleQ)) break;
         if (L.q == kIdleQ || L.done || L.hsize == 0) continue;
-        // one pop of this lane's search
+        // one pop of this lane's search: the top, looked at first (it is
+        // popped once the expansion is known to fit the workspace)
         uint64_t f, g;
         uint32_t v;
-        heap_pop(W.he, W.hc, L.hsize, f, v, g);
+        {
+            const uint4 top = W.he[0];
+            f = u64of(top.x, top.y);
+            g = u64of(top.z, top.w);
+            v = W.hc[0];
+        }
         // what the expansion reads and nothing in it writes — v's out-edges
         // and, per-row tables, v's incumbent values — is loaded beside v's
         // hash probe, one round trip for all of it
@@ -2944,6 +3092,7 @@ __global__ __launch_bounds__(256) void cpd_search(
         const uint32_t hi = hprobe(W.ent, W.mask, L.tag, v, found);
         const uint4 ev = W.ent[hi];
         if (g > u64of(ev.z, ev.w)) {  // stale entry
+            heap_pop(W.he, W.hc, L.hsize, f, v, g);
             ++L.surplus;
             continue;
         }
@@ -2956,6 +3105,34 @@ __global__ __launch_bounds__(256) void cpd_search(
             L.done = true;
             continue;
         }
+        // room for the expansion: <= KD heap entries (and, tables, columns);
+        // with walks the heads are walked first (the expansion would walk
+        // exactly these; their memo does not depend on the search)
+        bool room = L.hsize - 1u + KD <= C && (!TABLES || L.used + KD <= C);
+        if (room && !TABLES) {
+            if (SHIFT <= 2) {
+#pragma unroll
+                for (int k = 0; k < ND; ++k) {
+                    if (!room || ed[k].x == kNoEdge) break;  // edges are packed first
+                    uint32_t ui;
+                    room = cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, ed[k].x, ui);
+                }
+            } else {
+#pragma unroll 1
+                for (uint32_t k = 0; k < KD && room; ++k) {
+                    const uint32_t u = adj_w[((size_t)v << SHIFT) + k].x;
+                    if (u == kNoEdge) break;
+                    uint32_t ui;
+                    room = cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, u, ui);
+                }
+            }
+        }
+        if (!room) {  // stop whole, before the pop: spilled, or restarted
+            L.overflow = L.done = true;
+            L.spilled = spill();
+            continue;
+        }
+        heap_pop(W.he, W.hc, L.hsize, f, v, g);
         ++L.expanded;
         const uint32_t dv = W.aux[hi].x;
         {
@@ -3297,13 +3474,14 @@ static void launch_first_moves_t(const uint2* adj, uint32_t shift, const uint32_
 void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* dist,
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
                         uint32_t npad, uint32_t* fm, const uint32_t* leafbits,
-                        const uint16_t* fmleaf, NarrowRows nr, hipStream_t s) {
+                        const uint16_t* fmleaf, NarrowRows nr, hipStream_t s,
+                        const uint32_t* seg_order) {
     const uint32_t tpb = 64u * fm_wpb();  // a workgroup covers 4 * tpb targets
     const dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u) * (256u / tpb)), blk(tpb);
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     if (nr.d16 && shift == 2 && fm_n4()) {
         launch_shm(kern::first_moves_n4<2>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n, npad,
-                   xcd_remap(), fm, leafbits, fmleaf, nr);
+                   xcd_remap(), fm, leafbits, fmleaf, nr, seg_order);
     } else if (nr.d16)
         launch_first_moves_t<true>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
                                    grid, blk, s);
@@ -3340,7 +3518,7 @@ void launch_rle_count_ch(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint
                          uint8_t* rc, uint32_t* xs, uint32_t* cc, hipStream_t s) {
     if (!nrows) return;
     const uint32_t nch = rle_count_chunks(npad);
-    const kern::RleChunks rk{xs, cc};
+    const kern::RleChunks rk{xs, cc, xs + (size_t)nrows * nch};
     const dim3 grid((nch + 15u) / 16u, (nrows + 15u) / 16u), blk(256);
     launch(kern::rle_count_ch<32>, grid, blk, s, fm, npad, nrows, st, rc, rk);
 }
@@ -3349,7 +3527,7 @@ void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t*
                     uint8_t* rc, uint32_t* xs, uint32_t* cc, uint32_t* counts, uint32_t* hard,
                     hipStream_t s) {
     if (!nrows) return;
-    const kern::RleChunks rk{xs, cc};
+    const kern::RleChunks rk{xs, cc, xs + (size_t)nrows * rle_count_chunks(npad)};
     launch(kern::rle_fix<32>, dim3(nrows), dim3(64), s, fm, npad, nrows, st, rc, rk, counts,
            hard);
 }
@@ -3494,13 +3672,12 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
 }
 
 // Lane slots for nq searches: at most CPD_SEARCH_WAVES (1024) one-wave
-// workgroups, in multiples of 4 waves (64k lanes: 3,389 q/s at fscale 0 on
-// the 1M graph against 1,657 with 256 waves, profiles/search_lanes_ab/)
+// workgroups (64k lanes: 3,389 q/s at fscale 0 on the 1M graph against
+// 1,657 with 256 waves, profiles/search_lanes_ab/), a whole wave each
 uint32_t search_slots(uint32_t nq) {
-    static const uint32_t waves = std::max(4u, env_u32("CPD_SEARCH_WAVES", 1024));
+    static const uint32_t waves = std::max(1u, env_u32("CPD_SEARCH_WAVES", 1024));
     const uint32_t want = (nq + 63u) / 64u;
-    const uint32_t w = std::max(1u, std::min(waves, want));
-    return 64u * ((w + 3u) / 4u * 4u);
+    return 64u * std::max(1u, std::min(waves, want));
 }
 
 void launch_search_tables(const uint32_t* dense, uint32_t npad, uint32_t lb, const uint32_t* adj_f,
@@ -3545,10 +3722,11 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
                        const uint32_t* qs, const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
                        double hscale, double fscale, int32_t kmoves, int64_t itrs,
                        uint64_t time_ns, uint64_t tick_ns, void* ws, uint32_t cap,
-                       uint32_t slots, uint64_t* cost, uint32_t* plen, uint8_t* fin,
-                       uint32_t* qstats, unsigned long long* agg, hipStream_t s) {
+                       uint32_t slots, const SearchSpillArgs& spill, uint64_t* cost,
+                       uint32_t* plen, uint8_t* fin, uint32_t* qstats, unsigned long long* agg,
+                       hipStream_t s) {
     const bool tables = hrow != nullptr;
-    const uint32_t waves = slots / 64u;  // a multiple of 4 (search_slots)
+    const uint32_t waves = slots / 64u;  // a multiple of 64 lanes (search_slots)
     char* p = static_cast<char*>(ws);
     const size_t h2 = (size_t)slots * 2u * cap, h1 = (size_t)slots * cap;
     kern::SearchWs w;
@@ -3570,6 +3748,8 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     w.hc = reinterpret_cast<uint32_t*>(p);
     const kern::SearchOpt o{hscale, fscale, kmoves, itrs, time_ns, tick_ns};
     const kern::SearchTables tb{hrow, crow, lrow, n};
+    const kern::SearchSpill sp{spill.resume, spill.rin, spill.at, spill.rout, spill.top,
+                               spill.cap_words};
     // a wave per workgroup: the searches are latency chains, and 256 waves
     // as 64 four-wave workgroups sat on a quarter of the CUs (their L1s and
     // address units shared four ways) while the rest idled
@@ -3580,7 +3760,7 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     const uint32_t wpr = npad >> (5u - lb);
 #define CPD_SEARCH(SH, T)                                                                    \
     launch(kern::cpd_search<SH, T>, grid, blk, s, af, aw, dense, wpr, lb, tb, qs, qt, qrow, nq, c2, \
-           o, w, cost, plen, fin, qstats, agg)
+           o, w, sp, cost, plen, fin, qstats, agg)
 #define CPD_SEARCH_T(SH)          \
     if (tables) CPD_SEARCH(SH, true); \
     else CPD_SEARCH(SH, false)
@@ -3655,6 +3835,12 @@ void launch_scatter_u8(const uint8_t* in, const uint32_t* perm, uint32_t nq, uin
 // heap 16 + 4, and for memoised walks the memo (2 x 16) and walk stack (16).
 uint64_t search_ws_bytes_per_slot(uint32_t cap, bool tables) {
     return (tables ? 68ull : 116ull) * cap;
+}
+
+// a record: the head, <= cap heap entries of 5 words, <= cap columns of 5
+// (tables) or 9 (walks) words
+uint64_t search_spill_words(uint32_t cap, bool tables) {
+    return kern::kSpillHead + (tables ? 10ull : 14ull) * cap;
 }
 
 }  // namespace cpd

@@ -95,10 +95,13 @@ uint32_t fm_bits(uint32_t shift);
 // u16, 4 nibbles per lane, written by the down-sweep): leaf columns copy their
 // sets instead of recomputing them; both null = every column computed.  Only
 // for 4-bit sets (shift <= 2).
+// seg_order (may be null; npad / 32 entries, a permutation): the order the
+// 32-column segments are handed to the workgroups (the narrow 4-slot kernel).
 void launch_first_moves(const uint32_t* adj, uint32_t shift, const uint32_t* dist,
                         const uint32_t* tgt, uint32_t B, uint32_t rows, uint32_t n,
                         uint32_t npad, uint32_t* fm, const uint32_t* leafbits,
-                        const uint16_t* fmleaf, NarrowRows nr, hipStream_t s);
+                        const uint16_t* fmleaf, NarrowRows nr, hipStream_t s,
+                        const uint32_t* seg_order = nullptr);
 // Whether that launch reads each computed column's own distance row (the
 // pipelined narrow kernel derives it from the neighbour rows instead).
 bool first_moves_reads_own(uint32_t shift, bool narrow);
@@ -146,7 +149,8 @@ void launch_moves_runs(const uint32_t* dense, uint32_t stride, uint32_t lb, uint
 // from a guessed entry state; launch_rle_fix then repairs the chunk seams and
 // writes counts[row], or sets *hard (zeroed by the caller) when a row's runs
 // are too long for that to be cheap: the caller then runs launch_rle_count
-// on the batch instead.  xs / cc: nrows x rle_count_chunks(npad) u32 each.
+// on the batch instead.  cc: nrows x rle_count_chunks(npad) u32; xs: twice
+// that (the chunks' exit states, then their guessed entry states).
 // rle_count_chunks = 0: off (CPD_RLE_CH=0), use launch_rle_count.
 uint32_t rle_count_chunks(uint32_t npad);
 void launch_rle_count_ch(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
@@ -230,17 +234,34 @@ void launch_search_tables(const uint32_t* dense, uint32_t npad, uint32_t lb, con
                           uint32_t rows, uint32_t n, void* scratch, uint32_t chunk_rows,
                           uint64_t* hrow, uint64_t* crow, uint32_t* lrow, int write_h,
                           hipStream_t s);
-// Lane slots the search launches for nq queries (a multiple of 256); the
+// Lane slots the search launches for nq queries (a multiple of 64); the
 // workspace holds search_ws_bytes_per_slot(cap, tables) bytes per slot.
 uint32_t search_slots(uint32_t nq);
 uint64_t search_ws_bytes_per_slot(uint32_t cap, bool tables);
+// Resumable overflow (cpd_kernels.hip "Resumable overflow"): a search that
+// would outgrow its workspace stops before the pop and, when rout is set,
+// copies its state into that pool (a record of at most
+// search_spill_words(cap, tables) u32 words; *top bumps, cap_words bounds
+// it), reports fin = 3 and at[q] = the record's word offset (fin = 2: no
+// room in the pool, it restarts).  resume[q] != ~0 (resume may be null):
+// query q continues from its record at rin + resume[q].
+struct SearchSpillArgs {
+    const unsigned long long* resume = nullptr;
+    const uint32_t* rin = nullptr;
+    unsigned long long* at = nullptr;
+    uint32_t* rout = nullptr;
+    unsigned long long* top = nullptr;
+    unsigned long long cap_words = 0;
+};
+uint64_t search_spill_words(uint32_t cap, bool tables);
 void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t shift,
                        const uint32_t* dense, uint32_t npad, uint32_t lb, const uint64_t* hrow,
                        const uint64_t* crow, const uint32_t* lrow, uint32_t n,
                        const uint32_t* qs, const uint32_t* qt, const uint32_t* qrow, uint32_t nq,
                        double hscale, double fscale, int32_t kmoves, int64_t itrs,
                        uint64_t time_ns, uint64_t tick_ns, void* ws, uint32_t cap,
-                       uint32_t slots, uint64_t* cost, uint32_t* plen, uint8_t* fin,
-                       uint32_t* qstats, unsigned long long* agg, hipStream_t s);
+                       uint32_t slots, const SearchSpillArgs& spill, uint64_t* cost,
+                       uint32_t* plen, uint8_t* fin, uint32_t* qstats, unsigned long long* agg,
+                       hipStream_t s);
 
 }  // namespace cpd

@@ -5,7 +5,12 @@
 //                 --workerid I --maxworker W --outdir D
 //                 [--partition M]      README.md:89 spelling of --partmethod
 //                 [--device G]         default: I % (visible GPUs)
-//                 [--batch B]          rows per GPU sweep (multiple of 1024)
+//                 [--batch B]          rows per GPU sweep (multiple of 1024);
+//                                      0 (default) = what fits in HBM, at most
+//                                      2048 rows when files are written (the
+//                                      disk bounds the worker) and
+//                                      24576 with --discard (CPD_BATCH_MAX
+//                                      overrides), with or without the arena
 //                 [--no-arena]         allocate the batch buffers at graph setup
 //                                      instead of committing them on a host
 //                                      thread beside the plan (default)
@@ -372,7 +377,22 @@ int main(int argc, char** argv) {
     }
     const bool moves = format == "moves";
     // compact buckets striped over part files (DOSCPD03; 1 = one DOSCPD02 file)
-    const uint32_t stripes = (uint32_t)std::max<long long>(1, a.num("stripes", 16));
+    const long long stripes_arg = a.num("stripes", 16);
+    if (stripes_arg < 1 || stripes_arg > 4096) {  // what the reader accepts
+        std::fprintf(stderr, "make_cpd_auto: --stripes must be in [1, 4096]\n");
+        return 2;
+    }
+    const uint32_t stripes = (uint32_t)stripes_arg;
+    // the automatic batch's cap, the same with or without the arena: writing
+    // files, the sink bounds the worker (the GPU builds rows ~30x faster than
+    // a disk takes them), so a batch past 2048 rows only adds HBM
+    // to commit beside the plan; --discard keeps the build-bound cap
+    const uint32_t batch_cap = [&] {
+        const char* bm = std::getenv("CPD_BATCH_MAX");
+        const double dflt = a.has("discard") ? 24.0 : 2.0;
+        const double k = bm && *bm ? std::max(1.0, std::min(32.0, std::floor(std::atof(bm) / 1024))) : dflt;
+        return (uint32_t)k * 1024u;
+    }();
     std::string outdir = a.str("outdir", dir_of(input));
     ::mkdir(outdir.c_str(), 0755);
     double t_start = now();
@@ -431,14 +451,7 @@ int main(int argc, char** argv) {
                 const double fit = avail > 0 ? 0.85 * avail / (double)per1k : 0.0;
                 if (fit < 1.0)
                     throw std::runtime_error("HBM reserve leaves too little for a 1024-row batch");
-                // the library's cap (A/B knob).  Writing files, the sink bounds
-                // the worker (the GPU builds rows ~30x faster than a disk takes
-                // them), so a batch past 2048 rows only adds HBM to
-                // commit beside the plan; --discard keeps the build-bound cap
-                const char* bm = std::getenv("CPD_BATCH_MAX");
-                const double dflt = a.has("discard") ? 24.0 : 2.0;
-                const double cap = bm && *bm ? std::max(1.0, std::min(32.0, std::floor(std::atof(bm) / 1024))) : dflt;
-                batch = (uint32_t)std::min(cap, std::floor(fit)) * 1024u;
+                batch = (uint32_t)std::min((double)(batch_cap / 1024u), std::floor(fit)) * 1024u;
             }
             cli::check(cpd_batch_bytes(g.n, maxdeg, batch, &arena_bytes), "batch bytes");
             arena_thr = std::thread([&] {
@@ -526,6 +539,15 @@ int main(int argc, char** argv) {
         if (a.has("hbm-reserve"))
             cli::check(cpd_graph_set_hbm_reserve(dg, (uint64_t)(a.real("hbm-reserve", 0.0) * (1ull << 30))),
                        "hbm reserve");
+        if (batch == 0) {  // --no-arena: what fits in 85% of the free HBM, capped as above
+            uint32_t maxdeg = 1;
+            for (uint32_t v = 0; v < g.n; ++v) maxdeg = std::max(maxdeg, g.row_ptr[v + 1] - g.row_ptr[v]);
+            uint64_t fr = 0, tot = 0, per1k = 0;
+            cli::check(cpd_device_mem_info(device, &fr, &tot), "device memory");
+            cli::check(cpd_batch_bytes(g.n, maxdeg, 1024, &per1k), "batch bytes");
+            const double fit = std::floor(0.85 * std::max(0.0, (double)fr - hbm_reserve) / (double)per1k);
+            if (fit >= 1.0) batch = (uint32_t)std::min((double)(batch_cap / 1024u), fit) * 1024u;
+        }
         cli::check(cpd_graph_set_batch(dg, batch), "batch");
         const double t_batch = now() - t_g0 - t_graph;
         // the .xy coordinates order each batch's lanes (compact target groups)

@@ -391,9 +391,21 @@ void cpd_index_free(cpd_index* ix);
  * in each search's workspace, so an index of any size can be searched.  The
  * results and counters are the same either way.  A search's workspace holds
  * `capacity` columns (searched ones; with walks also the walked ones; 68 /
- * 116 B each): one that needs more (after capacity_max's reruns) stops
- * unfinished, with finished = 2 in cpd_query_fetch, and is counted in
- * `overflow`.  The time limit is wall clock (as fifo_auto runs it);
+ * 116 B each).  Before each pop a search checks that the expansion fits;
+ * when it might not, it stops there with its state whole and (when a
+ * larger pass can follow) copies it into a spill pool; the next pass, at
+ * 4x the capacity, resumes it from there — same pops, counters and results
+ * as one uninterrupted search (a search whose record finds the pool full
+ * restarts from scratch instead; `wasted_expanded` counts that work).  What
+ * still overflows at capacity_max (or when no larger workspace fits in
+ * HBM) stops unfinished, with finished = 2 in cpd_query_fetch, and is
+ * counted in `overflow`.  capacity = 0 selects the library's workspace
+ * policy (what fifo_auto runs): the first pass at 2^13 columns when fscale
+ * > 0 and 2^15 at fscale 0, lowered (to 2^10 at most) until every query of
+ * the request gets a lane; capacity_max 0 = 4 n rounded up to a power of 2
+ * (<= 2^24); workspace_frac 0 = 0.85 of the free HBM.  An explicit capacity
+ * keeps capacity_max 0 = no larger pass and workspace_frac 0 = 0.25.  The
+ * time limit is wall clock (as fifo_auto runs it);
  * virtual_tick_ns > 0 replaces it by a deterministic clock that advances
  * virtual_tick_ns per expansion and per edge touched (the oracle's
  * restatement, for tests).                                                   */
@@ -406,16 +418,17 @@ typedef struct cpd_search_opts {
     int32_t  k_moves;      /* -1: whole CPD paths */
     int64_t  itrs;         /* -1: no expansion limit */
     uint64_t time_ns;      /* 0: no time limit (per query) */
-    uint32_t capacity;     /* columns per search, power of 2 (0 = 32768) */
+    uint32_t capacity;     /* columns per search, power of 2 (0 = automatic) */
     uint64_t virtual_tick_ns; /* 0: wall-clock time limit; else virtual clock */
     int32_t  tables;       /* CPD_SEARCH_AUTO / _TABLES / _WALKS             */
-    double   workspace_frac; /* share of the free HBM the lanes' workspaces may
-                                take (0 = 0.25); more lanes search at once   */
-    uint32_t capacity_max; /* 0: none; else searches that overflow `capacity`
-                              run again, alone, at 4x the capacity (fewer
-                              lanes) up to capacity_max: many lanes for the
-                              common short searches, the big workspace only
-                              for the long ones                             */
+    double   workspace_frac; /* share of the free HBM the lanes' workspaces and
+                                spill pools may take (0 = automatic / 0.25);
+                                more lanes search at once                    */
+    uint32_t capacity_max; /* 0: automatic / none; else searches that overflow
+                              `capacity` continue in later passes at 4x the
+                              capacity (fewer lanes) up to capacity_max: many
+                              lanes for the common short searches, the big
+                              workspace only for the long ones              */
 } cpd_search_opts;
 
 typedef struct cpd_search_stats {
@@ -425,6 +438,12 @@ typedef struct cpd_search_stats {
     double   tables_ms;    /* device time spent (re)building the tables     */
     int32_t  tables;       /* the form used: CPD_SEARCH_TABLES or _WALKS    */
     uint64_t reruns;       /* searches run again at a larger capacity       */
+    uint64_t resumed;      /* ... of them continued from a spilled state    */
+    uint64_t restarted;    /* ... of them started over (spill pool full)    */
+    uint64_t wasted_expanded; /* expansions the restarted ones threw away  */
+    uint32_t passes;       /* search kernel launches (1 + escalations)      */
+    uint32_t capacity;     /* columns per lane of the first pass            */
+    uint32_t capacity_last;/* ... of the last pass                          */
 } cpd_search_stats;
 
 int  cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stats* st);

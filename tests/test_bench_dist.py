@@ -30,6 +30,7 @@ t0 = time.perf_counter()
 time.sleep(0.05 * (rank + 1))            # uneven ranks: max must win
 elapsed = time.perf_counter() - t0
 (emax,) = comm.reduce([elapsed], "MAX")
+ranks = bench.rank_table(1024, args.steps, [v[0] for v in comm.gather([elapsed])])
 qt = comm.reduce([1000.0, 10.0 * (rank + 1), 5000.0], "SUM")
 (qmax,) = comm.reduce([10.0 * (rank + 1)], "MAX")
 allowned = [None] * world
@@ -37,6 +38,7 @@ dist.all_gather_object(allowned, owned.tolist())
 if rank == 0:
     out = bench.assemble(args, world, (n, 4000), 1024, emax, qt, qmax, 1024, 2048, {}, None,
                          None, None)
+    out["ranks"] = ranks
     out["_owned"] = allowned
     out["_elapsed_local"] = elapsed
     print("RESULT " + json.dumps(out), flush=True)
@@ -64,6 +66,12 @@ def test_two_rank_gloo_aggregation(tmp_path):
     emax = 3 * 1024 * 2 / out["value"]
     assert emax >= 0.099  # rank 1 slept 0.1 s
     assert out["queries_per_s"] == pytest.approx(2000.0 / 0.020, rel=1e-6)
+    # the per-rank view: rank 1 slept twice as long and limits the line
+    rk = out["ranks"]
+    assert [r["rank"] for r in rk["per_rank"]] == [0, 1] and rk["slowest_rank"] == 1
+    assert rk["per_rank"][1]["ms_per_step"] > rk["per_rank"][0]["ms_per_step"]
+    assert rk["imbalance_max_over_min"] > 1.5
+    assert rk["per_rank"][1]["ms_per_step"] == pytest.approx(emax / 3 * 1e3, rel=1e-3)
     for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "higher_is_better",
               "vs_baseline", "dtype", "data", "config"):
         assert k in out
@@ -150,3 +158,8 @@ def test_eight_rank_full_build_plumbing(tmp_path, filecomm):
     assert fb["rows"] == sum(100 + r for r in range(8))
     assert fb["export_GB"] == round(8 * 5000 / 1e9, 2)
     assert fb["files_GB"] == round(1000 / 1e9, 2)    # rank 0's files
+    # each worker's own line; the slowest one named
+    assert [p["worker"] for p in fb["per_rank"]] == list(range(8))
+    assert [p["total_s"] for p in fb["per_rank"]] == [1.0 + 0.25 * r for r in range(8)]
+    assert fb["per_rank"][3]["rows_per_s"] == round(103 / 1.75, 1)
+    assert fb["slowest_rank"] == 7 and fb["imbalance_max_over_min"] == round(2.75 / 1.0, 4)

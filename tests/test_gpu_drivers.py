@@ -128,7 +128,8 @@ def _read_bucket(path):
 def _read_move_bucket(path):
     """The compact bucket layouts of csrc/cpd_io.cpp (MoveBucketFile): DOSCPD02
     (rows after the header) or DOSCPD03 (rows striped over part files
-    {path}.p{j}: unit u of stripe_rows rows is unit u // K of part u % K)."""
+    {path}.{fingerprint:016x}.p{j}: unit u of stripe_rows rows is unit u // K of
+    part u % K)."""
     raw = open(path, "rb").read()
     assert raw[:8] in (b"DOSCPD02", b"DOSCPD03")
     n, nrows, bid, method, key, maxworker, words, bits = (int(x) for x in np.frombuffer(raw, np.uint32, 8, 8))
@@ -147,7 +148,9 @@ def _read_move_bucket(path):
         targets = np.frombuffer(raw, np.uint32, nrows, p)
         counts = np.frombuffer(raw, np.uint32, nrows, p + 4 * nrows)
         assert len(raw) == p + 8 * nrows
-        parts = [np.fromfile(f"{path}.p{j}", np.uint32).reshape(-1, words) for j in range(K)]
+        fp = int(np.frombuffer(raw, np.uint64, 1, 48)[0])
+        parts = [np.fromfile(f"{path}.{fp:016x}.p{j}", np.uint32).reshape(-1, words)
+                 for j in range(K)]
         moves = np.empty((nrows, words), np.uint32)
         for u in range(-(-nrows // S)):
             r0, r1 = u * S, min(nrows, u * S + S)

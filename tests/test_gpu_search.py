@@ -104,9 +104,10 @@ def test_search_overflow_is_counted_tables(env):
     assert need > cap
     cost, plen, fin, cnt, st = ix.search(s, t, capacity=cap, tables="tables")
     assert st["overflow"] >= 1
-    # pushes = inserted + updated bound a search's nodes and heap entries:
-    # searches below the capacity are exact, those above it stop unfinished
-    small = rs[:, 1] + rs[:, 3] < cap
+    # pushes = inserted + updated bound a search's nodes and heap entries; a
+    # search stops before a pop whose expansion (<= 4 pushes on this graph)
+    # might not fit: those with room for it are exact, those above stop
+    small = rs[:, 1] + rs[:, 3] + 4 <= cap
     assert small.sum() > 100
     np.testing.assert_array_equal(cost[small], rc[small])
     np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small])
@@ -124,9 +125,9 @@ def test_search_overflow_is_counted_walks(env):
     cost, plen, fin, cnt, st = ix.search(s, t, capacity=cap, tables="walks")
     assert st["overflow"] >= 1
     # a search's workspace holds every column its walks and search met (the
-    # oracle's 6th stat) and its heap at most inserted + updated pushes:
-    # searches within the capacity are exact, those above it stop unfinished
-    small = (rs[:, 5] <= cap) & (rs[:, 1] + rs[:, 3] < cap)
+    # oracle's 6th stat) and its heap at most inserted + updated pushes (+ the
+    # room one expansion needs): searches within it are exact, the others stop
+    small = (rs[:, 5] <= cap) & (rs[:, 1] + rs[:, 3] + 4 <= cap)
     assert small.sum() > 100
     np.testing.assert_array_equal(cost[small], rc[small])
     np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small, :5])
@@ -136,16 +137,22 @@ def test_search_overflow_is_counted_walks(env):
 
 @pytest.mark.parametrize("form", ["tables", "walks"])
 def test_search_capacity_escalation(env, form):
-    """Searches that overflow a small workspace rerun at 4x capacity until
-    none does: every result and counter (and the sums) the oracle's."""
+    """Searches that overflow a small workspace stop before the pop, spill
+    their state and resume at 4x the capacity until none does: every result
+    and counter (and the sums) the oracle's, nothing thrown away."""
     g, plan, dev, targets, off, runs, s, t, wc = env
     ix = _index(env, "dense")
     ix.set_weights(wc)
     rc, rp, rf, rs = _oracle(env, wc)
     _, _, fin1, _, st1 = ix.search(s, t, capacity=64, tables=form)
-    assert st1["overflow"] > 0 and st1["reruns"] == 0
+    assert st1["overflow"] > 0 and st1["reruns"] == 0 and st1["passes"] == 1
     cost, plen, fin, cnt, st = ix.search(s, t, capacity=64, capacity_max=4096, tables=form)
-    assert st["overflow"] == 0 and st["reruns"] >= st1["overflow"]
+    assert st["overflow"] == 0 and st["reruns"] >= st1["overflow"] and st["resumed"] > 0
+    # no expansion is thrown away (with walks, a search whose first walk
+    # outgrows the workspace starts over before expanding anything)
+    assert st["wasted_expanded"] == 0 and st["passes"] >= 2
+    if form == "tables":
+        assert st["restarted"] == 0 and st["resumed"] >= st1["overflow"]
     np.testing.assert_array_equal(cost, rc)
     np.testing.assert_array_equal(plen, rp)
     np.testing.assert_array_equal(fin, rf)
@@ -155,6 +162,61 @@ def test_search_capacity_escalation(env, form):
     # a capacity_max that still leaves some overflowing: those report 2
     _, _, fin3, _, st3 = ix.search(s, t, capacity=64, capacity_max=256, tables=form)
     assert int((fin3 == 2).sum()) == st3["overflow"] <= st1["overflow"]
+    assert not (fin3 == 3).any()
+
+
+@pytest.mark.parametrize("form", ["tables", "walks"])
+def test_search_spill_pool_full_restarts(env, form, monkeypatch):
+    """A spill pool too small for every record: the searches whose records
+    do not fit restart from scratch at the next capacity (their first pass
+    counted as wasted), the others resume — the same results either way."""
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    rc, rp, rf, rs = _oracle(env, wc)
+    monkeypatch.setenv("CPD_SEARCH_POOL_WORDS", "60000")
+    cost, plen, fin, cnt, st = ix.search(s, t, capacity=64, capacity_max=4096, tables=form)
+    assert st["restarted"] > 0 and st["resumed"] > 0 and st["wasted_expanded"] > 0
+    assert st["overflow"] == 0
+    np.testing.assert_array_equal(cost, rc)
+    np.testing.assert_array_equal(plen, rp)
+    np.testing.assert_array_equal(fin, rf)
+    np.testing.assert_array_equal(cnt.astype(np.uint64), rs)
+    assert st["expanded"] == int(rs[:, 0].sum())
+
+
+def test_search_capacity_max_beyond_hbm(env):
+    """capacity_max far above what fits: the passes grow only
+    as far as 64 lanes fit in the workspace share, nothing is thrown, and
+    what still overflows reports finished = 2; the rest is exact."""
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    rc, rp, rf, rs = _oracle(env, wc, columns=True)
+    cost, plen, fin, cnt, st = ix.search(s, t, capacity=64, capacity_max=1 << 24, tables="walks",
+                                         workspace_frac=2e-5)
+    assert st["capacity_last"] < (1 << 24)
+    assert int((fin == 2).sum()) == st["overflow"]
+    ok = fin != 2
+    assert ok.sum() > 100
+    np.testing.assert_array_equal(cost[ok], rc[ok])
+    np.testing.assert_array_equal(cnt[ok].astype(np.uint64), rs[ok, :5])
+    np.testing.assert_array_equal(fin[ok], rf[ok])
+
+
+def test_search_auto_policy(env):
+    """capacity 0: the library's workspace policy (fifo_auto's) — a first
+    pass at <= 2^15 columns, escalation to 4 n, the whole request exact."""
+    g, plan, dev, targets, off, runs, s, t, wc = env
+    ix = _index(env, "dense")
+    ix.set_weights(wc)
+    for fs in (0.0, 0.1):
+        rc, rp, rf, rs = _oracle(env, wc, fscale=fs)
+        cost, plen, fin, cnt, st = ix.search(s, t, fscale=fs, tables="walks")
+        assert st["overflow"] == 0 and 1024 <= st["capacity"] <= (1 << 15)
+        np.testing.assert_array_equal(cost, rc)
+        np.testing.assert_array_equal(fin, rf)
+        np.testing.assert_array_equal(cnt.astype(np.uint64), rs)
 
 
 @pytest.mark.parametrize("form", ["tables", "walks"])
