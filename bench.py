@@ -108,7 +108,7 @@ def plan_path(args):
 # rocprofv3 kernel names -> the library's timing names
 KERNEL_NAMES = {"sweep_level<true": "sweep_up", "sweep_up_": "sweep_up",
                 "sweep_level<false": "sweep_down", "sweep_down8": "sweep_down",
-                "first_moves": "first_moves", "rle_scan<": "rle_count",
+                "first_moves": "first_moves", "rle_scan<": "rle_count", "rle_emit": "rle_emit",
                 "rle_moves": "rle_moves", "rle_count_ch": "rle_count", "rle_fix": "rle_fix",
                 "moves_runs": "moves_runs", "DenseRows": "table_search_dense",
                 "RleRows": "table_search", "table_search_dense": "table_search_dense",
@@ -416,7 +416,8 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
     }
 
 
-BUILD_KERNELS = ("sweep_up", "sweep_down", "first_moves", "rle_count", "rle_fix", "rle_moves")
+BUILD_KERNELS = ("sweep_up", "sweep_down", "first_moves", "rle_count", "rle_fix", "rle_moves",
+                 "rle_emit")
 
 
 def step_pmc(traffic, step_s):
@@ -716,7 +717,8 @@ def _serve_start(args, xy, outdir, W, device, alg, fifo):
     `fifo`): (process, its load record, seconds until it listens)."""
     cmd = [os.path.join(ROOT, "bin", "fifo_auto"), "--input", xy, xy + ".diff", "--partmethod",
            args.partmethod, "--partkey", str(args.partkey), "--workerid", "0", "--maxworker",
-           str(W), "--outdir", outdir, "--alg", alg, "--device", str(device), "--fifo", fifo]
+           str(W), "--outdir", outdir, "--alg", alg, "--device", str(device), "--fifo", fifo,
+           "--verbose"]
     t0 = time.time()
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
     rec = _read_ready(p, t0 + 300)
@@ -757,6 +759,8 @@ def _serve_request(fifo, outdir, name, s, t, diff="-", **conf):
 
 
 def _serve_stop(p, fifo):
+    """Ends the server ("quit"); returns its per-request phase records
+    (--verbose: read + parse, prepare, compute seconds)."""
     try:
         with open(fifo, "w") as f:
             f.write("quit\n")
@@ -765,6 +769,9 @@ def _serve_stop(p, fifo):
         if p.poll() is None:
             p.kill()
             p.wait()
+    err = p.stderr.read().decode(errors="replace") if p.stderr else ""
+    return [json.loads(ln.split(": ", 1)[1]) for ln in err.splitlines()
+            if ln.startswith("fifo_auto-req: ")]
 
 
 def _stats(line):
@@ -816,7 +823,7 @@ def serve_leg(args, xy, outdir, W, device, g, order, threads, nprobe=4, big=1_00
         _serve_request(fifo, outdir, "warm", bs, bt)  # first request of this size: buffers
         bline, bwall, _ = _serve_request(fifo, outdir, "big", bs, bt)
     finally:
-        _serve_stop(p, fifo)
+        reqs = _serve_stop(p, fifo)
     st = _stats(bline)
     out.update({"ready_s": round(ready, 3), "load": rec, "probe_queries": probe_q,
                 "probe_targets": nprobe, "answer": line, "bit_exact": exact,
@@ -825,6 +832,7 @@ def serve_leg(args, xy, outdir, W, device, g, order, threads, nprobe=4, big=1_00
                                  "queries_per_s": round(big / bwall, 1),
                                  "t_receive_s": st["t_receive_s"], "t_search_s": st["t_search_s"],
                                  "finished": st["finished"], "answer": bline,
+                                 "phases": reqs[-1] if reqs else None,
                                  "note": "wall = request written to answer read (the head's "
                                          "t_partition without ssh); the query file is written "
                                          "before, as process_query's t_prepare"}})
@@ -847,7 +855,7 @@ def serve_leg(args, xy, outdir, W, device, g, order, threads, nprobe=4, big=1_00
         sline, swall, _ = _serve_request(fifo, outdir, "sbig", ss, stt, diff=xy + ".diff",
                                          fscale=0.1)
     finally:
-        _serve_stop(p, fifo)
+        sreqs = _serve_stop(p, fifo)
     st2 = _stats(sline)
     out["cpd_search"] = {"ready_s": round(ready2, 3), "probe_queries": search_probe_q,
                          "probe_answer": line2, "bit_exact": sexact, "fscale": 0.1,
@@ -858,7 +866,7 @@ def serve_leg(args, xy, outdir, W, device, g, order, threads, nprobe=4, big=1_00
                          "queries_per_s_search": round(search_q / st2["t_search_s"], 1)
                          if st2["t_search_s"] else None,
                          "finished": st2["finished"], "mean_expanded": round(st2["n_expanded"] / search_q, 1),
-                         "answer": sline}
+                         "answer": sline, "phases": sreqs[-1] if sreqs else None}
     return out
 
 

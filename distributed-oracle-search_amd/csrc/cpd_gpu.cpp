@@ -171,14 +171,29 @@ uint32_t batch_max() {
 // chunk states (12 B per chunk: exit, count, entry) + leaf sets + two rows of move tables (npad / 2
 // each: the row set being built and the one a caller such as make_cpd_auto
 // is exporting).
+// CPD_RLE_FUSED=0: the count / seam repair / emit passes instead of the
+// fused one-pass emit (4-bit sets; A/B, identical rows)
+bool rle_fused_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("CPD_RLE_FUSED");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+bool rle_fused(uint32_t fmb) { return fmb == 4 && rle_fused_on(); }
+
 double batch_bytes_per_row(uint32_t n, uint32_t npad, uint32_t fmb, bool narrow, bool leaf_fm) {
-    return (narrow ? 6.0 : 4.0) * n + 2.0 * (fmb / 8.0 * npad + 5.0 / 32.0 * npad) +
-           (fmb == 4 ? 12.0 * rle_count_chunks(npad) : 0.0) + (leaf_fm ? 0.5 * n : 0.0) +
+    // the fused emit keeps no segment states: 12 B per chunk of 32k columns
+    const double rle = rle_fused(fmb) ? 12.0 * rle_emit_chunks(npad)
+                                      : 2.0 * 5.0 / 32.0 * npad +
+                                            (fmb == 4 ? 12.0 * rle_count_chunks(npad) : 0.0);
+    return (narrow ? 6.0 : 4.0) * n + 2.0 * fmb / 8.0 * npad + rle + (leaf_fm ? 0.5 * n : 0.0) +
            2.0 * 0.5 * npad;
 }
 bool up_priority_on();
 bool lane_key_on();
 bool seg_order_on();
+bool search_trace();
 std::vector<uint32_t> hilbert_keys(const int32_t* x, const int32_t* y, uint32_t n);
 
 }  // namespace
@@ -250,6 +265,7 @@ struct cpd_graph {
     // chunk exit states / run counts of the chunked count (read by rle_fix on
     // the same stream before the next batch: one set)
     DevBuf<uint32_t> rle_xs, rle_cc, rle_hard;
+    DevBuf<uint32_t> emit_ck;  // fused emit: the chunks' guessed entries, exits, breaks
     HostBuf<uint32_t> rle_hard_h;          // [1]
     // the buffer set the next batch uses, once the emit that last read it is done
     uint32_t acquire_set() {
@@ -485,8 +501,9 @@ struct cpd_graph {
         // the second buffer set when it takes under an eighth of the HBM
         // still free after the batch's own buffers (else one set: emits do
         // not overlap)
+        const bool fused = rle_fused(fmb);
         const size_t set_bytes = (size_t)B * (npad / (32u / fmb)) * 4u +
-                                 (size_t)B * (npad / 32u) * 5u + 4u * B;
+                                 (fused ? 0u : (size_t)B * (npad / 32u) * 5u) + 4u * B;
         for (int x = 0; x < 2; ++x) {
             if (x == 1) {
                 size_t free_b = 0, total_b = 0;
@@ -501,12 +518,19 @@ struct cpd_graph {
                 }
             }
             fmx[x].alloc((size_t)B * (npad / (32u / fmb)));
-            rle_stx[x].alloc((size_t)B * (npad / 32u));
-            rle_rcx[x].alloc((size_t)B * (npad / 32u));
+            if (fused) {
+                rle_stx[x].release();
+                rle_rcx[x].release();
+            } else {
+                rle_stx[x].alloc((size_t)B * (npad / 32u));
+                rle_rcx[x].alloc((size_t)B * (npad / 32u));
+            }
             lane_rowx[x].alloc(B);
         }
         cur = 0;
-        if (fmb == 4 && rle_count_chunks(npad)) {
+        if (fused) {
+            emit_ck.alloc(3ull * B * rle_emit_chunks(npad));
+        } else if (fmb == 4 && rle_count_chunks(npad)) {
             rle_xs.alloc(2ull * B * rle_count_chunks(npad));
             rle_cc.alloc((size_t)B * rle_count_chunks(npad));
             rle_hard.alloc(1);
@@ -1609,35 +1633,49 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     HIP_CHECK(hipMemcpyAsync(g->lane_rowx[x].p, rb->lane_rows.p, k * sizeof(uint32_t),
                              hipMemcpyHostToDevice, es));
     const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
-    if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
-        HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), es));
-        g->timed("rle_count", (fm_row + st_row + 12.0 * nch) * k, [&] {
-            launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, es);
+    if (rle_fused(g->fmb)) {
+        // one pass: each set read once, the tables written, the run counts
+        // summed from the chunks (rle_emit4 + the seam check rle_emit_fix)
+        const uint32_t ec = rle_emit_chunks(npad);
+        const size_t cks = (size_t)k * ec;
+        g->timed("rle_emit", (fm_row + 4.0 * r->wpr) * k + 24.0 * cks + 8.0 * k, [&] {
+            launch_rle_emit(fm, npad, k, g->lane_rowx[x].p, r->tlb, r->moves.p, g->emit_ck.p,
+                            g->emit_ck.p + cks, g->emit_ck.p + 2 * cks, g->counts.p, es);
         });
-        g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
-            launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
-                           g->rle_hard.p, es);
-        });
-        // runs too long for the seam repair: the bounded pass, which does
-        // nothing unless rle_fix raised rle_hard
-        g->timed("rle_recount", 0.0, [&] {
-            launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es, g->rle_hard.p);
-        });
-    } else {
-        g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
-            launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es);
+        HIP_CHECK(hipMemcpyAsync(rb->counts.p, g->counts.p, k * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, es));
+        HIP_CHECK(hipEventRecord(rb->ev, es));
+    } else {  // the count, the seam repair and the emit (8/16-bit sets, or CPD_RLE_FUSED=0)
+        if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
+            HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), es));
+            g->timed("rle_count", (fm_row + st_row + 12.0 * nch) * k, [&] {
+                launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, es);
+            });
+            g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
+                launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
+                               g->rle_hard.p, es);
+            });
+            // runs too long for the seam repair: the bounded pass, which does
+            // nothing unless rle_fix raised rle_hard
+            g->timed("rle_recount", 0.0, [&] {
+                launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es, g->rle_hard.p);
+            });
+        } else {
+            g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
+                launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es);
+            });
+        }
+        HIP_CHECK(hipMemcpyAsync(rb->counts.p, g->counts.p, k * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                 es));
+        HIP_CHECK(hipEventRecord(rb->ev, es));
+        // per row: the sets (fm_row), the segment states (4 B per 32 columns;
+        // the run counts are read only where the look-ahead needs them), the
+        // table (npad * bits / 8)
+        const double ebytes = (fm_row + 4.0 * npad / 32.0 + 4.0 * r->wpr) * k + 4.0 * k;
+        g->timed("rle_moves", ebytes, [&] {
+            launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, r->tlb, r->moves.p, es);
         });
     }
-    HIP_CHECK(hipMemcpyAsync(rb->counts.p, g->counts.p, k * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                             es));
-    HIP_CHECK(hipEventRecord(rb->ev, es));
-    // per row: the sets (fm_row), the segment states (4 B per 32 columns;
-    // the run counts are read only where the look-ahead needs them), the
-    // table (npad * bits / 8)
-    const double ebytes = (fm_row + 4.0 * npad / 32.0 + 4.0 * r->wpr) * k + 4.0 * k;
-    g->timed("rle_moves", ebytes, [&] {
-        launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, r->tlb, r->moves.p, es);
-    });
     if (!r->done) HIP_CHECK(hipEventCreateWithFlags(&r->done, hipEventDisableTiming));
     HIP_CHECK(hipEventRecord(r->done, es));
     if (g->async) {
@@ -1945,7 +1983,7 @@ std::unique_ptr<cpd_index> index_init(cpd_graph* g, const uint32_t* row_targets,
     }
     ix->offsets.assign(1, 0);
     ix->d_row_of_col.upload(ix->row_of_col.data(), g->n, g->stream);
-    ix->agg.alloc(3);
+    ix->agg.alloc(4);
     ix->flag.alloc(1);
     return ix;
 }
@@ -2460,7 +2498,7 @@ int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
         const uint32_t nq = ix->nq;
         const bool dense = ix->use_dense();
         if (dense && !ix->dense_ready) ensure_dense(ix);
-        HIP_CHECK(hipMemsetAsync(ix->agg.p, 0, 3 * sizeof(unsigned long long), g->stream));
+        HIP_CHECK(hipMemsetAsync(ix->agg.p, 0, 4 * sizeof(unsigned long long), g->stream));
         hipEvent_t a = g->get_event(), b = g->get_event();
         HIP_CHECK(hipEventRecord(a, g->stream));
         const uint32_t* adj = ix->custom_w ? ix->adj_sel.p : g->adj.p;
@@ -2475,9 +2513,12 @@ int cpd_query_run(cpd_index* ix, int32_t k_moves, cpd_query_stats* st) {
                                 ix->hops.p, ix->fin.p, ix->agg.p, g->stream);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipEventRecord(b, g->stream));
-        unsigned long long hagg[3] = {0, 0, 0};
+        unsigned long long hagg[4] = {0, 0, 0, 0};
         HIP_CHECK(hipMemcpyAsync(hagg, ix->agg.p, sizeof hagg, hipMemcpyDeviceToHost, g->stream));
         HIP_CHECK(hipStreamSynchronize(g->stream));
+        if (hagg[3] && search_trace())  // CPD_TS_SHARE: the moves suffix sharing skipped
+            std::fprintf(stderr, "[walk] %llu queries, %llu moves, %llu of them taken from "
+                         "earlier walks' suffixes\n", (unsigned long long)nq, hagg[1], hagg[3]);
         float ms = 0.f;
         HIP_CHECK(hipEventElapsedTime(&ms, a, b));
         g->ev_pool.push_back(a);

@@ -1636,6 +1636,309 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
     }
 }
 
+// ---------------------------------------------------------------------------
+// One pass per row chunk: count + emit fused (4-bit sets).
+// rle_count_ch + rle_fix + rle_moves4 read every first-move set twice (the
+// count, then the emit) and write and re-read the per-segment entry states:
+// ~50 GB of HBM per 24576-row step for 12.3 GB of sets and 12.3 GB of
+// tables.  Here a wave owns a chunk of kMoveTiles tiles of one row and:
+//   forward  resolves every segment's entry set itself: lane L guesses its
+//            entry by scanning lane L-1's last 16 columns from a wildcard
+//            set, scans its 32 columns, and takes lane L-1's exit instead
+//            wherever the guess differs — repeated until no lane changes (a
+//            fixed point reached left to right: one round as a rule); lane
+//            0 starts from the previous tile's exit.  The entry sets go to
+//            LDS (a byte per segment), the breaks are counted on the way;
+//   ahead    finds the closing set of the run open at the chunk's right
+//            edge: before the first break the running set is the exit set
+//            ANDed with every set passed, so a wave-wide prefix-AND of the
+//            segments' own ANDs finds the segment holding the break, which
+//            one lane scans (the row's last run: its set at the end);
+//   backward fills the move table right to left as rle_moves4 does, the
+//            entry sets from LDS and the look-ahead's closing set as carry;
+// so each set is read once from HBM (the backward pass re-reads the chunk's
+// 64 KiB per 4-row workgroup from L2) and only the tables are written.  The
+// chunk's own entry is a guess too (its first segment scanned from its left
+// neighbour's last 16 columns; exact for chunk 0): rle_emit_fix then walks
+// each row's chunks, and a chunk whose guess differs from its left
+// neighbour's exit is done again from the true entry by the same code —
+// only that chunk: its left neighbour's look-ahead started from its own
+// exact exit set.  Per chunk: the guessed entry, the exit set and the breaks
+// (xe, xs, cc, [nrows][nch] u32); the row's runs = its breaks + 1.
+struct EmitChunks {
+    uint32_t* xe;
+    uint32_t* xs;
+    uint32_t* cc;
+};
+
+// the greedy running set after 32 columns from S, and the breaks among them
+__device__ __forceinline__ uint32_t scan32_breaks(const uint32_t (&v)[4], uint32_t& S) {
+    uint32_t brk = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t f = (v[k >> 3] >> (4 * (k & 7))) & 0xFu;
+        const uint32_t T = S & f;
+        brk += T == 0u ? 1u : 0u;
+        S = T ? T : f;
+    }
+    return brk;
+}
+
+// The chunk [t0, t1) of row `brow` from entry set Sin (wave-cooperative; every
+// lane of the wave calls it with the same arguments).  ent: 64 * kMoveTiles
+// bytes of LDS for this wave.  Writes the chunk's move table; returns the
+// exit set (wave-uniform) and adds the chunk's breaks to `breaks` (per lane).
+__device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uint32_t nseg,
+                                uint32_t ntiles, uint32_t t0, uint32_t t1, uint32_t Sin,
+                                uint8_t* ent, uint32_t* __restrict__ orow, uint32_t lb,
+                                uint32_t lane, uint32_t& breaks) {
+    auto load = [&](uint32_t seg, uint32_t (&v)[4]) {
+        const uint4 q = f4[fm4_piece(brow, nseg, seg)];
+        v[0] = q.x;
+        v[1] = q.y;
+        v[2] = q.z;
+        v[3] = q.w;
+    };
+    // forward: the segments' entry sets
+    uint32_t carry = Sin;  // the set entering the tile in hand
+    for (uint32_t t = t0; t < t1; ++t) {
+        uint32_t v[4];
+        load(t * 64u + lane, v);
+        const uint32_t p2 = (uint32_t)__shfl_up((int)v[2], 1, 64);
+        const uint32_t p3 = (uint32_t)__shfl_up((int)v[3], 1, 64);
+        uint32_t in = 0xFu;  // the guess: lane - 1's last 16 columns from a wildcard
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t f = ((k < 8 ? p2 : p3) >> (4 * (k & 7))) & 0xFu;
+            const uint32_t T = in & f;
+            in = T ? T : f;
+        }
+        if (lane == 0) in = carry;
+        uint32_t out, nb;
+        for (;;) {
+            out = in;
+            nb = scan32_breaks(v, out);
+            uint32_t pe = (uint32_t)__shfl_up((int)out, 1, 64);
+            if (lane == 0) pe = carry;
+            const bool fix = pe != in;
+            if (!__any(fix)) break;
+            if (fix) in = pe;
+        }
+        ent[(t - t0) * 64u + lane] = (uint8_t)in;
+        breaks += nb;
+        carry = (uint32_t)__shfl((int)out, 63, 64);
+    }
+    const uint32_t exitS = carry;
+    // ahead: the closing set of the run open at the right edge
+    uint32_t close = 0;
+    {
+        uint32_t P = exitS;
+        bool found = false;  // wave-uniform
+        for (uint32_t t = t1; t < ntiles && !found; ++t) {
+            uint32_t v[4];
+            load(t * 64u + lane, v);
+            uint32_t a = v[0] & v[1] & v[2] & v[3];
+            a &= a >> 16;
+            a &= a >> 8;
+            a &= a >> 4;
+            const uint32_t A = a & 0xFu;
+            uint32_t incl = A;  // inclusive prefix-AND over the lanes
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+                if (lane >= (uint32_t)o) incl &= y;
+            }
+            uint32_t excl = (uint32_t)__shfl_up((int)incl, 1, 64);
+            if (lane == 0) excl = 0xFu;
+            const uint32_t Pl = P & excl;
+            const uint64_t m = __ballot((Pl & A) == 0u);
+            if (m) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                uint32_t c = 0;
+                if (lane == j) {  // the set just before the break
+                    uint32_t S = Pl;
+                    for (int k = 0; k < 32; ++k) {
+                        const uint32_t T = S & ((v[k >> 3] >> (4 * (k & 7))) & 0xFu);
+                        if (!T) break;
+                        S = T;
+                    }
+                    c = S;
+                }
+                close = (uint32_t)__shfl((int)c, (int)j, 64);
+                found = true;
+            } else {
+                P &= (uint32_t)__shfl((int)incl, 63, 64);
+            }
+        }
+        if (!found) close = P;  // no run closes right of the chunk: the row's last run
+    }
+    // backward: the move table (rle_moves4's fill)
+    carry = close;
+    for (uint32_t t = t1; t-- > t0;) {
+        uint32_t v[4];
+        load(t * 64u + lane, v);
+        const Seg4 r = seg4_scan(v, ent[(t - t0) * 64u + lane]);
+        const bool any = (r.Z[0] | r.Z[1] | r.Z[2] | r.Z[3]) != 0u;
+        const uint32_t fl = seg4_entry_set(r);
+        const uint64_t m = __ballot(any);
+        const uint64_t right = lane == 63u ? 0ull : (m >> (lane + 1u)) << (lane + 1u);
+        const uint32_t j = right ? (uint32_t)__builtin_ctzll(right) : lane;
+        const uint32_t fj = (uint32_t)__shfl((int)fl, (int)j, 64);
+        const uint32_t tail = right ? fj : carry;
+        uint32_t V[4], X[4];
+        {
+            uint32_t nz[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) nz[i] = r.Z[i] | (r.Z[i] - (r.Z[i] >> 3));
+            V[0] = __builtin_amdgcn_alignbit(nz[1], nz[0], 4);
+            V[1] = __builtin_amdgcn_alignbit(nz[2], nz[1], 4);
+            V[2] = __builtin_amdgcn_alignbit(nz[3], nz[2], 4);
+            V[3] = (nz[3] >> 4) | 0xF0000000u;
+            X[0] = r.S[0];
+            X[1] = r.S[1];
+            X[2] = r.S[2];
+            X[3] = (r.S[3] & 0x0FFFFFFFu) | (tail << 28);
+        }
+#pragma unroll
+        for (int sh = 4; sh <= 16; sh <<= 1) {
+            uint32_t xs[4], vs[4];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                xs[i] = __builtin_amdgcn_alignbit(X[i + 1], X[i], sh);
+                vs[i] = __builtin_amdgcn_alignbit(V[i + 1], V[i], sh);
+            }
+            xs[3] = X[3] >> sh;
+            vs[3] = V[3] >> sh;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
+                V[i] |= vs[i];
+            }
+        }
+#pragma unroll
+        for (int w = 1; w <= 2; w <<= 1) {
+            uint32_t xs[4], vs[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xs[i] = i + w < 4 ? X[i + w] : 0u;
+                vs[i] = i + w < 4 ? V[i + w] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
+                V[i] |= vs[i];
+            }
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t b0 = ~X[i] & 0x11111111u;
+            const uint32_t b1 = ~(X[i] >> 1) & b0;
+            const uint32_t b2 = ~(X[i] >> 2) & b1;
+            o[i] = b0 + b1 + b2;
+        }
+        store_cols32(orow, t * 64u + lane, lb, o);
+        if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
+    }
+    return exitS;
+}
+
+// wave per (row, chunk of kMoveTiles tiles); 4 waves per workgroup = 4 rows
+__global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm, uint32_t npad,
+                                                 uint32_t nrows, const uint32_t* __restrict__ out_row,
+                                                 uint32_t lb, uint32_t* __restrict__ dense,
+                                                 EmitChunks ck) {
+    __shared__ uint8_t ent_all[4 * 64 * kMoveTiles];
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t brow = blockIdx.y * 4u + wv;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (brow >= nrows) return;  // wave-uniform
+    const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
+    const uint32_t nch = (ntiles + kMoveTiles - 1u) / kMoveTiles;
+    const uint32_t ch = blockIdx.x;
+    const uint32_t t0 = ch * kMoveTiles;
+    if (t0 >= ntiles) return;
+    const uint32_t t1 = min(ntiles, t0 + kMoveTiles);
+    const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
+    // the chunk's entry: a wildcard at column 0, else the guess from the
+    // last 16 columns left of the chunk (one segment, scanned by every lane)
+    uint32_t Sin = 0xFu;
+    if (t0) {
+        const uint4 q = f4[fm4_piece(brow, nseg, t0 * 64u - 1u)];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t f = ((k < 8 ? q.z : q.w) >> (4 * (k & 7))) & 0xFu;
+            const uint32_t T = Sin & f;
+            Sin = T ? T : f;
+        }
+    }
+    uint32_t* __restrict__ orow = dense + (size_t)out_row[brow] * (npad >> (5u - lb));
+    uint32_t breaks = 0;
+    const uint32_t xs = emit_chunk4(f4, brow, nseg, ntiles, t0, t1, Sin, ent_all + wv * 64u * kMoveTiles,
+                                    orow, lb, lane, breaks);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) breaks += (uint32_t)__shfl_xor((int)breaks, o, 64);
+    if (lane == 0) {
+        const size_t at = (size_t)brow * nch + ch;
+        ck.xe[at] = Sin;
+        ck.xs[at] = xs;
+        ck.cc[at] = breaks;
+    }
+}
+
+// The chunks' seams, a wave per row: lane j holds chunk b + j's guessed entry,
+// exit and breaks; the first chunk whose guess differs from its left
+// neighbour's (true) exit is done again from that exit (emit_chunk4, the
+// whole wave), which may change its exit for the next comparison.
+// counts[row] = the row's runs.
+__global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ fm, uint32_t npad,
+                                                   uint32_t nrows, const uint32_t* __restrict__ out_row,
+                                                   uint32_t lb, uint32_t* __restrict__ dense,
+                                                   EmitChunks ck, uint32_t* __restrict__ counts) {
+    __shared__ uint8_t ent[64 * kMoveTiles];
+    const uint32_t row = blockIdx.x;
+    if (row >= nrows) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
+    const uint32_t nch = (ntiles + kMoveTiles - 1u) / kMoveTiles;
+    const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
+    uint32_t* __restrict__ orow = dense + (size_t)out_row[row] * (npad >> (5u - lb));
+    uint32_t carry = 0xFu, total = 0;
+    for (uint32_t b = 0; b < nch; b += 64u) {
+        const uint32_t c = b + lane;
+        const bool valid = c < nch;
+        const size_t at = (size_t)row * nch + c;
+        uint32_t in = valid ? ck.xe[at] : 0u;
+        uint32_t ex = valid ? ck.xs[at] : 0u;
+        uint32_t cnt = valid ? ck.cc[at] : 0u;
+        for (;;) {
+            uint32_t pred = (uint32_t)__shfl_up((int)ex, 1, 64);
+            if (lane == 0) pred = carry;
+            const uint64_t m = __ballot(valid && pred != in);
+            if (!m) break;
+            const uint32_t j = (uint32_t)__builtin_ctzll(m);
+            const uint32_t Sj = (uint32_t)__shfl((int)pred, (int)j, 64);
+            const uint32_t t0 = (b + j) * kMoveTiles;
+            uint32_t br = 0;
+            const uint32_t xj = emit_chunk4(f4, row, nseg, ntiles, t0, min(ntiles, t0 + kMoveTiles), Sj,
+                                            ent, orow, lb, lane, br);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) br += (uint32_t)__shfl_xor((int)br, o, 64);
+            if (lane == j) {
+                in = Sj;
+                ex = xj;
+                cnt = br;
+            }
+        }
+        uint32_t sum = cnt;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o, 64);
+        total += sum;
+        carry = (uint32_t)__shfl((int)ex, 63, 64);
+    }
+    if (lane == 0) counts[row] = total + 1u;  // + the row's first run
+}
+
 // The compact form on the wire and on disk: a move per column in `bits` =
 // 1, 2 or 4 bits (every move of a graph whose out-degrees are <= 2^bits fits:
 // a move indexes its column's out-list, and a wildcard run's lowest set bit
@@ -2436,6 +2739,124 @@ __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
     }
 }
 
+// Suffix sharing between the walks of one wave (the
+// experiment behind CPD_TS_SHARE=1, dense rows, 4-slot adjacency): a wave's
+// chunk is target-sorted, and walks to one target follow one tree of CPD
+// moves, so a walk that reaches a column an earlier walk to the same target
+// passed can add that walk's remaining (cost, moves) and stop — bit-exact,
+// both being sums along one deterministic path.  Per wave, in LDS: a lossy
+// table of (column -> walk, its cost and moves so far), overwritten by every
+// hop, and the totals of the walks that finished.  A walk looks its column
+// up before each hop; a hit on a finished walk of the same row ends it.
+constexpr uint32_t kShareCols = 1024, kShareFin = 256;
+
+__global__ __launch_bounds__(64) void table_walk_share(
+    const uint2* __restrict__ adj, DenseRows rows, const uint32_t* __restrict__ qs,
+    const uint32_t* __restrict__ qt, const uint32_t* __restrict__ qrow, uint32_t nq,
+    uint32_t chunk, uint32_t limit, uint64_t* __restrict__ cost_out,
+    uint32_t* __restrict__ hops_out, uint8_t* __restrict__ fin_out,
+    unsigned long long* __restrict__ agg, unsigned long long* __restrict__ saved) {
+    __shared__ uint4 col_tab[kShareCols];  // column, walk (query) + 1, cost so far (lo, hi)
+    __shared__ uint32_t col_hops[kShareCols];
+    __shared__ uint4 fin_tab[kShareFin];   // walk + 1, row, total cost lo, hi
+    __shared__ uint32_t fin_hops[kShareFin];
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t i = lane; i < kShareCols; i += 64u) col_tab[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i = lane; i < kShareFin; i += 64u) fin_tab[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t wave = blockIdx.x;
+    const uint64_t q0l = wave * chunk;
+    const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
+    const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
+    uint64_t sum_cost = 0;
+    uint32_t sum_hops = 0, sum_fin = 0;
+    unsigned long long skipped = 0;
+    WalkState w;
+    w.q = kIdleQ;
+    w.cur = 0;
+    w.t = 0;
+    w.hops = 0;
+    w.bad = false;
+    w.cost = 0;
+    w.row = rows.dense;
+    uint32_t myrow = 0;
+    uint32_t next = q0;
+    if (q0 + lane < q1) {
+        walk_begin(w, q0 + lane, qs, qt, qrow, rows);
+        myrow = qrow[q0 + lane];
+    }
+    next = min(q1, q0 + 64u);
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    for (;;) {
+        const bool idle = w.q == kIdleQ;
+        // a column an earlier finished walk to this row passed: its suffix
+        if (!idle && w.cur != w.t && !w.bad) {
+            const uint32_t h = (w.cur * 0x9E3779B1u) >> 22;  // kShareCols = 2^10
+            const uint4 e = col_tab[h];
+            if (e.x == w.cur && e.y) {
+                const uint32_t fq = e.y - 1u;
+                const uint4 fe = fin_tab[fq & (kShareFin - 1u)];
+                if (fe.x == e.y && fe.y == myrow) {
+                    const uint32_t rest = fin_hops[fq & (kShareFin - 1u)] - col_hops[h];
+                    if (w.hops + rest <= limit) {
+                        w.cost += (((uint64_t)fe.w << 32) | fe.z) - (((uint64_t)e.w << 32) | e.z);
+                        w.hops += rest;
+                        w.cur = w.t;
+                        skipped += rest;
+                    }
+                }
+            }
+        }
+        const bool done = !idle && (w.cur == w.t || w.hops >= limit || w.bad);
+        const uint64_t m = __ballot(done);
+        if (m) {
+            if (done) {
+                const uint32_t fin = w.cur == w.t ? 1u : 0u;
+                cost_out[w.q] = w.cost;
+                hops_out[w.q] = w.hops;
+                fin_out[w.q] = (uint8_t)fin;
+                sum_cost += w.cost;
+                sum_hops += w.hops;
+                sum_fin += fin;
+                if (fin) {
+                    const uint32_t fi = w.q & (kShareFin - 1u);
+                    fin_tab[fi] = make_uint4(w.q + 1u, myrow, (uint32_t)w.cost, (uint32_t)(w.cost >> 32));
+                    fin_hops[fi] = w.hops;
+                }
+                const uint32_t nqi = next + (uint32_t)__builtin_popcountll(m & lt_mask);
+                if (nqi < q1) {
+                    walk_begin(w, nqi, qs, qt, qrow, rows);
+                    myrow = qrow[nqi];
+                } else {
+                    w.q = kIdleQ;
+                }
+            }
+            next = min(q1, next + (uint32_t)__builtin_popcountll(m));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (!__any(w.q != kIdleQ)) break;
+        if (w.q != kIdleQ && w.cur != w.t) {  // record this column, then one hop
+            const uint32_t h = (w.cur * 0x9E3779B1u) >> 22;
+            col_tab[h] = make_uint4(w.cur, w.q + 1u, (uint32_t)w.cost, (uint32_t)(w.cost >> 32));
+            col_hops[h] = w.hops;
+        }
+        WalkState one[1] = {w};
+        walk_hops<2, 1>(one, adj, rows);
+        w = one[0];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    wave_stats(sum_cost, sum_hops, sum_fin, agg);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) skipped += __shfl_xor(skipped, o, 64);
+    if (lane == 0 && saved) atomicAdd(saved, skipped);
+}
+
 // ---------------------------------------------------------------------------
 // CPD-heuristic search (semantics restated in
 // oracle/cpd_oracle.c ora_cpd_search, [U]).
@@ -2566,6 +2987,13 @@ struct SearchWs {
     uint32_t* hc;   // [slots][C] heap: column
     uint4* stk;     // [slots][C] walk stack: hash slot, w free, w selected, -
     uint32_t cap;   // C (power of 2)
+    // lane-major (stride != 0): slot s's arrays lie together in one block at
+    // base + s * stride (ent, aux, he, hc, then memo and stk with walks), so
+    // a search touches one contiguous region of a few MB instead of six
+    // regions spread over the whole workspace (fewer pages in flight per
+    // lane for the address translation); array-major above when 0
+    char* base;
+    uint64_t stride;
 };
 
 struct SearchOpt {
@@ -2625,17 +3053,23 @@ __device__ __forceinline__ uint32_t hprobe_from(const uint4* __restrict__ ent, u
     }
 }
 
-// The search heap: 4-ary (children of i at 4i+1 .. 4i+4), so a pop
-// descends log4 of the size in levels whose four child loads go out
-// together — half the dependent round trips of a binary heap.  The keys
-// (f, column, g) are a total order over the entries a search can hold (a
-// column is pushed again only with a strictly smaller g), so the pop
-// sequence — and every counter — is the oracle's binary heap's.
+// The search heap: kHeapK-ary (children of i at K i + 1 .. K i + K), so a
+// pop descends log_K of the size in levels whose K child loads go out
+// together — a binary heap's dependent round trips / log2 K.  The arrays
+// start K - 1 entries into their block (128-B aligned), so the K children
+// of every entry are one aligned group: 8 x 16 B = one 128-B line of keys
+// and 32 B of columns (round 4's 4-ary groups straddled lines every other
+// level).  The keys (f, column, g) are a total order over the entries a
+// search can hold (a column is pushed again only with a strictly smaller
+// g), so the pop sequence — and every counter — is the oracle's binary
+// heap's whatever the arity.
+constexpr uint32_t kHeapK = 8;
+
 __device__ __forceinline__ void heap_push(uint4* __restrict__ he, uint32_t* __restrict__ hc,
                                           uint32_t& size, uint64_t f, uint32_t c, uint64_t g) {
     uint32_t i = size++;
     while (i) {
-        const uint32_t p = (i - 1u) >> 2;
+        const uint32_t p = (i - 1u) / kHeapK;
         const uint4 pe = he[p];
         const uint32_t pc = hc[p];
         if (!hkey_less(f, c, g, u64of(pe.x, pe.y), pc, u64of(pe.z, pe.w))) break;
@@ -2660,13 +3094,13 @@ __device__ __forceinline__ void heap_pop(uint4* __restrict__ he, uint32_t* __res
     const uint64_t lf = u64of(le.x, le.y), lg = u64of(le.z, le.w);
     uint32_t i = 0;
     for (;;) {
-        const uint32_t k0 = 4u * i + 1u;
+        const uint32_t k0 = kHeapK * i + 1u;
         if (k0 >= size) break;
-        const uint32_t nk = min(4u, size - k0);
-        uint4 e[4];
-        uint32_t ec[4];
+        const uint32_t nk = min(kHeapK, size - k0);
+        uint4 e[kHeapK];
+        uint32_t ec[kHeapK];
 #pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j) {  // the live children, loaded together
+        for (uint32_t j = 0; j < kHeapK; ++j) {  // the live children, loaded together
             if (j < nk) {
                 e[j] = he[k0 + j];
                 ec[j] = hc[k0 + j];
@@ -2675,7 +3109,7 @@ __device__ __forceinline__ void heap_pop(uint4* __restrict__ he, uint32_t* __res
         uint4 be = e[0];
         uint32_t bc = ec[0], bk = k0;
 #pragma unroll
-        for (uint32_t j = 1; j < 4u; ++j) {
+        for (uint32_t j = 1; j < kHeapK; ++j) {
             if (j < nk && hkey_less(u64of(e[j].x, e[j].y), ec[j], u64of(e[j].z, e[j].w),
                                     u64of(be.x, be.y), bc, u64of(be.z, be.w))) {
                 be = e[j];
@@ -2690,6 +3124,120 @@ __device__ __forceinline__ void heap_pop(uint4* __restrict__ he, uint32_t* __res
     }
     he[i] = le;
     hc[i] = lc;
+}
+
+// heap_pop with the root's children (positions 1..K, those < size) and the
+// last entry already in registers — loaded beside the peek at the top, one
+// round trip before the expansion needs them — so the descent starts a
+// level down.  The root itself is the caller's.
+__device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ he, uint32_t* __restrict__ hc,
+                                             uint32_t& size, const uint4 (&e1)[kHeapK],
+                                             const uint32_t (&c1)[kHeapK], const uint4 le,
+                                             const uint32_t lc) {
+    --size;
+    if (!size) return;
+    const uint64_t lf = u64of(le.x, le.y), lg = u64of(le.z, le.w);
+    const uint32_t nk = min(kHeapK, size - 1u);  // live children of the root (< size)
+    if (!nk) {
+        he[0] = le;
+        hc[0] = lc;
+        return;
+    }
+    uint4 be = e1[0];
+    uint32_t bc = c1[0], bk = 1;
+#pragma unroll
+    for (uint32_t j = 1; j < kHeapK; ++j) {
+        if (j < nk && hkey_less(u64of(e1[j].x, e1[j].y), c1[j], u64of(e1[j].z, e1[j].w),
+                                u64of(be.x, be.y), bc, u64of(be.z, be.w))) {
+            be = e1[j];
+            bc = c1[j];
+            bk = 1u + j;
+        }
+    }
+    if (!hkey_less(u64of(be.x, be.y), bc, u64of(be.z, be.w), lf, lc, lg)) {
+        he[0] = le;
+        hc[0] = lc;
+        return;
+    }
+    he[0] = be;
+    hc[0] = bc;
+    uint32_t i = bk;
+    for (;;) {
+        const uint32_t k0 = kHeapK * i + 1u;
+        if (k0 >= size) break;
+        const uint32_t nc = min(kHeapK, size - k0);
+        uint4 e[kHeapK];
+        uint32_t ec[kHeapK];
+#pragma unroll
+        for (uint32_t j = 0; j < kHeapK; ++j) {
+            if (j < nc) {
+                e[j] = he[k0 + j];
+                ec[j] = hc[k0 + j];
+            }
+        }
+        uint4 ce = e[0];
+        uint32_t cc = ec[0], ck = k0;
+#pragma unroll
+        for (uint32_t j = 1; j < kHeapK; ++j) {
+            if (j < nc && hkey_less(u64of(e[j].x, e[j].y), ec[j], u64of(e[j].z, e[j].w),
+                                    u64of(ce.x, ce.y), cc, u64of(ce.z, ce.w))) {
+                ce = e[j];
+                cc = ec[j];
+                ck = k0 + j;
+            }
+        }
+        if (!hkey_less(u64of(ce.x, ce.y), cc, u64of(ce.z, ce.w), lf, lc, lg)) break;
+        he[i] = ce;
+        hc[i] = cc;
+        i = ck;
+    }
+    he[i] = le;
+    hc[i] = lc;
+}
+
+// The expansion's pushes (one per out-edge at most, `valid`), their parents
+// loaded together: a new entry no less than its parent stays where it lands
+// (the rule in A* with a consistent heuristic: children's f are no smaller);
+// the first that must rise goes through heap_push, and so do the ones after
+// it (their parents may have moved).  The heap ends as valid as pushing one
+// by one, and pops depend only on the keys.
+template <int N>
+__device__ __forceinline__ void heap_push_n(uint4* __restrict__ he, uint32_t* __restrict__ hc,
+                                            uint32_t& size, const bool (&valid)[N],
+                                            const uint64_t (&f)[N], const uint32_t (&c)[N],
+                                            const uint64_t (&g)[N]) {
+    const uint32_t s0 = size;
+    uint4 pe[N];
+    uint32_t pcol[N];
+    uint32_t at = s0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (valid[k]) {
+            const uint32_t p = at ? (at - 1u) / kHeapK : 0u;
+            if (at && p < s0) {
+                pe[k] = he[p];
+                pcol[k] = hc[p];
+            }
+            ++at;
+        }
+    }
+    bool slow = false;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        if (!valid[k]) continue;
+        const uint32_t i = size;
+        const uint32_t p = i ? (i - 1u) / kHeapK : 0u;
+        if (!slow && (i == 0 || (p < s0 && !hkey_less(f[k], c[k], g[k], u64of(pe[k].x, pe[k].y),
+                                                     pcol[k], u64of(pe[k].z, pe[k].w))))) {
+            he[i] = make_uint4((uint32_t)f[k], (uint32_t)(f[k] >> 32), (uint32_t)g[k],
+                               (uint32_t)(g[k] >> 32));
+            hc[i] = c[k];
+            ++size;
+        } else {
+            slow = true;
+            heap_push(he, hc, size, f[k], c[k], g[k]);
+        }
+    }
 }
 
 struct Lane {
@@ -2880,9 +3428,23 @@ __global__ __launch_bounds__(256) void cpd_search(
     const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
     const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
     const uint32_t C = ws.cap;
-    const LaneWs W{ws.ent + slot * 2u * C, TABLES ? nullptr : ws.memo + slot * 2u * C,
-                   ws.aux + slot * 2u * C, ws.he + slot * C, ws.hc + slot * C,
-                   TABLES ? nullptr : ws.stk + slot * C, C, 2u * C - 1u, Tbl{lb}};
+    // lane-major (stride != 0): the slot's block = he, hc (C + K entries
+    // each), ent, aux, then memo and stk with walks; array-major: each array
+    // over all slots.  The heap pointers start K - 1 entries in (aligned
+    // child groups, see heap_pop).
+    char* const lb0 = ws.base + slot * ws.stride;
+    const uint64_t C2 = 2ull * C, CH = (uint64_t)C + kHeapK;
+    const LaneWs W = ws.stride
+        ? LaneWs{reinterpret_cast<uint4*>(lb0 + CH * 20ull),
+                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 20ull + C2 * 24ull),
+                 reinterpret_cast<uint2*>(lb0 + CH * 20ull + C2 * 16ull),
+                 reinterpret_cast<uint4*>(lb0) + (kHeapK - 1u),
+                 reinterpret_cast<uint32_t*>(lb0 + CH * 16ull) + (kHeapK - 1u),
+                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 20ull + C2 * 40ull), C,
+                 2u * C - 1u, Tbl{lb}}
+        : LaneWs{ws.ent + slot * C2, TABLES ? nullptr : ws.memo + slot * C2, ws.aux + slot * C2,
+                 ws.he + slot * CH + (kHeapK - 1u), ws.hc + slot * CH + (kHeapK - 1u),
+                 TABLES ? nullptr : ws.stk + slot * C, C, 2u * C - 1u, Tbl{lb}};
     unsigned long long s_exp = 0, s_ins = 0, s_tou = 0, s_upd = 0, s_sur = 0, s_len = 0,
                        s_fin = 0, s_ovf = 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -3067,11 +3629,22 @@ __global__ __launch_bounds__(256) void cpd_search(
         // popped once the expansion is known to fit the workspace)
         uint64_t f, g;
         uint32_t v;
+        uint4 e1[kHeapK], lst;  // the root's children and the last entry (heap_pop_pre)
+        uint32_t c1[kHeapK], lstc;
         {
             const uint4 top = W.he[0];
             f = u64of(top.x, top.y);
             g = u64of(top.z, top.w);
             v = W.hc[0];
+#pragma unroll
+            for (uint32_t j = 0; j < kHeapK; ++j) {
+                if (1u + j < L.hsize) {
+                    e1[j] = W.he[1u + j];
+                    c1[j] = W.hc[1u + j];
+                }
+            }
+            lst = W.he[L.hsize - 1u];
+            lstc = W.hc[L.hsize - 1u];
         }
         // what the expansion reads and nothing in it writes — v's out-edges
         // and, per-row tables, v's incumbent values — is loaded beside v's
@@ -3092,7 +3665,7 @@ __global__ __launch_bounds__(256) void cpd_search(
         const uint32_t hi = hprobe(W.ent, W.mask, L.tag, v, found);
         const uint4 ev = W.ent[hi];
         if (g > u64of(ev.z, ev.w)) {  // stale entry
-            heap_pop(W.he, W.hc, L.hsize, f, v, g);
+            heap_pop_pre(W.he, W.hc, L.hsize, e1, c1, lst, lstc);
             ++L.surplus;
             continue;
         }
@@ -3132,7 +3705,7 @@ __global__ __launch_bounds__(256) void cpd_search(
             L.spilled = spill();
             continue;
         }
-        heap_pop(W.he, W.hc, L.hsize, f, v, g);
+        heap_pop_pre(W.he, W.hc, L.hsize, e1, c1, lst, lstc);
         ++L.expanded;
         const uint32_t dv = W.aux[hi].x;
         {
@@ -3160,9 +3733,13 @@ if (SHIFT <= 2) {
             uint4 e0[ND];
             uint64_t hr[ND];
             uint32_t wr[ND];  // slot this expansion wrote for edge k
+            bool pv[ND];      // edge k's push (heap_push_n after the edges)
+            uint64_t pf[ND], pg[ND];
+            uint32_t pcn[ND], np = 0;
 #pragma unroll
             for (int k = 0; k < ND; ++k) {
                 wr[k] = 0xFFFFFFFFu;
+                pv[k] = false;
                 if (TABLES && ed[k].x != kNoEdge) {
                     e0[k] = W.ent[(ed[k].x * 0x9E3779B1u) & W.mask];
                     hr[k] = tb.hrow[rb + ed[k].x];
@@ -3205,7 +3782,7 @@ if (SHIFT <= 2) {
                     hu = u64of(mu.x, mu.y);
                     if (hu == kInf64) continue;
                 }
-                if (L.hsize >= C) {
+                if (L.hsize + np >= C) {
                     L.overflow = L.done = true;
                     break;
                 }
@@ -3214,9 +3791,13 @@ if (SHIFT <= 2) {
                 W.aux[ui].x = dv + 1u;
                 wr[k] = ui;
                 ++L.inserted;
-                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
+                pv[k] = true;
+                pf[k] = ng + (uint64_t)(opt.hscale * (double)hu);
+                pg[k] = ng;
+                pcn[k] = u;
+                ++np;
             } else if (ng < u64of(eu.z, eu.w)) {
-                if (L.hsize >= C) {
+                if (L.hsize + np >= C) {
                     L.overflow = L.done = true;
                     break;
                 }
@@ -3226,9 +3807,14 @@ if (SHIFT <= 2) {
                 wr[k] = ui;
                 ++L.updated;
                 const uint64_t hu = TABLES ? hr[k] : u64of(W.memo[ui].x, W.memo[ui].y);
-                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
+                pv[k] = true;
+                pf[k] = ng + (uint64_t)(opt.hscale * (double)hu);
+                pg[k] = ng;
+                pcn[k] = u;
+                ++np;
             }
         }
+        heap_push_n<ND>(W.he, W.hc, L.hsize, pv, pf, pcn, pg);
         } else {
 #pragma unroll 1
         for (int k = 0; k < (1 << SHIFT); ++k) {
@@ -3532,6 +4118,22 @@ void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t*
            hard);
 }
 
+uint32_t rle_emit_chunks(uint32_t npad) {
+    const uint32_t ntiles = npad / kern::kTile;
+    return (ntiles + kern::kMoveTiles - 1u) / kern::kMoveTiles;
+}
+
+void launch_rle_emit(const uint32_t* fm, uint32_t npad, uint32_t nrows, const uint32_t* out_row,
+                     uint32_t lb, uint32_t* dense, uint32_t* xe, uint32_t* xs, uint32_t* cc,
+                     uint32_t* counts, hipStream_t s) {
+    if (!nrows) return;
+    const kern::EmitChunks ck{xe, xs, cc};
+    launch(kern::rle_emit4, dim3(rle_emit_chunks(npad), (nrows + 3u) / 4u), dim3(256), s, fm, npad,
+           nrows, out_row, lb, dense, ck);
+    launch(kern::rle_emit_fix, dim3(nrows), dim3(64), s, fm, npad, nrows, out_row, lb, dense, ck,
+           counts);
+}
+
 void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
                       const uint32_t* st, const uint8_t* rc, const uint32_t* out_row,
                       uint32_t lb, uint32_t* dense, hipStream_t s) {
@@ -3655,10 +4257,21 @@ void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32
                                uint32_t nq, int32_t kmoves, uint32_t n, uint64_t* cost,
                                uint32_t* hops, uint8_t* fin, unsigned long long* agg,
                                hipStream_t s) {
-    launch_walk(reinterpret_cast<const uint2*>(adj), shift,
-                kern::DenseRows{dense, npad >> (5u - lb), kern::Tbl{lb}}, qs,
-                qt, qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(1024),
-                ts_chunk_max(1024), s, 1u);
+    const kern::DenseRows rows{dense, npad >> (5u - lb), kern::Tbl{lb}};
+    static const bool share = env_u32("CPD_TS_SHARE", 0) != 0;  // experiment
+    if (share && shift == 2 && nq) {
+        const uint64_t chunk = std::max<uint64_t>(
+            64u, std::min<uint64_t>(ts_chunk_max(1024), ((uint64_t)nq + ts_waves(1024) - 1u) /
+                                                            ts_waves(1024) + 63u) / 64u * 64u);
+        const uint32_t waves = (uint32_t)(((uint64_t)nq + chunk - 1u) / chunk);
+        launch(kern::table_walk_share, dim3(waves), dim3(64), s, reinterpret_cast<const uint2*>(adj),
+               rows, qs, qt, qrow, nq, (uint32_t)chunk, walk_limit(kmoves, n), cost, hops, fin, agg,
+               agg + 3);
+        return;
+    }
+    launch_walk(reinterpret_cast<const uint2*>(adj), shift, rows, qs, qt, qrow, nq,
+                walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(1024), ts_chunk_max(1024), s,
+                1u);
 }
 
 void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* row_of_col,
@@ -3669,6 +4282,11 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::RleRows{offsets, runs}, qs, qt,
                 qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(8192),
                 ts_chunk_max(1u << 30), s, 4u);
+}
+
+static bool search_lane_major() {
+    static const bool on = env_u32("CPD_SEARCH_LANE_MAJOR", 1) != 0;
+    return on;
 }
 
 // Lane slots for nq searches: at most CPD_SEARCH_WAVES (1024) one-wave
@@ -3728,24 +4346,30 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     const bool tables = hrow != nullptr;
     const uint32_t waves = slots / 64u;  // a multiple of 64 lanes (search_slots)
     char* p = static_cast<char*>(ws);
-    const size_t h2 = (size_t)slots * 2u * cap, h1 = (size_t)slots * cap;
+    const size_t h2 = (size_t)slots * 2u * cap;
     kern::SearchWs w;
     w.cap = cap;
+    // lane-major blocks (CPD_SEARCH_LANE_MAJOR=0: array-major, A/B):
+    // search_ws_bytes_per_slot each, 128-B aligned; the heap first
+    w.base = static_cast<char*>(ws);
+    w.stride = search_lane_major() ? search_ws_bytes_per_slot(cap, tables) : 0u;
+    const size_t hk = (size_t)slots * (cap + kern::kHeapK);
+    w.he = reinterpret_cast<uint4*>(p);
+    p += hk * 16u;
+    w.hc = reinterpret_cast<uint32_t*>(p);
+    p += (hk * 4u + 127u) / 128u * 128u;
     w.ent = reinterpret_cast<uint4*>(p);
     p += h2 * 16u;
+    w.aux = reinterpret_cast<uint2*>(p);
+    p += h2 * 8u;
     if (!tables) {
         w.memo = reinterpret_cast<uint4*>(p);
         p += h2 * 16u;
+        w.stk = reinterpret_cast<uint4*>(p);
     } else {
         w.memo = nullptr;
+        w.stk = nullptr;
     }
-    w.aux = reinterpret_cast<uint2*>(p);
-    p += h2 * 8u;
-    w.he = reinterpret_cast<uint4*>(p);
-    p += h1 * 16u;
-    w.stk = tables ? nullptr : reinterpret_cast<uint4*>(p);
-    if (!tables) p += h1 * 16u;
-    w.hc = reinterpret_cast<uint32_t*>(p);
     const kern::SearchOpt o{hscale, fscale, kmoves, itrs, time_ns, tick_ns};
     const kern::SearchTables tb{hrow, crow, lrow, n};
     const kern::SearchSpill sp{spill.resume, spill.rin, spill.at, spill.rout, spill.top,
@@ -3833,8 +4457,11 @@ void launch_scatter_u8(const uint8_t* in, const uint32_t* perm, uint32_t nq, uin
 
 // Workspace per lane slot and column of capacity: hash entries 2 x (16 + 8),
 // heap 16 + 4, and for memoised walks the memo (2 x 16) and walk stack (16).
+// per slot: ent 32C, aux 16C (+ memo 32C, stk 16C with walks) and the heap,
+// 20 (C + kHeapK) B; a multiple of 128 B (aligned lane-major blocks)
 uint64_t search_ws_bytes_per_slot(uint32_t cap, bool tables) {
-    return (tables ? 68ull : 116ull) * cap;
+    const uint64_t b = (tables ? 68ull : 116ull) * cap + 20ull * kern::kHeapK;
+    return (b + 127u) / 128u * 128u;
 }
 
 // a record: the head, <= cap heap entries of 5 words, <= cap columns of 5

@@ -125,6 +125,15 @@ void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
 void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
                       const uint32_t* st, const uint8_t* rc, const uint32_t* out_row,
                       uint32_t lb, uint32_t* dense, hipStream_t s);
+// Count and emit fused (4-bit sets; cpd_kernels.hip rle_emit4): the move
+// tables as launch_rle_moves writes them and counts[r] = row r's runs, each
+// set read once, no segment states; then rle_emit_fix redoes the rare chunk
+// whose guessed entry was wrong.  xe / xs / cc: nrows x rle_emit_chunks(npad)
+// u32 each (the chunks' guessed entries, exits and breaks).
+uint32_t rle_emit_chunks(uint32_t npad);
+void launch_rle_emit(const uint32_t* fm, uint32_t npad, uint32_t nrows, const uint32_t* out_row,
+                     uint32_t lb, uint32_t* dense, uint32_t* xe, uint32_t* xs, uint32_t* cc,
+                     uint32_t* counts, hipStream_t s);
 // Rows of moves from one width to another: src rows of s_bits per column at
 // s_stride words per row (s_words of them valid), dst rows of d_bits at
 // d_stride, d_words written per row (input past s_words reads as 0).  The

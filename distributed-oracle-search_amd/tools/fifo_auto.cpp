@@ -5,6 +5,7 @@
 //             --workerid I --maxworker W --outdir D --alg {table-search|cpd-search}
 //             [--partition M] [--device G] [--fifo PATH] [--once]
 //             [--index auto|rle|dense] [--read-threads T] [--parse-threads P]
+//             [--verbose]  (per request on stderr: read+parse / prepare / compute)
 //
 // Creates its request FIFO, streams the CPD buckets this worker owns onto its
 // GPU (as move tables at the graph's packed width when they are smaller
@@ -142,6 +143,7 @@ int main(int argc, char** argv) {
     bool once = a.has("once");
     // threads parsing a request's query file (a 1M-query file is ~14 MB)
     const int parse_threads = (int)a.num("parse-threads", 16);
+    const bool verbose = a.has("verbose");
     signal(SIGINT, on_signal);
     signal(SIGTERM, on_signal);
     signal(SIGPIPE, SIG_IGN);
@@ -386,6 +388,7 @@ int main(int argc, char** argv) {
             double t0 = now();
             std::vector<uint32_t> s, t;
             cpd::io::read_query_file(qfile, parse_threads, s, t);
+            const double t_read = now() - t0;
             if (diff != active_diff) {
                 if (diff == "-" ) {
                     cli::check(cpd_index_set_weights(ix, nullptr), "weights");
@@ -446,6 +449,10 @@ int main(int argc, char** argv) {
                               (unsigned long long)st.finished, (long long)(t_receive * 1e9),
                               (long long)(st.kernel_ms * 1e6));
             line = buf;
+            if (verbose)  // the receive phase split (stderr: nothing reads stdout by then)
+                std::fprintf(stderr, "fifo_auto-req: {\"queries\": %zu, \"read_parse_s\": %.6f, "
+                             "\"prepare_s\": %.6f, \"compute_s\": %.6f}\n", nq, t_read,
+                             t_receive - t_read, search ? ss.kernel_ms * 1e-3 : st.kernel_ms * 1e-3);
         } catch (const std::exception& e) {
             std::fprintf(stderr, "fifo_auto: request failed: %s\n", e.what());
         }

@@ -13,12 +13,19 @@ oracle, walk queries over them dense and RLE.  What each reaches:
   CPD_XCD=0       identity block mapping
   CPD_FM_N4=0     first_moves<4, 2, true> (generic narrow first moves)
   CPD_ASYNC=0     the emit in line (one buffer set)
-  CPD_RLE_CH=0    rle_scan<4> counts (no chunked count / seam repair)
+  CPD_RLE_FUSED=0 the count (rle_count_ch + rle_fix), then rle_moves4, instead
+                  of the one-pass rle_emit4 + rle_emit_fix
+  CPD_RLE_CH=0    rle_scan<4> counts (no chunked count / seam repair; with
+                  CPD_RLE_FUSED=0, the path that counts)
   CPD_LEAFFM=0    leaf first-move sets recomputed by first_moves
   CPD_OVERLAP=0   each batch's up-sweep after the previous batch's first moves
   CPD_MOVES_SWAR=0  rle_moves<4> (per-column move-table emit) instead of rle_moves4
+                    (with CPD_RLE_FUSED=0)
   CPD_TABLE_BITS=4  4-bit move tables whatever the degree (the rows' export
                     and the index then repack to / from the packed width)
+  CPD_FM_ORDER=0  first_moves' segments in column order (not Hilbert order)
+  CPD_TS_SHARE=1  (an experiment, off by default) dense walks that end on an
+                  earlier walk's suffix (table_walk_share)
 """
 import json
 import os
@@ -68,15 +75,18 @@ print(json.dumps(out))
 """
 
 SWITCHES = ["CPD_LIVE", "CPD_SORT", "CPD_LANE_KEY", "CPD_XCD", "CPD_FM_N4", "CPD_ASYNC",
-            "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP", "CPD_MOVES_SWAR", "CPD_TABLE_BITS"]
-OFF = {"CPD_TABLE_BITS": "4"}
+            "CPD_RLE_FUSED", "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP", "CPD_MOVES_SWAR",
+            "CPD_TABLE_BITS", "CPD_FM_ORDER", "CPD_TS_SHARE"]
+OFF = {"CPD_TABLE_BITS": "4", "CPD_TS_SHARE": "1"}
+# switches that only matter on the unfused emit path
+WITH = {"CPD_RLE_CH": {"CPD_RLE_FUSED": "0"}, "CPD_MOVES_SWAR": {"CPD_RLE_FUSED": "0"}}
 
 
 @pytest.mark.parametrize("switch", SWITCHES)
 def test_switch_off_bit_exact(switch):
     code = CHILD % (HERE, os.path.join(ROOT, "distributed-oracle-search_amd"),
                     os.path.join(ROOT, "oracle"))
-    env = dict(os.environ, **{switch: OFF.get(switch, "0")})
+    env = dict(os.environ, **{switch: OFF.get(switch, "0")}, **WITH.get(switch, {}))
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]

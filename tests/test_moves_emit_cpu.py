@@ -255,3 +255,153 @@ def test_table_width_conversions():
             nib = sum(m << (4 * k) for k, m in enumerate(mv))
             assert to(nib) == narrow, (bits, mv)
             assert frm(narrow) == nib, (bits, mv)
+
+
+# The fused one-pass emit (cpd_kernels.hip rle_emit4 / emit_chunk4 /
+# rle_emit_fix), restated: per chunk of KT tiles the segments' entry sets by
+# the lanes' guesses and a fixed point, the closing set of the run open at
+# the chunk's right edge by a prefix-AND look-ahead, the backward fill of
+# moves4 from those entries; the chunk's own entry guessed from the 16
+# columns left of it, and the seam check redoing a chunk from the true entry.
+def _segments(fm):
+    vseg = []
+    for s in range(len(fm) // 32):
+        w = [0, 0, 0, 0]
+        for k in range(32):
+            w[k >> 3] |= fm[s * 32 + k] << (4 * (k & 7))
+        vseg.append(w)
+    return vseg
+
+
+def _scan_breaks(v, S):
+    brk = 0
+    for k in range(32):
+        f = (v[k >> 3] >> (4 * (k & 7))) & 0xF
+        T = S & f
+        brk += T == 0
+        S = T if T else f
+    return S, brk
+
+
+def _guess16(w2, w3):
+    S = 0xF
+    for k in range(16):
+        f = ((w2 if k < 8 else w3) >> (4 * (k & 7))) & 0xF
+        T = S & f
+        S = T if T else f
+    return S
+
+
+def _fill_tile(vseg, t, ent, carry, out):
+    """moves4's backward step for tile t from the lanes' entry sets."""
+    lanes = [seg4_scan(vseg[t * 64 + l], ent[l]) for l in range(64)]
+    anyl = [any(z for z in L[2]) for L in lanes]
+    fl = [entry_set(L[1], L[2]) for L in lanes]
+    for l in range(64):
+        Sw, P, Z = lanes[l]
+        right = [j for j in range(l + 1, 64) if anyl[j]]
+        tail = fl[right[0]] if right else carry
+        nz = [(Z[i] | ((Z[i] - (Z[i] >> 3)) & M32)) & M32 for i in range(4)]
+        V = [alignbit(nz[1], nz[0], 4), alignbit(nz[2], nz[1], 4), alignbit(nz[3], nz[2], 4),
+             ((nz[3] >> 4) | 0xF0000000)]
+        X = [Sw[0], Sw[1], Sw[2], (Sw[3] & 0x0FFFFFFF) | (tail << 28)]
+        for sh in (4, 8, 16):
+            xs = [alignbit(X[i + 1], X[i], sh) for i in range(3)] + [X[3] >> sh]
+            vs = [alignbit(V[i + 1], V[i], sh) for i in range(3)] + [V[3] >> sh]
+            for i in range(4):
+                X[i] = (V[i] & X[i]) | (~V[i] & xs[i] & M32); V[i] |= vs[i]
+        for w in (1, 2):
+            xs = [X[i + w] if i + w < 4 else 0 for i in range(4)]
+            vs = [V[i + w] if i + w < 4 else 0 for i in range(4)]
+            for i in range(4):
+                X[i] = (V[i] & X[i]) | (~V[i] & xs[i] & M32); V[i] |= vs[i]
+        for i in range(4):
+            b0 = ~X[i] & 0x11111111; b1 = ~(X[i] >> 1) & b0; b2 = ~(X[i] >> 2) & b1
+            o = (b0 + b1 + b2) & M32
+            for k in range(8):
+                out[(t * 64 + l) * 32 + i * 8 + k] = (o >> (4 * k)) & 0xF
+    return fl[anyl.index(True)] if any(anyl) else carry
+
+
+def _emit_chunk(vseg, ntiles, t0, t1, Sin, out):
+    ents, breaks, carry = [], 0, Sin
+    for t in range(t0, t1):  # forward: the lanes' entries, a fixed point
+        v = [vseg[t * 64 + l] for l in range(64)]
+        ins = [carry] + [_guess16(v[l - 1][2], v[l - 1][3]) for l in range(1, 64)]
+        while True:
+            outs = [_scan_breaks(v[l], ins[l]) for l in range(64)]
+            pe = [carry] + [outs[l - 1][0] for l in range(1, 64)]
+            if pe == ins:
+                break
+            ins = pe  # SIMT: every mismatching lane takes its predecessor's exit
+        ents.append(ins)
+        breaks += sum(b for _, b in outs)
+        carry = outs[63][0]
+    exit_s = carry
+    P, close = exit_s, None  # ahead: prefix-AND over the segments right of the chunk
+    for t in range(t1, ntiles):
+        A = []
+        for l in range(64):
+            a = 0xF
+            for k in range(32):
+                a &= (vseg[t * 64 + l][k >> 3] >> (4 * (k & 7))) & 0xF
+            A.append(a)
+        excl = 0xF
+        for l in range(64):
+            Pl = P & excl
+            if Pl & A[l] == 0:
+                S = Pl
+                for k in range(32):
+                    T = S & ((vseg[t * 64 + l][k >> 3] >> (4 * (k & 7))) & 0xF)
+                    if not T:
+                        break
+                    S = T
+                close = S
+                break
+            excl &= A[l]
+        if close is not None:
+            break
+        P &= excl
+    if close is None:
+        close = P
+    carry = close
+    for t in range(t1 - 1, t0 - 1, -1):  # backward
+        carry = _fill_tile(vseg, t, ents[t - t0], carry, out)
+    return exit_s, breaks
+
+
+def fused4(fm, KT=16):
+    vseg = _segments(fm)
+    ntiles = len(fm) // 2048
+    out = [0] * len(fm)
+    chunks = []
+    for t0 in range(0, ntiles, KT):
+        t1 = min(ntiles, t0 + KT)
+        sin = 0xF if t0 == 0 else _guess16(vseg[t0 * 64 - 1][2], vseg[t0 * 64 - 1][3])
+        ex, br = _emit_chunk(vseg, ntiles, t0, t1, sin, out)
+        chunks.append([sin, ex, br])
+    redone, carry, total = 0, 0xF, 0  # the seam check, chunk by chunk
+    for c, ck in enumerate(chunks):
+        if ck[0] != carry:
+            t0 = c * KT
+            ex, br = _emit_chunk(vseg, ntiles, t0, min(ntiles, t0 + KT), carry, out)
+            chunks[c] = [carry, ex, br]
+            redone += 1
+        total += chunks[c][2]
+        carry = chunks[c][1]
+    return out, total + 1, redone
+
+
+def test_fused_emit_matches_greedy():
+    """Tables and run counts of the one-pass emit equal the greedy rule's,
+    over rows whose chunk guesses hold (short runs) and fail (long runs)."""
+    redone = 0
+    # a run over the whole row whose set is fixed by its first column: every
+    # chunk's guess (16 wildcard columns) differs from the true set
+    crafted = [[1] + [0xF] * 6143, [2, 3] + [0xF] * 4094 + [4] + [0xF] * 2047]
+    for i, fm in enumerate(crafted + list(_rows(4, [0, 1, 2, 3, 1, 0], [2048, 4096, 6144], 3))):
+        mv, runs = greedy_moves(fm)
+        out, count, r = fused4(fm, KT=[1, 2, 16][i % 3])
+        assert out == mv and count == len(runs)
+        redone += r
+    assert redone > 0  # the seam check redid at least one chunk
