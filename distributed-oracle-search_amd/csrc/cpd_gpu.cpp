@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <cmath>
 #include <cstring>
@@ -181,6 +182,13 @@ bool rle_fused_on() {
     return on;
 }
 bool rle_fused(uint32_t fmb) { return fmb == 4 && rle_fused_on(); }
+bool emit_defer_on() {  // CPD_EMIT_DEFER=1: emit deferred past the next batch's sweeps (A/B)
+    static const bool on = [] {
+        const char* e = std::getenv("CPD_EMIT_DEFER");
+        return e && *e == '1';
+    }();
+    return on;
+}
 
 double batch_bytes_per_row(uint32_t n, uint32_t npad, uint32_t fmb, bool narrow, bool leaf_fm) {
     // the fused emit keeps no segment states: 12 B per chunk of 32k columns
@@ -277,7 +285,19 @@ struct cpd_graph {
         }
         return x;
     }
+    // A batch's emit (count + move tables, emit stream) deferred until the
+    // next batch's down-sweep is queued, so that it runs beside that batch's
+    // first moves instead of beside its up-sweep's latency-bound narrow
+    // levels (profiles/r05e traces: the emit there stretched them 3x and the
+    // down-sweep waited).  flush_emit launches it (gated on `gate` when
+    // given); every reader of the rows, a rebuild, a sync and the graph's
+    // end flush first.  Opt-in (CPD_EMIT_DEFER=1): measured neutral, r05h.
+    std::mutex emit_mu;
+    std::function<void()> pend_emit;
+    cpd_rows* pend_rows = nullptr;
+    void flush_emit(hipEvent_t gate = nullptr);
     void drain_emits() {
+        flush_emit();
         if (estream) HIP_CHECK(hipStreamSynchronize(estream));
         emit_pending[0] = emit_pending[1] = false;
     }
@@ -358,6 +378,10 @@ struct cpd_graph {
 
     ~cpd_graph() {
         if (hipSetDevice(device) == hipSuccess) {
+            try {
+                flush_emit();
+            } catch (...) {
+            }
             if (estream) (void)hipStreamSynchronize(estream);
             for (auto e : ev_emit)
                 if (e) (void)hipEventDestroy(e);
@@ -559,10 +583,20 @@ struct cpd_rows {
     uint32_t nrows = 0;
     mutable uint64_t total = 0;  // runs of all rows (valid after settle())
     hipEvent_t done = nullptr;   // after the last batch's count + emit (emit stream)
+    // the graph holding this rows' last emit deferred (cpd_graph::pend_emit)
+    mutable std::atomic<cpd_graph*> pend_graph{nullptr};
+    void flush() const {
+        if (cpd_graph* g = pend_graph.load()) g->flush_emit();
+    }
     void wait() const {
+        flush();
         if (done) HIP_CHECK(hipEventSynchronize(done));
     }
     ~cpd_rows() {
+        try {
+            flush();
+        } catch (...) {
+        }
         if (done) {
             (void)hipEventSynchronize(done);
             (void)hipEventDestroy(done);
@@ -711,10 +745,22 @@ struct cpd_index {
     DevBuf<unsigned long long> agg;
 };
 
+void cpd_graph::flush_emit(hipEvent_t gate) {
+    std::lock_guard<std::mutex> l(emit_mu);
+    if (!pend_emit) return;
+    std::function<void()> f;
+    f.swap(pend_emit);
+    if (pend_rows) pend_rows->pend_graph.store(nullptr);
+    pend_rows = nullptr;
+    HIP_CHECK(hipSetDevice(device));
+    if (gate && estream) HIP_CHECK(hipStreamWaitEvent(estream, gate, 0));
+    f();  // under the lock: launched before anything that follows a flush
+}
+
 void cpd_rows::settle() const {
     std::lock_guard<std::mutex> l(settle_mu);
     HIP_CHECK(hipSetDevice(device));
-    wait();
+    wait();  // (a deferred emit of these rows is launched first)
     for (auto& b : retired) spare.push_back(std::move(b));
     retired.clear();
     if (pending.empty()) return;
@@ -1584,6 +1630,9 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     const double st_row = 5.0 * npad / 32.0;
     const bool narrow = g->narrow;
     launch_down_fm(g, k, narrow, fm, slot);
+    // the previous batch's emit, deferred: now, after this batch's down-sweep
+    // (beside its first moves and the next up-sweep's wide levels)
+    g->flush_emit(g->ev_down);
     const double t1 = now_seconds();
     // the next batch's up-sweep, beside this batch's first moves and count:
     // after this batch's down-sweep (ev_down: it reads the up rows, live and
@@ -1621,7 +1670,10 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     }
     const double t2 = now_seconds();
     hipStream_t es = g->async ? g->estream : g->stream;
-    if (es != g->stream) HIP_CHECK(hipStreamWaitEvent(es, g->ev_fm, 0));
+    // deferred (g->pend_emit) while another batch follows: launched by the
+    // next batch once its down-sweep is queued (cpd_graph::flush_emit)
+    const bool defer = g->async && next && next_k && emit_defer_on();
+    if (es != g->stream && !defer) HIP_CHECK(hipStreamWaitEvent(es, g->ev_fm, 0));
     // the batch's rows become table rows r->nrows + i, written by lane pos_of[i]
     const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
     CPD_REQUIRE(r->moves.n >= (size_t)(r->nrows + k) * r->wpr, CPD_E_ARG,
@@ -1630,57 +1682,67 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     rb->k = k;
     rb->pos_of.assign(pos_of.begin(), pos_of.begin() + k);
     for (uint32_t i = 0; i < k; ++i) rb->lane_rows.p[pos_of[i]] = r->nrows + i;
-    HIP_CHECK(hipMemcpyAsync(g->lane_rowx[x].p, rb->lane_rows.p, k * sizeof(uint32_t),
-                             hipMemcpyHostToDevice, es));
-    const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
-    if (rle_fused(g->fmb)) {
-        // one pass: each set read once, the tables written, the run counts
-        // summed from the chunks (rle_emit4 + the seam check rle_emit_fix)
-        const uint32_t ec = rle_emit_chunks(npad);
-        const size_t cks = (size_t)k * ec;
-        g->timed("rle_emit", (fm_row + 4.0 * r->wpr) * k + 24.0 * cks + 8.0 * k, [&] {
-            launch_rle_emit(fm, npad, k, g->lane_rowx[x].p, r->tlb, r->moves.p, g->emit_ck.p,
-                            g->emit_ck.p + cks, g->emit_ck.p + 2 * cks, g->counts.p, es);
-        });
-        HIP_CHECK(hipMemcpyAsync(rb->counts.p, g->counts.p, k * sizeof(uint32_t),
-                                 hipMemcpyDeviceToHost, es));
-        HIP_CHECK(hipEventRecord(rb->ev, es));
-    } else {  // the count, the seam repair and the emit (8/16-bit sets, or CPD_RLE_FUSED=0)
-        if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
-            HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), es));
-            g->timed("rle_count", (fm_row + st_row + 12.0 * nch) * k, [&] {
-                launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, es);
+    auto emit = [=]() {
+        HIP_CHECK(hipMemcpyAsync(g->lane_rowx[x].p, rb->lane_rows.p, k * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, es));
+        const uint32_t nch = g->fmb == 4 ? rle_count_chunks(npad) : 0u;
+        if (rle_fused(g->fmb)) {
+            // one pass: each set read once, the tables written, the run counts
+            // summed from the chunks (rle_emit4 + the seam check rle_emit_fix)
+            const uint32_t ec = rle_emit_chunks(npad);
+            const size_t cks = (size_t)k * ec;
+            g->timed("rle_emit", (fm_row + 4.0 * r->wpr) * k + 24.0 * cks + 8.0 * k, [&] {
+                launch_rle_emit(fm, npad, k, g->lane_rowx[x].p, r->tlb, r->moves.p, g->emit_ck.p,
+                                g->emit_ck.p + cks, g->emit_ck.p + 2 * cks, g->counts.p, es);
             });
-            g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
-                launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
-                               g->rle_hard.p, es);
-            });
-            // runs too long for the seam repair: the bounded pass, which does
-            // nothing unless rle_fix raised rle_hard
-            g->timed("rle_recount", 0.0, [&] {
-                launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es, g->rle_hard.p);
-            });
-        } else {
-            g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
-                launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es);
+            HIP_CHECK(hipMemcpyAsync(rb->counts.p, g->counts.p, k * sizeof(uint32_t),
+                                     hipMemcpyDeviceToHost, es));
+            HIP_CHECK(hipEventRecord(rb->ev, es));
+        } else {  // the count, the seam repair and the emit (8/16-bit sets, or CPD_RLE_FUSED=0)
+            if (nch) {  // chunked count + seam repair (rescans are rare and not counted)
+                HIP_CHECK(hipMemsetAsync(g->rle_hard.p, 0, sizeof(uint32_t), es));
+                g->timed("rle_count", (fm_row + st_row + 12.0 * nch) * k, [&] {
+                    launch_rle_count_ch(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, es);
+                });
+                g->timed("rle_fix", (12.0 * nch + 4.0) * k, [&] {
+                    launch_rle_fix(fm, npad, k, rst, rrc, g->rle_xs.p, g->rle_cc.p, g->counts.p,
+                                   g->rle_hard.p, es);
+                });
+                // runs too long for the seam repair: the bounded pass, which does
+                // nothing unless rle_fix raised rle_hard
+                g->timed("rle_recount", 0.0, [&] {
+                    launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es, g->rle_hard.p);
+                });
+            } else {
+                g->timed("rle_count", (fm_row + st_row) * k + 4.0 * k, [&] {
+                    launch_rle_count(fm, g->fmb, npad, k, g->counts.p, rst, rrc, es);
+                });
+            }
+            HIP_CHECK(hipMemcpyAsync(rb->counts.p, g->counts.p, k * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                     es));
+            HIP_CHECK(hipEventRecord(rb->ev, es));
+            // per row: the sets (fm_row), the segment states (4 B per 32 columns;
+            // the run counts are read only where the look-ahead needs them), the
+            // table (npad * bits / 8)
+            const double ebytes = (fm_row + 4.0 * npad / 32.0 + 4.0 * r->wpr) * k + 4.0 * k;
+            g->timed("rle_moves", ebytes, [&] {
+                launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, r->tlb, r->moves.p, es);
             });
         }
-        HIP_CHECK(hipMemcpyAsync(rb->counts.p, g->counts.p, k * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                 es));
-        HIP_CHECK(hipEventRecord(rb->ev, es));
-        // per row: the sets (fm_row), the segment states (4 B per 32 columns;
-        // the run counts are read only where the look-ahead needs them), the
-        // table (npad * bits / 8)
-        const double ebytes = (fm_row + 4.0 * npad / 32.0 + 4.0 * r->wpr) * k + 4.0 * k;
-        g->timed("rle_moves", ebytes, [&] {
-            launch_rle_moves(fm, g->fmb, npad, k, rst, rrc, g->lane_rowx[x].p, r->tlb, r->moves.p, es);
-        });
-    }
-    if (!r->done) HIP_CHECK(hipEventCreateWithFlags(&r->done, hipEventDisableTiming));
-    HIP_CHECK(hipEventRecord(r->done, es));
-    if (g->async) {
-        HIP_CHECK(hipEventRecord(g->ev_emit[x], es));
-        g->emit_pending[x] = true;
+        if (!r->done) HIP_CHECK(hipEventCreateWithFlags(&r->done, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(r->done, es));
+        if (g->async) {
+            HIP_CHECK(hipEventRecord(g->ev_emit[x], es));
+            g->emit_pending[x] = true;
+        }
+    };
+    if (defer) {
+        std::lock_guard<std::mutex> l(g->emit_mu);
+        g->pend_emit = emit;
+        g->pend_rows = r;
+        r->pend_graph.store(g);
+    } else {
+        emit();
     }
     if (g->timing) {  // the up levels' bytes need this batch's stats (after its first moves)
         g->sync();
@@ -2847,17 +2909,32 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             HIP_CHECK(hipMemcpyAsync(hq.data() + 2ull * m, pq_r, 4ull * m, hipMemcpyDeviceToHost, sm));
             if (sa.rout) HIP_CHECK(hipMemcpyAsync(at.data(), ix->sat.p, 8ull * m, hipMemcpyDeviceToHost, sm));
             HIP_CHECK(hipStreamSynchronize(sm));
-            // the next capacity: 4x, or less when that does not fit 64 lanes
-            // in the share (never throw there — what cannot grow
-            // reports finished = 2)
+            // The next capacity, 2x to 4x: the largest at which every search
+            // left gets a lane (one round: the long searches run side by side
+            // instead of waiting for lanes), else the largest at which 64
+            // lanes fit (never throw there — what cannot grow
+            // reports finished = 2).  With resumed searches a smaller step
+            // wastes nothing.  CPD_SEARCH_GROW=4: always 4x (A/B).
             uint32_t next = 0;
             if (more) {
+                uint32_t left = 0;
+                for (uint32_t i = 0; i < m; ++i) left += f[i] == 2u || f[i] == 3u;
                 const size_t av2 = avail(sa.rout ? ix->spool[pin ^ 1].n * 4u : 0u);
-                for (uint32_t c = std::min(cap * 4u, cap_max); c > cap; c >>= 1)
-                    if (64ull * search_ws_bytes_per_slot(c, tables) <= (size_t)(wfrac * (double)av2)) {
+                const double share2 = wfrac * (double)av2;
+                static const uint32_t grow = [] {
+                    const char* e = std::getenv("CPD_SEARCH_GROW");
+                    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+                }();
+                for (uint32_t c = std::min(cap * 4u, cap_max); c > cap; c >>= 1) {
+                    const double per = (double)search_ws_bytes_per_slot(c, tables);
+                    if (64.0 * per > share2) continue;
+                    if (!next) next = c;
+                    if (grow == 4) break;
+                    if ((double)search_slots(left) * per <= 0.9 * share2) {
                         next = c;
                         break;
                     }
+                }
             }
             std::vector<uint32_t> idx, sub;
             std::vector<unsigned long long> res;

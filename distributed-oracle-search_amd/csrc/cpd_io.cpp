@@ -226,9 +226,47 @@ Pairs read_query_file(const std::string& path) {
     return q;
 }
 
+// The whole file in one buffer: its size from fstat, then pread in pieces
+// of up to 1 GiB (split over `threads` when large) — no growth by appends.
+static std::string read_whole(const std::string& path, int threads) {
+    const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) throw Error(CPD_E_IO, "cannot open " + path);
+    struct stat st {};
+    if (::fstat(fd, &st) != 0) {
+        ::close(fd);
+        throw Error(CPD_E_IO, "cannot stat " + path);
+    }
+    std::string out((size_t)st.st_size, '\0');
+    const size_t total = out.size();
+    const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), total >> 22));
+    std::vector<char> ok(T, 1);
+    auto piece = [&](size_t k) {
+        size_t a = total * k / T, b = total * (k + 1) / T;
+        while (a < b) {
+            const ssize_t r = ::pread(fd, &out[a], std::min<size_t>(b - a, size_t(1) << 30), (off_t)a);
+            if (r <= 0) {
+                ok[k] = 0;
+                return;
+            }
+            a += (size_t)r;
+        }
+    };
+    if (T == 1) {
+        piece(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t k = 0; k < T; ++k) th.emplace_back(piece, k);
+        for (auto& x : th) x.join();
+    }
+    ::close(fd);
+    for (char c : ok)
+        if (!c) throw Error(CPD_E_IO, path + ": short read");
+    return out;
+}
+
 void read_query_file(const std::string& path, int threads, std::vector<uint32_t>& s,
                      std::vector<uint32_t>& t) {
-    const std::string text = slurp(path);
+    const std::string text = read_whole(path, threads);
     const char* const b = text.data();
     const char* const e = b + text.size();
     // header: the query count (process_query.py:95); a file without one is empty
