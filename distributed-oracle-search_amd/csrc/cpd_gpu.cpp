@@ -182,6 +182,28 @@ bool rle_fused_on() {
     return on;
 }
 bool rle_fused(uint32_t fmb) { return fmb == 4 && rle_fused_on(); }
+// CPD_CU_RESERVE=q (1..7, A/B): q CUs of every 8 kept free of the main and
+// emit streams' kernels for the high-priority up-sweep stream, spread over
+// every XCD whichever way the mask's bit order maps to XCDs (bit i reserved
+// when (i - i/32) mod 8 < q); CPD_CU_RESERVE_MAIN=0 masks the emit stream only.
+uint32_t cu_reserve() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("CPD_CU_RESERVE");
+        const unsigned long q = e && *e ? std::strtoul(e, nullptr, 10) : 0ul;
+        return (uint32_t)std::min(q, 7ul);
+    }();
+    return v;
+}
+void create_stream_masked(hipStream_t* st, uint32_t q, int ncu) {
+    if (!q || ncu <= 0) {
+        HIP_CHECK(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+        return;
+    }
+    std::vector<uint32_t> mask(((size_t)ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i)
+        if ((uint32_t)((i - i / 32) & 7) >= q) mask[(size_t)i / 32] |= 1u << (i % 32);
+    HIP_CHECK(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
+}
 bool emit_defer_on() {  // CPD_EMIT_DEFER=1: emit deferred past the next batch's sweeps (A/B)
     static const bool on = [] {
         const char* e = std::getenv("CPD_EMIT_DEFER");
@@ -350,6 +372,7 @@ struct cpd_graph {
     // and targets it was launched for, ev_up its end.
     hipStream_t ustream = nullptr;
     hipEvent_t ev_up = nullptr, ev_down = nullptr, ev_fm = nullptr;
+    hipEvent_t ev_uph = nullptr;  // the early up-sweep's head (CPD_UP_HEAD)
     bool prepped = false;
     uint32_t prep_slot = 0;
     std::vector<uint32_t> prep_targets, hint;
@@ -387,7 +410,7 @@ struct cpd_graph {
                 if (e) (void)hipEventDestroy(e);
             if (estream) (void)hipStreamDestroy(estream);
             if (ustream) (void)hipStreamSynchronize(ustream);
-            for (auto e : {ev_up, ev_down, ev_fm})
+            for (auto e : {ev_up, ev_down, ev_fm, ev_uph})
                 if (e) (void)hipEventDestroy(e);
             if (ustream) (void)hipStreamDestroy(ustream);
             if (stream) (void)hipStreamSynchronize(stream);
@@ -1017,9 +1040,14 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         auto g = std::make_unique<cpd_graph>();
         g->device = device;
         g->select();
-        HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
-        // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step)
-        HIP_CHECK(hipStreamCreateWithFlags(&g->estream, hipStreamNonBlocking));
+        {
+            int ncu = 0;
+            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+            const char* mm = std::getenv("CPD_CU_RESERVE_MAIN");
+            create_stream_masked(&g->stream, (mm && *mm == '0') ? 0u : cu_reserve(), ncu);
+            // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step)
+            create_stream_masked(&g->estream, cu_reserve(), ncu);
+        }
         // the early up-sweep's stream at the highest priority: its small,
         // latency-bound level kernels must get CUs while the first moves'
         // 600k workgroups are queued (at equal priority they waited for all
@@ -1030,7 +1058,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             HIP_CHECK(hipStreamCreateWithPriority(&g->ustream, hipStreamNonBlocking,
                                                   up_priority_on() ? greatest : least));
         }
-        for (hipEvent_t* e : {&g->ev_up, &g->ev_down, &g->ev_fm})
+        for (hipEvent_t* e : {&g->ev_up, &g->ev_down, &g->ev_fm, &g->ev_uph})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         for (auto& e : g->ev_emit) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (trace_on()) std::fprintf(stderr, "[cpd] graph streams %.3f s\n", now_seconds() - tg0);
@@ -1376,7 +1404,12 @@ void narrow_decide(cpd_graph* g) {
 // stream st: the target mask, the leaf-form init of the chunked levels and the
 // up-sweep levels.  Writes dist (up rows), live and tmask, which the previous
 // batch's down-sweep reads: the caller orders st after it.
-void launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st) {
+// In two parts when asked: from level `from` (0: the whole sweep, its init
+// included), stopping before the chunked level that would be the
+// (head_levels + 1)-th; returns the level it stopped at (the sweep's end
+// when done), where a second call resumes.
+size_t launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st, size_t from = 0,
+                 uint32_t head_levels = UINT32_MAX) {
     const uint32_t B = g->B;
     auto& S = g->bs[slot];
     const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
@@ -1384,9 +1417,9 @@ void launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st) {
     uint32_t* live = live_on() ? g->live.p : nullptr;
     unsigned int* stat = g->timing ? S.stat.p : nullptr;
     const size_t nasc = g->asc_lvl.size();
-    S.up_late.clear();
-    if (stat) HIP_CHECK(hipMemsetAsync(stat, 0, S.stat.n * sizeof(unsigned int), st));
-    if (live) {
+    if (from == 0) S.up_late.clear();
+    if (stat && from == 0) HIP_CHECK(hipMemsetAsync(stat, 0, S.stat.n * sizeof(unsigned int), st));
+    if (live && from == 0) {
         HIP_CHECK(hipMemsetAsync(g->tmask.p, 0, (size_t)g->n * sizeof(uint32_t), st));
         launch_target_mask(S.tgt.p, active, g->tmask.p, st);
         g->timed("sweep_up_init", 4.0 * g->n_init_cols * active, [&] {
@@ -1402,9 +1435,13 @@ void launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st) {
     // masks 4 B, node slot 12 B + masks 8 B, once per node — known once the
     // batch's live_stats have run (added by build_batch from S.up_late).
     g->group_begin("sweep_up", st);
-    for (size_t l = 2; l + 1 < nasc; ++l) {
+    uint32_t chunked = 0;
+    size_t l = std::max<size_t>(from, 2);
+    for (; l + 1 < nasc; ++l) {
         uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
         if (!cnt) continue;
+        const bool chunk_level = live && g->up_item_first[l + 1] > g->up_item_first[l];
+        if (chunk_level && chunked++ == head_levels) break;
         double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
         double dense = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + 8.0 * arcs_l * slabs +
                        12.0 * cnt * slabs;
@@ -1427,6 +1464,7 @@ void launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st) {
         });
     }
     g->group_end();
+    return l;
 }
 
 // The up levels' sparse bytes of a batch whose stats have arrived (S.stat_h).
@@ -1445,9 +1483,8 @@ void add_up_late_bytes(cpd_graph* g, uint32_t slot) {
 
 // Phase D of the batch in `slot` (its up-sweep done or ordered before), on
 // g->stream: the down-sweep, the wide-row count (narrow; its value lands in
-// g->ovf_h), the live stats (timing runs), then ev_down; the first moves
-// into fm, then ev_fm.
-void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slot) {
+// g->ovf_h), the live stats (timing runs), then ev_down.
+void launch_down(cpd_graph* g, uint32_t k, bool narrow, uint32_t slot) {
     const uint32_t B = g->B, n = g->n;
     auto& S = g->bs[slot];
     const NarrowRows nr = g->narrow_rows(narrow);
@@ -1500,6 +1537,16 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
         });
     }
     HIP_CHECK(hipEventRecord(g->ev_down, g->stream));
+}
+
+// Phase F: the first moves of the batch in `slot` into fm (after its
+// down-sweep on g->stream), then ev_fm; the timing stats' copy.
+void launch_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slot) {
+    const uint32_t B = g->B, n = g->n;
+    auto& S = g->bs[slot];
+    const NarrowRows nr = g->narrow_rows(narrow);
+    const double drow = narrow ? 2.0 + 4.0 / 256.0 : 4.0;
+    unsigned int* stat = g->timing ? S.stat.p : nullptr;
     // per row: own distance 4n (kernels that read it) + neighbour distances
     // 4m + first-move write npad * fmb / 8; the packed adjacency (8 B per
     // slot) is read once per 1024-target slab.  Leaf columns (leaf_fm) read
@@ -1522,12 +1569,18 @@ void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_
                                  hipMemcpyDeviceToHost, g->stream));
 }
 
+void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slot) {
+    launch_down(g, k, narrow, slot);
+    launch_fm(g, k, narrow, fm, slot);
+}
+
 // Upload a batch's targets as columns into `slot`, on stream st.  With
 // sorting on, lanes hold the targets in column order (DFS preorder is
 // spatially coherent, so a 1024-lane slab covers one compact region and the
 // up-sweep skips most rows); pos_of[i] = lane of the caller's target i.
-void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t slot,
-                    hipStream_t st) {
+// The batch's lane order and columns into the slot's host buffers (host
+// work only; upload_targets copies them to the device).
+void prepare_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t slot) {
     auto& S = g->bs[slot];
     CPD_REQUIRE(g->has_ch, CPD_E_ARG,
                 "graph was created from a plan without hierarchy: it can serve queries "
@@ -1574,6 +1627,12 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t 
     for (uint32_t i = k; i < g->B; ++i) cols[i] = cols[0];  // padding lanes
     S.tgt_col = cols;
     std::copy(cols.begin(), cols.end(), S.tgt_h.p);
+}
+
+void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t slot,
+                    hipStream_t st, bool prepared = false) {
+    if (!prepared) prepare_targets(g, targets, k, slot);
+    auto& S = g->bs[slot];
     HIP_CHECK(hipMemcpyAsync(S.tgt.p, S.tgt_h.p, (size_t)g->B * sizeof(uint32_t),
                              hipMemcpyHostToDevice, st));
 }
@@ -1582,6 +1641,21 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t 
 bool up_priority_on() {
     static const bool on = env_on("CPD_UP_PRIO");
     return on;
+}
+
+// CPD_UP_HEAD=h >= 0 (A/B): the next batch's up-sweep queued before this
+// batch's first moves, which wait for its wide levels and its first h
+// chunked levels; its narrow levels were to run beside the first moves.
+// They do not: a level's last workgroups wait for the first moves' to be
+// dispatched (profiles/up_head_ab/), so the up-sweep's head is added to the
+// step.  Default -1: the first moves first, the up-sweep beside them on the
+// high-priority stream.
+int up_head() {
+    static const int v = [] {
+        const char* e = std::getenv("CPD_UP_HEAD");
+        return e && *e ? std::atoi(e) : -1;
+    }();
+    return v;
 }
 
 // CPD_OVERLAP=0: no early up-sweep of the next batch (A/B; identical rows).
@@ -1629,34 +1703,54 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     // + per 32-column segment a 4-B entry state and a 1-B count (fmb == 4)
     const double st_row = 5.0 * npad / 32.0;
     const bool narrow = g->narrow;
-    launch_down_fm(g, k, narrow, fm, slot);
+    launch_down(g, k, narrow, slot);
     // the previous batch's emit, deferred: now, after this batch's down-sweep
     // (beside its first moves and the next up-sweep's wide levels)
     g->flush_emit(g->ev_down);
     const double t1 = now_seconds();
-    // the next batch's up-sweep, beside this batch's first moves and count:
-    // after this batch's down-sweep (ev_down: it reads the up rows, live and
-    // tmask the up-sweep rewrites), and after its first moves too if they
-    // read 32-bit rows (wide group rows, or no narrow rows at all)
-    auto prep_next = [&] {
+    // The next batch's up-sweep (ustream, high priority): after this batch's
+    // down-sweep (ev_down: it reads the up rows, live and tmask the up-sweep
+    // rewrites), and after its first moves too if they read 32-bit rows (wide
+    // group rows, or no narrow rows at all).  Otherwise it goes first: these
+    // first moves wait for its head (CPD_UP_HEAD) and run beside its tail.
+    // (The slot's target buffers are last read by the previous batch's first
+    // moves, ordered before this down-sweep: the copy waits for ev_down.)
+    bool fm_queued = false, prepared = false;
+    const uint32_t ns = slot ^ 1u;
+    auto prep_next = [&](bool head) {
         if (!(next && next_k && overlap_on())) return;
-        const uint32_t ns = slot ^ 1u;
-        upload_targets(g, next, next_k, ns, g->ustream);
-        HIP_CHECK(hipEventSynchronize(g->ev_down));  // g->ovf_h has landed
         HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
+        upload_targets(g, next, next_k, ns, g->ustream, prepared);
+        HIP_CHECK(hipEventSynchronize(g->ev_down));  // g->ovf_h has landed
         if (!narrow || g->ovf_h()) HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm, 0));
-        launch_up(g, next_k, ns, g->ustream);
+        if (head) {
+            const size_t at = launch_up(g, next_k, ns, g->ustream, 0, (uint32_t)up_head());
+            HIP_CHECK(hipEventRecord(g->ev_uph, g->ustream));
+            HIP_CHECK(hipStreamWaitEvent(g->stream, g->ev_uph, 0));
+            launch_fm(g, k, narrow, fm, slot);
+            fm_queued = true;
+            launch_up(g, next_k, ns, g->ustream, at);
+        } else {
+            launch_up(g, next_k, ns, g->ustream);
+        }
         HIP_CHECK(hipEventRecord(g->ev_up, g->ustream));
         g->prepped = true;
         g->prep_slot = ns;
         g->prep_targets.assign(next, next + next_k);
     };
+    if (up_head() >= 0 && next && next_k && overlap_on() && narrow) {
+        prepare_targets(g, next, next_k, ns);  // host work while the down-sweep runs
+        prepared = true;
+        HIP_CHECK(hipEventSynchronize(g->ev_down));
+        if (!g->ovf_h()) prep_next(true);
+    }
+    if (!fm_queued) launch_fm(g, k, narrow, fm, slot);
     // The count, the seam repair and the move-table emit of this batch go to
     // the emit stream (estream; `stream` when the overlap is off), after its
     // first moves (ev_fm): they run beside the next batch's sweeps, and the
     // run counts land in a page-locked buffer the rows settle from later
     // (cpd_rows::settle) — the host waits for none of it here.
-    prep_next();  // this batch's sweeps and first moves are queued: start the next up-sweep
+    if (!fm_queued) prep_next(false);  // this batch's sweeps and first moves are queued: start the next up-sweep
     if (!g->prepped) HIP_CHECK(hipEventSynchronize(g->ev_down));  // ovf_h (prep_next did it otherwise)
     const bool probe = narrow && g->narrow_probe && k == g->B;
     const uint64_t groups = (uint64_t)g->n * (g->B / 256u);

@@ -1522,6 +1522,80 @@ __device__ __forceinline__ uint32_t seg4_entry_set(const Seg4& r) {
     return nib_at(r.P[0], r.P[1], r.P[2], r.P[3], b0);
 }
 
+// One tile's move table from its segments' scans (lane = segment), right to
+// left: `carry` is the closing set of the run open at the tile's right edge
+// on entry, at its left edge on exit.  Each column takes the set of the run
+// it belongs to, the move = that set's lowest bit.
+__device__ __forceinline__ void fill_tile4(const Seg4& r, uint32_t& carry,
+                                           uint32_t* __restrict__ orow, uint32_t seg,
+                                           uint32_t lb, uint32_t lane) {
+    const bool any = (r.Z[0] | r.Z[1] | r.Z[2] | r.Z[3]) != 0u;
+    const uint32_t fl = seg4_entry_set(r);
+    const uint64_t m = __ballot(any);
+    const uint64_t right = lane == 63u ? 0ull : (m >> (lane + 1u)) << (lane + 1u);
+    const uint32_t j = right ? (uint32_t)__builtin_ctzll(right) : lane;
+    const uint32_t fj = (uint32_t)__shfl((int)fl, (int)j, 64);
+    const uint32_t tail = right ? fj : carry;
+    // run ends: a break at the next column (nibble mask, shifted down one
+    // nibble), and column 31 carrying the tail run's set
+    uint32_t V[4], X[4];
+    {
+        uint32_t nz[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nz[i] = r.Z[i] | (r.Z[i] - (r.Z[i] >> 3));
+        V[0] = __builtin_amdgcn_alignbit(nz[1], nz[0], 4);
+        V[1] = __builtin_amdgcn_alignbit(nz[2], nz[1], 4);
+        V[2] = __builtin_amdgcn_alignbit(nz[3], nz[2], 4);
+        V[3] = (nz[3] >> 4) | 0xF0000000u;
+        X[0] = r.S[0];
+        X[1] = r.S[1];
+        X[2] = r.S[2];
+        X[3] = (r.S[3] & 0x0FFFFFFFu) | (tail << 28);
+    }
+    // every other column copies the nearest run end to its right
+#pragma unroll
+    for (int sh = 4; sh <= 16; sh <<= 1) {
+        uint32_t xs[4], vs[4];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            xs[i] = __builtin_amdgcn_alignbit(X[i + 1], X[i], sh);
+            vs[i] = __builtin_amdgcn_alignbit(V[i + 1], V[i], sh);
+        }
+        xs[3] = X[3] >> sh;
+        vs[3] = V[3] >> sh;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
+            V[i] |= vs[i];
+        }
+    }
+#pragma unroll
+    for (int w = 1; w <= 2; w <<= 1) {  // 32- and 64-bit steps: whole words
+        uint32_t xs[4], vs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            xs[i] = i + w < 4 ? X[i + w] : 0u;
+            vs[i] = i + w < 4 ? V[i + w] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
+            V[i] |= vs[i];
+        }
+    }
+    // lowest set bit of every (non-empty) nibble
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t b0 = ~X[i] & 0x11111111u;
+        const uint32_t b1 = ~(X[i] >> 1) & b0;
+        const uint32_t b2 = ~(X[i] >> 2) & b1;
+        o[i] = b0 + b1 + b2;
+    }
+    store_cols32(orow, seg, lb, o);
+    if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
+}
+
 __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ fm, uint32_t npad,
                                                   uint32_t nrows, const uint32_t* __restrict__ st,
                                                   const uint8_t* __restrict__ rc,
@@ -1567,72 +1641,7 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
         const uint32_t seg = t * 64u + lane;
         uint32_t v[4];
         load(seg, v);
-        const Seg4 r = seg4_scan(v, strow[seg] & 0xFu);
-        const bool any = (r.Z[0] | r.Z[1] | r.Z[2] | r.Z[3]) != 0u;
-        const uint32_t fl = seg4_entry_set(r);
-        const uint64_t m = __ballot(any);
-        const uint64_t right = lane == 63u ? 0ull : (m >> (lane + 1u)) << (lane + 1u);
-        const uint32_t j = right ? (uint32_t)__builtin_ctzll(right) : lane;
-        const uint32_t fj = (uint32_t)__shfl((int)fl, (int)j, 64);
-        const uint32_t tail = right ? fj : carry;
-        // run ends: a break at the next column (nibble mask, shifted down one
-        // nibble), and column 31 carrying the tail run's set
-        uint32_t V[4], X[4];
-        {
-            uint32_t nz[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) nz[i] = r.Z[i] | (r.Z[i] - (r.Z[i] >> 3));
-            V[0] = __builtin_amdgcn_alignbit(nz[1], nz[0], 4);
-            V[1] = __builtin_amdgcn_alignbit(nz[2], nz[1], 4);
-            V[2] = __builtin_amdgcn_alignbit(nz[3], nz[2], 4);
-            V[3] = (nz[3] >> 4) | 0xF0000000u;
-            X[0] = r.S[0];
-            X[1] = r.S[1];
-            X[2] = r.S[2];
-            X[3] = (r.S[3] & 0x0FFFFFFFu) | (tail << 28);
-        }
-        // every other column copies the nearest run end to its right
-#pragma unroll
-        for (int sh = 4; sh <= 16; sh <<= 1) {
-            uint32_t xs[4], vs[4];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                xs[i] = __builtin_amdgcn_alignbit(X[i + 1], X[i], sh);
-                vs[i] = __builtin_amdgcn_alignbit(V[i + 1], V[i], sh);
-            }
-            xs[3] = X[3] >> sh;
-            vs[3] = V[3] >> sh;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
-                V[i] |= vs[i];
-            }
-        }
-#pragma unroll
-        for (int w = 1; w <= 2; w <<= 1) {  // 32- and 64-bit steps: whole words
-            uint32_t xs[4], vs[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                xs[i] = i + w < 4 ? X[i + w] : 0u;
-                vs[i] = i + w < 4 ? V[i + w] : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
-                V[i] |= vs[i];
-            }
-        }
-        // lowest set bit of every (non-empty) nibble
-        uint32_t o[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t b0 = ~X[i] & 0x11111111u;
-            const uint32_t b1 = ~(X[i] >> 1) & b0;
-            const uint32_t b2 = ~(X[i] >> 2) & b1;
-            o[i] = b0 + b1 + b2;
-        }
-        store_cols32(orow, t * 64u + lane, lb, o);
-        if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
+        fill_tile4(seg4_scan(v, strow[seg] & 0xFu), carry, orow, seg, lb, lane);
     }
 }
 
@@ -1688,6 +1697,9 @@ __device__ __forceinline__ uint32_t scan32_breaks(const uint32_t (&v)[4], uint32
 // lane of the wave calls it with the same arguments).  ent: 64 * kMoveTiles
 // bytes of LDS for this wave.  Writes the chunk's move table; returns the
 // exit set (wave-uniform) and adds the chunk's breaks to `breaks` (per lane).
+// The chunk's sets stay in registers (64 VGPRs a lane), loaded all at once
+// up front: the wave has its whole 16 KiB in flight instead of one tile per
+// dependent scan, and the backward pass reads nothing again.
 __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uint32_t nseg,
                                 uint32_t ntiles, uint32_t t0, uint32_t t1, uint32_t Sin,
                                 uint8_t* ent, uint32_t* __restrict__ orow, uint32_t lb,
@@ -1699,11 +1711,17 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
         v[2] = q.z;
         v[3] = q.w;
     };
+    const uint32_t L = t1 - t0;  // tiles in the chunk, 1..kMoveTiles (wave-uniform)
+    uint32_t C[kMoveTiles][4];
+#pragma unroll
+    for (uint32_t i = 0; i < kMoveTiles; ++i)
+        if (i < L) load((t0 + i) * 64u + lane, C[i]);
     // forward: the segments' entry sets
     uint32_t carry = Sin;  // the set entering the tile in hand
-    for (uint32_t t = t0; t < t1; ++t) {
-        uint32_t v[4];
-        load(t * 64u + lane, v);
+#pragma unroll
+    for (uint32_t i = 0; i < kMoveTiles; ++i) {
+        if (i < L) {
+        const uint32_t(&v)[4] = C[i];
         const uint32_t p2 = (uint32_t)__shfl_up((int)v[2], 1, 64);
         const uint32_t p3 = (uint32_t)__shfl_up((int)v[3], 1, 64);
         uint32_t in = 0xFu;  // the guess: lane - 1's last 16 columns from a wildcard
@@ -1724,9 +1742,10 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
             if (!__any(fix)) break;
             if (fix) in = pe;
         }
-        ent[(t - t0) * 64u + lane] = (uint8_t)in;
+        ent[i * 64u + lane] = (uint8_t)in;
         breaks += nb;
         carry = (uint32_t)__shfl((int)out, 63, 64);
+        }
     }
     const uint32_t exitS = carry;
     // ahead: the closing set of the run open at the right edge
@@ -1772,73 +1791,23 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
         }
         if (!found) close = P;  // no run closes right of the chunk: the row's last run
     }
-    // backward: the move table (rle_moves4's fill)
+    // backward: the move table, right to left; the tile in hand is always
+    // C[kMoveTiles - 1] (static register indices: the array shifts up a tile
+    // per step, after a shift by kMoveTiles - L for a short chunk)
+    for (uint32_t s = L; s < kMoveTiles; ++s) {
+#pragma unroll
+        for (int i = (int)kMoveTiles - 1; i >= 1; --i)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) C[i][w] = C[i - 1][w];
+    }
     carry = close;
     for (uint32_t t = t1; t-- > t0;) {
-        uint32_t v[4];
-        load(t * 64u + lane, v);
-        const Seg4 r = seg4_scan(v, ent[(t - t0) * 64u + lane]);
-        const bool any = (r.Z[0] | r.Z[1] | r.Z[2] | r.Z[3]) != 0u;
-        const uint32_t fl = seg4_entry_set(r);
-        const uint64_t m = __ballot(any);
-        const uint64_t right = lane == 63u ? 0ull : (m >> (lane + 1u)) << (lane + 1u);
-        const uint32_t j = right ? (uint32_t)__builtin_ctzll(right) : lane;
-        const uint32_t fj = (uint32_t)__shfl((int)fl, (int)j, 64);
-        const uint32_t tail = right ? fj : carry;
-        uint32_t V[4], X[4];
-        {
-            uint32_t nz[4];
+        fill_tile4(seg4_scan(C[kMoveTiles - 1], ent[(t - t0) * 64u + lane]), carry, orow,
+                   t * 64u + lane, lb, lane);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) nz[i] = r.Z[i] | (r.Z[i] - (r.Z[i] >> 3));
-            V[0] = __builtin_amdgcn_alignbit(nz[1], nz[0], 4);
-            V[1] = __builtin_amdgcn_alignbit(nz[2], nz[1], 4);
-            V[2] = __builtin_amdgcn_alignbit(nz[3], nz[2], 4);
-            V[3] = (nz[3] >> 4) | 0xF0000000u;
-            X[0] = r.S[0];
-            X[1] = r.S[1];
-            X[2] = r.S[2];
-            X[3] = (r.S[3] & 0x0FFFFFFFu) | (tail << 28);
-        }
+        for (int i = (int)kMoveTiles - 1; i >= 1; --i)
 #pragma unroll
-        for (int sh = 4; sh <= 16; sh <<= 1) {
-            uint32_t xs[4], vs[4];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                xs[i] = __builtin_amdgcn_alignbit(X[i + 1], X[i], sh);
-                vs[i] = __builtin_amdgcn_alignbit(V[i + 1], V[i], sh);
-            }
-            xs[3] = X[3] >> sh;
-            vs[3] = V[3] >> sh;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
-                V[i] |= vs[i];
-            }
-        }
-#pragma unroll
-        for (int w = 1; w <= 2; w <<= 1) {
-            uint32_t xs[4], vs[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                xs[i] = i + w < 4 ? X[i + w] : 0u;
-                vs[i] = i + w < 4 ? V[i + w] : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                X[i] = (V[i] & X[i]) | (~V[i] & xs[i]);
-                V[i] |= vs[i];
-            }
-        }
-        uint32_t o[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t b0 = ~X[i] & 0x11111111u;
-            const uint32_t b1 = ~(X[i] >> 1) & b0;
-            const uint32_t b2 = ~(X[i] >> 2) & b1;
-            o[i] = b0 + b1 + b2;
-        }
-        store_cols32(orow, t * 64u + lane, lb, o);
-        if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
+            for (int w = 0; w < 4; ++w) C[i][w] = C[i - 1][w];
     }
     return exitS;
 }
@@ -4066,7 +4035,11 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
     const dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u) * (256u / tpb)), blk(tpb);
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     if (nr.d16 && shift == 2 && fm_n4()) {
-        launch_shm(kern::first_moves_n4<2>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n, npad,
+        // CPD_FM_LDS (A/B): more LDS per workgroup than the stage needs caps
+        // the first moves' workgroups per CU, leaving wave slots free
+        static const uint32_t lds_min = env_u32("CPD_FM_LDS", 0);
+        launch_shm(kern::first_moves_n4<2>, grid, blk, std::max(64u * tpb, lds_min), s, adj, dist,
+                   tgt, B, n, npad,
                    xcd_remap(), fm, leafbits, fmleaf, nr, seg_order);
     } else if (nr.d16)
         launch_first_moves_t<true>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,

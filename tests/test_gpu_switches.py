@@ -28,6 +28,8 @@ oracle, walk queries over them dense and RLE.  What each reaches:
                   earlier walk's suffix (table_walk_share)
   CPD_EMIT_DEFER=1  (opt-in) each batch's emit launched after the next batch's
                     down-sweep is queued
+  CPD_UP_HEAD=0   (opt-in) the next batch's up-sweep queued before this batch's
+                  first moves, which wait for its wide levels
 """
 import json
 import os
@@ -78,8 +80,8 @@ print(json.dumps(out))
 
 SWITCHES = ["CPD_LIVE", "CPD_SORT", "CPD_LANE_KEY", "CPD_XCD", "CPD_FM_N4", "CPD_ASYNC",
             "CPD_RLE_FUSED", "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP", "CPD_MOVES_SWAR",
-            "CPD_TABLE_BITS", "CPD_FM_ORDER", "CPD_TS_SHARE", "CPD_EMIT_DEFER"]
-OFF = {"CPD_TABLE_BITS": "4", "CPD_TS_SHARE": "1", "CPD_EMIT_DEFER": "1"}
+            "CPD_TABLE_BITS", "CPD_FM_ORDER", "CPD_TS_SHARE", "CPD_EMIT_DEFER", "CPD_UP_HEAD"]
+OFF = {"CPD_TABLE_BITS": "4", "CPD_TS_SHARE": "1", "CPD_EMIT_DEFER": "1", "CPD_UP_HEAD": "0"}
 # switches that only matter on the unfused emit path
 WITH = {"CPD_RLE_CH": {"CPD_RLE_FUSED": "0"}, "CPD_MOVES_SWAR": {"CPD_RLE_FUSED": "0"}}
 
