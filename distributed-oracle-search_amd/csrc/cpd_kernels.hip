@@ -2953,7 +2953,7 @@ struct SearchWs {
     uint4* memo;    // [slots][2C]
     uint2* aux;     // [slots][2C]
     uint4* he;      // [slots][C] heap: f lo, f hi, g lo, g hi
-    uint32_t* hc;   // [slots][C] heap: column
+    uint2* hc;      // [slots][C] heap: column, hash slot
     uint4* stk;     // [slots][C] walk stack: hash slot, w free, w selected, -
     uint32_t cap;   // C (power of 2)
     // lane-major (stride != 0): slot s's arrays lie together in one block at
@@ -3034,14 +3034,17 @@ __device__ __forceinline__ uint32_t hprobe_from(const uint4* __restrict__ ent, u
 // heap's whatever the arity.
 constexpr uint32_t kHeapK = 8;
 
-__device__ __forceinline__ void heap_push(uint4* __restrict__ he, uint32_t* __restrict__ hc,
-                                          uint32_t& size, uint64_t f, uint32_t c, uint64_t g) {
+// hc[i] = (column, hash slot of the column): the slot rides with the entry,
+// so a pop finds its column's hash entry without probing (slots never move
+// within a search; a resumed search's are probed again once).
+__device__ __forceinline__ void heap_push(uint4* __restrict__ he, uint2* __restrict__ hc,
+                                          uint32_t& size, uint64_t f, uint2 c, uint64_t g) {
     uint32_t i = size++;
     while (i) {
         const uint32_t p = (i - 1u) / kHeapK;
         const uint4 pe = he[p];
-        const uint32_t pc = hc[p];
-        if (!hkey_less(f, c, g, u64of(pe.x, pe.y), pc, u64of(pe.z, pe.w))) break;
+        const uint2 pc = hc[p];
+        if (!hkey_less(f, c.x, g, u64of(pe.x, pe.y), pc.x, u64of(pe.z, pe.w))) break;
         he[i] = pe;
         hc[i] = pc;
         i = p;
@@ -3050,115 +3053,115 @@ __device__ __forceinline__ void heap_push(uint4* __restrict__ he, uint32_t* __re
     hc[i] = c;
 }
 
-__device__ __forceinline__ void heap_pop(uint4* __restrict__ he, uint32_t* __restrict__ hc,
-                                         uint32_t& size, uint64_t& f, uint32_t& c, uint64_t& g) {
-    const uint4 top = he[0];
-    f = u64of(top.x, top.y);
-    g = u64of(top.z, top.w);
-    c = hc[0];
-    --size;
-    if (!size) return;
-    const uint4 le = he[size];
-    const uint32_t lc = hc[size];
-    const uint64_t lf = u64of(le.x, le.y), lg = u64of(le.z, le.w);
-    uint32_t i = 0;
-    for (;;) {
-        const uint32_t k0 = kHeapK * i + 1u;
-        if (k0 >= size) break;
-        const uint32_t nk = min(kHeapK, size - k0);
-        uint4 e[kHeapK];
-        uint32_t ec[kHeapK];
-#pragma unroll
-        for (uint32_t j = 0; j < kHeapK; ++j) {  // the live children, loaded together
-            if (j < nk) {
-                e[j] = he[k0 + j];
-                ec[j] = hc[k0 + j];
-            }
-        }
-        uint4 be = e[0];
-        uint32_t bc = ec[0], bk = k0;
-#pragma unroll
-        for (uint32_t j = 1; j < kHeapK; ++j) {
-            if (j < nk && hkey_less(u64of(e[j].x, e[j].y), ec[j], u64of(e[j].z, e[j].w),
-                                    u64of(be.x, be.y), bc, u64of(be.z, be.w))) {
-                be = e[j];
-                bc = ec[j];
-                bk = k0 + j;
-            }
-        }
-        if (!hkey_less(u64of(be.x, be.y), bc, u64of(be.z, be.w), lf, lc, lg)) break;
-        he[i] = be;
-        hc[i] = bc;
-        i = bk;
-    }
-    he[i] = le;
-    hc[i] = lc;
-}
+// The pop, in two steps so that its descent starts one round trip early.
+// heap_pick (the caller, with the root's children and the last entry in
+// registers, before the pop is decided): the root's least live child (be,
+// bc at position bk; nk live children) and that child's own children group
+// loaded (e2, c2: nc2 live) — beside the expansion's other loads.
+// heap_pop_pre then moves the last entry down from the root with no load for
+// its first two levels.
+struct HeapPick {
+    uint4 be;
+    uint2 bc;
+    uint32_t bk, nk, nc2;
+};
 
-// heap_pop with the root's children (positions 1..K, those < size) and the
-// last entry already in registers — loaded beside the peek at the top, one
-// round trip before the expansion needs them — so the descent starts a
-// level down.  The root itself is the caller's.
-__device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ he, uint32_t* __restrict__ hc,
-                                             uint32_t& size, const uint4 (&e1)[kHeapK],
-                                             const uint32_t (&c1)[kHeapK], const uint4 le,
-                                             const uint32_t lc) {
-    --size;
-    if (!size) return;
-    const uint64_t lf = u64of(le.x, le.y), lg = u64of(le.z, le.w);
-    const uint32_t nk = min(kHeapK, size - 1u);  // live children of the root (< size)
-    if (!nk) {
-        he[0] = le;
-        hc[0] = lc;
-        return;
-    }
-    uint4 be = e1[0];
-    uint32_t bc = c1[0], bk = 1;
+__device__ __forceinline__ HeapPick heap_pick(const uint4* __restrict__ he,
+                                              const uint2* __restrict__ hc, uint32_t size,
+                                              const uint4 (&e1)[kHeapK],
+                                              const uint2 (&c1)[kHeapK], uint4 (&e2)[kHeapK],
+                                              uint2 (&c2)[kHeapK]) {
+    HeapPick p;
+    const uint32_t sz = size - 1u;  // after the pop
+    p.nk = sz ? min(kHeapK, sz - 1u) : 0u;  // live children of the root (< sz)
+    p.be = e1[0];
+    p.bc = c1[0];
+    p.bk = 1;
 #pragma unroll
     for (uint32_t j = 1; j < kHeapK; ++j) {
-        if (j < nk && hkey_less(u64of(e1[j].x, e1[j].y), c1[j], u64of(e1[j].z, e1[j].w),
-                                u64of(be.x, be.y), bc, u64of(be.z, be.w))) {
-            be = e1[j];
-            bc = c1[j];
-            bk = 1u + j;
+        if (j < p.nk && hkey_less(u64of(e1[j].x, e1[j].y), c1[j].x, u64of(e1[j].z, e1[j].w),
+                                  u64of(p.be.x, p.be.y), p.bc.x, u64of(p.be.z, p.be.w))) {
+            p.be = e1[j];
+            p.bc = c1[j];
+            p.bk = 1u + j;
         }
     }
-    if (!hkey_less(u64of(be.x, be.y), bc, u64of(be.z, be.w), lf, lc, lg)) {
+    const uint32_t k0 = kHeapK * p.bk + 1u;
+    p.nc2 = (p.nk && k0 < sz) ? min(kHeapK, sz - k0) : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < kHeapK; ++j) {
+        if (j < p.nc2) {
+            e2[j] = he[k0 + j];
+            c2[j] = hc[k0 + j];
+        }
+    }
+    return p;
+}
+
+__device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ he, uint2* __restrict__ hc,
+                                             uint32_t& size, const HeapPick& p,
+                                             const uint4 (&e2)[kHeapK], const uint2 (&c2)[kHeapK],
+                                             const uint4 le, const uint2 lc) {
+    --size;
+    if (!size) return;
+    const uint64_t lf = u64of(le.x, le.y), lg = u64of(le.z, le.w);
+    if (!p.nk || !hkey_less(u64of(p.be.x, p.be.y), p.bc.x, u64of(p.be.z, p.be.w), lf, lc.x, lg)) {
         he[0] = le;
         hc[0] = lc;
         return;
     }
-    he[0] = be;
-    hc[0] = bc;
-    uint32_t i = bk;
-    for (;;) {
+    he[0] = p.be;
+    hc[0] = p.bc;
+    uint32_t i = p.bk;
+    if (p.nc2) {  // the second level from registers
         const uint32_t k0 = kHeapK * i + 1u;
-        if (k0 >= size) break;
-        const uint32_t nc = min(kHeapK, size - k0);
-        uint4 e[kHeapK];
-        uint32_t ec[kHeapK];
-#pragma unroll
-        for (uint32_t j = 0; j < kHeapK; ++j) {
-            if (j < nc) {
-                e[j] = he[k0 + j];
-                ec[j] = hc[k0 + j];
-            }
-        }
-        uint4 ce = e[0];
-        uint32_t cc = ec[0], ck = k0;
+        uint4 ce = e2[0];
+        uint2 cc = c2[0];
+        uint32_t ck = k0;
 #pragma unroll
         for (uint32_t j = 1; j < kHeapK; ++j) {
-            if (j < nc && hkey_less(u64of(e[j].x, e[j].y), ec[j], u64of(e[j].z, e[j].w),
-                                    u64of(ce.x, ce.y), cc, u64of(ce.z, ce.w))) {
-                ce = e[j];
-                cc = ec[j];
+            if (j < p.nc2 && hkey_less(u64of(e2[j].x, e2[j].y), c2[j].x, u64of(e2[j].z, e2[j].w),
+                                       u64of(ce.x, ce.y), cc.x, u64of(ce.z, ce.w))) {
+                ce = e2[j];
+                cc = c2[j];
                 ck = k0 + j;
             }
         }
-        if (!hkey_less(u64of(ce.x, ce.y), cc, u64of(ce.z, ce.w), lf, lc, lg)) break;
-        he[i] = ce;
-        hc[i] = cc;
-        i = ck;
+        if (hkey_less(u64of(ce.x, ce.y), cc.x, u64of(ce.z, ce.w), lf, lc.x, lg)) {
+            he[i] = ce;
+            hc[i] = cc;
+            i = ck;
+            for (;;) {
+                const uint32_t k1 = kHeapK * i + 1u;
+                if (k1 >= size) break;
+                const uint32_t nc = min(kHeapK, size - k1);
+                uint4 e[kHeapK];
+                uint2 ec[kHeapK];
+#pragma unroll
+                for (uint32_t j = 0; j < kHeapK; ++j) {
+                    if (j < nc) {
+                        e[j] = he[k1 + j];
+                        ec[j] = hc[k1 + j];
+                    }
+                }
+                uint4 me = e[0];
+                uint2 mc = ec[0];
+                uint32_t mk = k1;
+#pragma unroll
+                for (uint32_t j = 1; j < kHeapK; ++j) {
+                    if (j < nc && hkey_less(u64of(e[j].x, e[j].y), ec[j].x, u64of(e[j].z, e[j].w),
+                                            u64of(me.x, me.y), mc.x, u64of(me.z, me.w))) {
+                        me = e[j];
+                        mc = ec[j];
+                        mk = k1 + j;
+                    }
+                }
+                if (!hkey_less(u64of(me.x, me.y), mc.x, u64of(me.z, me.w), lf, lc.x, lg)) break;
+                he[i] = me;
+                hc[i] = mc;
+                i = mk;
+            }
+        }
     }
     he[i] = le;
     hc[i] = lc;
@@ -3171,13 +3174,13 @@ __device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ he, uint32_t* _
 // it (their parents may have moved).  The heap ends as valid as pushing one
 // by one, and pops depend only on the keys.
 template <int N>
-__device__ __forceinline__ void heap_push_n(uint4* __restrict__ he, uint32_t* __restrict__ hc,
+__device__ __forceinline__ void heap_push_n(uint4* __restrict__ he, uint2* __restrict__ hc,
                                             uint32_t& size, const bool (&valid)[N],
-                                            const uint64_t (&f)[N], const uint32_t (&c)[N],
+                                            const uint64_t (&f)[N], const uint2 (&c)[N],
                                             const uint64_t (&g)[N]) {
     const uint32_t s0 = size;
     uint4 pe[N];
-    uint32_t pcol[N];
+    uint32_t pcol[N];  // the parents' columns
     uint32_t at = s0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
@@ -3185,7 +3188,7 @@ __device__ __forceinline__ void heap_push_n(uint4* __restrict__ he, uint32_t* __
             const uint32_t p = at ? (at - 1u) / kHeapK : 0u;
             if (at && p < s0) {
                 pe[k] = he[p];
-                pcol[k] = hc[p];
+                pcol[k] = hc[p].x;
             }
             ++at;
         }
@@ -3196,7 +3199,7 @@ __device__ __forceinline__ void heap_push_n(uint4* __restrict__ he, uint32_t* __
         if (!valid[k]) continue;
         const uint32_t i = size;
         const uint32_t p = i ? (i - 1u) / kHeapK : 0u;
-        if (!slow && (i == 0 || (p < s0 && !hkey_less(f[k], c[k], g[k], u64of(pe[k].x, pe[k].y),
+        if (!slow && (i == 0 || (p < s0 && !hkey_less(f[k], c[k].x, g[k], u64of(pe[k].x, pe[k].y),
                                                      pcol[k], u64of(pe[k].z, pe[k].w))))) {
             he[i] = make_uint4((uint32_t)f[k], (uint32_t)(f[k] >> 32), (uint32_t)g[k],
                                (uint32_t)(g[k] >> 32));
@@ -3223,7 +3226,7 @@ struct Lane {
 // When it could, the search stops there with its state whole and, given a
 // spill pool, copies it out as a record: the heap verbatim, then every
 // column it holds (column, g, depth, moves | state, and with walks the memo)
-// — ~20-36 B per column, not the 68-116 B per column of capacity a
+// — ~20-36 B per column, not the 72-120 B per column of capacity a
 // workspace costs.  The next pass (4x the capacity) rebuilds the hash from
 // the record and continues from the same pop: the heap keys (f, column, g)
 // are a total order, so pops, counters and results are those of one
@@ -3247,7 +3250,7 @@ struct LaneWs {
     uint4* __restrict__ memo;
     uint2* __restrict__ aux;
     uint4* __restrict__ he;
-    uint32_t* __restrict__ hc;
+    uint2* __restrict__ hc;
     uint4* __restrict__ stk;
     uint32_t C, mask;
     Tbl tb;  // the move tables' bits per column
@@ -3404,12 +3407,12 @@ __global__ __launch_bounds__(256) void cpd_search(
     char* const lb0 = ws.base + slot * ws.stride;
     const uint64_t C2 = 2ull * C, CH = (uint64_t)C + kHeapK;
     const LaneWs W = ws.stride
-        ? LaneWs{reinterpret_cast<uint4*>(lb0 + CH * 20ull),
-                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 20ull + C2 * 24ull),
-                 reinterpret_cast<uint2*>(lb0 + CH * 20ull + C2 * 16ull),
+        ? LaneWs{reinterpret_cast<uint4*>(lb0 + CH * 24ull),
+                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 24ull + C2 * 24ull),
+                 reinterpret_cast<uint2*>(lb0 + CH * 24ull + C2 * 16ull),
                  reinterpret_cast<uint4*>(lb0) + (kHeapK - 1u),
-                 reinterpret_cast<uint32_t*>(lb0 + CH * 16ull) + (kHeapK - 1u),
-                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 20ull + C2 * 40ull), C,
+                 reinterpret_cast<uint2*>(lb0 + CH * 16ull) + (kHeapK - 1u),
+                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 24ull + C2 * 40ull), C,
                  2u * C - 1u, Tbl{lb}}
         : LaneWs{ws.ent + slot * C2, TABLES ? nullptr : ws.memo + slot * C2, ws.aux + slot * C2,
                  ws.he + slot * CH + (kHeapK - 1u), ws.hc + slot * CH + (kHeapK - 1u),
@@ -3456,10 +3459,6 @@ __global__ __launch_bounds__(256) void cpd_search(
             L.t0 -= u64of(r[10], r[11]);
             const uint32_t ne = r[12];
             const uint32_t* __restrict__ h = r + kSpillHead;
-            for (uint32_t i = 0; i < L.hsize; ++i) {
-                W.he[i] = make_uint4(h[5u * i], h[5u * i + 1u], h[5u * i + 2u], h[5u * i + 3u]);
-                W.hc[i] = h[5u * i + 4u];
-            }
             constexpr uint32_t per = TABLES ? 5u : 9u;
             const uint32_t* __restrict__ en = h + 5ull * L.hsize;
             for (uint32_t k = 0; k < ne; ++k) {
@@ -3469,6 +3468,13 @@ __global__ __launch_bounds__(256) void cpd_search(
                 W.ent[i] = make_uint4(L.tag, o[0], o[1], o[2]);
                 W.aux[i] = make_uint2(o[3], o[4]);
                 if (!TABLES) W.memo[i] = make_uint4(o[5], o[6], o[7], o[8]);
+            }
+            // the heap after the hash: its entries' slots in this workspace
+            for (uint32_t i = 0; i < L.hsize; ++i) {
+                W.he[i] = make_uint4(h[5u * i], h[5u * i + 1u], h[5u * i + 2u], h[5u * i + 3u]);
+                bool f;
+                const uint32_t c = h[5u * i + 4u];
+                W.hc[i] = make_uint2(c, hprobe(W.ent, W.mask, L.tag, c, f));
             }
             return;
         }
@@ -3495,7 +3501,8 @@ __global__ __launch_bounds__(256) void cpd_search(
             W.ent[si].w = 0u;
             W.aux[si].x = 0u;
             L.inserted = 1;
-            heap_push(W.he, W.hc, L.hsize, (uint64_t)(opt.hscale * (double)hs), L.s, 0ull);
+            heap_push(W.he, W.hc, L.hsize, (uint64_t)(opt.hscale * (double)hs), make_uint2(L.s, si),
+                      0ull);
         }
     };
     // a search stopped before a pop that could outgrow the workspace: its
@@ -3516,7 +3523,7 @@ __global__ __launch_bounds__(256) void cpd_search(
             h[5u * i + 1u] = e.y;
             h[5u * i + 2u] = e.z;
             h[5u * i + 3u] = e.w;
-            h[5u * i + 4u] = W.hc[i];
+            h[5u * i + 4u] = W.hc[i].x;
         }
         uint32_t* __restrict__ en = h + 5ull * L.hsize;
         uint32_t k = 0;
@@ -3597,14 +3604,16 @@ __global__ __launch_bounds__(256) void cpd_search(
         // one pop of this lane's search: the top, looked at first (it is
         // popped once the expansion is known to fit the workspace)
         uint64_t f, g;
-        uint32_t v;
-        uint4 e1[kHeapK], lst;  // the root's children and the last entry (heap_pop_pre)
-        uint32_t c1[kHeapK], lstc;
+        uint32_t v, hi;
+        uint4 e1[kHeapK], lst;  // the root's children and the last entry (heap_pick)
+        uint2 c1[kHeapK], lstc;
         {
             const uint4 top = W.he[0];
             f = u64of(top.x, top.y);
             g = u64of(top.z, top.w);
-            v = W.hc[0];
+            const uint2 vc = W.hc[0];
+            v = vc.x;
+            hi = vc.y;  // v's hash slot
 #pragma unroll
             for (uint32_t j = 0; j < kHeapK; ++j) {
                 if (1u + j < L.hsize) {
@@ -3615,9 +3624,9 @@ __global__ __launch_bounds__(256) void cpd_search(
             lst = W.he[L.hsize - 1u];
             lstc = W.hc[L.hsize - 1u];
         }
-        // what the expansion reads and nothing in it writes — v's out-edges
-        // and, per-row tables, v's incumbent values — is loaded beside v's
-        // hash probe, one round trip for all of it
+        // what the expansion reads and nothing in it writes — v's out-edges,
+        // its hash entry and, per-row tables, its incumbent values — is
+        // loaded together, one round trip for all of it
         constexpr int ND = SHIFT <= 2 ? (1 << SHIFT) : 1;
         uint2 ed[ND];
         if (SHIFT <= 2) {
@@ -3630,11 +3639,13 @@ __global__ __launch_bounds__(256) void cpd_search(
             cw_t = tb.crow[rb + v];
             lw_t = tb.lrow[rb + v];
         }
-        bool found;
-        const uint32_t hi = hprobe(W.ent, W.mask, L.tag, v, found);
         const uint4 ev = W.ent[hi];
+        const uint2 av = W.aux[hi];
+        uint4 e2[kHeapK];  // the pop's second level (heap_pick)
+        uint2 c2[kHeapK];
+        const HeapPick hp = heap_pick(W.he, W.hc, L.hsize, e1, c1, e2, c2);
         if (g > u64of(ev.z, ev.w)) {  // stale entry
-            heap_pop_pre(W.he, W.hc, L.hsize, e1, c1, lst, lstc);
+            heap_pop_pre(W.he, W.hc, L.hsize, hp, e2, c2, lst, lstc);
             ++L.surplus;
             continue;
         }
@@ -3674,9 +3685,24 @@ __global__ __launch_bounds__(256) void cpd_search(
             L.spilled = spill();
             continue;
         }
-        heap_pop_pre(W.he, W.hc, L.hsize, e1, c1, lst, lstc);
+        // the heads' first hash slots and (per-row tables) heuristics,
+        // issued with the pop's descent: they arrive together
+        uint4 e0[ND];
+        uint64_t hr[ND];
+        if (SHIFT <= 2) {
+#pragma unroll
+            for (int k = 0; k < ND; ++k) {
+                if (TABLES && ed[k].x != kNoEdge) {
+                    e0[k] = W.ent[(ed[k].x * 0x9E3779B1u) & W.mask];
+                    hr[k] = tb.hrow[rb + ed[k].x];
+                } else if (ed[k].x != kNoEdge) {
+                    e0[k] = W.ent[(ed[k].x * 0x9E3779B1u) & W.mask];
+                }
+            }
+        }
+        heap_pop_pre(W.he, W.hc, L.hsize, hp, e2, c2, lst, lstc);
         ++L.expanded;
-        const uint32_t dv = W.aux[hi].x;
+        const uint32_t dv = av.x;
         {
             uint64_t cw;
             uint32_t lw;
@@ -3697,24 +3723,15 @@ __global__ __launch_bounds__(256) void cpd_search(
             }
         }
 if (SHIFT <= 2) {
-            // per-row tables: every head's heuristic and first hash slot,
-            // loaded together before the edges are taken in order
-            uint4 e0[ND];
-            uint64_t hr[ND];
             uint32_t wr[ND];  // slot this expansion wrote for edge k
             bool pv[ND];      // edge k's push (heap_push_n after the edges)
             uint64_t pf[ND], pg[ND];
-            uint32_t pcn[ND], np = 0;
+            uint2 pcn[ND];
+            uint32_t np = 0;
 #pragma unroll
             for (int k = 0; k < ND; ++k) {
                 wr[k] = 0xFFFFFFFFu;
                 pv[k] = false;
-                if (TABLES && ed[k].x != kNoEdge) {
-                    e0[k] = W.ent[(ed[k].x * 0x9E3779B1u) & W.mask];
-                    hr[k] = tb.hrow[rb + ed[k].x];
-                } else if (ed[k].x != kNoEdge) {
-                    e0[k] = W.ent[(ed[k].x * 0x9E3779B1u) & W.mask];
-                }
             }
 #pragma unroll
         for (int k = 0; k < ND; ++k) {
@@ -3763,7 +3780,7 @@ if (SHIFT <= 2) {
                 pv[k] = true;
                 pf[k] = ng + (uint64_t)(opt.hscale * (double)hu);
                 pg[k] = ng;
-                pcn[k] = u;
+                pcn[k] = make_uint2(u, ui);
                 ++np;
             } else if (ng < u64of(eu.z, eu.w)) {
                 if (L.hsize + np >= C) {
@@ -3779,7 +3796,7 @@ if (SHIFT <= 2) {
                 pv[k] = true;
                 pf[k] = ng + (uint64_t)(opt.hscale * (double)hu);
                 pg[k] = ng;
-                pcn[k] = u;
+                pcn[k] = make_uint2(u, ui);
                 ++np;
             }
         }
@@ -3821,7 +3838,8 @@ if (SHIFT <= 2) {
                 W.ent[ui].w = (uint32_t)(ng >> 32);
                 W.aux[ui].x = dv + 1u;
                 ++L.inserted;
-                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
+                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu),
+                          make_uint2(u, ui), ng);
             } else if (ng < u64of(W.ent[ui].z, W.ent[ui].w)) {
                 if (L.hsize >= C) {
                     L.overflow = L.done = true;
@@ -3833,7 +3851,8 @@ if (SHIFT <= 2) {
                 ++L.updated;
                 const uint64_t hu = TABLES ? tb.hrow[rb + u]
                                            : u64of(W.memo[ui].x, W.memo[ui].y);
-                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu), u, ng);
+                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu),
+                          make_uint2(u, ui), ng);
             }
         }
         }
@@ -4329,8 +4348,8 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     const size_t hk = (size_t)slots * (cap + kern::kHeapK);
     w.he = reinterpret_cast<uint4*>(p);
     p += hk * 16u;
-    w.hc = reinterpret_cast<uint32_t*>(p);
-    p += (hk * 4u + 127u) / 128u * 128u;
+    w.hc = reinterpret_cast<uint2*>(p);
+    p += (hk * 8u + 127u) / 128u * 128u;
     w.ent = reinterpret_cast<uint4*>(p);
     p += h2 * 16u;
     w.aux = reinterpret_cast<uint2*>(p);
@@ -4429,11 +4448,12 @@ void launch_scatter_u8(const uint8_t* in, const uint32_t* perm, uint32_t nq, uin
 }
 
 // Workspace per lane slot and column of capacity: hash entries 2 x (16 + 8),
-// heap 16 + 4, and for memoised walks the memo (2 x 16) and walk stack (16).
-// per slot: ent 32C, aux 16C (+ memo 32C, stk 16C with walks) and the heap,
-// 20 (C + kHeapK) B; a multiple of 128 B (aligned lane-major blocks)
+// heap 16 + 8 (keys; column and hash slot), and for memoised walks the memo
+// (2 x 16) and walk stack (16).  Per slot: ent 32C, aux 16C (+ memo 32C, stk
+// 16C with walks) and the heap, 24 (C + kHeapK) B; a multiple of 128 B
+// (aligned lane-major blocks)
 uint64_t search_ws_bytes_per_slot(uint32_t cap, bool tables) {
-    const uint64_t b = (tables ? 68ull : 116ull) * cap + 20ull * kern::kHeapK;
+    const uint64_t b = (tables ? 72ull : 120ull) * cap + 24ull * kern::kHeapK;
     return (b + 127u) / 128u * 128u;
 }
 

@@ -390,8 +390,8 @@ void cpd_index_free(cpd_index* ix);
  * not fit); else (_WALKS, or AUTO on a large index) from CPD walks memoised
  * in each search's workspace, so an index of any size can be searched.  The
  * results and counters are the same either way.  A search's workspace holds
- * `capacity` columns (searched ones; with walks also the walked ones; 68 /
- * 116 B each).  Before each pop a search checks that the expansion fits;
+ * `capacity` columns (searched ones; with walks also the walked ones; 72 /
+ * 120 B each).  Before each pop a search checks that the expansion fits;
  * when it might not, it stops there with its state whole and (when a
  * larger pass can follow) copies it into a spill pool; the next pass, at
  * 4x the capacity, resumes it from there — same pops, counters and results
