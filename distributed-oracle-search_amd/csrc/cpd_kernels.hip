@@ -2977,11 +2977,11 @@ __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// (f, column, g) lexicographic, without branches (the heap loops compare
+// eight children at once; short-circuit forms compiled to a branch each)
 __device__ __forceinline__ bool hkey_less(uint64_t f1, uint32_t c1, uint64_t g1, uint64_t f2,
                                           uint32_t c2, uint64_t g2) {
-    if (f1 != f2) return f1 < f2;
-    if (c1 != c2) return c1 < c2;
-    return g1 < g2;
+    return (f1 < f2) | ((f1 == f2) & ((c1 < c2) | ((c1 == c2) & (g1 < g2))));
 }
 
 // Hash probe: slot of column c (found = true) or the free slot to insert it
@@ -3060,6 +3060,15 @@ __device__ __forceinline__ void heap_push(uint4* __restrict__ he, uint2* __restr
 // loaded (e2, c2: nc2 live) — beside the expansion's other loads.
 // heap_pop_pre then moves the last entry down from the root with no load for
 // its first two levels.
+// component-wise selects (a select of whole vectors became a select of
+// their addresses, which put the children arrays in scratch)
+__device__ __forceinline__ uint4 sel4(bool t, const uint4& a, const uint4& b) {
+    return make_uint4(t ? a.x : b.x, t ? a.y : b.y, t ? a.z : b.z, t ? a.w : b.w);
+}
+__device__ __forceinline__ uint2 sel2(bool t, const uint2& a, const uint2& b) {
+    return make_uint2(t ? a.x : b.x, t ? a.y : b.y);
+}
+
 struct HeapPick {
     uint4 be;
     uint2 bc;
@@ -3079,18 +3088,18 @@ __device__ __forceinline__ HeapPick heap_pick(const uint4* __restrict__ he,
     p.bk = 1;
 #pragma unroll
     for (uint32_t j = 1; j < kHeapK; ++j) {
-        if (j < p.nk && hkey_less(u64of(e1[j].x, e1[j].y), c1[j].x, u64of(e1[j].z, e1[j].w),
-                                  u64of(p.be.x, p.be.y), p.bc.x, u64of(p.be.z, p.be.w))) {
-            p.be = e1[j];
-            p.bc = c1[j];
-            p.bk = 1u + j;
-        }
+        const bool t = (j < p.nk) & hkey_less(u64of(e1[j].x, e1[j].y), c1[j].x,
+                                              u64of(e1[j].z, e1[j].w), u64of(p.be.x, p.be.y),
+                                              p.bc.x, u64of(p.be.z, p.be.w));
+        p.be = sel4(t, e1[j], p.be);
+        p.bc = sel2(t, c1[j], p.bc);
+        p.bk = t ? 1u + j : p.bk;
     }
     const uint32_t k0 = kHeapK * p.bk + 1u;
     p.nc2 = (p.nk && k0 < sz) ? min(kHeapK, sz - k0) : 0u;
+    if (p.nc2) {  // the whole group: in bounds (k0 < size, arrays C + K long)
 #pragma unroll
-    for (uint32_t j = 0; j < kHeapK; ++j) {
-        if (j < p.nc2) {
+        for (uint32_t j = 0; j < kHeapK; ++j) {
             e2[j] = he[k0 + j];
             c2[j] = hc[k0 + j];
         }
@@ -3120,12 +3129,12 @@ __device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ he, uint2* __re
         uint32_t ck = k0;
 #pragma unroll
         for (uint32_t j = 1; j < kHeapK; ++j) {
-            if (j < p.nc2 && hkey_less(u64of(e2[j].x, e2[j].y), c2[j].x, u64of(e2[j].z, e2[j].w),
-                                       u64of(ce.x, ce.y), cc.x, u64of(ce.z, ce.w))) {
-                ce = e2[j];
-                cc = c2[j];
-                ck = k0 + j;
-            }
+            const bool t = (j < p.nc2) & hkey_less(u64of(e2[j].x, e2[j].y), c2[j].x,
+                                                   u64of(e2[j].z, e2[j].w), u64of(ce.x, ce.y),
+                                                   cc.x, u64of(ce.z, ce.w));
+            ce = sel4(t, e2[j], ce);
+            cc = sel2(t, c2[j], cc);
+            ck = t ? k0 + j : ck;
         }
         if (hkey_less(u64of(ce.x, ce.y), cc.x, u64of(ce.z, ce.w), lf, lc.x, lg)) {
             he[i] = ce;
@@ -3138,23 +3147,21 @@ __device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ he, uint2* __re
                 uint4 e[kHeapK];
                 uint2 ec[kHeapK];
 #pragma unroll
-                for (uint32_t j = 0; j < kHeapK; ++j) {
-                    if (j < nc) {
-                        e[j] = he[k1 + j];
-                        ec[j] = hc[k1 + j];
-                    }
+                for (uint32_t j = 0; j < kHeapK; ++j) {  // in bounds (k1 < size)
+                    e[j] = he[k1 + j];
+                    ec[j] = hc[k1 + j];
                 }
                 uint4 me = e[0];
                 uint2 mc = ec[0];
                 uint32_t mk = k1;
 #pragma unroll
                 for (uint32_t j = 1; j < kHeapK; ++j) {
-                    if (j < nc && hkey_less(u64of(e[j].x, e[j].y), ec[j].x, u64of(e[j].z, e[j].w),
-                                            u64of(me.x, me.y), mc.x, u64of(me.z, me.w))) {
-                        me = e[j];
-                        mc = ec[j];
-                        mk = k1 + j;
-                    }
+                    const bool t = (j < nc) & hkey_less(u64of(e[j].x, e[j].y), ec[j].x,
+                                                        u64of(e[j].z, e[j].w), u64of(me.x, me.y),
+                                                        mc.x, u64of(me.z, me.w));
+                    me = sel4(t, e[j], me);
+                    mc = sel2(t, ec[j], mc);
+                    mk = t ? k1 + j : mk;
                 }
                 if (!hkey_less(u64of(me.x, me.y), mc.x, u64of(me.z, me.w), lf, lc.x, lg)) break;
                 he[i] = me;
@@ -3384,7 +3391,9 @@ struct SearchTables {
 };
 
 template <int SHIFT, bool TABLES>
-__global__ __launch_bounds__(256) void cpd_search(
+// (one wave per SIMD: the register budget of 512 leaves the children arrays in
+// registers; 1024 one-wave workgroups fill the 1024 SIMDs)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cpd_search(
     const uint2* __restrict__ adj_f, const uint2* __restrict__ adj_w,
     const uint32_t* __restrict__ dense, uint32_t wpr, uint32_t lb, SearchTables tb,
     const uint32_t* __restrict__ qs,
@@ -3615,11 +3624,9 @@ __global__ __launch_bounds__(256) void cpd_search(
             v = vc.x;
             hi = vc.y;  // v's hash slot
 #pragma unroll
-            for (uint32_t j = 0; j < kHeapK; ++j) {
-                if (1u + j < L.hsize) {
-                    e1[j] = W.he[1u + j];
-                    c1[j] = W.hc[1u + j];
-                }
+            for (uint32_t j = 0; j < kHeapK; ++j) {  // positions 1..K: in bounds
+                e1[j] = W.he[1u + j];
+                c1[j] = W.hc[1u + j];
             }
             lst = W.he[L.hsize - 1u];
             lstc = W.hc[L.hsize - 1u];
