@@ -20,7 +20,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcpd.so")
+# CPD_LIB: another build of the library (A/B runs of two builds in one job)
+LIB_PATH = os.environ.get("CPD_LIB") or os.path.join(_HERE, "libcpd.so")
 
 CPD_OK = 0
 CPD_E_ARG = -1

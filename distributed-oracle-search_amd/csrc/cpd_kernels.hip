@@ -2952,12 +2952,11 @@ struct SearchWs {
     uint4* ent;     // [slots][2C]
     uint4* memo;    // [slots][2C]
     uint2* aux;     // [slots][2C]
-    uint4* he;      // [slots][C] heap: f lo, f hi, g lo, g hi
-    uint2* hc;      // [slots][C] heap: column, hash slot
+    uint4* hk;      // [slots][C + K] heap: f lo, f hi, column, hash slot
     uint4* stk;     // [slots][C] walk stack: hash slot, w free, w selected, -
     uint32_t cap;   // C (power of 2)
     // lane-major (stride != 0): slot s's arrays lie together in one block at
-    // base + s * stride (ent, aux, he, hc, then memo and stk with walks), so
+    // base + s * stride (heap, ent, aux, then memo and stk with walks), so
     // a search touches one contiguous region of a few MB instead of six
     // regions spread over the whole workspace (fewer pages in flight per
     // lane for the address translation); array-major above when 0
@@ -2975,13 +2974,6 @@ struct SearchOpt {
 
 __device__ __forceinline__ uint64_t u64of(uint32_t lo, uint32_t hi) {
     return ((uint64_t)hi << 32) | lo;
-}
-
-// (f, column, g) lexicographic, without branches (the heap loops compare
-// eight children at once; short-circuit forms compiled to a branch each)
-__device__ __forceinline__ bool hkey_less(uint64_t f1, uint32_t c1, uint64_t g1, uint64_t f2,
-                                          uint32_t c2, uint64_t g2) {
-    return (f1 < f2) | ((f1 == f2) & ((c1 < c2) | ((c1 == c2) & (g1 < g2))));
 }
 
 // Hash probe: slot of column c (found = true) or the free slot to insert it
@@ -3024,154 +3016,131 @@ __device__ __forceinline__ uint32_t hprobe_from(const uint4* __restrict__ ent, u
 
 // The search heap: kHeapK-ary (children of i at K i + 1 .. K i + K), so a
 // pop descends log_K of the size in levels whose K child loads go out
-// together — a binary heap's dependent round trips / log2 K.  The arrays
-// start K - 1 entries into their block (128-B aligned), so the K children
-// of every entry are one aligned group: 8 x 16 B = one 128-B line of keys
-// and 32 B of columns (round 4's 4-ary groups straddled lines every other
-// level).  The keys (f, column, g) are a total order over the entries a
-// search can hold (a column is pushed again only with a strictly smaller
-// g), so the pop sequence — and every counter — is the oracle's binary
-// heap's whatever the arity.
+// together — a binary heap's dependent round trips / log2 K.  An entry is
+// one 16-B word, (f lo, f hi, column, hash slot of the column): the slot
+// rides with the entry, so a pop finds its column's hash entry without
+// probing (slots never move within a search; a resumed search's are probed
+// again once).  The array starts K - 1 entries into its block (128-B
+// aligned), so the K children of every entry are one aligned 128-B line.
+// The oracle orders its heap by (f, column, g); g is implied by (f,
+// column): f = g + h(column) with h fixed per column, and a column is pushed
+// again only with a strictly smaller g — so (f, column) is a total order
+// over the entries a search holds, its pops (and every counter) those of the
+// oracle's binary heap, and a popped entry is stale exactly when its f
+// exceeds the column's current g + h.
 constexpr uint32_t kHeapK = 8;
 
-// hc[i] = (column, hash slot of the column): the slot rides with the entry,
-// so a pop finds its column's hash entry without probing (slots never move
-// within a search; a resumed search's are probed again once).
-__device__ __forceinline__ void heap_push(uint4* __restrict__ he, uint2* __restrict__ hc,
-                                          uint32_t& size, uint64_t f, uint2 c, uint64_t g) {
+__device__ __forceinline__ uint64_t hkey_f(const uint4& e) { return u64of(e.x, e.y); }
+
+// (f, column) lexicographic, without branches (the heap loops compare eight
+// children at once; short-circuit forms compiled to a branch each)
+__device__ __forceinline__ bool hkey_less(const uint4& a, const uint4& b) {
+    const uint64_t fa = hkey_f(a), fb = hkey_f(b);
+    return (fa < fb) | ((fa == fb) & (a.z < b.z));
+}
+
+__device__ __forceinline__ uint4 hkey_make(uint64_t f, uint32_t col, uint32_t slot) {
+    return make_uint4((uint32_t)f, (uint32_t)(f >> 32), col, slot);
+}
+
+// component-wise select (a select of whole vectors became a select of their
+// addresses, which put the children arrays in scratch)
+__device__ __forceinline__ uint4 sel4(bool t, const uint4& a, const uint4& b) {
+    return make_uint4(t ? a.x : b.x, t ? a.y : b.y, t ? a.z : b.z, t ? a.w : b.w);
+}
+
+__device__ __forceinline__ void heap_push(uint4* __restrict__ hk, uint32_t& size, const uint4 e) {
     uint32_t i = size++;
     while (i) {
         const uint32_t p = (i - 1u) / kHeapK;
-        const uint4 pe = he[p];
-        const uint2 pc = hc[p];
-        if (!hkey_less(f, c.x, g, u64of(pe.x, pe.y), pc.x, u64of(pe.z, pe.w))) break;
-        he[i] = pe;
-        hc[i] = pc;
+        const uint4 pe = hk[p];
+        if (!hkey_less(e, pe)) break;
+        hk[i] = pe;
         i = p;
     }
-    he[i] = make_uint4((uint32_t)f, (uint32_t)(f >> 32), (uint32_t)g, (uint32_t)(g >> 32));
-    hc[i] = c;
+    hk[i] = e;
 }
 
 // The pop, in two steps so that its descent starts one round trip early.
 // heap_pick (the caller, with the root's children and the last entry in
-// registers, before the pop is decided): the root's least live child (be,
-// bc at position bk; nk live children) and that child's own children group
-// loaded (e2, c2: nc2 live) — beside the expansion's other loads.
-// heap_pop_pre then moves the last entry down from the root with no load for
-// its first two levels.
-// component-wise selects (a select of whole vectors became a select of
-// their addresses, which put the children arrays in scratch)
-__device__ __forceinline__ uint4 sel4(bool t, const uint4& a, const uint4& b) {
-    return make_uint4(t ? a.x : b.x, t ? a.y : b.y, t ? a.z : b.z, t ? a.w : b.w);
-}
-__device__ __forceinline__ uint2 sel2(bool t, const uint2& a, const uint2& b) {
-    return make_uint2(t ? a.x : b.x, t ? a.y : b.y);
-}
-
+// registers, before the pop is decided): the root's least live child (be at
+// position bk; nk live children) and that child's own children group
+// loaded (e2: nc2 live) — beside the expansion's other loads.  heap_pop_pre
+// then moves the last entry down from the root with no load for its first
+// two levels.
 struct HeapPick {
     uint4 be;
-    uint2 bc;
     uint32_t bk, nk, nc2;
 };
 
-__device__ __forceinline__ HeapPick heap_pick(const uint4* __restrict__ he,
-                                              const uint2* __restrict__ hc, uint32_t size,
-                                              const uint4 (&e1)[kHeapK],
-                                              const uint2 (&c1)[kHeapK], uint4 (&e2)[kHeapK],
-                                              uint2 (&c2)[kHeapK]) {
+__device__ __forceinline__ HeapPick heap_pick(const uint4* __restrict__ hk, uint32_t size,
+                                              const uint4 (&e1)[kHeapK], uint4 (&e2)[kHeapK]) {
     HeapPick p;
     const uint32_t sz = size - 1u;  // after the pop
     p.nk = sz ? min(kHeapK, sz - 1u) : 0u;  // live children of the root (< sz)
     p.be = e1[0];
-    p.bc = c1[0];
     p.bk = 1;
 #pragma unroll
     for (uint32_t j = 1; j < kHeapK; ++j) {
-        const bool t = (j < p.nk) & hkey_less(u64of(e1[j].x, e1[j].y), c1[j].x,
-                                              u64of(e1[j].z, e1[j].w), u64of(p.be.x, p.be.y),
-                                              p.bc.x, u64of(p.be.z, p.be.w));
+        const bool t = (j < p.nk) & hkey_less(e1[j], p.be);
         p.be = sel4(t, e1[j], p.be);
-        p.bc = sel2(t, c1[j], p.bc);
         p.bk = t ? 1u + j : p.bk;
     }
     const uint32_t k0 = kHeapK * p.bk + 1u;
     p.nc2 = (p.nk && k0 < sz) ? min(kHeapK, sz - k0) : 0u;
-    if (p.nc2) {  // the whole group: in bounds (k0 < size, arrays C + K long)
+    if (p.nc2) {  // the whole group: in bounds (k0 < size, the array is C + K long)
 #pragma unroll
-        for (uint32_t j = 0; j < kHeapK; ++j) {
-            e2[j] = he[k0 + j];
-            c2[j] = hc[k0 + j];
-        }
+        for (uint32_t j = 0; j < kHeapK; ++j) e2[j] = hk[k0 + j];
     }
     return p;
 }
 
-__device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ he, uint2* __restrict__ hc,
-                                             uint32_t& size, const HeapPick& p,
-                                             const uint4 (&e2)[kHeapK], const uint2 (&c2)[kHeapK],
-                                             const uint4 le, const uint2 lc) {
+__device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ hk, uint32_t& size,
+                                             const HeapPick& p, const uint4 (&e2)[kHeapK],
+                                             const uint4 le) {
     --size;
     if (!size) return;
-    const uint64_t lf = u64of(le.x, le.y), lg = u64of(le.z, le.w);
-    if (!p.nk || !hkey_less(u64of(p.be.x, p.be.y), p.bc.x, u64of(p.be.z, p.be.w), lf, lc.x, lg)) {
-        he[0] = le;
-        hc[0] = lc;
+    if (!p.nk || !hkey_less(p.be, le)) {
+        hk[0] = le;
         return;
     }
-    he[0] = p.be;
-    hc[0] = p.bc;
+    hk[0] = p.be;
     uint32_t i = p.bk;
     if (p.nc2) {  // the second level from registers
         const uint32_t k0 = kHeapK * i + 1u;
         uint4 ce = e2[0];
-        uint2 cc = c2[0];
         uint32_t ck = k0;
 #pragma unroll
         for (uint32_t j = 1; j < kHeapK; ++j) {
-            const bool t = (j < p.nc2) & hkey_less(u64of(e2[j].x, e2[j].y), c2[j].x,
-                                                   u64of(e2[j].z, e2[j].w), u64of(ce.x, ce.y),
-                                                   cc.x, u64of(ce.z, ce.w));
+            const bool t = (j < p.nc2) & hkey_less(e2[j], ce);
             ce = sel4(t, e2[j], ce);
-            cc = sel2(t, c2[j], cc);
             ck = t ? k0 + j : ck;
         }
-        if (hkey_less(u64of(ce.x, ce.y), cc.x, u64of(ce.z, ce.w), lf, lc.x, lg)) {
-            he[i] = ce;
-            hc[i] = cc;
+        if (hkey_less(ce, le)) {
+            hk[i] = ce;
             i = ck;
             for (;;) {
                 const uint32_t k1 = kHeapK * i + 1u;
                 if (k1 >= size) break;
                 const uint32_t nc = min(kHeapK, size - k1);
                 uint4 e[kHeapK];
-                uint2 ec[kHeapK];
 #pragma unroll
-                for (uint32_t j = 0; j < kHeapK; ++j) {  // in bounds (k1 < size)
-                    e[j] = he[k1 + j];
-                    ec[j] = hc[k1 + j];
-                }
+                for (uint32_t j = 0; j < kHeapK; ++j) e[j] = hk[k1 + j];  // in bounds (k1 < size)
                 uint4 me = e[0];
-                uint2 mc = ec[0];
                 uint32_t mk = k1;
 #pragma unroll
                 for (uint32_t j = 1; j < kHeapK; ++j) {
-                    const bool t = (j < nc) & hkey_less(u64of(e[j].x, e[j].y), ec[j].x,
-                                                        u64of(e[j].z, e[j].w), u64of(me.x, me.y),
-                                                        mc.x, u64of(me.z, me.w));
+                    const bool t = (j < nc) & hkey_less(e[j], me);
                     me = sel4(t, e[j], me);
-                    mc = sel2(t, ec[j], mc);
                     mk = t ? k1 + j : mk;
                 }
-                if (!hkey_less(u64of(me.x, me.y), mc.x, u64of(me.z, me.w), lf, lc.x, lg)) break;
-                he[i] = me;
-                hc[i] = mc;
+                if (!hkey_less(me, le)) break;
+                hk[i] = me;
                 i = mk;
             }
         }
     }
-    he[i] = le;
-    hc[i] = lc;
+    hk[i] = le;
 }
 
 // The expansion's pushes (one per out-edge at most, `valid`), their parents
@@ -3181,22 +3150,16 @@ __device__ __forceinline__ void heap_pop_pre(uint4* __restrict__ he, uint2* __re
 // it (their parents may have moved).  The heap ends as valid as pushing one
 // by one, and pops depend only on the keys.
 template <int N>
-__device__ __forceinline__ void heap_push_n(uint4* __restrict__ he, uint2* __restrict__ hc,
-                                            uint32_t& size, const bool (&valid)[N],
-                                            const uint64_t (&f)[N], const uint2 (&c)[N],
-                                            const uint64_t (&g)[N]) {
+__device__ __forceinline__ void heap_push_n(uint4* __restrict__ hk, uint32_t& size,
+                                            const bool (&valid)[N], const uint4 (&e)[N]) {
     const uint32_t s0 = size;
     uint4 pe[N];
-    uint32_t pcol[N];  // the parents' columns
     uint32_t at = s0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
         if (valid[k]) {
             const uint32_t p = at ? (at - 1u) / kHeapK : 0u;
-            if (at && p < s0) {
-                pe[k] = he[p];
-                pcol[k] = hc[p].x;
-            }
+            if (at && p < s0) pe[k] = hk[p];
             ++at;
         }
     }
@@ -3206,15 +3169,12 @@ __device__ __forceinline__ void heap_push_n(uint4* __restrict__ he, uint2* __res
         if (!valid[k]) continue;
         const uint32_t i = size;
         const uint32_t p = i ? (i - 1u) / kHeapK : 0u;
-        if (!slow && (i == 0 || (p < s0 && !hkey_less(f[k], c[k].x, g[k], u64of(pe[k].x, pe[k].y),
-                                                     pcol[k], u64of(pe[k].z, pe[k].w))))) {
-            he[i] = make_uint4((uint32_t)f[k], (uint32_t)(f[k] >> 32), (uint32_t)g[k],
-                               (uint32_t)(g[k] >> 32));
-            hc[i] = c[k];
+        if (!slow && (i == 0 || (p < s0 && !hkey_less(e[k], pe[k])))) {
+            hk[i] = e[k];
             ++size;
         } else {
             slow = true;
-            heap_push(he, hc, size, f[k], c[k], g[k]);
+            heap_push(hk, size, e[k]);
         }
     }
 }
@@ -3239,8 +3199,8 @@ struct Lane {
 // are a total order, so pops, counters and results are those of one
 // uninterrupted search.  Record (u32 words): hsize, used, ub lo/hi,
 // best_len, the five counters, elapsed ticks lo/hi, entries, 0 | heap
-// hsize x (f lo, f hi, g lo, g hi, column) | entries x (column, g lo, g hi,
-// depth, moves | state [, memo x4]).
+// hsize x (f lo, f hi, column) | entries x (column, g lo, g hi, depth,
+// moves | state [, memo x4]).
 struct SearchSpill {
     const unsigned long long* resume;  // [nq] record of query q in rin, ~0 = fresh (null: all)
     const uint32_t* rin;
@@ -3256,8 +3216,7 @@ struct LaneWs {
     uint4* __restrict__ ent;
     uint4* __restrict__ memo;
     uint2* __restrict__ aux;
-    uint4* __restrict__ he;
-    uint2* __restrict__ hc;
+    uint4* __restrict__ hk;
     uint4* __restrict__ stk;
     uint32_t C, mask;
     Tbl tb;  // the move tables' bits per column
@@ -3409,23 +3368,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
     const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
     const uint32_t C = ws.cap;
-    // lane-major (stride != 0): the slot's block = he, hc (C + K entries
-    // each), ent, aux, then memo and stk with walks; array-major: each array
-    // over all slots.  The heap pointers start K - 1 entries in (aligned
-    // child groups, see heap_pop).
+    // lane-major (stride != 0): the slot's block = the heap (C + K entries),
+    // ent, aux, then memo and stk with walks; array-major: each array over
+    // all slots.  The heap pointer starts K - 1 entries in (aligned child
+    // groups).
     char* const lb0 = ws.base + slot * ws.stride;
     const uint64_t C2 = 2ull * C, CH = (uint64_t)C + kHeapK;
     const LaneWs W = ws.stride
-        ? LaneWs{reinterpret_cast<uint4*>(lb0 + CH * 24ull),
-                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 24ull + C2 * 24ull),
-                 reinterpret_cast<uint2*>(lb0 + CH * 24ull + C2 * 16ull),
+        ? LaneWs{reinterpret_cast<uint4*>(lb0 + CH * 16ull),
+                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 16ull + C2 * 24ull),
+                 reinterpret_cast<uint2*>(lb0 + CH * 16ull + C2 * 16ull),
                  reinterpret_cast<uint4*>(lb0) + (kHeapK - 1u),
-                 reinterpret_cast<uint2*>(lb0 + CH * 16ull) + (kHeapK - 1u),
-                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 24ull + C2 * 40ull), C,
+                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 16ull + C2 * 40ull), C,
                  2u * C - 1u, Tbl{lb}}
         : LaneWs{ws.ent + slot * C2, TABLES ? nullptr : ws.memo + slot * C2, ws.aux + slot * C2,
-                 ws.he + slot * CH + (kHeapK - 1u), ws.hc + slot * CH + (kHeapK - 1u),
-                 TABLES ? nullptr : ws.stk + slot * C, C, 2u * C - 1u, Tbl{lb}};
+                 ws.hk + slot * CH + (kHeapK - 1u), TABLES ? nullptr : ws.stk + slot * C, C,
+                 2u * C - 1u, Tbl{lb}};
     unsigned long long s_exp = 0, s_ins = 0, s_tou = 0, s_upd = 0, s_sur = 0, s_len = 0,
                        s_fin = 0, s_ovf = 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -3469,7 +3427,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             const uint32_t ne = r[12];
             const uint32_t* __restrict__ h = r + kSpillHead;
             constexpr uint32_t per = TABLES ? 5u : 9u;
-            const uint32_t* __restrict__ en = h + 5ull * L.hsize;
+            const uint32_t* __restrict__ en = h + 3ull * L.hsize;
             for (uint32_t k = 0; k < ne; ++k) {
                 const uint32_t* __restrict__ o = en + (size_t)per * k;
                 bool f;
@@ -3480,10 +3438,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             }
             // the heap after the hash: its entries' slots in this workspace
             for (uint32_t i = 0; i < L.hsize; ++i) {
-                W.he[i] = make_uint4(h[5u * i], h[5u * i + 1u], h[5u * i + 2u], h[5u * i + 3u]);
                 bool f;
-                const uint32_t c = h[5u * i + 4u];
-                W.hc[i] = make_uint2(c, hprobe(W.ent, W.mask, L.tag, c, f));
+                const uint32_t c = h[3u * i + 2u];
+                W.hk[i] = make_uint4(h[3u * i], h[3u * i + 1u], c, hprobe(W.ent, W.mask, L.tag, c, f));
             }
             return;
         }
@@ -3510,8 +3467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             W.ent[si].w = 0u;
             W.aux[si].x = 0u;
             L.inserted = 1;
-            heap_push(W.he, W.hc, L.hsize, (uint64_t)(opt.hscale * (double)hs), make_uint2(L.s, si),
-                      0ull);
+            heap_push(W.hk, L.hsize, hkey_make((uint64_t)(opt.hscale * (double)hs), L.s, si));
         }
     };
     // a search stopped before a pop that could outgrow the workspace: its
@@ -3521,20 +3477,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (!sp.rout) return false;
         constexpr uint32_t per = TABLES ? 5u : 9u;
         const unsigned long long words =
-            kSpillHead + 5ull * L.hsize + (unsigned long long)per * L.used;
+            kSpillHead + 3ull * L.hsize + (unsigned long long)per * L.used;
         const unsigned long long off = atomicAdd(sp.top, words);
         if (off + words > sp.cap) return false;
         uint32_t* __restrict__ r = sp.rout + off;
         uint32_t* __restrict__ h = r + kSpillHead;
         for (uint32_t i = 0; i < L.hsize; ++i) {
-            const uint4 e = W.he[i];
-            h[5u * i] = e.x;
-            h[5u * i + 1u] = e.y;
-            h[5u * i + 2u] = e.z;
-            h[5u * i + 3u] = e.w;
-            h[5u * i + 4u] = W.hc[i].x;
+            const uint4 e = W.hk[i];
+            h[3u * i] = e.x;
+            h[3u * i + 1u] = e.y;
+            h[3u * i + 2u] = e.z;
         }
-        uint32_t* __restrict__ en = h + 5ull * L.hsize;
+        uint32_t* __restrict__ en = h + 3ull * L.hsize;
         uint32_t k = 0;
         for (uint32_t i = 0; i < 2u * C && k < L.used; ++i) {
             const uint4 e = W.ent[i];
@@ -3612,24 +3566,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (L.q == kIdleQ || L.done || L.hsize == 0) continue;
         // one pop of this lane's search: the top, looked at first (it is
         // popped once the expansion is known to fit the workspace)
-        uint64_t f, g;
+        uint64_t f;
         uint32_t v, hi;
         uint4 e1[kHeapK], lst;  // the root's children and the last entry (heap_pick)
-        uint2 c1[kHeapK], lstc;
         {
-            const uint4 top = W.he[0];
-            f = u64of(top.x, top.y);
-            g = u64of(top.z, top.w);
-            const uint2 vc = W.hc[0];
-            v = vc.x;
-            hi = vc.y;  // v's hash slot
+            const uint4 top = W.hk[0];
+            f = hkey_f(top);
+            v = top.z;
+            hi = top.w;  // v's hash slot
 #pragma unroll
-            for (uint32_t j = 0; j < kHeapK; ++j) {  // positions 1..K: in bounds
-                e1[j] = W.he[1u + j];
-                c1[j] = W.hc[1u + j];
-            }
-            lst = W.he[L.hsize - 1u];
-            lstc = W.hc[L.hsize - 1u];
+            for (uint32_t j = 0; j < kHeapK; ++j) e1[j] = W.hk[1u + j];  // positions 1..K: in bounds
+            lst = W.hk[L.hsize - 1u];
         }
         // what the expansion reads and nothing in it writes — v's out-edges,
         // its hash entry and, per-row tables, its incumbent values — is
@@ -3640,19 +3587,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
             for (int k = 0; k < ND; ++k) ed[k] = adj_w[((size_t)v << SHIFT) + k];
         }
-        uint64_t cw_t = 0;
+        uint64_t cw_t = 0, hv;
         uint32_t lw_t = 0;
         if (TABLES) {
             cw_t = tb.crow[rb + v];
             lw_t = tb.lrow[rb + v];
+            hv = tb.hrow[rb + v];
+        } else {
+            const uint4 mv = W.memo[hi];  // walked when it was inserted
+            hv = u64of(mv.x, mv.y);
         }
         const uint4 ev = W.ent[hi];
         const uint2 av = W.aux[hi];
         uint4 e2[kHeapK];  // the pop's second level (heap_pick)
-        uint2 c2[kHeapK];
-        const HeapPick hp = heap_pick(W.he, W.hc, L.hsize, e1, c1, e2, c2);
-        if (g > u64of(ev.z, ev.w)) {  // stale entry
-            heap_pop_pre(W.he, W.hc, L.hsize, hp, e2, c2, lst, lstc);
+        const HeapPick hp = heap_pick(W.hk, L.hsize, e1, e2);
+        // the entry's g is the column's current one unless the entry is
+        // stale (its f above current g + h: a better g came later)
+        const uint64_t g = u64of(ev.z, ev.w);
+        if (f > g + (uint64_t)(opt.hscale * (double)hv)) {  // stale entry
+            heap_pop_pre(W.hk, L.hsize, hp, e2, lst);
             ++L.surplus;
             continue;
         }
@@ -3707,7 +3660,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 }
             }
         }
-        heap_pop_pre(W.he, W.hc, L.hsize, hp, e2, c2, lst, lstc);
+        heap_pop_pre(W.hk, L.hsize, hp, e2, lst);
         ++L.expanded;
         const uint32_t dv = av.x;
         {
@@ -3732,8 +3685,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 if (SHIFT <= 2) {
             uint32_t wr[ND];  // slot this expansion wrote for edge k
             bool pv[ND];      // edge k's push (heap_push_n after the edges)
-            uint64_t pf[ND], pg[ND];
-            uint2 pcn[ND];
+            uint4 pk[ND];     // its heap entry
             uint32_t np = 0;
 #pragma unroll
             for (int k = 0; k < ND; ++k) {
@@ -3785,9 +3737,7 @@ if (SHIFT <= 2) {
                 wr[k] = ui;
                 ++L.inserted;
                 pv[k] = true;
-                pf[k] = ng + (uint64_t)(opt.hscale * (double)hu);
-                pg[k] = ng;
-                pcn[k] = make_uint2(u, ui);
+                pk[k] = hkey_make(ng + (uint64_t)(opt.hscale * (double)hu), u, ui);
                 ++np;
             } else if (ng < u64of(eu.z, eu.w)) {
                 if (L.hsize + np >= C) {
@@ -3801,13 +3751,11 @@ if (SHIFT <= 2) {
                 ++L.updated;
                 const uint64_t hu = TABLES ? hr[k] : u64of(W.memo[ui].x, W.memo[ui].y);
                 pv[k] = true;
-                pf[k] = ng + (uint64_t)(opt.hscale * (double)hu);
-                pg[k] = ng;
-                pcn[k] = make_uint2(u, ui);
+                pk[k] = hkey_make(ng + (uint64_t)(opt.hscale * (double)hu), u, ui);
                 ++np;
             }
         }
-        heap_push_n<ND>(W.he, W.hc, L.hsize, pv, pf, pcn, pg);
+        heap_push_n<ND>(W.hk, L.hsize, pv, pk);
         } else {
 #pragma unroll 1
         for (int k = 0; k < (1 << SHIFT); ++k) {
@@ -3845,8 +3793,7 @@ if (SHIFT <= 2) {
                 W.ent[ui].w = (uint32_t)(ng >> 32);
                 W.aux[ui].x = dv + 1u;
                 ++L.inserted;
-                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu),
-                          make_uint2(u, ui), ng);
+                heap_push(W.hk, L.hsize, hkey_make(ng + (uint64_t)(opt.hscale * (double)hu), u, ui));
             } else if (ng < u64of(W.ent[ui].z, W.ent[ui].w)) {
                 if (L.hsize >= C) {
                     L.overflow = L.done = true;
@@ -3858,8 +3805,7 @@ if (SHIFT <= 2) {
                 ++L.updated;
                 const uint64_t hu = TABLES ? tb.hrow[rb + u]
                                            : u64of(W.memo[ui].x, W.memo[ui].y);
-                heap_push(W.he, W.hc, L.hsize, ng + (uint64_t)(opt.hscale * (double)hu),
-                          make_uint2(u, ui), ng);
+                heap_push(W.hk, L.hsize, hkey_make(ng + (uint64_t)(opt.hscale * (double)hu), u, ui));
             }
         }
         }
@@ -4353,10 +4299,8 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     w.base = static_cast<char*>(ws);
     w.stride = search_lane_major() ? search_ws_bytes_per_slot(cap, tables) : 0u;
     const size_t hk = (size_t)slots * (cap + kern::kHeapK);
-    w.he = reinterpret_cast<uint4*>(p);
+    w.hk = reinterpret_cast<uint4*>(p);
     p += hk * 16u;
-    w.hc = reinterpret_cast<uint2*>(p);
-    p += (hk * 8u + 127u) / 128u * 128u;
     w.ent = reinterpret_cast<uint4*>(p);
     p += h2 * 16u;
     w.aux = reinterpret_cast<uint2*>(p);
@@ -4455,19 +4399,19 @@ void launch_scatter_u8(const uint8_t* in, const uint32_t* perm, uint32_t nq, uin
 }
 
 // Workspace per lane slot and column of capacity: hash entries 2 x (16 + 8),
-// heap 16 + 8 (keys; column and hash slot), and for memoised walks the memo
-// (2 x 16) and walk stack (16).  Per slot: ent 32C, aux 16C (+ memo 32C, stk
-// 16C with walks) and the heap, 24 (C + kHeapK) B; a multiple of 128 B
-// (aligned lane-major blocks)
+// heap 16 (f, column, hash slot), and for memoised walks the memo (2 x 16)
+// and walk stack (16).  Per slot: ent 32C, aux 16C (+ memo 32C, stk 16C with
+// walks) and the heap, 16 (C + kHeapK) B; a multiple of 128 B (aligned
+// lane-major blocks)
 uint64_t search_ws_bytes_per_slot(uint32_t cap, bool tables) {
-    const uint64_t b = (tables ? 72ull : 120ull) * cap + 24ull * kern::kHeapK;
+    const uint64_t b = (tables ? 64ull : 112ull) * cap + 16ull * kern::kHeapK;
     return (b + 127u) / 128u * 128u;
 }
 
-// a record: the head, <= cap heap entries of 5 words, <= cap columns of 5
+// a record: the head, <= cap heap entries of 3 words, <= cap columns of 5
 // (tables) or 9 (walks) words
 uint64_t search_spill_words(uint32_t cap, bool tables) {
-    return kern::kSpillHead + (tables ? 10ull : 14ull) * cap;
+    return kern::kSpillHead + (tables ? 8ull : 12ull) * cap;
 }
 
 }  // namespace cpd
