@@ -2765,8 +2765,11 @@ namespace {
 // The search workspace policy (fifo_auto and the bench
 // run the same one).  capacity 0 = automatic: the first pass's columns per
 // lane are 2^13 when fscale > 0 (a bounded-suboptimal search expands ~140
-// nodes on the 1M bench graph) and 2^15 at fscale 0 (~49k expansions: a
-// larger first pass spills fewer searches), lowered to 2^10 at most until
+// nodes on the 1M bench graph) and 2^14 at fscale 0 (~47k expansions on
+// average, heavy-tailed: a first pass that stops the long searches early and
+// resumes them in fuller waves beats one that spills fewer —
+// profiles/search_heap_ab/r05y_*: 5.08k q/s from 2^14, 4.73k from 2^15),
+// lowered to 2^10 at most until
 // every search of the request gets a lane (profiles/search_cap_ab/,
 // search_lanes_ab/); capacity_max 0 = 4x the graph's columns rounded up to
 // a power of 2 (a search holds each column once, its heap some stale
@@ -2875,7 +2878,7 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
         };
         uint32_t cap = o.capacity;
         if (auto_cap) {
-            cap = std::min(o.fscale > 0.0 ? (1u << 13) : (1u << 15), cap_max);
+            cap = std::min(o.fscale > 0.0 ? (1u << 13) : (1u << 14), cap_max);
             const size_t budget = (size_t)(wfrac * (double)avail(0) * (cap < cap_max ? 0.75 : 1.0));
             const uint64_t lanes = nq ? search_slots(nq) : 64u;
             while (cap > (1u << 10) && lanes * search_ws_bytes_per_slot(cap, tables) > budget) cap >>= 1;
