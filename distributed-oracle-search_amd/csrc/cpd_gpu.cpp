@@ -3011,7 +3011,7 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             // instead of waiting for lanes), else the largest at which 64
             // lanes fit (never throw there — what cannot grow
             // reports finished = 2).  With resumed searches a smaller step
-            // wastes nothing.  CPD_SEARCH_GROW=4: always 4x (A/B).
+            // wastes nothing.  CPD_SEARCH_GROW=4 / 2: always 4x / at most 2x (A/B).
             uint32_t next = 0;
             if (more) {
                 uint32_t left = 0;
@@ -3022,7 +3022,8 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
                     const char* e = std::getenv("CPD_SEARCH_GROW");
                     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
                 }();
-                for (uint32_t c = std::min(cap * 4u, cap_max); c > cap; c >>= 1) {
+                const uint32_t top = grow == 2 ? cap * 2u : cap * 4u;  // CPD_SEARCH_GROW=2: 2x steps
+                for (uint32_t c = std::min(top, cap_max); c > cap; c >>= 1) {
                     const double per = (double)search_ws_bytes_per_slot(c, tables);
                     if (64.0 * per > share2) continue;
                     if (!next) next = c;
