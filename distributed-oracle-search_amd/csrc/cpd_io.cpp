@@ -228,7 +228,11 @@ Pairs read_query_file(const std::string& path) {
 
 // The whole file in one buffer: its size from fstat, then pread in pieces
 // of up to 1 GiB (split over `threads` when large) — no growth by appends.
-static std::string read_whole(const std::string& path, int threads) {
+// The file into `out` (resized to it; a buffer kept across calls, so a
+// server's requests after the first read into pages already mapped — a
+// fresh 14-MB buffer cost ~8 ms of page faults per 1M-query request), by up
+// to `threads` positional reads of >= 4 MB.
+static void read_whole(const std::string& path, int threads, std::vector<char>& out) {
     const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
     if (fd < 0) throw Error(CPD_E_IO, "cannot open " + path);
     struct stat st {};
@@ -236,14 +240,14 @@ static std::string read_whole(const std::string& path, int threads) {
         ::close(fd);
         throw Error(CPD_E_IO, "cannot stat " + path);
     }
-    std::string out((size_t)st.st_size, '\0');
+    out.resize((size_t)st.st_size);
     const size_t total = out.size();
     const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), total >> 22));
     std::vector<char> ok(T, 1);
     auto piece = [&](size_t k) {
         size_t a = total * k / T, b = total * (k + 1) / T;
         while (a < b) {
-            const ssize_t r = ::pread(fd, &out[a], std::min<size_t>(b - a, size_t(1) << 30), (off_t)a);
+            const ssize_t r = ::pread(fd, out.data() + a, std::min<size_t>(b - a, size_t(1) << 30), (off_t)a);
             if (r <= 0) {
                 ok[k] = 0;
                 return;
@@ -261,12 +265,19 @@ static std::string read_whole(const std::string& path, int threads) {
     ::close(fd);
     for (char c : ok)
         if (!c) throw Error(CPD_E_IO, path + ": short read");
-    return out;
 }
 
 void read_query_file(const std::string& path, int threads, std::vector<uint32_t>& s,
                      std::vector<uint32_t>& t) {
-    const std::string text = read_whole(path, threads);
+    // buffers kept per calling thread across calls (fifo_auto's requests)
+    thread_local std::vector<char> text_buf;
+    thread_local std::vector<std::vector<uint32_t>> ps_buf, pt_buf;
+    // (the parse threads reach them through these references: a
+    // thread_local named in their code would be their own, empty)
+    std::vector<char>& text = text_buf;
+    std::vector<std::vector<uint32_t>>& ps = ps_buf;
+    std::vector<std::vector<uint32_t>>& pt = pt_buf;
+    read_whole(path, threads, text);
     const char* const b = text.data();
     const char* const e = b + text.size();
     // header: the query count (process_query.py:95); a file without one is empty
@@ -291,27 +302,71 @@ void read_query_file(const std::string& path, int threads, std::vector<uint32_t>
         const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
         cut[k] = nl ? nl + 1 : e;
     }
-    std::vector<std::vector<uint32_t>> ps(T), pt(T);
+    if (ps.size() < T) {
+        ps.resize(T);
+        pt.resize(T);
+    }
     std::vector<const char*> bad(T, nullptr);
     auto parse = [&](size_t k) {
         const char* p = cut[k];
         const char* end = cut[k + 1];
-        ps[k].reserve((size_t)(end - p) / 12 + 1);
-        pt[k].reserve((size_t)(end - p) / 12 + 1);
-        while (p < end) {
-            const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(end - p)));
-            const char* le = nl ? nl : end;
-            Line ln{p, le};
-            int64_t x, y;
-            if (ln.i64(x)) {  // else blank
-                if (!ln.i64(y) || x < 0 || y < 0 || x > 0xFFFFFFFFll || y > 0xFFFFFFFFll) {
-                    bad[k] = p;
-                    return;
-                }
-                ps[k].push_back((uint32_t)x);
-                pt[k].push_back((uint32_t)y);
+        // into vectors of this thread's own (taken over from ps[k] / pt[k]
+        // and handed back at the end): pushing through ps[k] rewrote its
+        // end pointer, which shares a cache line with its neighbours' —
+        // 4 threads parsed 3-5x slower than 1 (profiles/query_parse/)
+        std::vector<uint32_t> ls, lt;
+        ls.swap(ps[k]);
+        lt.swap(pt[k]);
+        ls.clear();
+        lt.clear();
+        ls.reserve((size_t)(end - p) / 12 + 1);
+        lt.reserve((size_t)(end - p) / 12 + 1);
+        struct Back {  // the vectors go back on every exit
+            std::vector<uint32_t>& a;
+            std::vector<uint32_t>& b;
+            std::vector<uint32_t>& la;
+            std::vector<uint32_t>& lb;
+            ~Back() {
+                a.swap(la);
+                b.swap(lb);
             }
-            p = le + 1;
+        } back{ps[k], pt[k], ls, lt};
+        // one scan per line (what Line::i64 twice accepts: blanks, tabs and
+        // CRs around, a sign; a line whose first field is no number is
+        // skipped as blank); magnitudes clamp above 2^32 so they are refused
+        auto ws = [](char c) { return c == ' ' || c == '\t' || c == '\r'; };
+        auto num = [&](const char*& q, int64_t& v) {
+            while (q < end && ws(*q)) ++q;
+            bool neg = false;
+            if (q < end && (*q == '-' || *q == '+')) neg = *q++ == '-';
+            if (q >= end || *q < '0' || *q > '9') return false;
+            int64_t r = 0;
+            while (q < end && *q >= '0' && *q <= '9') {
+                r = std::min<int64_t>(r * 10 + (*q++ - '0'), int64_t(1) << 33);
+            }
+            v = neg ? -r : r;
+            return true;
+        };
+        while (p < end) {
+            const char* q = p;
+            int64_t x, y;
+            if (!num(q, x)) {  // blank (or no number first): the next line
+                const char* nl = static_cast<const char*>(std::memchr(q, '\n', (size_t)(end - q)));
+                p = nl ? nl + 1 : end;
+                continue;
+            }
+            if (!num(q, y) || x < 0 || y < 0 || x > 0xFFFFFFFFll || y > 0xFFFFFFFFll) {
+                bad[k] = p;
+                return;
+            }
+            ls.push_back((uint32_t)x);
+            lt.push_back((uint32_t)y);
+            if (q < end && *q == '\n') {
+                p = q + 1;
+            } else {
+                const char* nl = static_cast<const char*>(std::memchr(q, '\n', (size_t)(end - q)));
+                p = nl ? nl + 1 : end;
+            }
         }
     };
     if (T == 1) {

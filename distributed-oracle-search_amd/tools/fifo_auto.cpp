@@ -386,7 +386,8 @@ int main(int argc, char** argv) {
         std::string line = "0,0,0,0,0,0,0,0,0,0";
         try {
             double t0 = now();
-            std::vector<uint32_t> s, t;
+            // kept across requests: their pages stay mapped
+            static std::vector<uint32_t> s, t;
             cpd::io::read_query_file(qfile, parse_threads, s, t);
             const double t_read = now() - t0;
             if (diff != active_diff) {
