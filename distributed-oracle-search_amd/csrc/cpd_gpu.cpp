@@ -204,6 +204,13 @@ void create_stream_masked(hipStream_t* st, uint32_t q, int ncu) {
         if ((uint32_t)((i - i / 32) & 7) >= q) mask[(size_t)i / 32] |= 1u << (i % 32);
     HIP_CHECK(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
 }
+bool rows_nibble() {  // CPD_ROWS_NIBBLE=1: built rows as nibble tables (A/B)
+    static const bool on = [] {
+        const char* e = std::getenv("CPD_ROWS_NIBBLE");
+        return e && *e == '1';
+    }();
+    return on;
+}
 bool emit_defer_on() {  // CPD_EMIT_DEFER=1: emit deferred past the next batch's sweeps (A/B)
     static const bool on = [] {
         const char* e = std::getenv("CPD_EMIT_DEFER");
@@ -1872,11 +1879,14 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         r->lanes.clear();
         r->offsets.assign(1, 0);
         r->n = g->n;
-        // built rows stay nibble tables: the emit narrowing its stores cost
-        // ~0.5 ms per 24576-row step (rle_moves 7.9 against 7.4 ms, the step
-        // 68.2 against 67.2); the export and an index narrow them instead
-        r->tlb = 2u;
-        r->wpr = g->npad / 8u;
+        // built rows at the graph's packed width (2 bits per column on the
+        // bench graph): the register-resident fused emit writes them with
+        // 16-B stores, half the bytes of nibble tables (6.2 against 12.3 GB
+        // per 24576-row step), and the export and an index take them as
+        // they are.  CPD_ROWS_NIBBLE=1: nibble tables, narrowed on the way out
+        // (round 4's choice, when narrowing cost the unfused emit ~0.5 ms)
+        r->tlb = rows_nibble() ? 2u : g->tlb;
+        r->wpr = g->npad >> (5u - r->tlb);
         r->bits = g->move_bits;
         if (r->moves.n < (size_t)ntargets * r->wpr) {
             r->wait();  // an earlier build's emit may still write the old table

@@ -1317,6 +1317,30 @@ __device__ __forceinline__ void store_cols32(uint32_t* __restrict__ row, uint32_
         row[g] = nib_to1(o[0]) | (nib_to1(o[1]) << 8) | (nib_to1(o[2]) << 16) | (nib_to1(o[3]) << 24);
     }
 }
+
+// store_cols32 by a whole wave whose lane l holds segment g0 + l: the packed
+// widths' 8-B (2-bit) and 4-B (1-bit) pieces gathered into 16-B stores by
+// every second / fourth lane (CPD_EMIT_WIDE=0: per-lane stores, A/B)
+__device__ __forceinline__ void store_cols32_wave(uint32_t* __restrict__ row, uint32_t g,
+                                                  uint32_t lb, const uint32_t (&o)[4],
+                                                  uint32_t lane, uint32_t wide) {
+    if (lb == 2u || !wide) {
+        store_cols32(row, g, lb, o);
+    } else if (lb == 1u) {
+        const uint32_t a = nib_to2(o[0]) | (nib_to2(o[1]) << 16);
+        const uint32_t b = nib_to2(o[2]) | (nib_to2(o[3]) << 16);
+        const uint32_t na = (uint32_t)__shfl_down((int)a, 1, 64);
+        const uint32_t nb = (uint32_t)__shfl_down((int)b, 1, 64);
+        if (!(lane & 1u)) reinterpret_cast<uint4*>(row)[g >> 1] = make_uint4(a, b, na, nb);
+    } else {
+        const uint32_t w = nib_to1(o[0]) | (nib_to1(o[1]) << 8) | (nib_to1(o[2]) << 16) |
+                           (nib_to1(o[3]) << 24);
+        const uint32_t w1 = (uint32_t)__shfl_down((int)w, 1, 64);
+        const uint32_t w2 = (uint32_t)__shfl_down((int)w, 2, 64);
+        const uint32_t w3 = (uint32_t)__shfl_down((int)w, 3, 64);
+        if (!(lane & 3u)) reinterpret_cast<uint4*>(row)[g >> 2] = make_uint4(w, w1, w2, w3);
+    }
+}
 __device__ __forceinline__ void load_cols32(const uint32_t* __restrict__ row, uint32_t g, uint32_t lb,
                                             uint32_t (&x)[4]) {
     if (lb == 2u) {
@@ -1528,7 +1552,7 @@ __device__ __forceinline__ uint32_t seg4_entry_set(const Seg4& r) {
 // it belongs to, the move = that set's lowest bit.
 __device__ __forceinline__ void fill_tile4(const Seg4& r, uint32_t& carry,
                                            uint32_t* __restrict__ orow, uint32_t seg,
-                                           uint32_t lb, uint32_t lane) {
+                                           uint32_t lb, uint32_t lane, uint32_t emit_wide) {
     const bool any = (r.Z[0] | r.Z[1] | r.Z[2] | r.Z[3]) != 0u;
     const uint32_t fl = seg4_entry_set(r);
     const uint64_t m = __ballot(any);
@@ -1592,7 +1616,7 @@ __device__ __forceinline__ void fill_tile4(const Seg4& r, uint32_t& carry,
         const uint32_t b2 = ~(X[i] >> 2) & b1;
         o[i] = b0 + b1 + b2;
     }
-    store_cols32(orow, seg, lb, o);
+    store_cols32_wave(orow, seg, lb, o, lane, emit_wide);
     if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
 }
 
@@ -1641,7 +1665,7 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
         const uint32_t seg = t * 64u + lane;
         uint32_t v[4];
         load(seg, v);
-        fill_tile4(seg4_scan(v, strow[seg] & 0xFu), carry, orow, seg, lb, lane);
+        fill_tile4(seg4_scan(v, strow[seg] & 0xFu), carry, orow, seg, lb, lane, 1u);
     }
 }
 
@@ -1703,7 +1727,7 @@ __device__ __forceinline__ uint32_t scan32_breaks(const uint32_t (&v)[4], uint32
 __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uint32_t nseg,
                                 uint32_t ntiles, uint32_t t0, uint32_t t1, uint32_t Sin,
                                 uint8_t* ent, uint32_t* __restrict__ orow, uint32_t lb,
-                                uint32_t lane, uint32_t& breaks) {
+                                uint32_t lane, uint32_t& breaks, uint32_t wide) {
     auto load = [&](uint32_t seg, uint32_t (&v)[4]) {
         const uint4 q = f4[fm4_piece(brow, nseg, seg)];
         v[0] = q.x;
@@ -1803,7 +1827,7 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
     carry = close;
     for (uint32_t t = t1; t-- > t0;) {
         fill_tile4(seg4_scan(C[kMoveTiles - 1], ent[(t - t0) * 64u + lane]), carry, orow,
-                   t * 64u + lane, lb, lane);
+                   t * 64u + lane, lb, lane, wide);
 #pragma unroll
         for (int i = (int)kMoveTiles - 1; i >= 1; --i)
 #pragma unroll
@@ -1816,7 +1840,7 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
 __global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm, uint32_t npad,
                                                  uint32_t nrows, const uint32_t* __restrict__ out_row,
                                                  uint32_t lb, uint32_t* __restrict__ dense,
-                                                 EmitChunks ck) {
+                                                 EmitChunks ck, uint32_t wide) {
     __shared__ uint8_t ent_all[4 * 64 * kMoveTiles];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t brow = blockIdx.y * 4u + wv;
@@ -1844,7 +1868,7 @@ __global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm
     uint32_t* __restrict__ orow = dense + (size_t)out_row[brow] * (npad >> (5u - lb));
     uint32_t breaks = 0;
     const uint32_t xs = emit_chunk4(f4, brow, nseg, ntiles, t0, t1, Sin, ent_all + wv * 64u * kMoveTiles,
-                                    orow, lb, lane, breaks);
+                                    orow, lb, lane, breaks, wide);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) breaks += (uint32_t)__shfl_xor((int)breaks, o, 64);
     if (lane == 0) {
@@ -1863,7 +1887,8 @@ __global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm
 __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ fm, uint32_t npad,
                                                    uint32_t nrows, const uint32_t* __restrict__ out_row,
                                                    uint32_t lb, uint32_t* __restrict__ dense,
-                                                   EmitChunks ck, uint32_t* __restrict__ counts) {
+                                                   EmitChunks ck, uint32_t* __restrict__ counts,
+                                                   uint32_t wide) {
     __shared__ uint8_t ent[64 * kMoveTiles];
     const uint32_t row = blockIdx.x;
     if (row >= nrows) return;
@@ -1890,7 +1915,7 @@ __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ 
             const uint32_t t0 = (b + j) * kMoveTiles;
             uint32_t br = 0;
             const uint32_t xj = emit_chunk4(f4, row, nseg, ntiles, t0, min(ntiles, t0 + kMoveTiles), Sj,
-                                            ent, orow, lb, lane, br);
+                                            ent, orow, lb, lane, br, wide);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) br += (uint32_t)__shfl_xor((int)br, o, 64);
             if (lane == j) {
@@ -4073,10 +4098,11 @@ void launch_rle_emit(const uint32_t* fm, uint32_t npad, uint32_t nrows, const ui
                      uint32_t* counts, hipStream_t s) {
     if (!nrows) return;
     const kern::EmitChunks ck{xe, xs, cc};
+    static const uint32_t wide = env_u32("CPD_EMIT_WIDE", 1) ? 1u : 0u;  // 16-B table stores
     launch(kern::rle_emit4, dim3(rle_emit_chunks(npad), (nrows + 3u) / 4u), dim3(256), s, fm, npad,
-           nrows, out_row, lb, dense, ck);
+           nrows, out_row, lb, dense, ck, wide);
     launch(kern::rle_emit_fix, dim3(nrows), dim3(64), s, fm, npad, nrows, out_row, lb, dense, ck,
-           counts);
+           counts, wide);
 }
 
 void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,

@@ -30,6 +30,10 @@ oracle, walk queries over them dense and RLE.  What each reaches:
                     down-sweep is queued
   CPD_UP_HEAD=0   (opt-in) the next batch's up-sweep queued before this batch's
                   first moves, which wait for its wide levels
+  CPD_EMIT_WIDE=0 the fused emit's packed tables stored per lane (8 / 4 B)
+                  instead of gathered into 16-B stores
+  CPD_ROWS_NIBBLE=1 built rows as nibble tables (narrowed on export / index)
+                  instead of at the graph's packed width
 """
 import json
 import os
@@ -80,8 +84,10 @@ print(json.dumps(out))
 
 SWITCHES = ["CPD_LIVE", "CPD_SORT", "CPD_LANE_KEY", "CPD_XCD", "CPD_FM_N4", "CPD_ASYNC",
             "CPD_RLE_FUSED", "CPD_RLE_CH", "CPD_LEAFFM", "CPD_OVERLAP", "CPD_MOVES_SWAR",
-            "CPD_TABLE_BITS", "CPD_FM_ORDER", "CPD_TS_SHARE", "CPD_EMIT_DEFER", "CPD_UP_HEAD"]
-OFF = {"CPD_TABLE_BITS": "4", "CPD_TS_SHARE": "1", "CPD_EMIT_DEFER": "1", "CPD_UP_HEAD": "0"}
+            "CPD_TABLE_BITS", "CPD_FM_ORDER", "CPD_TS_SHARE", "CPD_EMIT_DEFER", "CPD_UP_HEAD", "CPD_EMIT_WIDE",
+            "CPD_ROWS_NIBBLE"]
+OFF = {"CPD_TABLE_BITS": "4", "CPD_TS_SHARE": "1", "CPD_EMIT_DEFER": "1", "CPD_UP_HEAD": "0",
+       "CPD_ROWS_NIBBLE": "1"}
 # switches that only matter on the unfused emit path
 WITH = {"CPD_RLE_CH": {"CPD_RLE_FUSED": "0"}, "CPD_MOVES_SWAR": {"CPD_RLE_FUSED": "0"}}
 
