@@ -3364,6 +3364,22 @@ __device__ bool cpd_walk(Lane& L, const LaneWs& W, const uint2* __restrict__ adj
     return true;
 }
 
+// h = (uint64_t)(hscale * (double)hu), the oracle's expression; with hscale
+// 1 (a kernel-uniform test) and hu < 2^53 it is hu exactly, and the double
+// conversions (~25 instructions a push) are skipped
+__device__ __forceinline__ uint64_t hval(const SearchOpt& opt, uint64_t hu) {
+    if (opt.hscale == 1.0 && hu < (1ull << 53)) return hu;
+    return (uint64_t)(opt.hscale * (double)hu);
+}
+
+// the stop rule (double)f * (1 + fscale) >= (double)ub; at fscale 0 with
+// both below 2^53 (or ub INF) the integer compare is the same
+__device__ __forceinline__ bool f_stops(const SearchOpt& opt, uint64_t f, uint64_t ub) {
+    if (opt.fscale == 0.0 && f < (1ull << 53) && (ub < (1ull << 53) || ub == kInf64))
+        return f >= ub;
+    return (double)f * (1.0 + opt.fscale) >= (double)ub;
+}
+
 // TABLES: the CPD path values come from the per-row tables (hrow / crow /
 // lrow, n per row) instead of memoised walks; the workspace then holds only
 // the searched columns (no memo, no walk stack).  Same results and counters.
@@ -3492,7 +3508,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             W.ent[si].w = 0u;
             W.aux[si].x = 0u;
             L.inserted = 1;
-            heap_push(W.hk, L.hsize, hkey_make((uint64_t)(opt.hscale * (double)hs), L.s, si));
+            heap_push(W.hk, L.hsize, hkey_make(hval(opt, hs), L.s, si));
         }
     };
     // a search stopped before a pop that could outgrow the workspace: its
@@ -3629,7 +3645,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // the entry's g is the column's current one unless the entry is
         // stale (its f above current g + h: a better g came later)
         const uint64_t g = u64of(ev.z, ev.w);
-        if (f > g + (uint64_t)(opt.hscale * (double)hv)) {  // stale entry
+        if (f > g + hval(opt, hv)) {  // stale entry
             heap_pop_pre(W.hk, L.hsize, hp, e2, lst);
             ++L.surplus;
             continue;
@@ -3637,7 +3653,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const uint64_t elapsed =
             opt.tick_ns ? opt.tick_ns * ((uint64_t)L.expanded + L.touched)
                         : 10ull * (__builtin_amdgcn_s_memrealtime() - L.t0);
-        if ((double)f * (1.0 + opt.fscale) >= (double)L.ub ||
+        if (f_stops(opt, f, L.ub) ||
             (opt.itrs >= 0 && (int64_t)L.expanded >= opt.itrs) ||
             (opt.time_ns && elapsed > opt.time_ns)) {
             L.done = true;
@@ -3762,7 +3778,7 @@ if (SHIFT <= 2) {
                 wr[k] = ui;
                 ++L.inserted;
                 pv[k] = true;
-                pk[k] = hkey_make(ng + (uint64_t)(opt.hscale * (double)hu), u, ui);
+                pk[k] = hkey_make(ng + hval(opt, hu), u, ui);
                 ++np;
             } else if (ng < u64of(eu.z, eu.w)) {
                 if (L.hsize + np >= C) {
@@ -3776,7 +3792,7 @@ if (SHIFT <= 2) {
                 ++L.updated;
                 const uint64_t hu = TABLES ? hr[k] : u64of(W.memo[ui].x, W.memo[ui].y);
                 pv[k] = true;
-                pk[k] = hkey_make(ng + (uint64_t)(opt.hscale * (double)hu), u, ui);
+                pk[k] = hkey_make(ng + hval(opt, hu), u, ui);
                 ++np;
             }
         }
@@ -3818,7 +3834,7 @@ if (SHIFT <= 2) {
                 W.ent[ui].w = (uint32_t)(ng >> 32);
                 W.aux[ui].x = dv + 1u;
                 ++L.inserted;
-                heap_push(W.hk, L.hsize, hkey_make(ng + (uint64_t)(opt.hscale * (double)hu), u, ui));
+                heap_push(W.hk, L.hsize, hkey_make(ng + hval(opt, hu), u, ui));
             } else if (ng < u64of(W.ent[ui].z, W.ent[ui].w)) {
                 if (L.hsize >= C) {
                     L.overflow = L.done = true;
@@ -3830,7 +3846,7 @@ if (SHIFT <= 2) {
                 ++L.updated;
                 const uint64_t hu = TABLES ? tb.hrow[rb + u]
                                            : u64of(W.memo[ui].x, W.memo[ui].y);
-                heap_push(W.hk, L.hsize, hkey_make(ng + (uint64_t)(opt.hscale * (double)hu), u, ui));
+                heap_push(W.hk, L.hsize, hkey_make(ng + hval(opt, hu), u, ui));
             }
         }
         }
