@@ -2987,6 +2987,7 @@ struct SearchWs {
     // lane for the address translation); array-major above when 0
     char* base;
     uint64_t stride;
+    uint32_t lpw;  // lanes per wave that search (64 / 32 / 16 / 8)
 };
 
 struct SearchOpt {
@@ -3404,7 +3405,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     constexpr uint32_t KD = 1u << SHIFT;  // most new columns / heap entries of one expansion
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint64_t slot = wave * 64u + lane;  // this lane's workspace
+    // ws.lpw lanes per wave search (64, or fewer when few searches are left:
+    // more waves, each issuing for fewer divergent lanes); the others idle
+    const uint32_t lpw = ws.lpw;
+    const bool active = lane < lpw;
+    const uint64_t slot = wave * lpw + (active ? lane : 0u);  // this lane's workspace
     const uint64_t q0l = wave * chunk;
     const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
     const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
@@ -3430,7 +3435,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     // tag = query index + 1 of the search that wrote a slot; cleared once per
     // launch so stale tags never match
-    for (uint32_t i = 0; i < 2u * C; ++i) W.ent[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (active)
+        for (uint32_t i = 0; i < 2u * C; ++i) W.ent[i] = make_uint4(0u, 0u, 0u, 0u);
 
     Lane L;
     L.q = kIdleQ;
@@ -3568,8 +3574,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         return true;
     };
     uint32_t next = q0;
-    if (q0 + lane < q1) begin(q0 + lane);
-    next = min(q1, q0 + 64u);
+    if (active && q0 + lane < q1) begin(q0 + lane);
+    next = min(q1, q0 + lpw);
     for (;;) {
         // retire finished searches, refill from the chunk
         const bool fin_now = L.q != kIdleQ && (L.done || L.hsize == 0);
@@ -4331,7 +4337,17 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
                        uint32_t* plen, uint8_t* fin, uint32_t* qstats, unsigned long long* agg,
                        hipStream_t s) {
     const bool tables = hrow != nullptr;
-    const uint32_t waves = slots / 64u;  // a multiple of 64 lanes (search_slots)
+    // Few searches left (a late pass): fewer lanes per wave, more waves —
+    // each wave issues for fewer divergent lanes, and the SIMDs a full-wave
+    // launch would leave idle take the rest (CPD_SEARCH_LPW_MIN: the fewest
+    // lanes per wave allowed, default 8; 64 = off — profiles/search_heap_ab/
+    // r05aj: fscale 0 5.51-5.69k against 5.03k q/s)
+    static const uint32_t lpw_min = std::max(8u, std::min(64u, env_u32("CPD_SEARCH_LPW_MIN", 8)));
+    // (the fewest lanes, a multiple of 8, at which the slots' waves still fit
+    // one per SIMD: 1024 one-wave workgroups)
+    const uint32_t fit = (uint32_t)(((uint64_t)slots + 1023u) / 1024u);
+    const uint32_t lpw = std::max(lpw_min, std::min(64u, (fit + 7u) / 8u * 8u));
+    const uint32_t waves = slots / lpw;  // waves x lpw <= slots workspaces
     char* p = static_cast<char*>(ws);
     const size_t h2 = (size_t)slots * 2u * cap;
     kern::SearchWs w;
@@ -4340,6 +4356,7 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     // search_ws_bytes_per_slot each, 128-B aligned; the heap first
     w.base = static_cast<char*>(ws);
     w.stride = search_lane_major() ? search_ws_bytes_per_slot(cap, tables) : 0u;
+    w.lpw = lpw;
     const size_t hk = (size_t)slots * (cap + kern::kHeapK);
     w.hk = reinterpret_cast<uint4*>(p);
     p += hk * 16u;
