@@ -66,7 +66,7 @@ def parse(argv=None):
     ap.add_argument("--partmethod", default="")
     ap.add_argument("--partkey", type=int, default=0)
     ap.add_argument("--batch", type=int, default=0,
-                    help="rows per step (multiple of 1024); 0 = what fits in HBM, <= 24576")
+                    help="rows per step (multiple of 1024); 0 = what fits in HBM, <= 28672")
     ap.add_argument("--queries", type=int, default=0, help="0 = the workload's")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = every host thread this job may use (OMP_NUM_THREADS or affinity)")

@@ -158,10 +158,12 @@ bool async_on();  // CPD_ASYNC (defined with the other switches)
 hipStream_t thread_stream(int device);
 
 // Largest auto batch (CPD_BATCH_MAX, a multiple of 1024 <= 32768; A/B knob).
+// 28672 since the rows are built at the packed width (8.0 MB per target at
+// 1M nodes; profiles/batch_ab/r05am: 387.3k against 380.8k rows/s at 24576).
 uint32_t batch_max() {
     static const uint32_t v = [] {
         const char* e = std::getenv("CPD_BATCH_MAX");
-        const unsigned long b = e && *e ? std::strtoul(e, nullptr, 10) : 24576ul;
+        const unsigned long b = e && *e ? std::strtoul(e, nullptr, 10) : 28672ul;
         return (uint32_t)std::max(1024ul, std::min(32768ul, b / 1024ul * 1024ul));
     }();
     return v;
@@ -219,13 +221,14 @@ bool emit_defer_on() {  // CPD_EMIT_DEFER=1: emit deferred past the next batch's
     return on;
 }
 
-double batch_bytes_per_row(uint32_t n, uint32_t npad, uint32_t fmb, bool narrow, bool leaf_fm) {
+double batch_bytes_per_row(uint32_t n, uint32_t npad, uint32_t fmb, bool narrow, bool leaf_fm,
+                           uint32_t mbits) {
     // the fused emit keeps no segment states: 12 B per chunk of 32k columns
     const double rle = rle_fused(fmb) ? 12.0 * rle_emit_chunks(npad)
                                       : 2.0 * 5.0 / 32.0 * npad +
                                             (fmb == 4 ? 12.0 * rle_count_chunks(npad) : 0.0);
     return (narrow ? 6.0 : 4.0) * n + 2.0 * fmb / 8.0 * npad + rle + (leaf_fm ? 0.5 * n : 0.0) +
-           2.0 * 0.5 * npad;
+           2.0 * mbits / 8.0 * npad;
 }
 bool up_priority_on();
 bool lane_key_on();
@@ -538,7 +541,8 @@ struct cpd_graph {
             // 24 slabs.  Larger batches amortise the latency-bound
             // narrow levels: at 1M nodes 20480 rows per batch measured 310.5k
             // rows/s against 296.1k for 16384 (round 2).
-            const double per = batch_bytes_per_row(n, npad, fmb, narrow, leaf_fm);
+            const double per = batch_bytes_per_row(n, npad, fmb, narrow, leaf_fm,
+                                                   rows_nibble() ? 4u : 1u << tlb);
             const double avail = free_b > hbm_reserve ? (double)(free_b - hbm_reserve) : 0.0;
             const double fit = 0.85 * avail / per;
             CPD_REQUIRE(hbm_reserve == 0 || fit >= 1024.0, CPD_E_OOM,
@@ -1029,7 +1033,8 @@ int cpd_batch_bytes(uint32_t n, uint32_t max_degree, uint32_t batch, uint64_t* b
         const uint32_t npad = (n + kFmTile - 1u) / kFmTile * kFmTile;
         // narrow rows and leaf sets assumed (their upper bound), plus the
         // per-column arrays and the lane tables
-        *bytes = (uint64_t)(batch_bytes_per_row(n, npad, fmb, true, fmb == 4) * batch) +
+        const uint32_t mbits = rows_nibble() ? 4u : max_degree <= 2u ? 1u : max_degree <= 4u ? 2u : 4u;
+        *bytes = (uint64_t)(batch_bytes_per_row(n, npad, fmb, true, fmb == 4, mbits) * batch) +
                  (uint64_t)batch * (n / 256u + 1u) * 4u + 512ull * n + (64ull << 20);
     });
 }

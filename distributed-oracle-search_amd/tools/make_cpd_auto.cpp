@@ -9,7 +9,7 @@
 //                                      0 (default) = what fits in HBM, at most
 //                                      2048 rows when files are written (the
 //                                      disk bounds the worker) and
-//                                      24576 with --discard (CPD_BATCH_MAX
+//                                      28672 with --discard (CPD_BATCH_MAX
 //                                      overrides), with or without the arena
 //                 [--no-arena]         allocate the batch buffers at graph setup
 //                                      instead of committing them on a host
@@ -389,7 +389,7 @@ int main(int argc, char** argv) {
     // to commit beside the plan; --discard keeps the build-bound cap
     const uint32_t batch_cap = [&] {
         const char* bm = std::getenv("CPD_BATCH_MAX");
-        const double dflt = a.has("discard") ? 24.0 : 2.0;
+        const double dflt = a.has("discard") ? 28.0 : 2.0;
         const double k = bm && *bm ? std::max(1.0, std::min(32.0, std::floor(std::atof(bm) / 1024))) : dflt;
         return (uint32_t)k * 1024u;
     }();

@@ -18,7 +18,7 @@ def test_hbm_reserve_bounds_the_auto_batch():
     plan = cpd.Plan(g)
     dev = cpd.Graph(plan, batch=0)
     full = dev.batch
-    assert full == 24576  # a 3600-node graph: the cap, far below free HBM
+    assert full == 28672  # a 3600-node graph: the cap, far below free HBM
 
     free0, _ = cpd.device_mem_info(0)
     dev.set_hbm_reserve(free0 + (1 << 30))
