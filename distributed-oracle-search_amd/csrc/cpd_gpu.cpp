@@ -2893,7 +2893,10 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
         };
         uint32_t cap = o.capacity;
         if (auto_cap) {
-            cap = std::min(o.fscale > 0.0 ? (1u << 13) : (1u << 14), cap_max);
+            // (walks: 2^14 at fscale > 0 too — a walk's columns count, and
+            // at 2^13 the few searches that outgrew it took a second pass of
+            // 10% of the time: 271-280k against 245-252k q/s, r05ap)
+            cap = std::min(o.fscale > 0.0 && tables ? (1u << 13) : (1u << 14), cap_max);
             const size_t budget = (size_t)(wfrac * (double)avail(0) * (cap < cap_max ? 0.75 : 1.0));
             const uint64_t lanes = nq ? search_slots(nq) : 64u;
             while (cap > (1u << 10) && lanes * search_ws_bytes_per_slot(cap, tables) > budget) cap >>= 1;

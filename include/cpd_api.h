@@ -401,7 +401,8 @@ void cpd_index_free(cpd_index* ix);
  * HBM) stops unfinished, with finished = 2 in cpd_query_fetch, and is
  * counted in `overflow`.  capacity = 0 selects the library's workspace
  * policy (what fifo_auto runs): the first pass at 2^13 columns when fscale
- * > 0 and 2^14 at fscale 0, lowered (to 2^10 at most) until every query of
+ * > 0 with tables (2^14 with walks) and 2^14 at fscale 0, lowered (to 2^10
+ * at most) until every query of
  * the request gets a lane; capacity_max 0 = 4 n rounded up to a power of 2
  * (<= 2^24); workspace_frac 0 = 0.85 of the free HBM.  An explicit capacity
  * keeps capacity_max 0 = no larger pass and workspace_frac 0 = 0.25.  The
