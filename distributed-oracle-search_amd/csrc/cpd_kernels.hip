@@ -3798,7 +3798,10 @@ if (SHIFT <= 2) {
                         break;
                     }
                 } else {
-                    if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, u, ui)) {
+                    // walked (and so in the hash) by the room check above:
+                    // its memo is final; no walk here (a second inlined walk
+                    // per edge only grew the kernel)
+                    if (!fu) {  // cannot happen: the heads were all walked
                         L.overflow = L.done = true;
                         break;
                     }
@@ -3856,7 +3859,10 @@ if (SHIFT <= 2) {
                         break;
                     }
                 } else {
-                    if (!cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, u, ui)) {
+                    // walked (and so in the hash) by the room check above:
+                    // its memo is final; no walk here (a second inlined walk
+                    // per edge only grew the kernel)
+                    if (!fu) {  // cannot happen: the heads were all walked
                         L.overflow = L.done = true;
                         break;
                     }
