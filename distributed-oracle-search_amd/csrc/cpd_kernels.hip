@@ -3703,11 +3703,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         bool room = L.hsize - 1u + KD <= C && (!TABLES || L.used + KD <= C);
         if (room && !TABLES) {
             if (SHIFT <= 2) {
+                // one walk call site, not one per unrolled edge (the walk is
+                // large): the heads picked by index from registers
+#pragma unroll 1
+                for (int k = 0; k < ND && room; ++k) {
+                    uint32_t u = ed[0].x;
 #pragma unroll
-                for (int k = 0; k < ND; ++k) {
-                    if (!room || ed[k].x == kNoEdge) break;  // edges are packed first
+                    for (int j = 1; j < ND; ++j) u = k == j ? ed[j].x : u;
+                    if (u == kNoEdge) break;  // edges are packed first
                     uint32_t ui;
-                    room = cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, ed[k].x, ui);
+                    room = cpd_walk<SHIFT>(L, W, adj_f, adj_w, row, u, ui);
                 }
             } else {
 #pragma unroll 1
