@@ -3606,12 +3606,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         return true;
     };
     uint32_t next = q0;
-    if (active && q0 + lane < q1) begin(q0 + lane);
-    next = min(q1, q0 + lpw);
+    // the first round hands every searching lane its first query through the
+    // refill below: one call site of begin() (which holds a walk and the
+    // resume loops), not two
+    bool want = active;
     for (;;) {
         // retire finished searches, refill from the chunk
         const bool fin_now = L.q != kIdleQ && (L.done || L.hsize == 0);
-        const uint64_t m = __ballot(fin_now);
+        const bool take = fin_now || want;
+        const uint64_t m = __ballot(take);
+        want = false;
         if (m) {
             if (fin_now) {
                 const bool found = L.ub != kInf64 && !L.overflow;
@@ -3635,6 +3639,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 s_len += found ? L.best_len : 0u;
                 s_fin += found ? 1u : 0u;
                 s_ovf += L.overflow ? 1u : 0u;
+            }
+            if (take) {
                 const uint32_t nqi = next + (uint32_t)__builtin_popcountll(m & lt_mask);
                 if (nqi < q1) begin(nqi);
                 else L.q = kIdleQ;
