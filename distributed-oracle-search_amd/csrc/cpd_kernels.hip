@@ -1264,6 +1264,11 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
 // is the lowest bit of the set at the row's end.  One 16-B store per lane per
 // tile: a wave writes 1 KiB contiguous.
 constexpr uint32_t kMoveTiles = 16;
+#ifndef CPD_EMIT_TILES
+#define CPD_EMIT_TILES 16
+#endif
+// tiles per chunk of the fused emit (its chunk lives in 4 * kEmitTiles VGPRs)
+constexpr uint32_t kEmitTiles = CPD_EMIT_TILES;
 
 // Move tables at 2^lb bits per column (lb = 0, 1, 2: 1, 2 or 4 bits, by the
 // graph's max out-degree — a move indexes its column's out-list, so every
@@ -1674,7 +1679,7 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
 // rle_count_ch + rle_fix + rle_moves4 read every first-move set twice (the
 // count, then the emit) and write and re-read the per-segment entry states:
 // ~50 GB of HBM per 24576-row step for 12.3 GB of sets and 12.3 GB of
-// tables.  Here a wave owns a chunk of kMoveTiles tiles of one row and:
+// tables.  Here a wave owns a chunk of kEmitTiles tiles of one row and:
 //   forward  resolves every segment's entry set itself: lane L guesses its
 //            entry by scanning lane L-1's last 16 columns from a wildcard
 //            set, scans its 32 columns, and takes lane L-1's exit instead
@@ -1718,7 +1723,7 @@ __device__ __forceinline__ uint32_t scan32_breaks(const uint32_t (&v)[4], uint32
 }
 
 // The chunk [t0, t1) of row `brow` from entry set Sin (wave-cooperative; every
-// lane of the wave calls it with the same arguments).  ent: 64 * kMoveTiles
+// lane of the wave calls it with the same arguments).  ent: 64 * kEmitTiles
 // bytes of LDS for this wave.  Writes the chunk's move table; returns the
 // exit set (wave-uniform) and adds the chunk's breaks to `breaks` (per lane).
 // The chunk's sets stay in registers (64 VGPRs a lane), loaded all at once
@@ -1735,15 +1740,15 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
         v[2] = q.z;
         v[3] = q.w;
     };
-    const uint32_t L = t1 - t0;  // tiles in the chunk, 1..kMoveTiles (wave-uniform)
-    uint32_t C[kMoveTiles][4];
+    const uint32_t L = t1 - t0;  // tiles in the chunk, 1..kEmitTiles (wave-uniform)
+    uint32_t C[kEmitTiles][4];
 #pragma unroll
-    for (uint32_t i = 0; i < kMoveTiles; ++i)
+    for (uint32_t i = 0; i < kEmitTiles; ++i)
         if (i < L) load((t0 + i) * 64u + lane, C[i]);
     // forward: the segments' entry sets
     uint32_t carry = Sin;  // the set entering the tile in hand
 #pragma unroll
-    for (uint32_t i = 0; i < kMoveTiles; ++i) {
+    for (uint32_t i = 0; i < kEmitTiles; ++i) {
         if (i < L) {
         const uint32_t(&v)[4] = C[i];
         const uint32_t p2 = (uint32_t)__shfl_up((int)v[2], 1, 64);
@@ -1816,42 +1821,42 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
         if (!found) close = P;  // no run closes right of the chunk: the row's last run
     }
     // backward: the move table, right to left; the tile in hand is always
-    // C[kMoveTiles - 1] (static register indices: the array shifts up a tile
-    // per step, after a shift by kMoveTiles - L for a short chunk)
-    for (uint32_t s = L; s < kMoveTiles; ++s) {
+    // C[kEmitTiles - 1] (static register indices: the array shifts up a tile
+    // per step, after a shift by kEmitTiles - L for a short chunk)
+    for (uint32_t s = L; s < kEmitTiles; ++s) {
 #pragma unroll
-        for (int i = (int)kMoveTiles - 1; i >= 1; --i)
+        for (int i = (int)kEmitTiles - 1; i >= 1; --i)
 #pragma unroll
             for (int w = 0; w < 4; ++w) C[i][w] = C[i - 1][w];
     }
     carry = close;
     for (uint32_t t = t1; t-- > t0;) {
-        fill_tile4(seg4_scan(C[kMoveTiles - 1], ent[(t - t0) * 64u + lane]), carry, orow,
+        fill_tile4(seg4_scan(C[kEmitTiles - 1], ent[(t - t0) * 64u + lane]), carry, orow,
                    t * 64u + lane, lb, lane, wide);
 #pragma unroll
-        for (int i = (int)kMoveTiles - 1; i >= 1; --i)
+        for (int i = (int)kEmitTiles - 1; i >= 1; --i)
 #pragma unroll
             for (int w = 0; w < 4; ++w) C[i][w] = C[i - 1][w];
     }
     return exitS;
 }
 
-// wave per (row, chunk of kMoveTiles tiles); 4 waves per workgroup = 4 rows
+// wave per (row, chunk of kEmitTiles tiles); 4 waves per workgroup = 4 rows
 __global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm, uint32_t npad,
                                                  uint32_t nrows, const uint32_t* __restrict__ out_row,
                                                  uint32_t lb, uint32_t* __restrict__ dense,
                                                  EmitChunks ck, uint32_t wide) {
-    __shared__ uint8_t ent_all[4 * 64 * kMoveTiles];
+    __shared__ uint8_t ent_all[4 * 64 * kEmitTiles];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t brow = blockIdx.y * 4u + wv;
     const uint32_t lane = threadIdx.x & 63u;
     if (brow >= nrows) return;  // wave-uniform
     const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
-    const uint32_t nch = (ntiles + kMoveTiles - 1u) / kMoveTiles;
+    const uint32_t nch = (ntiles + kEmitTiles - 1u) / kEmitTiles;
     const uint32_t ch = blockIdx.x;
-    const uint32_t t0 = ch * kMoveTiles;
+    const uint32_t t0 = ch * kEmitTiles;
     if (t0 >= ntiles) return;
-    const uint32_t t1 = min(ntiles, t0 + kMoveTiles);
+    const uint32_t t1 = min(ntiles, t0 + kEmitTiles);
     const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
     // the chunk's entry: a wildcard at column 0, else the guess from the
     // last 16 columns left of the chunk (one segment, scanned by every lane)
@@ -1867,7 +1872,7 @@ __global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm
     }
     uint32_t* __restrict__ orow = dense + (size_t)out_row[brow] * (npad >> (5u - lb));
     uint32_t breaks = 0;
-    const uint32_t xs = emit_chunk4(f4, brow, nseg, ntiles, t0, t1, Sin, ent_all + wv * 64u * kMoveTiles,
+    const uint32_t xs = emit_chunk4(f4, brow, nseg, ntiles, t0, t1, Sin, ent_all + wv * 64u * kEmitTiles,
                                     orow, lb, lane, breaks, wide);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) breaks += (uint32_t)__shfl_xor((int)breaks, o, 64);
@@ -1889,12 +1894,12 @@ __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ 
                                                    uint32_t lb, uint32_t* __restrict__ dense,
                                                    EmitChunks ck, uint32_t* __restrict__ counts,
                                                    uint32_t wide) {
-    __shared__ uint8_t ent[64 * kMoveTiles];
+    __shared__ uint8_t ent[64 * kEmitTiles];
     const uint32_t row = blockIdx.x;
     if (row >= nrows) return;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
-    const uint32_t nch = (ntiles + kMoveTiles - 1u) / kMoveTiles;
+    const uint32_t nch = (ntiles + kEmitTiles - 1u) / kEmitTiles;
     const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
     uint32_t* __restrict__ orow = dense + (size_t)out_row[row] * (npad >> (5u - lb));
     uint32_t carry = 0xFu, total = 0;
@@ -1912,9 +1917,9 @@ __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ 
             if (!m) break;
             const uint32_t j = (uint32_t)__builtin_ctzll(m);
             const uint32_t Sj = (uint32_t)__shfl((int)pred, (int)j, 64);
-            const uint32_t t0 = (b + j) * kMoveTiles;
+            const uint32_t t0 = (b + j) * kEmitTiles;
             uint32_t br = 0;
-            const uint32_t xj = emit_chunk4(f4, row, nseg, ntiles, t0, min(ntiles, t0 + kMoveTiles), Sj,
+            const uint32_t xj = emit_chunk4(f4, row, nseg, ntiles, t0, min(ntiles, t0 + kEmitTiles), Sj,
                                             ent, orow, lb, lane, br, wide);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) br += (uint32_t)__shfl_xor((int)br, o, 64);
@@ -4161,7 +4166,7 @@ void launch_rle_fix(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t*
 
 uint32_t rle_emit_chunks(uint32_t npad) {
     const uint32_t ntiles = npad / kern::kTile;
-    return (ntiles + kern::kMoveTiles - 1u) / kern::kMoveTiles;
+    return (ntiles + kern::kEmitTiles - 1u) / kern::kEmitTiles;
 }
 
 void launch_rle_emit(const uint32_t* fm, uint32_t npad, uint32_t nrows, const uint32_t* out_row,
