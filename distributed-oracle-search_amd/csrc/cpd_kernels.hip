@@ -4175,8 +4175,11 @@ void launch_rle_emit(const uint32_t* fm, uint32_t npad, uint32_t nrows, const ui
     if (!nrows) return;
     const kern::EmitChunks ck{xe, xs, cc};
     static const uint32_t wide = env_u32("CPD_EMIT_WIDE", 1) ? 1u : 0u;  // 16-B table stores
-    launch(kern::rle_emit4, dim3(rle_emit_chunks(npad), (nrows + 3u) / 4u), dim3(256), s, fm, npad,
-           nrows, out_row, lb, dense, ck, wide);
+    // CPD_EMIT_LDS (A/B): extra LDS per workgroup, capping the emit's
+    // workgroups per CU so that it takes less from the sweeps beside it
+    static const uint32_t xlds = env_u32("CPD_EMIT_LDS", 0);
+    launch_shm(kern::rle_emit4, dim3(rle_emit_chunks(npad), (nrows + 3u) / 4u), dim3(256), xlds, s,
+               fm, npad, nrows, out_row, lb, dense, ck, wide);
     launch(kern::rle_emit_fix, dim3(nrows), dim3(64), s, fm, npad, nrows, out_row, lb, dense, ck,
            counts, wide);
 }
