@@ -4402,7 +4402,10 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     static const uint32_t lpw_min = std::max(8u, std::min(64u, env_u32("CPD_SEARCH_LPW_MIN", 8)));
     // (the fewest lanes, a multiple of 8, at which the slots' waves still fit
     // one per SIMD: 1024 one-wave workgroups)
-    const uint32_t fit = (uint32_t)(((uint64_t)slots + 1023u) / 1024u);
+    // (CPD_SEARCH_RESIDENT, A/B: more waves than SIMDs queue behind the
+    // resident ones)
+    static const uint32_t resident = std::max(64u, env_u32("CPD_SEARCH_RESIDENT", 1024));
+    const uint32_t fit = (uint32_t)(((uint64_t)slots + resident - 1u) / resident);
     const uint32_t lpw = std::max(lpw_min, std::min(64u, (fit + 7u) / 8u * 8u));
     const uint32_t waves = slots / lpw;  // waves x lpw <= slots workspaces
     char* p = static_cast<char*>(ws);
