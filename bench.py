@@ -361,6 +361,9 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": round(t["bytes_per_launch"], 1) if t else None,
                 "traffic_unit": "bytes/launch (PMC: 2*FETCH_SIZE + WRITE_SIZE, KiB->B)",
+                "traffic_scope": ("rank 0's GPU, one step of its own targets (every rank "
+                                  "builds the same batch shape)" if world > 1 else "this GPU")
+                if t else "not collected (--no-pmc, no rocprofv3, or a shared-GPU rehearsal)",
                 "launches": k["launches"],
                 "avg_launch_us": round(k["ms"] * 1e3 / max(1, k["launches"]), 3),
                 "bytes_per_launch": round(k["bytes"] / max(1, k["launches"]), 1)}
@@ -400,6 +403,8 @@ def assemble(args, world, graph_info, B, elapsed_max, q_totals, q_ms_max, nrows,
         # narrow distance rows: 256-target groups kept wide (u32) / all groups
         "narrow_rows": {"wide_groups": (kt or {}).get("wide_rows", {}).get("launches"),
                         "groups": (kt or {}).get("group_rows", {}).get("launches")},
+        # first-move buffer sets the emit overlap rotates through (libcpd kSets)
+        "emit_sets": (kt or {}).get("emit_sets", {}).get("launches"),
         "hierarchy": {"arcs": pinfo["ch_up_arcs"] + pinfo["ch_dn_arcs"],
                       "levels": [pinfo["levels_up"], pinfo["levels_dn"]],
                       "build_s": round(pinfo["ch_seconds"], 2),
@@ -432,7 +437,7 @@ def step_pmc(traffic, step_s):
 
 
 # libcpd reports these counters through the timing table (launches = count)
-_COUNTERS = ("wide_rows", "group_rows")
+_COUNTERS = ("wide_rows", "group_rows", "emit_sets")
 
 
 # --------------------------------------------------------------------------
@@ -865,6 +870,15 @@ def serve_leg(args, xy, outdir, W, device, g, order, threads, nprobe=4, big=1_00
                          "t_search_s": st2["t_search_s"],
                          "queries_per_s_search": round(search_q / st2["t_search_s"], 1)
                          if st2["t_search_s"] else None,
+                         # t_search = the passes + the per-row tables (round 5
+                         # on; t_receive excluded), t_astar = the passes only
+                         # (ADVICE r05): the receive-inclusive rate compares
+                         # with round-4 records
+                         "queries_per_s_receive_and_search":
+                             round(search_q / (st2["t_receive_s"] + st2["t_search_s"]), 1)
+                             if st2["t_search_s"] else None,
+                         "t_search_definition": "t_search = search passes + per-row tables "
+                                                "(t_receive not included); t_astar = passes",
                          "finished": st2["finished"], "mean_expanded": round(st2["n_expanded"] / search_q, 1),
                          "answer": sline, "phases": sreqs[-1] if sreqs else None}
     return out
@@ -966,17 +980,20 @@ def main():
     fb_xy = None
     if not args.no_full_build and args.sample is None and local == 0:
         fb_xy = full_build_xy(args)
-    # PMC passes: children, before this process initialises the GPU
-    traffic = None
-    if world == 1 and not args.no_pmc:
-        traffic = pmc_traffic(args)
-
+    # PMC passes: children, before this process initialises the GPU.  At N > 1
+    # on rank 0 only, on its own GPU (device 0 = local rank 0's), while the
+    # other ranks wait in the process group's rendezvous: every rank builds
+    # the same shape of batch, so rank 0's bytes per launch stand for all
+    # (an N > 1 roofline says where its traffic is from)
     # CPD_BENCH_SHARE_GPU=1 (rehearsal on a 1-GPU box only): every rank uses
     # GPU 0 and the harness collectives go over gloo.  Never used for numbers.
     share = os.environ.get("CPD_BENCH_SHARE_GPU") == "1"
     gpu = 0 if share else local
     if share and args.batch == 0:  # ranks sized from one card's free HBM would overcommit it
         args.batch = 4096
+    traffic = None
+    if rank == 0 and local == 0 and not args.no_pmc:
+        traffic = pmc_traffic(args)
     # CPD_BENCH_PG=1: the process group (RCCL) even at one rank, so the N>1
     # collectives' code path runs on a 1-GPU box too
     use_pg = world > 1 or os.environ.get("CPD_BENCH_PG") == "1"
@@ -1162,21 +1179,35 @@ def main():
                     "passes": int(stt["passes"]), "reruns": int(stt["reruns"]),
                     "resumed": int(stt["resumed"]), "restarted": int(stt["restarted"]),
                     "wasted_expanded": int(stt["wasted_expanded"])}
-        search = {"queries_per_s": round(tot[0] / (smax / 1e3), 1) if smax else 0.0,
-                  "config": "256-row dense index, .diff stand-in weights, hscale 1, fscale 0.1, "
-                            "library workspace policy",
-                  "queries": sq, "mean_expanded": round(float(scnt[:, 0].mean()), 1),
-                  "finished": int(sfin.sum()), "overflow": int(sst["overflow"]),
-                  "kernel_ms": round(sst["kernel_ms"], 3), "lanes": int(sst["lanes"]),
-                  **passes(sst),
-                  "form": {1: "per-row tables", 2: "memoised walks"}[sst["tables"]],
-                  "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
+        # the headline is the memoised-walk form: what a
+        # worker-sized index runs (fifo_auto; per-row tables of a div-8
+        # worker's 125k rows would need 2.5 PB); the per-row tables form,
+        # which only a small index holds, is reported beside it
+        tables_form = {"queries_per_s": round(tot[0] / (smax / 1e3), 1) if smax else 0.0,
+                       "queries": sq, "mean_expanded": round(float(scnt[:, 0].mean()), 1),
+                       "finished": int(sfin.sum()), "overflow": int(sst["overflow"]),
+                       "kernel_ms": round(sst["kernel_ms"], 3), "lanes": int(sst["lanes"]),
+                       **passes(sst),
+                       "form": {1: "per-row tables", 2: "memoised walks"}[sst["tables"]],
+                       "tables_ms_per_row": round(wst["tables_ms"] / len(srows), 3)}
         # fscale 0 (optimal under the .diff weights): a 1M-node search expands
         # ~49k nodes; 65536 searches start at once in 2^15-column workspaces
         # and the ~60% that outgrow them spill their state and resume at 2^17
         # (then 2^19): each search is a latency chain, so lanes buy throughput
         # (profiles/search_lanes_ab/).  Ranks sharing one card in a rehearsal
         # split its HBM.
+        # the fscale-0.1 queries with the memoised-walk form: the headline
+        _, _, wfin, wcnt, wsst = six.search(ss, st_, fscale=0.1, tables="walks")
+        wtot = comm.reduce([float(sq)], "SUM")
+        (wmax,) = comm.reduce([wsst["kernel_ms"]], "MAX")
+        search = {"queries_per_s": round(wtot[0] / (wmax / 1e3), 1) if wmax else 0.0,
+                  "form": "memoised walks (what a worker-sized index runs)",
+                  "config": "256-row dense index, .diff stand-in weights, hscale 1, fscale 0.1, "
+                            "library workspace policy",
+                  "queries": sq, "mean_expanded": round(float(wcnt[:, 0].mean()), 1),
+                  "finished": int(wfin.sum()), "overflow": int(wsst["overflow"]),
+                  "kernel_ms": round(wsst["kernel_ms"], 3), "lanes": int(wsst["lanes"]),
+                  **passes(wsst), "tables_form": tables_form}
         zq = 65536
         zs = rng.integers(0, g.n, zq).astype(np.uint32)
         zt = srows[rng.integers(0, len(srows), zq)]
@@ -1186,6 +1217,7 @@ def main():
         (zmax,) = comm.reduce([zst["kernel_ms"]], "MAX")
         search["fscale0"] = {
             "queries_per_s": round(ztot[0] / (zmax / 1e3), 1) if zmax else 0.0,
+            "form": {1: "per-row tables", 2: "memoised walks"}[zst["tables"]],
             "queries": zq, **passes(zst), "lanes": int(zst["lanes"]),
             "mean_expanded": round(float(zcnt[:, 0].mean()), 1),
             "finished": int(zfin.sum()), "overflow": int(zst["overflow"]),
@@ -1193,13 +1225,7 @@ def main():
             # per-lane latency: one search's expansions in series
             "us_per_expansion_per_lane": round(zst["kernel_ms"] * 1e3 * int(zst["lanes"]) /
                                                max(1.0, float(zcnt[:, 0].sum())), 2)}
-        # the fscale-0.1 queries with the memoised-walk form (what a
-        # worker-sized index, whose tables do not fit, runs)
-        _, _, _, _, wsst = six.search(ss, st_, fscale=0.1, tables="walks")
-        search["walks_form"] = {
-            "queries": sq, "lanes": int(wsst["lanes"]), "fscale": 0.1, **passes(wsst),
-            "queries_per_s": round(sq / (wsst["kernel_ms"] / 1e3), 1) if wsst["kernel_ms"]
-            else 0.0}
+
         search_sample = (six, ss[:2000], st_[:2000], srows, ss, st_, zs, zt)
     # walk kernel vs its roofline: per query 8 (s, t) + 4 (row) + 13 (cost,
     # moves, flag) bytes, per move the 4-B word holding the move + the 8-B edge
@@ -1270,6 +1296,8 @@ def main():
                                             "targets_npy": snpy, "legs": spec_legs}, threads))
                 legs = [r["fscale0.1"], r["fscale0"]]
                 gpu_q = (search["queries_per_s"], search["fscale0"]["queries_per_s"])
+                # (the GPU's fscale-0.1 figure is the walks form; the oracle
+                # walks its rows' runs the same way, memo included)
                 search["cpu_baseline"] = {
                     "kind": "port", "cores": threads,
                     "what": "oracle ora_cpd_search (restated cpd_search, OpenMP over queries) in "
@@ -1309,6 +1337,9 @@ def main():
                          f"child process, {leg['rows_s']:.1f}s); table-search {cq} queries over "
                          f"them in {leg['queries_s']:.2f}s",
                "queries_per_s": round(leg["queries"] / leg["queries_s"], 1),
+               "queries_form": "RLE rows, get_move by binary search over each row's runs (the "
+                               "oracle's walk) — the GPU's queries_per_s walks dense move "
+                               "tables, queries_per_s_rle the same RLE rows",
                "host": host_info(threads)}
         if not args.no_cpu_partitioned:
             try:

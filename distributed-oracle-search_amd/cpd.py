@@ -53,7 +53,7 @@ EXPORTED = [
     "cpd_rows_lanes", "cpd_graph_hint_next", "cpd_graph_set_hbm_reserve",
     "cpd_device_mem_info", "cpd_rows_move_words", "cpd_rows_export_moves",
     "cpd_index_append_moves", "cpd_device_arena", "cpd_device_arena_release", "cpd_batch_bytes",
-    "cpd_rows_move_bits", "cpd_graph_move_bits",
+    "cpd_rows_move_bits", "cpd_graph_move_bits", "cpd_bucket_bytes", "cpd_space_check",
 ]
 # generator styles (cpd_synth_road_graph_ex flags): "shuffled" is round 1's
 # graph (ids permuted, one-way streets, out-edge order shuffled); "spec" is
@@ -200,6 +200,22 @@ def owned_nodes(nodenum: int, maxworker: int, method: str, key: int, wid: int) -
     else:
         raise ValueError("partmethod must be div or mod")
     return nodes[(bid % maxworker) == wid].astype(np.uint32)
+
+
+def bucket_bytes(n: int, bits: int, nrows: int, nbuckets: int = 1, stripes: int = 16) -> int:
+    """Bytes of a worker's compact bucket files (cpd_bucket_bytes)."""
+    out = C.c_uint64()
+    _check(lib.cpd_bucket_bytes(C.c_uint32(n), C.c_uint32(bits), C.c_uint64(nrows),
+                                C.c_uint32(nbuckets), C.c_uint32(stripes), C.byref(out)))
+    return out.value
+
+
+def space_check(directory: str, nbytes: int) -> int:
+    """Free bytes of the file system holding `directory`; CpdError (CPD_E_IO)
+    when fewer than `nbytes` (cpd_space_check: make_cpd_auto's preflight)."""
+    avail = C.c_uint64()
+    _check(lib.cpd_space_check(directory.encode(), C.c_uint64(nbytes), C.byref(avail)))
+    return avail.value
 
 
 def dfs_preorder(row_ptr, dst) -> np.ndarray:

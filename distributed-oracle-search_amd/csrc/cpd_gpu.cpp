@@ -169,11 +169,6 @@ uint32_t batch_max() {
     return v;
 }
 
-// HBM per row of batch width: dist 4n (+ 2n narrow) + two buffer sets of
-// first-move rows and RLE segment states (emit overlap) + the chunked count's
-// chunk states (12 B per chunk: exit, count, entry) + leaf sets + two rows of move tables (npad / 2
-// each: the row set being built and the one a caller such as make_cpd_auto
-// is exporting).
 // CPD_RLE_FUSED=0: the count / seam repair / emit passes instead of the
 // fused one-pass emit (4-bit sets; A/B, identical rows)
 bool rle_fused_on() {
@@ -184,53 +179,60 @@ bool rle_fused_on() {
     return on;
 }
 bool rle_fused(uint32_t fmb) { return fmb == 4 && rle_fused_on(); }
-// CPD_CU_RESERVE=q (1..7, A/B): q CUs of every 8 kept free of the main and
-// emit streams' kernels for the high-priority up-sweep stream, spread over
-// every XCD whichever way the mask's bit order maps to XCDs (bit i reserved
-// when (i - i/32) mod 8 < q); CPD_CU_RESERVE_MAIN=0 masks the emit stream only.
-uint32_t cu_reserve() {
+bool up_persist_on();
+// chunked up levels of at most this many chunk items run together in one
+// persistent launch (larger ones fill the GPU as launches of their own)
+constexpr uint32_t kPersistItems = 256;
+
+// CPD_UP_CUS = q (0..4): q of every 8 CUs kept for the up-sweep stream, the
+// rest for the main and emit streams (0: no masks).  Bit i of a mask is CU
+// i; the reserved set is spread over every XCD whichever way the bit order
+// maps to XCDs (CU i reserved when (i - i / 32) mod 8 < q).
+uint32_t up_cus() {
     static const uint32_t v = [] {
-        const char* e = std::getenv("CPD_CU_RESERVE");
+        const char* e = std::getenv("CPD_UP_CUS");
         const unsigned long q = e && *e ? std::strtoul(e, nullptr, 10) : 0ul;
-        return (uint32_t)std::min(q, 7ul);
+        return (uint32_t)std::min(q, 4ul);
     }();
     return v;
 }
-void create_stream_masked(hipStream_t* st, uint32_t q, int ncu) {
+void create_cu_stream(hipStream_t* st, uint32_t q, int ncu, bool reserved) {
     if (!q || ncu <= 0) {
         HIP_CHECK(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
         return;
     }
     std::vector<uint32_t> mask(((size_t)ncu + 31) / 32, 0u);
     for (int i = 0; i < ncu; ++i)
-        if ((uint32_t)((i - i / 32) & 7) >= q) mask[(size_t)i / 32] |= 1u << (i % 32);
+        if (((uint32_t)((i - i / 32) & 7) < q) == reserved) mask[(size_t)i / 32] |= 1u << (i % 32);
     HIP_CHECK(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
 }
-bool rows_nibble() {  // CPD_ROWS_NIBBLE=1: built rows as nibble tables (A/B)
-    static const bool on = [] {
-        const char* e = std::getenv("CPD_ROWS_NIBBLE");
-        return e && *e == '1';
-    }();
-    return on;
-}
-bool emit_defer_on() {  // CPD_EMIT_DEFER=1: emit deferred past the next batch's sweeps (A/B)
-    static const bool on = [] {
-        const char* e = std::getenv("CPD_EMIT_DEFER");
-        return e && *e == '1';
-    }();
-    return on;
+
+// Pool rows (1 KiB: one 256-target group row kept 32-bit) of a narrow batch
+// of B targets: an eighth of its group rows, and at least every group row of
+// one 1024-target slab, so that a batch whose wide rows overflow the pool is
+// rebuilt in pieces of pool_cap / (4 n) slabs that cannot.
+uint64_t pool_rows(uint32_t n, uint32_t B) {
+    return std::max<uint64_t>((uint64_t)n * (B / 256u) / 8u, 4ull * n);
 }
 
-double batch_bytes_per_row(uint32_t n, uint32_t npad, uint32_t fmb, bool narrow, bool leaf_fm,
-                           uint32_t mbits) {
+// HBM per row of batch width: the final rows (narrow: 2n of u16 offsets, the
+// bases and the wide-row pool; else 4n of u32) + two compact up stores (4 B
+// per node of up-level >= 2 each: batch k + 1's up-sweep runs beside batch
+// k's down-sweep) + three buffer sets of first-move rows and RLE segment states
+// (emit overlap) + the chunked count's chunk states (12 B per chunk: exit,
+// count, entry) + leaf sets + two rows of move tables (npad / 2 each: the
+// row set being built and the one a caller such as make_cpd_auto is
+// exporting).  The pool's 1024-row floor is in the fixed part (pool_rows).
+double batch_bytes_per_row(uint32_t n, uint32_t n_up, uint32_t npad, uint32_t fmb, bool narrow,
+                           bool leaf_fm, uint32_t mbits) {
     // the fused emit keeps no segment states: 12 B per chunk of 32k columns
     const double rle = rle_fused(fmb) ? 12.0 * rle_emit_chunks(npad)
-                                      : 2.0 * 5.0 / 32.0 * npad +
+                                      : 3.0 * 5.0 / 32.0 * npad +
                                             (fmb == 4 ? 12.0 * rle_count_chunks(npad) : 0.0);
-    return (narrow ? 6.0 : 4.0) * n + 2.0 * fmb / 8.0 * npad + rle + (leaf_fm ? 0.5 * n : 0.0) +
+    const double fin = narrow ? (2.0 + 4.0 / 256.0 + 0.5) * n : 4.0 * n;
+    return fin + 8.0 * n_up + 3.0 * fmb / 8.0 * npad + rle + (leaf_fm ? 0.5 * n : 0.0) +
            2.0 * mbits / 8.0 * npad;
 }
-bool up_priority_on();
 bool lane_key_on();
 bool seg_order_on();
 bool search_trace();
@@ -283,25 +285,35 @@ struct cpd_graph {
     // column's out-list (wildcard runs take bit 0), so out-degrees <= 2^bits
     uint32_t move_bits = 4;
     // the move tables in HBM (built rows, dense indexes) at the same width:
-    // 2^tlb bits per column (CPD_TABLE_BITS=4: nibble tables whatever the
-    // degree, the round-4 layout, for A/B)
+    // 2^tlb bits per column
     uint32_t tlb = 2;
+    // dist: the dense final rows (narrow rows off only); counts: run counts
     DevBuf<uint32_t> dist, counts;
+    // The compact up stores, one per batch slot (see BatchSlot): up[u][B],
+    // u = ascending slot - ubase for the n_up nodes of up-level >= 2, their
+    // live masks and the batch's target masks.
+    uint32_t ubase = 0, n_up = 0;
+    DevBuf<uint32_t> upx[2], livex[2], tmaskx[2];
+    DevBuf<uint32_t> dsc_up;  // descending slot -> up index (~0: closed form)
     // Emit overlap (CPD_ASYNC, default on): a batch's move-table emit
     // (rle_moves) runs on `estream` while the next batch's sweeps start on
     // `stream` — the sweeps' narrow, latency-bound levels overlap the emit.
     // The buffers the emit reads (first-move rows, RLE segment states, lane ->
-    // row map) are doubled: set x serves every other batch and is reused only
-    // after the emit that read it (ev_emit[x]) has finished.
+    // row map) come in up to kSets sets used round robin: set x is reused
+    // only after the emit that read it (ev_emit[x]) has finished.  Three
+    // sets give an emit two steps to finish: it runs at low occupancy beside
+    // the sweeps, and with two sets the next-but-one batch's first moves
+    // waited ~16 ms per step for it (profiles/up_store_ab/, round 6).
+    static constexpr uint32_t kSets = 3;
     hipStream_t estream = nullptr;
     bool async = false;
-    uint32_t cur = 0;
-    hipEvent_t ev_emit[2] = {nullptr, nullptr};
-    bool emit_pending[2] = {false, false};
-    DevBuf<uint32_t> fmx[2];      // [B][npad] fmb-bit sets
-    DevBuf<uint32_t> rle_stx[2];  // [B][npad/32] RLE segment entry states
-    DevBuf<uint8_t> rle_rcx[2];   // [B][npad/32] runs ending in each segment
-    DevBuf<uint32_t> lane_rowx[2];  // [B] table row of each batch lane
+    uint32_t nsets = 1, cur = 0;
+    hipEvent_t ev_emit[kSets] = {nullptr, nullptr, nullptr};
+    bool emit_pending[kSets] = {false, false, false};
+    DevBuf<uint32_t> fmx[kSets];      // [B][npad] fmb-bit sets
+    DevBuf<uint32_t> rle_stx[kSets];  // [B][npad/32] RLE segment entry states
+    DevBuf<uint8_t> rle_rcx[kSets];   // [B][npad/32] runs ending in each segment
+    DevBuf<uint32_t> lane_rowx[kSets];  // [B] table row of each batch lane
     // chunk exit states / run counts of the chunked count (read by rle_fix on
     // the same stream before the next batch: one set)
     DevBuf<uint32_t> rle_xs, rle_cc, rle_hard;
@@ -309,32 +321,18 @@ struct cpd_graph {
     HostBuf<uint32_t> rle_hard_h;          // [1]
     // the buffer set the next batch uses, once the emit that last read it is done
     uint32_t acquire_set() {
-        const uint32_t x = async ? cur : 0u;
-        if (async) cur ^= 1u;
+        const uint32_t x = cur;
+        cur = (cur + 1u) % nsets;
         if (emit_pending[x]) {
             HIP_CHECK(hipStreamWaitEvent(stream, ev_emit[x], 0));
             emit_pending[x] = false;
         }
         return x;
     }
-    // A batch's emit (count + move tables, emit stream) deferred until the
-    // next batch's down-sweep is queued, so that it runs beside that batch's
-    // first moves instead of beside its up-sweep's latency-bound narrow
-    // levels (profiles/r05e traces: the emit there stretched them 3x and the
-    // down-sweep waited).  flush_emit launches it (gated on `gate` when
-    // given); every reader of the rows, a rebuild, a sync and the graph's
-    // end flush first.  Opt-in (CPD_EMIT_DEFER=1): measured neutral, r05h.
-    std::mutex emit_mu;
-    std::function<void()> pend_emit;
-    cpd_rows* pend_rows = nullptr;
-    void flush_emit(hipEvent_t gate = nullptr);
     void drain_emits() {
-        flush_emit();
         if (estream) HIP_CHECK(hipStreamSynchronize(estream));
-        emit_pending[0] = emit_pending[1] = false;
+        for (auto& p : emit_pending) p = false;
     }
-    DevBuf<uint32_t> live;   // [col] slab mask of the up-sweep rows stored
-    DevBuf<uint32_t> tmask;  // [col] slab mask of the batch's targets
     // leaf first moves from the down-sweep (4-bit sets only): leafbits[col/32]
     // bit = column is a CH leaf; fmleaf [col][B/4] u16 = its sets, 4 per lane
     bool leaf_fm = false;
@@ -342,7 +340,8 @@ struct cpd_graph {
     DevBuf<uint16_t> fmleaf;
     // narrow final-distance rows (NarrowRows, cpd_kernels.hpp): on unless
     // CPD_NARROW=0 at graph creation or a finite distance could reach the
-    // wide-row marker; group rows that do not fit are kept wide (counted)
+    // wide-row marker; group rows that do not fit are kept wide in the pool
+    // (counted: ovf)
     bool narrow = false;
     // the first kNarrowProbe full batches count their wide group rows; if
     // most are wide (long edges: the spread of 256 distances passes 0xFFFF),
@@ -353,19 +352,22 @@ struct cpd_graph {
     HostBuf<uint32_t> ovf_hb;  // [1] wide group rows of the last down-sweep
     uint32_t ovf_h() const { return ovf_hb.p ? ovf_hb.p[0] : 0u; }
     DevBuf<uint16_t> d16;
-    DevBuf<uint32_t> dbase, ovf;
+    DevBuf<uint32_t> dbase, ovf, pool;
+    uint32_t pool_cap = 0;
     NarrowRows narrow_rows(bool on) {
-        if (!on) return NarrowRows{nullptr, nullptr, n, nullptr};
-        return NarrowRows{d16.p, dbase.p, n, ovf.p};
+        if (!on) return NarrowRows{nullptr, nullptr, n, nullptr, nullptr, 0};
+        return NarrowRows{d16.p, dbase.p, n, ovf.p, pool.p, pool_cap};
     }
     double n_leaf = 0, m_leaf = 0;    // leaves, their out-edges
     std::vector<double> dsc_lvl_leaves;
-    // Per-batch state, two slots: a batch's up-sweep may run (on ustream)
-    // while the previous batch's first moves still read their own targets.
-    // tgt: the batch's target columns by lane; pos_of[i] = lane of the
-    // caller's target i; stat: per-level sweep counters (timing runs; 2 per
-    // launch: stored / own rows, gathered rows), stat_h its host copy;
-    // up_late: (level, arcs, nodes) of the up levels whose bytes wait for it.
+    // Per-batch state, two slots (batches alternate): a batch's up-sweep runs
+    // (on ustream) while the previous batch's down-sweep reads the other
+    // slot's up store.  tgt: the batch's target columns by lane; pos_of[i] =
+    // lane of the caller's target i; stat: per-level sweep counters (timing
+    // runs; 2 per launch: stored / own rows, gathered rows), stat_h its host
+    // copy; up_late: (level, arcs, nodes) of the up levels whose bytes wait
+    // for it.  ev_fm[slot] marks the end of the slot's batch (its first moves
+    // are the last reader of its targets, up store and stats).
     struct BatchSlot {
         DevBuf<uint32_t> tgt;
         std::vector<uint32_t> pos_of, tgt_col;
@@ -375,14 +377,24 @@ struct cpd_graph {
         std::vector<std::array<double, 3>> up_late;
     };
     BatchSlot bs[2];
+    // Timing runs: a batch's sweep bytes that depend on its live-row counts
+    // (stat_h, copied out after its first moves), folded into agg once those
+    // have landed — at the end of the next batch, or at timing_get / reset.
+    // up: (level, arcs, nodes) per up level; down: (stat index, known bytes).
+    struct LateRec {
+        uint32_t slot = 0;
+        std::vector<std::array<double, 3>> up;
+        std::vector<std::array<double, 2>> down;
+    };
+    std::vector<LateRec> late_q;
     uint32_t next_slot = 0;
-    // Early up-sweep of the next batch: build_batch
-    // launches it on ustream once the current batch's down-sweep is done, so
-    // it runs beside that batch's first moves and RLE count.  prep: the slot
-    // and targets it was launched for, ev_up its end.
+    // Early up-sweep of the next batch:
+    // build_batch launches it on ustream right after queueing the current
+    // batch's down-sweep, into the other slot's up store, so it runs beside
+    // that down-sweep.  prep: the slot and targets it was launched for, ev_up
+    // its end.
     hipStream_t ustream = nullptr;
-    hipEvent_t ev_up = nullptr, ev_down = nullptr, ev_fm = nullptr;
-    hipEvent_t ev_uph = nullptr;  // the early up-sweep's head (CPD_UP_HEAD)
+    hipEvent_t ev_up = nullptr, ev_down = nullptr, ev_fm[2] = {nullptr, nullptr};
     bool prepped = false;
     uint32_t prep_slot = 0;
     std::vector<uint32_t> prep_targets, hint;
@@ -393,10 +405,13 @@ struct cpd_graph {
     DevBuf<uint32_t> asc_lvl_of, dsc_lvl_of;  // slot -> level
     // narrow upward levels (<= kNarrow nodes) run chunked: per level l,
     // items [up_item_first[l], up_item_first[l+1]) of (slot, a0, a1, 0);
-    // up_init_cols = the columns of all their nodes (leaf-form init)
+    // up_init_slots = the ascending slots of all their nodes (leaf-form init)
     std::vector<uint32_t> up_item_first;
-    DevBuf<uint32_t> up_items, up_init_cols;
-    uint32_t n_init_cols = 0;
+    DevBuf<uint32_t> up_items, up_init_slots;
+    // the same offsets on the device, and per batch slot the persistent
+    // narrow-level launch's barrier counters (one per slab)
+    DevBuf<uint32_t> up_item_first_d, ubar[2];
+    uint32_t n_init_slots = 0;
     // lane position of each caller target in the current batch (sorted by
     // lane_key when the caller gave coordinates, else by column)
     std::vector<uint32_t> lane_key;  // node -> Hilbert key of its coordinates (may be empty)
@@ -411,16 +426,12 @@ struct cpd_graph {
 
     ~cpd_graph() {
         if (hipSetDevice(device) == hipSuccess) {
-            try {
-                flush_emit();
-            } catch (...) {
-            }
             if (estream) (void)hipStreamSynchronize(estream);
             for (auto e : ev_emit)
                 if (e) (void)hipEventDestroy(e);
             if (estream) (void)hipStreamDestroy(estream);
             if (ustream) (void)hipStreamSynchronize(ustream);
-            for (auto e : {ev_up, ev_down, ev_fm, ev_uph})
+            for (auto e : {ev_up, ev_down, ev_fm[0], ev_fm[1]})
                 if (e) (void)hipEventDestroy(e);
             if (ustream) (void)hipStreamDestroy(ustream);
             if (stream) (void)hipStreamSynchronize(stream);
@@ -541,9 +552,11 @@ struct cpd_graph {
             // 24 slabs.  Larger batches amortise the latency-bound
             // narrow levels: at 1M nodes 20480 rows per batch measured 310.5k
             // rows/s against 296.1k for 16384 (round 2).
-            const double per = batch_bytes_per_row(n, npad, fmb, narrow, leaf_fm,
-                                                   rows_nibble() ? 4u : 1u << tlb);
-            const double avail = free_b > hbm_reserve ? (double)(free_b - hbm_reserve) : 0.0;
+            const double per = batch_bytes_per_row(n, n_up, npad, fmb, narrow, leaf_fm,
+                                                   1u << tlb);
+            const double fixed = narrow ? 4096.0 * n : 0.0;  // the pool's floor (pool_rows)
+            const double avail = free_b > hbm_reserve + fixed ? (double)free_b - hbm_reserve - fixed
+                                                              : 0.0;
             const double fit = 0.85 * avail / per;
             CPD_REQUIRE(hbm_reserve == 0 || fit >= 1024.0, CPD_E_OOM,
                         "HBM reserve of " + std::to_string(hbm_reserve >> 20) + " MiB leaves " +
@@ -551,29 +564,37 @@ struct cpd_graph {
             want = (uint32_t)std::min((double)batch_max(), std::max(1024.0, std::floor(fit / 1024) * 1024));
         }
         want = (want + 1023u) / 1024u * 1024u;
-        if (want == B && dist.p) return;
+        if (want == B && upx[0].p) return;
         drain_emits();
         drop_prep();
         B = want;
-        dist.alloc((size_t)n * B);
-        // the second buffer set when it takes under an eighth of the HBM
-        // still free after the batch's own buffers (else one set: emits do
-        // not overlap)
+        for (int s = 0; s < 2; ++s) {
+            upx[s].alloc(std::max<size_t>((size_t)n_up * B, 1));
+            livex[s].alloc(std::max<uint32_t>(n_up, 1u));
+            tmaskx[s].alloc(n);
+        }
+        alloc_final_rows();
+        // each further buffer set when it takes under an eighth of the HBM
+        // still free after the batch's own buffers (one set: emits do not
+        // overlap)
         const bool fused = rle_fused(fmb);
         const size_t set_bytes = (size_t)B * (npad / (32u / fmb)) * 4u +
                                  (fused ? 0u : (size_t)B * (npad / 32u) * 5u) + 4u * B;
-        for (int x = 0; x < 2; ++x) {
-            if (x == 1) {
+        nsets = 1;
+        for (uint32_t x = 0; x < kSets; ++x) {
+            if (x >= 1) {
                 size_t free_b = 0, total_b = 0;
                 HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-                async = async_on() && set_bytes * 8 < (free_b > hbm_reserve ? free_b - hbm_reserve : 0);
-                if (!async) {
-                    fmx[1].release();
-                    rle_stx[1].release();
-                    rle_rcx[1].release();
-                    lane_rowx[1].release();
+                if (!(async_on() && set_bytes * 8 < (free_b > hbm_reserve ? free_b - hbm_reserve : 0))) {
+                    for (uint32_t y = x; y < kSets; ++y) {
+                        fmx[y].release();
+                        rle_stx[y].release();
+                        rle_rcx[y].release();
+                        lane_rowx[y].release();
+                    }
                     break;
                 }
+                nsets = x + 1;
             }
             fmx[x].alloc((size_t)B * (npad / (32u / fmb)));
             if (fused) {
@@ -585,6 +606,7 @@ struct cpd_graph {
             }
             lane_rowx[x].alloc(B);
         }
+        async = nsets > 1;
         cur = 0;
         if (fused) {
             emit_ck.alloc(3ull * B * rle_emit_chunks(npad));
@@ -593,14 +615,7 @@ struct cpd_graph {
             rle_cc.alloc((size_t)B * rle_count_chunks(npad));
             rle_hard.alloc(1);
         }
-        live.alloc(n);
-        tmask.alloc(n);
         if (leaf_fm) fmleaf.alloc((size_t)n * (B / 4u));
-        if (narrow) {
-            d16.alloc((size_t)n * B);
-            dbase.alloc((size_t)n * (B / 256u));
-            ovf.alloc(1);
-        }
         for (auto& b : bs) {
             b.tgt.alloc(B);
             b.tgt_h.alloc(B);
@@ -610,6 +625,25 @@ struct cpd_graph {
         ovf_hb.alloc(1);
         ovf_hb.p[0] = 0;
     }
+    // The final rows of a batch of B: narrow (u16 offsets, bases, the pool of
+    // wide group rows) or the dense 32-bit rows.
+    void alloc_final_rows() {
+        ArenaScope carve;
+        if (narrow) {
+            dist.release();
+            d16.alloc((size_t)n * B);
+            dbase.alloc((size_t)n * (B / 256u));
+            pool_cap = (uint32_t)std::min<uint64_t>(pool_rows(n, B), 0xFFFFFFFEull);
+            pool.alloc((size_t)pool_cap * 256u);
+            ovf.alloc(1);
+        } else {
+            d16.release();
+            dbase.release();
+            pool.release();
+            pool_cap = 0;
+            dist.alloc((size_t)n * B);
+        }
+    }
 };
 
 struct cpd_rows {
@@ -617,20 +651,10 @@ struct cpd_rows {
     uint32_t nrows = 0;
     mutable uint64_t total = 0;  // runs of all rows (valid after settle())
     hipEvent_t done = nullptr;   // after the last batch's count + emit (emit stream)
-    // the graph holding this rows' last emit deferred (cpd_graph::pend_emit)
-    mutable std::atomic<cpd_graph*> pend_graph{nullptr};
-    void flush() const {
-        if (cpd_graph* g = pend_graph.load()) g->flush_emit();
-    }
     void wait() const {
-        flush();
         if (done) HIP_CHECK(hipEventSynchronize(done));
     }
     ~cpd_rows() {
-        try {
-            flush();
-        } catch (...) {
-        }
         if (done) {
             (void)hipEventSynchronize(done);
             (void)hipEventDestroy(done);
@@ -779,22 +803,10 @@ struct cpd_index {
     DevBuf<unsigned long long> agg;
 };
 
-void cpd_graph::flush_emit(hipEvent_t gate) {
-    std::lock_guard<std::mutex> l(emit_mu);
-    if (!pend_emit) return;
-    std::function<void()> f;
-    f.swap(pend_emit);
-    if (pend_rows) pend_rows->pend_graph.store(nullptr);
-    pend_rows = nullptr;
-    HIP_CHECK(hipSetDevice(device));
-    if (gate && estream) HIP_CHECK(hipStreamWaitEvent(estream, gate, 0));
-    f();  // under the lock: launched before anything that follows a flush
-}
-
 void cpd_rows::settle() const {
     std::lock_guard<std::mutex> l(settle_mu);
     HIP_CHECK(hipSetDevice(device));
-    wait();  // (a deferred emit of these rows is launched first)
+    wait();
     for (auto& b : retired) spare.push_back(std::move(b));
     retired.clear();
     if (pending.empty()) return;
@@ -869,11 +881,14 @@ std::vector<uint32_t> level_order(const cpd_plan& p, const std::vector<uint32_t>
 // (self loops and parallel edges included) instead of its up-arcs — the same
 // minimum, and the list position is the move index for the leaf's first-move
 // set (the down-sweep computes leaf sets, cpd_kernels.hip sweep_down8c).
+// Nodes of up-level >= 2 own a row of the compact up store, u = ascending
+// slot - ubase: ascending arcs into them carry u; uidx (descending only)
+// gets each slot's u (~0 for the closed forms).
 void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& asc_slot,
-                 std::vector<uint32_t>& nodes, std::vector<uint32_t>& off,
+                 uint32_t ubase, std::vector<uint32_t>& nodes, std::vector<uint32_t>& off,
                  std::vector<uint32_t>& arcs, std::vector<uint32_t>& lvl_first,
                  std::vector<double>& lvl_arcs, std::vector<double>& lvl_reads,
-                 bool leaf_edges = false) {
+                 bool leaf_edges = false, std::vector<uint32_t>* uidx = nullptr) {
     const Hierarchy& H = p.ch;
     const uint32_t n = p.n;
     const std::vector<uint32_t>& level = ascend ? H.level_up : H.level_dn;
@@ -894,9 +909,11 @@ void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& as
         return p.order[v];
     };
     nodes.assign(n, 0);
+    if (uidx) uidx->assign(n, 0xFFFFFFFFu);
     for (uint32_t s = 0; s < n; ++s) {
         uint32_t v = node_of_slot[s];
         nodes[s] = ascend ? p.order[v] : ref(v);  // descending: closed-form init
+        if (uidx && lup[v] >= 2) (*uidx)[s] = asc_slot[v] - ubase;
     }
     const bool leaf_rows = !ascend && leaf_edges;  // a leaf's arcs: its out-edges
     off.assign(n + 1, 0);
@@ -928,8 +945,10 @@ void build_sweep(const cpd_plan& p, bool ascend, const std::vector<uint32_t>& as
             for (uint64_t e = aoff[v]; e < aoff[v + 1]; ++e) tmp.push_back({p.order[adst[e]], aw[e]});
             std::sort(tmp.begin(), tmp.end());
             for (auto& a : tmp) {
-                // ascending arcs into upward levels 0/1 use the closed forms
-                const uint32_t r = ascend ? ref(p.inv[a.first]) : a.first;
+                // ascending arcs into upward levels 0/1 use the closed forms,
+                // the others the head's up-store row
+                const uint32_t h = p.inv[a.first];
+                const uint32_t r = !ascend ? a.first : lup[h] >= 2 ? asc_slot[h] - ubase : ref(h);
                 *out++ = r;
                 *out++ = a.second;
                 if (!(r & (kLeafBit | kL1Bit))) la[t][level[v]] += 1.0;
@@ -1031,11 +1050,12 @@ int cpd_batch_bytes(uint32_t n, uint32_t max_degree, uint32_t batch, uint64_t* b
         while ((1u << shift) < std::max(1u, max_degree)) ++shift;
         const uint32_t fmb = fm_bits(shift);
         const uint32_t npad = (n + kFmTile - 1u) / kFmTile * kFmTile;
-        // narrow rows and leaf sets assumed (their upper bound), plus the
-        // per-column arrays and the lane tables
-        const uint32_t mbits = rows_nibble() ? 4u : max_degree <= 2u ? 1u : max_degree <= 4u ? 2u : 4u;
-        *bytes = (uint64_t)(batch_bytes_per_row(n, npad, fmb, true, fmb == 4, mbits) * batch) +
-                 (uint64_t)batch * (n / 256u + 1u) * 4u + 512ull * n + (64ull << 20);
+        // narrow rows and leaf sets assumed, every node with a row in the up
+        // stores (their upper bounds: the hierarchy is not known yet), plus the
+        // pool's floor, the per-column arrays and the lane tables
+        const uint32_t mbits = max_degree <= 2u ? 1u : max_degree <= 4u ? 2u : 4u;
+        *bytes = (uint64_t)(batch_bytes_per_row(n, n, npad, fmb, true, fmb == 4, mbits) * batch) +
+                 (uint64_t)batch * (n / 256u + 1u) * 4u + 4096ull * n + 512ull * n + (64ull << 20);
     });
 }
 
@@ -1052,25 +1072,31 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         auto g = std::make_unique<cpd_graph>();
         g->device = device;
         g->select();
-        {
-            int ncu = 0;
-            HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-            const char* mm = std::getenv("CPD_CU_RESERVE_MAIN");
-            create_stream_masked(&g->stream, (mm && *mm == '0') ? 0u : cu_reserve(), ncu);
-            // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step)
-            create_stream_masked(&g->estream, cu_reserve(), ncu);
-        }
-        // the early up-sweep's stream at the highest priority: its small,
-        // latency-bound level kernels must get CUs while the first moves'
-        // 600k workgroups are queued (at equal priority they waited for all
-        // of them to be dispatched: 15 ms for a 0.7-ms init kernel)
-        {
+        // The up-sweep stream: the next batch's up-sweep runs beside this
+        // batch's down-sweep and first moves.  Its ~150 narrow levels are a
+        // chain of small latency-bound launches: beside the other streams'
+        // large launches each waits for CUs (at the highest priority they
+        // still spanned ~46 ms per step, profiles/up_store_ab/).  With
+        // CPD_UP_CUS = q (1..4), q of every 8 CUs are the up-sweep's own and
+        // the main and emit streams run on the rest (hipExtStreamCreateWithCUMask).
+        const uint32_t q = up_cus();
+        int ncu = 0;
+        HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+        create_cu_stream(&g->stream, q, ncu, false);
+        // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step)
+        create_cu_stream(&g->estream, q, ncu, false);
+        if (q) {
+            create_cu_stream(&g->ustream, q, ncu, true);
+        } else {
+            // the highest priority: its small, latency-bound level kernels
+            // must get CUs while the other streams' workgroups are queued (at
+            // equal priority they waited for all of them to be dispatched:
+            // 15 ms for a 0.7-ms init kernel)
             int least = 0, greatest = 0;
             HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            HIP_CHECK(hipStreamCreateWithPriority(&g->ustream, hipStreamNonBlocking,
-                                                  up_priority_on() ? greatest : least));
+            HIP_CHECK(hipStreamCreateWithPriority(&g->ustream, hipStreamNonBlocking, greatest));
         }
-        for (hipEvent_t* e : {&g->ev_up, &g->ev_down, &g->ev_fm, &g->ev_uph})
+        for (hipEvent_t* e : {&g->ev_up, &g->ev_down, &g->ev_fm[0], &g->ev_fm[1]})
             HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         for (auto& e : g->ev_emit) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (trace_on()) std::fprintf(stderr, "[cpd] graph streams %.3f s\n", now_seconds() - tg0);
@@ -1105,11 +1131,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         while ((1u << g->adj_shift) < maxdeg) ++g->adj_shift;
         g->fmb = fm_bits(g->adj_shift);
         g->move_bits = maxdeg <= 2 ? 1u : maxdeg <= 4 ? 2u : 4u;
-        {
-            const char* tb = std::getenv("CPD_TABLE_BITS");  // 4: nibble tables (A/B)
-            const bool nib = tb && std::strcmp(tb, "4") == 0;
-            g->tlb = nib ? 2u : g->move_bits == 1u ? 0u : g->move_bits == 2u ? 1u : 2u;
-        }
+        g->tlb = g->move_bits == 1u ? 0u : g->move_bits == 2u ? 1u : 2u;
         hipStream_t s = g->stream;
         g->order_d.upload(g->order.data(), n, s);
         g->row_ptr.upload(g->rowc_host.data(), n + 1, s);
@@ -1132,15 +1154,18 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 level_order(*p, p->ch.level_up, p->ch.nlev_up, lvl);
             for (uint32_t s2 = 0; s2 < n; ++s2) asc_slot[node_of_slot[s2]] = s2;
         }
+        // the up store's rows: the nodes of up-level >= 2, in ascending slot order
+        g->ubase = lvl.size() > 2 ? lvl[2] : n;
+        g->n_up = n - g->ubase;
         // the two sweeps' lists are independent host work (~0.1 s each at 1M
         // nodes): the down-sweep's is built on a second thread meanwhile
         g->leaf_fm = g->fmb == 4 && env_on("CPD_LEAFFM");
-        std::vector<uint32_t> dnodes, doff, darcs;
+        std::vector<uint32_t> dnodes, doff, darcs, dup;
         std::exception_ptr derr;
         std::thread dthr([&] {
             try {
-                build_sweep(*p, false, asc_slot, dnodes, doff, darcs, g->dsc_lvl, g->dsc_lvl_arcs,
-                            g->dsc_lvl_reads, g->leaf_fm);
+                build_sweep(*p, false, asc_slot, g->ubase, dnodes, doff, darcs, g->dsc_lvl,
+                            g->dsc_lvl_arcs, g->dsc_lvl_reads, g->leaf_fm, &dup);
             } catch (...) {
                 derr = std::current_exception();
             }
@@ -1151,7 +1176,8 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 if (t.joinable()) t.join();
             }
         } djoin{dthr};
-        build_sweep(*p, true, asc_slot, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs, unused);
+        build_sweep(*p, true, asc_slot, g->ubase, nodes, off, arcs, g->asc_lvl, g->asc_lvl_arcs,
+                    unused);
         g->asc_off_host = off;
         const std::vector<uint32_t> nodes_asc_host = nodes, asc_arcs_host = arcs;
         g->asc_nodes.upload(nodes.data(), nodes.size(), s);
@@ -1169,6 +1195,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         g->dsc_nodes.upload(nodes.data(), nodes.size(), s);
         g->dsc_off.upload(off.data(), off.size(), s);
         g->dsc_arcs.upload(arcs.data(), arcs.size(), s);
+        g->dsc_up.upload(dup.data(), dup.size(), s);
         {
             const uint32_t na = down_desc_arcs();
             std::vector<uint32_t> desc((size_t)n * 32u, 0u);
@@ -1180,6 +1207,7 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 d[0] = nodes[x];
                 d[1] = off[x];
                 d[2] = off[x + 1];
+                d[3] = dup[x];
                 for (uint32_t i = 0; i < na; ++i) {
                     const bool in = off[x] + i < off[x + 1];
                     d[4 + 2 * i] = in ? arcs[2 * (size_t)(off[x] + i)] : 0xFFFFFFFFu;
@@ -1241,23 +1269,25 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 1024u;
             }();
             const uint32_t C = sweep_chunk_arcs();
-            std::vector<uint32_t> items, cols;
+            std::vector<uint32_t> items, slots;
             g->up_item_first.assign(g->asc_lvl.size(), 0);
             for (size_t l = 0; l + 1 < g->asc_lvl.size(); ++l) {
                 g->up_item_first[l] = (uint32_t)(items.size() / 4);
                 const uint32_t s0 = g->asc_lvl[l], s1 = g->asc_lvl[l + 1];
                 if (l < 2 || s1 - s0 > kNarrow) continue;
                 for (uint32_t x = s0; x < s1; ++x) {
-                    cols.push_back(nodes_asc_host[x]);
+                    slots.push_back(x);
                     for (uint32_t a = g->asc_off_host[x]; a < g->asc_off_host[x + 1]; a += C)
                         items.insert(items.end(),
                                      {x, a, std::min(a + C, g->asc_off_host[x + 1]), 0u});
                 }
             }
             g->up_item_first.back() = (uint32_t)(items.size() / 4);
+            g->up_item_first_d.upload(g->up_item_first.data(), g->up_item_first.size(), s);
+            for (auto& b : g->ubar) b.alloc(32u * 4u);  // (slab, quarter) barrier counters
             g->up_items.upload(items.data(), items.size(), s);
-            g->up_init_cols.upload(cols.data(), cols.size(), s);
-            g->n_init_cols = (uint32_t)cols.size();
+            g->up_init_slots.upload(slots.data(), slots.size(), s);
+            g->n_init_slots = (uint32_t)slots.size();
         }
         std::vector<uint32_t> la = lvl_of(g->asc_lvl), ld = lvl_of(g->dsc_lvl);
         g->asc_lvl_of.upload(la.data(), n, s);
@@ -1399,44 +1429,44 @@ bool async_on() {  // CPD_ASYNC=0: every emit finishes before its batch returns
 bool trace_on();
 
 // After a full narrow batch (g->ovf_h = its wide group rows): switch narrow
-// rows off for good when most group rows had to be kept wide.
-void narrow_decide(cpd_graph* g) {
+// rows off for good when most group rows had to be kept wide — the dense
+// final rows replace the narrow rows and the pool (nothing may still read
+// them: the caller has synchronised the main stream).  True if switched.
+bool narrow_decide(cpd_graph* g) {
     const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
-    if (2ull * g->ovf_h() <= groups) return;
+    if (2ull * g->ovf_h() <= groups) return false;
     g->narrow = false;
     g->narrow_probe = 0;
-    g->d16.release();
-    g->dbase.release();
+    g->alloc_final_rows();
     if (trace_on())
         std::fprintf(stderr, "[cpd] narrow rows off: %u of %llu group rows wide\n", g->ovf_h(),
                      (unsigned long long)groups);
+    return true;
 }
 
 // Phase U of a batch of k targets (slot's columns already uploaded), on
 // stream st: the target mask, the leaf-form init of the chunked levels and the
-// up-sweep levels.  Writes dist (up rows), live and tmask, which the previous
-// batch's down-sweep reads: the caller orders st after it.
-// In two parts when asked: from level `from` (0: the whole sweep, its init
-// included), stopping before the chunked level that would be the
-// (head_levels + 1)-th; returns the level it stopped at (the sweep's end
-// when done), where a second call resumes.
-size_t launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st, size_t from = 0,
-                 uint32_t head_levels = UINT32_MAX) {
+// up-sweep levels, into the slot's up store, live and target masks — which
+// only this slot's down-sweep reads: the caller orders st after the slot's
+// previous batch (its first moves, ev_fm[slot]).
+void launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st) {
     const uint32_t B = g->B;
     auto& S = g->bs[slot];
     const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
     const uint32_t active = slabs * 1024u;
-    uint32_t* live = live_on() ? g->live.p : nullptr;
+    uint32_t* up = g->upx[slot].p;
+    uint32_t* tmask = g->tmaskx[slot].p;
+    uint32_t* live = live_on() ? g->livex[slot].p : nullptr;
     unsigned int* stat = g->timing ? S.stat.p : nullptr;
     const size_t nasc = g->asc_lvl.size();
-    if (from == 0) S.up_late.clear();
-    if (stat && from == 0) HIP_CHECK(hipMemsetAsync(stat, 0, S.stat.n * sizeof(unsigned int), st));
-    if (live && from == 0) {
-        HIP_CHECK(hipMemsetAsync(g->tmask.p, 0, (size_t)g->n * sizeof(uint32_t), st));
-        launch_target_mask(S.tgt.p, active, g->tmask.p, st);
-        g->timed("sweep_up_init", 4.0 * g->n_init_cols * active, [&] {
-            launch_sweep_up_init(g->up_init_cols.p, g->n_init_cols, g->dist.p, S.tgt.p, B, slabs,
-                                 live, g->tmask.p, st);
+    S.up_late.clear();
+    if (stat) HIP_CHECK(hipMemsetAsync(stat, 0, S.stat.n * sizeof(unsigned int), st));
+    if (live) {
+        HIP_CHECK(hipMemsetAsync(tmask, 0, (size_t)g->n * sizeof(uint32_t), st));
+        launch_target_mask(S.tgt.p, active, tmask, st);
+        g->timed("sweep_up_init", 4.0 * g->n_init_slots * active, [&] {
+            launch_sweep_up_init(g->up_init_slots.p, g->n_init_slots, g->asc_nodes.p, up, g->ubase,
+                                 S.tgt.p, B, slabs, live, tmask, st);
         });
     }
     // ascending sweep: each level reads lower levels' rows.  Levels 0 and 1
@@ -1447,55 +1477,76 @@ size_t launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st, size_t
     // masks 4 B, node slot 12 B + masks 8 B, once per node — known once the
     // batch's live_stats have run (added by build_batch from S.up_late).
     g->group_begin("sweep_up", st);
-    uint32_t chunked = 0;
-    size_t l = std::max<size_t>(from, 2);
-    for (; l + 1 < nasc; ++l) {
-        uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
-        if (!cnt) continue;
-        const bool chunk_level = live && g->up_item_first[l + 1] > g->up_item_first[l];
-        if (chunk_level && chunked++ == head_levels) break;
-        double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
-        double dense = (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + 8.0 * arcs_l * slabs +
-                       12.0 * cnt * slabs;
+    // bytes of level l (0 when they wait for the batch's stats)
+    auto level_bytes = [&](size_t l) {
+        const uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
+        const double arcs_l = (double)(g->asc_off_host[g->asc_lvl[l + 1]] - g->asc_off_host[s0]);
         if (live && stat) {
             S.up_late.push_back({(double)l, arcs_l, (double)cnt});
-            dense = 0.0;
+            return 0.0;
         }
-        const uint32_t i0 = g->up_item_first[l], ni = g->up_item_first[l + 1] - i0;
+        return (4.0 * g->asc_lvl_arcs[l] + 4.0 * cnt) * active + 8.0 * arcs_l * slabs +
+               12.0 * cnt * slabs;
+    };
+    auto items_of = [&](size_t l) { return g->up_item_first[l + 1] - g->up_item_first[l]; };
+    for (size_t l = 2; l + 1 < nasc; ++l) {
+        uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
+        if (!cnt) continue;
+        const uint32_t i0 = g->up_item_first[l], ni = items_of(l);
+        if (live && ni && ni <= kPersistItems && up_persist_on()) {
+            // a run of chunked levels with few items each: one launch
+            size_t l2 = l;
+            double dense = 0.0;
+            while (l2 + 1 < nasc && items_of(l2) && items_of(l2) <= kPersistItems)
+                dense += level_bytes(l2++);
+            g->timed("sweep_up", dense, [&] {
+                launch_sweep_up_narrow(g->up_items.p, g->up_item_first_d.p, (uint32_t)l,
+                                       (uint32_t)l2, g->asc_arcs.p, up, g->ubase, S.tgt.p, B,
+                                       slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
+                                       tmask, g->ubar[slot].p, st);
+            });
+            l = l2 - 1;
+            continue;
+        }
+        const double dense = level_bytes(l);
         g->timed("sweep_up", dense, [&] {
             if (live && ni)
-                launch_sweep_up_chunks(g->up_items.p + 4 * (size_t)i0, ni, g->asc_nodes.p,
-                                       g->asc_arcs.p, g->dist.p, S.tgt.p, B, slabs,
-                                       g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
-                                       g->tmask.p, st);
+                launch_sweep_up_chunks(g->up_items.p + 4 * (size_t)i0, ni, g->asc_arcs.p, up,
+                                       g->ubase, S.tgt.p, B, slabs, g->asc_nodes.p,
+                                       g->asc_off.p, g->asc_arcs.p, live, tmask, st);
             else
-                launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt,
-                             g->dist.p, S.tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p,
-                             g->asc_arcs.p, live, g->tmask.p, g->adj.p, g->adj_shift, nullptr,
-                             g->narrow_rows(false), nullptr, st);
+                launch_sweep(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, s0, cnt, nullptr,
+                             up, g->ubase, nullptr, S.tgt.p, B, slabs, g->asc_nodes.p,
+                             g->asc_off.p, g->asc_arcs.p, live, tmask, g->adj.p, g->adj_shift,
+                             nullptr, g->narrow_rows(false), nullptr, st);
         });
     }
     g->group_end();
-    return l;
 }
 
-// The up levels' sparse bytes of a batch whose stats have arrived (S.stat_h).
-void add_up_late_bytes(cpd_graph* g, uint32_t slot) {
-    auto& S = g->bs[slot];
-    if (S.up_late.empty()) return;
-    double b = 0.0;
-    for (const auto& u : S.up_late) {
-        const size_t l = (size_t)u[0];
-        b += 4096.0 * ((double)S.stat_h.p[2 * l] + (double)S.stat_h.p[2 * l + 1]) + 12.0 * u[1] +
-             20.0 * u[2];
+// Fold the late bytes of all but the newest `keep` batches: their stats
+// (stat_h of their slot) have landed — the caller has seen a later point of
+// the main stream (the next batch's down-sweep end, or a full sync).
+void fold_late(cpd_graph* g, size_t keep) {
+    while (g->late_q.size() > keep) {
+        const auto& rec = g->late_q.front();
+        const unsigned int* sh = g->bs[rec.slot].stat_h.p;
+        double up = 0.0, down = 0.0;
+        for (const auto& u : rec.up) {
+            const size_t l = (size_t)u[0];
+            up += 4096.0 * ((double)sh[2 * l] + (double)sh[2 * l + 1]) + 12.0 * u[1] + 20.0 * u[2];
+        }
+        for (const auto& d : rec.down) down += 4096.0 * (double)sh[(size_t)d[0]] + d[1];
+        g->agg["sweep_up"].bytes += up;
+        g->agg["sweep_down"].bytes += down;
+        g->late_q.erase(g->late_q.begin());
     }
-    g->agg["sweep_up"].bytes += b;
-    S.up_late.clear();
 }
 
 // Phase D of the batch in `slot` (its up-sweep done or ordered before), on
-// g->stream: the down-sweep, the wide-row count (narrow; its value lands in
-// g->ovf_h), the live stats (timing runs), then ev_down.
+// g->stream: the down-sweep (own rows from the slot's up store), the pool
+// rows it took (narrow; the count lands in g->ovf_h), the live stats
+// (timing runs), then ev_down.
 void launch_down(cpd_graph* g, uint32_t k, bool narrow, uint32_t slot) {
     const uint32_t B = g->B, n = g->n;
     auto& S = g->bs[slot];
@@ -1506,10 +1557,12 @@ void launch_down(cpd_graph* g, uint32_t k, bool narrow, uint32_t slot) {
     const double drow = narrow ? 2.0 + 4.0 / 256.0 : 4.0;
     const uint32_t slabs = (k + 1023u) / 1024u;  // active 1024-target slabs
     const uint32_t active = slabs * 1024u;
-    uint32_t* live = live_on() ? g->live.p : nullptr;
+    uint32_t* live = live_on() ? g->livex[slot].p : nullptr;
     unsigned int* stat = g->timing ? S.stat.p : nullptr;
     const size_t nasc = g->asc_lvl.size();
-    const unsigned int* sh = S.stat_h.p;  // filled by the batch's D2H copy
+    cpd_graph::LateRec rec;
+    rec.slot = slot;
+    rec.up.swap(S.up_late);  // this batch's up levels (launch_up)
     g->group_begin("sweep_down", g->stream);
     for (size_t l = 0; l + 1 < g->dsc_lvl.size(); ++l) {
         uint32_t s0 = g->dsc_lvl[l], cnt = g->dsc_lvl[l + 1] - s0;
@@ -1519,40 +1572,40 @@ void launch_down(cpd_graph* g, uint32_t k, bool narrow, uint32_t slot) {
                       8.0 * g->dsc_lvl_arcs[l] * slabs + 12.0 * cnt * slabs;
         if (g->leaf_fm) base += 0.5 * g->dsc_lvl_leaves[l] * active;  // leaf sets
         double dense = base + 4.0 * g->dsc_lvl_reads[l] * active;
-        std::function<double()> late;
-        if (live && stat)
-            late = [sh, si, base, l, g, slabs] {
-                return base + 4096.0 * (double)sh[si] + 4.0 * g->dsc_lvl_reads[l] * slabs;
-            };
+        if (live && stat) {  // own rows: 4 KiB per live (row, slab), counted by live_stats
+            rec.down.push_back({(double)si, 4.0 * g->dsc_lvl_reads[l] * slabs});
+            dense = base;
+        }
         g->timed("sweep_down", dense, [&] {
             launch_sweep(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p, s0, cnt, g->dist.p,
-                         S.tgt.p, B, slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
-                         g->tmask.p, g->adj.p, g->adj_shift, g->leaf_fm ? g->fmleaf.p : nullptr,
-                         nr, g->dsc_desc.p, g->stream);
-        }, std::move(late));
+                         g->upx[slot].p, g->ubase, g->dsc_up.p, S.tgt.p, B, slabs, g->asc_nodes.p,
+                         g->asc_off.p, g->asc_arcs.p, live, g->tmaskx[slot].p, g->adj.p,
+                         g->adj_shift, g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->dsc_desc.p,
+                         g->stream);
+        });
     }
     g->group_end();
-    if (narrow) {
-        launch_count_wide_rows(g->dbase.p, (size_t)n * (B / 256u),
-                               reinterpret_cast<unsigned int*>(g->ovf.p), g->stream);
+    if (stat) g->late_q.push_back(std::move(rec));
+    if (narrow)
         HIP_CHECK(hipMemcpyAsync(g->ovf_hb.p, g->ovf.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                  g->stream));
-    }
     if (live && stat && nasc > 2) {  // row counts behind the late byte counts
         g->timed("live_stats", 0.0, [&] {
             launch_live_stats(true, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p,
-                              g->asc_lvl_of.p, g->asc_lvl[2], n, live, stat, g->stream);
+                              g->asc_lvl_of.p, g->asc_lvl[2], n, g->ubase, g->dsc_up.p, live,
+                              stat, g->stream);
         });
         g->timed("live_stats", 0.0, [&] {
             launch_live_stats(false, g->dsc_nodes.p, g->dsc_off.p, g->dsc_arcs.p,
-                              g->dsc_lvl_of.p, 0, n, live, stat + 2 * nasc, g->stream);
+                              g->dsc_lvl_of.p, 0, n, g->ubase, g->dsc_up.p, live,
+                              stat + 2 * nasc, g->stream);
         });
     }
     HIP_CHECK(hipEventRecord(g->ev_down, g->stream));
 }
 
 // Phase F: the first moves of the batch in `slot` into fm (after its
-// down-sweep on g->stream), then ev_fm; the timing stats' copy.
+// down-sweep on g->stream), then ev_fm[slot]; the timing stats' copy.
 void launch_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slot) {
     const uint32_t B = g->B, n = g->n;
     auto& S = g->bs[slot];
@@ -1575,10 +1628,10 @@ void launch_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slo
                            fm, g->leaf_fm ? g->leafbits.p : nullptr,
                            g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream, g->seg_order.p);
     });
-    HIP_CHECK(hipEventRecord(g->ev_fm, g->stream));
     if (stat)
         HIP_CHECK(hipMemcpyAsync(S.stat_h.p, stat, S.stat.n * sizeof(unsigned int),
                                  hipMemcpyDeviceToHost, g->stream));
+    HIP_CHECK(hipEventRecord(g->ev_fm[slot], g->stream));
 }
 
 void launch_down_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slot) {
@@ -1649,25 +1702,13 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t 
                              hipMemcpyHostToDevice, st));
 }
 
-// CPD_UP_PRIO=0: the early up-sweep's stream at normal priority (A/B).
-bool up_priority_on() {
-    static const bool on = env_on("CPD_UP_PRIO");
-    return on;
-}
 
-// CPD_UP_HEAD=h >= 0 (A/B): the next batch's up-sweep queued before this
-// batch's first moves, which wait for its wide levels and its first h
-// chunked levels; its narrow levels were to run beside the first moves.
-// They do not: a level's last workgroups wait for the first moves' to be
-// dispatched (profiles/up_head_ab/), so the up-sweep's head is added to the
-// step.  Default -1: the first moves first, the up-sweep beside them on the
-// high-priority stream.
-int up_head() {
-    static const int v = [] {
-        const char* e = std::getenv("CPD_UP_HEAD");
-        return e && *e ? std::atoi(e) : -1;
-    }();
-    return v;
+// CPD_UP_PERSIST=0: every chunked up level its own launch (A/B; identical
+// rows).  Default: runs of levels of at most kPersistItems chunk items in
+// one launch (sweep_up_narrow).
+bool up_persist_on() {
+    static const bool on = env_on("CPD_UP_PERSIST");
+    return on;
 }
 
 // CPD_OVERLAP=0: no early up-sweep of the next batch (A/B; identical rows).
@@ -1687,16 +1728,12 @@ bool trace_on() {
 
 // Build rows for one batch of k <= B targets; append to r (device).  next /
 // next_k (may be null / 0): the targets of the batch that follows; its
-// up-sweep is launched early, on ustream, as soon as this batch's down-sweep
-// is done (when this batch's first moves read no 32-bit rows, which the
-// up-sweep overwrites: narrow rows with no wide group row).
+// up-sweep is queued first, on ustream behind this batch's own: it writes
+// the other slot's up store, so it starts as soon as this batch's up-sweep
+// ends — with this batch's down-sweep — and runs beside it.
 void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
                  const uint32_t* next, uint32_t next_k) {
     const double t0 = now_seconds();
-    const uint32_t x = g->acquire_set();
-    uint32_t* fm = g->fmx[x].p;
-    uint32_t* rst = g->rle_stx[x].p;
-    uint8_t* rrc = g->rle_rcx[x].p;
     uint32_t slot;
     if (g->prepped && g->prep_targets.size() == k &&
         std::equal(targets, targets + k, g->prep_targets.begin())) {
@@ -1715,71 +1752,82 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     // + per 32-column segment a 4-B entry state and a 1-B count (fmb == 4)
     const double st_row = 5.0 * npad / 32.0;
     const bool narrow = g->narrow;
-    launch_down(g, k, narrow, slot);
-    // the previous batch's emit, deferred: now, after this batch's down-sweep
-    // (beside its first moves and the next up-sweep's wide levels)
-    g->flush_emit(g->ev_down);
-    const double t1 = now_seconds();
-    // The next batch's up-sweep (ustream, high priority): after this batch's
-    // down-sweep (ev_down: it reads the up rows, live and tmask the up-sweep
-    // rewrites), and after its first moves too if they read 32-bit rows (wide
-    // group rows, or no narrow rows at all).  Otherwise it goes first: these
-    // first moves wait for its head (CPD_UP_HEAD) and run beside its tail.
-    // (The slot's target buffers are last read by the previous batch's first
-    // moves, ordered before this down-sweep: the copy waits for ev_down.)
-    bool fm_queued = false, prepared = false;
+    // The next batch's up-sweep (ustream, high priority) into the other slot,
+    // after that slot's last batch (its first moves: the last reader of the
+    // slot's targets and up store).  Queued before this down-sweep, so that
+    // the host's launch latency never delays it: its wide levels run beside
+    // this down-sweep's narrow top levels, its narrow latency-bound levels
+    // beside the wide ones.
     const uint32_t ns = slot ^ 1u;
-    auto prep_next = [&](bool head) {
-        if (!(next && next_k && overlap_on())) return;
-        HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
-        upload_targets(g, next, next_k, ns, g->ustream, prepared);
-        HIP_CHECK(hipEventSynchronize(g->ev_down));  // g->ovf_h has landed
-        if (!narrow || g->ovf_h()) HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm, 0));
-        if (head) {
-            const size_t at = launch_up(g, next_k, ns, g->ustream, 0, (uint32_t)up_head());
-            HIP_CHECK(hipEventRecord(g->ev_uph, g->ustream));
-            HIP_CHECK(hipStreamWaitEvent(g->stream, g->ev_uph, 0));
-            launch_fm(g, k, narrow, fm, slot);
-            fm_queued = true;
-            launch_up(g, next_k, ns, g->ustream, at);
-        } else {
-            launch_up(g, next_k, ns, g->ustream);
-        }
+    if (next && next_k && overlap_on()) {
+        prepare_targets(g, next, next_k, ns);
+        HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm[ns], 0));
+        upload_targets(g, next, next_k, ns, g->ustream, true);
+        launch_up(g, next_k, ns, g->ustream);
         HIP_CHECK(hipEventRecord(g->ev_up, g->ustream));
         g->prepped = true;
         g->prep_slot = ns;
         g->prep_targets.assign(next, next + next_k);
-    };
-    if (up_head() >= 0 && next && next_k && overlap_on() && narrow) {
-        prepare_targets(g, next, next_k, ns);  // host work while the down-sweep runs
-        prepared = true;
-        HIP_CHECK(hipEventSynchronize(g->ev_down));
-        if (!g->ovf_h()) prep_next(true);
     }
-    if (!fm_queued) launch_fm(g, k, narrow, fm, slot);
+    launch_down(g, k, narrow, slot);
+    // the first moves' buffer set, once the emit that last read it is done
+    const uint32_t x = g->acquire_set();
+    uint32_t* fm = g->fmx[x].p;
+    uint32_t* rst = g->rle_stx[x].p;
+    uint8_t* rrc = g->rle_rcx[x].p;
+    launch_fm(g, k, narrow, fm, slot);
+    const double t1 = now_seconds();
+    // Narrow rows: the pool rows the down-sweep took (wide group rows).  Past
+    // the pool the batch is rebuilt below; the first full batches decide
+    // whether narrow rows pay at all (narrow_decide).
+    // (The host waits for this down-sweep in any case: the next batch's
+    // target staging buffers are then free.)
+    HIP_CHECK(hipEventSynchronize(g->ev_down));  // g->ovf_h has landed
+    bool rebuild = false;
+    if (narrow) {
+        const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
+        if (g->timing) {  // group rows kept wide / all group rows
+            g->agg["wide_rows"].launches += g->ovf_h();
+            g->agg["group_rows"].launches += groups;
+        }
+        if (g->timing) g->agg["emit_sets"].launches = g->nsets;  // the emit overlap's depth
+        rebuild = g->ovf_h() > g->pool_cap;
+        if (g->narrow_probe && k == g->B) {
+            --g->narrow_probe;
+            if (2ull * g->ovf_h() > groups) {
+                HIP_CHECK(hipStreamSynchronize(g->stream));  // nothing reads the narrow rows
+                narrow_decide(g);
+            }
+        }
+    }
+    if (rebuild) {
+        // This batch's rows are not emitted: they are built again, with the
+        // dense rows when narrow rows were just switched off, else in pieces
+        // of pool_cap / (4 n) slabs, whose group rows all fit the pool.
+        HIP_CHECK(hipStreamSynchronize(g->stream));
+        g->drop_prep();
+        if (trace_on())
+            std::fprintf(stderr, "[cpd] batch of %u rows: %u wide group rows past the pool's %u, rebuilt\n",
+                         k, g->ovf_h(), g->pool_cap);
+        const uint32_t piece =
+            g->narrow ? std::min(g->B, std::max(1024u, (uint32_t)(g->pool_cap / (4ull * g->n)) * 1024u))
+                      : g->B;
+        for (uint32_t b = 0; b < k; b += piece) {
+            const uint32_t kk = std::min(piece, k - b);
+            const bool last = b + kk >= k;
+            build_batch(g, targets + b, kk, r, last ? next : targets + b + kk,
+                        last ? next_k : std::min(piece, k - b - kk));
+        }
+        return;
+    }
+    const double t2 = now_seconds();
     // The count, the seam repair and the move-table emit of this batch go to
     // the emit stream (estream; `stream` when the overlap is off), after its
     // first moves (ev_fm): they run beside the next batch's sweeps, and the
     // run counts land in a page-locked buffer the rows settle from later
     // (cpd_rows::settle) — the host waits for none of it here.
-    if (!fm_queued) prep_next(false);  // this batch's sweeps and first moves are queued: start the next up-sweep
-    if (!g->prepped) HIP_CHECK(hipEventSynchronize(g->ev_down));  // ovf_h (prep_next did it otherwise)
-    const bool probe = narrow && g->narrow_probe && k == g->B;
-    const uint64_t groups = (uint64_t)g->n * (g->B / 256u);
-    if (narrow && g->timing) {  // group rows kept wide / all group rows
-        g->agg["wide_rows"].launches += g->ovf_h();
-        g->agg["group_rows"].launches += groups;
-    }
-    if (probe) {
-        --g->narrow_probe;
-        narrow_decide(g);
-    }
-    const double t2 = now_seconds();
     hipStream_t es = g->async ? g->estream : g->stream;
-    // deferred (g->pend_emit) while another batch follows: launched by the
-    // next batch once its down-sweep is queued (cpd_graph::flush_emit)
-    const bool defer = g->async && next && next_k && emit_defer_on();
-    if (es != g->stream && !defer) HIP_CHECK(hipStreamWaitEvent(es, g->ev_fm, 0));
+    if (es != g->stream) HIP_CHECK(hipStreamWaitEvent(es, g->ev_fm[slot], 0));
     // the batch's rows become table rows r->nrows + i, written by lane pos_of[i]
     const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
     CPD_REQUIRE(r->moves.n >= (size_t)(r->nrows + k) * r->wpr, CPD_E_ARG,
@@ -1842,18 +1890,9 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
             g->emit_pending[x] = true;
         }
     };
-    if (defer) {
-        std::lock_guard<std::mutex> l(g->emit_mu);
-        g->pend_emit = emit;
-        g->pend_rows = r;
-        r->pend_graph.store(g);
-    } else {
-        emit();
-    }
-    if (g->timing) {  // the up levels' bytes need this batch's stats (after its first moves)
-        g->sync();
-        add_up_late_bytes(g, slot);
-    }
+    emit();
+    // the previous batch's sweep bytes: its stats landed before this down-sweep
+    if (g->timing) fold_late(g, 1);
     if (trace_on())
         std::fprintf(stderr, "[cpd] batch %u rows: launch sweeps+fm %.2f ms, to down-sweep end %.2f "
                              "ms, count+emit queued %.2f ms\n",
@@ -1888,9 +1927,9 @@ int cpd_build_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets,
         // bench graph): the register-resident fused emit writes them with
         // 16-B stores, half the bytes of nibble tables (6.2 against 12.3 GB
         // per 24576-row step), and the export and an index take them as
-        // they are.  CPD_ROWS_NIBBLE=1: nibble tables, narrowed on the way out
-        // (round 4's choice, when narrowing cost the unfused emit ~0.5 ms)
-        r->tlb = rows_nibble() ? 2u : g->tlb;
+        // they are (round 4 built nibble tables and narrowed them on the way
+        // out, when narrowing cost the unfused emit ~0.5 ms)
+        r->tlb = g->tlb;
         r->wpr = g->npad >> (5u - r->tlb);
         r->bits = g->move_bits;
         if (r->moves.n < (size_t)ntargets * r->wpr) {
@@ -2068,33 +2107,50 @@ int cpd_debug_rows(cpd_graph* g, const uint32_t* targets, uint32_t ntargets, uin
         g->select();
         if (!g->B) g->reserve_batch(0);
         CPD_REQUIRE(ntargets > 0 && ntargets <= g->B, CPD_E_ARG, "debug: 0 < ntargets <= batch");
-        const uint32_t x = g->acquire_set();
         if (g->prepped) g->drop_prep();
         const uint32_t slot = g->next_slot;
         upload_targets(g, targets, ntargets, slot, g->stream);
-        const bool narrow = g->narrow;
         launch_up(g, ntargets, slot, g->stream);
-        launch_down_fm(g, ntargets, narrow, g->fmx[x].p, slot);
-        g->sync();
-        g->bs[slot].up_late.clear();
+        uint32_t x = 0;
+        for (;;) {
+            x = g->acquire_set();
+            const bool narrow = g->narrow;
+            launch_down_fm(g, ntargets, narrow, g->fmx[x].p, slot);
+            g->sync();
+            // wide group rows past the pool: again with the dense rows
+            if (!narrow || g->ovf_h() <= g->pool_cap) break;
+            g->ovf_hb.p[0] = 2u * g->n * (g->B / 256u);
+            narrow_decide(g);
+        }
+        fold_late(g, 0);
         const std::vector<uint32_t>& pos_of = g->bs[slot].pos_of;
         const std::vector<uint32_t>& tgt_col = g->bs[slot].tgt_col;
         const uint32_t n = g->n, B = g->B;
         // lane p holds the caller's target i = pos_of^-1(p)
         std::vector<uint32_t> h((size_t)n * B);
-        HIP_CHECK(hipMemcpy(h.data(), g->dist.p, h.size() * sizeof(uint32_t),
-                            hipMemcpyDeviceToHost));
-        if (narrow) {  // base + u16 offset (0xFFFF = unreachable), or a wide row
+        if (!g->narrow) {
+            HIP_CHECK(hipMemcpy(h.data(), g->dist.p, h.size() * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost));
+        } else {  // base + u16 offset (0xFFFF = unreachable), or a pool row
             std::vector<uint16_t> q((size_t)n * B);
             std::vector<uint32_t> b((size_t)n * (B / 256u));
+            std::vector<uint32_t> pr((size_t)std::min(g->ovf_h(), g->pool_cap) * 256u);
             HIP_CHECK(hipMemcpy(q.data(), g->d16.p, q.size() * sizeof(uint16_t),
                                 hipMemcpyDeviceToHost));
             HIP_CHECK(hipMemcpy(b.data(), g->dbase.p, b.size() * sizeof(uint32_t),
                                 hipMemcpyDeviceToHost));
+            if (!pr.empty())
+                HIP_CHECK(hipMemcpy(pr.data(), g->pool.p, pr.size() * sizeof(uint32_t),
+                                    hipMemcpyDeviceToHost));
             for (uint32_t c = 0; c < n; ++c)
                 for (uint32_t p = 0; p < B; ++p) {
                     const uint32_t base = b[(size_t)(p / 256u) * n + c];
-                    if (base == 0xFFFFFFFEu) continue;  // kept wide
+                    if (base == 0xFFFFFFFEu) {  // kept wide: the pool row in its d16 words
+                        const size_t w = ((size_t)c * B + (p & ~1u)) / 2u * 2u;
+                        const uint32_t idx = (uint32_t)q[w] | ((uint32_t)q[w + 1] << 16);
+                        h[(size_t)c * B + p] = pr[(size_t)idx * 256u + (p & 255u)];
+                        continue;
+                    }
                     const uint16_t d = q[(size_t)c * B + p];
                     h[(size_t)c * B + p] = d == 0xFFFFu ? CPD_INF : base + d;
                 }
@@ -3029,23 +3085,17 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             // instead of waiting for lanes), else the largest at which 64
             // lanes fit (never throw there — what cannot grow
             // reports finished = 2).  With resumed searches a smaller step
-            // wastes nothing.  CPD_SEARCH_GROW=4 / 2: always 4x / at most 2x (A/B).
+            // wastes nothing.  (Fixed 4x or 2x steps lost their A/Bs, rounds 4-5.)
             uint32_t next = 0;
             if (more) {
                 uint32_t left = 0;
                 for (uint32_t i = 0; i < m; ++i) left += f[i] == 2u || f[i] == 3u;
                 const size_t av2 = avail(sa.rout ? ix->spool[pin ^ 1].n * 4u : 0u);
                 const double share2 = wfrac * (double)av2;
-                static const uint32_t grow = [] {
-                    const char* e = std::getenv("CPD_SEARCH_GROW");
-                    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
-                }();
-                const uint32_t top = grow == 2 ? cap * 2u : cap * 4u;  // CPD_SEARCH_GROW=2: 2x steps
-                for (uint32_t c = std::min(top, cap_max); c > cap; c >>= 1) {
+                for (uint32_t c = std::min(cap * 4u, cap_max); c > cap; c >>= 1) {
                     const double per = (double)search_ws_bytes_per_slot(c, tables);
                     if (64.0 * per > share2) continue;
                     if (!next) next = c;
-                    if (grow == 4) break;
                     if ((double)search_slots(left) * per <= 0.9 * share2) {
                         next = c;
                         break;
@@ -3058,9 +3108,12 @@ int cpd_query_search(cpd_index* ix, const cpd_search_opts* opts, cpd_search_stat
             for (uint32_t i = 0; i < m; ++i) {
                 if (f[i] != 2u && f[i] != 3u) continue;
                 const bool spilled = f[i] == 3u;
-                if (!spilled) {  // restarted: its first pass leaves the sums
+                // restarted: its first pass leaves the sums — only when a
+                // next pass runs it again; otherwise it ends here as an
+                // overflow and its counters stay
+                if (!spilled && next) {
                     for (int k = 0; k < 5; ++k) h[k] -= qst[5ull * i + k];
-                    if (next) wasted += qst[5ull * i];
+                    wasted += qst[5ull * i];
                 }
                 idx.push_back(i);
                 res.push_back(spilled ? at[i] : ~0ull);
@@ -3192,6 +3245,7 @@ int cpd_timing_reset(cpd_graph* g) {
         CPD_REQUIRE(g, CPD_E_ARG, "null graph");
         g->select();
         g->sync(true);
+        fold_late(g, 0);
         g->agg.clear();
     });
 }
@@ -3203,6 +3257,7 @@ int cpd_timing_get(const cpd_graph* g, cpd_kernel_time* out, int max, int* count
         auto* gm = const_cast<cpd_graph*>(g);
         gm->select();
         gm->sync(true);
+        fold_late(gm, 0);
         int k = 0;
         for (auto& kv : g->agg) {
             if (out && k < max) {

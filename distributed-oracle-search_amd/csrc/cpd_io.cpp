@@ -752,12 +752,6 @@ void MoveBucketFile::close(uint64_t total_runs) {
         if (old_fp != fp_ || j >= part_fd_.size()) ::unlink(move_part_path(path_, old_fp, j).c_str());
 }
 
-static uint64_t file_size(const std::string& path) {
-    struct stat st {};
-    if (::stat(path.c_str(), &st) != 0) throw Error(CPD_E_IO, "cannot open " + path);
-    return (uint64_t)st.st_size;
-}
-
 MoveBucket read_move_bucket_head(const std::string& path, bool check_parts) {
     std::ifstream f(path, std::ios::binary | std::ios::ate);
     if (!f) throw Error(CPD_E_IO, "cannot open " + path);
@@ -797,9 +791,20 @@ MoveBucket read_move_bucket_head(const std::string& path, bool check_parts) {
     b.counts.resize(nrows);
     if (striped) {
         if (size != b.head_bytes()) throw Error(CPD_E_IO, path + ": size does not match its header");
-        for (uint32_t j = 0; check_parts && j < b.stripes; ++j)
-            if (file_size(move_part_path(path, b.fingerprint, j)) != b.part_rows(j) * 4ull * b.words)
-                throw Error(CPD_E_IO, move_part_path(path, b.fingerprint, j) + ": size does not match its bucket");
+        for (uint32_t j = 0; check_parts && j < b.stripes; ++j) {
+            const std::string pp = move_part_path(path, b.fingerprint, j);
+            struct stat st {};
+            if (::stat(pp.c_str(), &st) != 0) {
+                // round-4 builds named their parts {path}.p{j} (no fingerprint)
+                struct stat old {};
+                if (::stat((path + ".p" + std::to_string(j)).c_str(), &old) == 0)
+                    throw Error(CPD_E_IO, path + ": its part files use the older {bucket}.p{j} "
+                                          "names (built by an earlier make_cpd_auto): rebuild it");
+                throw Error(CPD_E_IO, "cannot open " + pp);
+            }
+            if ((uint64_t)st.st_size != b.part_rows(j) * 4ull * b.words)
+                throw Error(CPD_E_IO, pp + ": size does not match its bucket");
+        }
     } else if (size != b.rows_offset() + 4ull * b.words * nrows) {
         throw Error(CPD_E_IO, path + ": size does not match its header");
     }

@@ -81,7 +81,8 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t total) {
 //   kLeafBit | column            -> leaf closed form
 //   kL1Bit   | ascending slot s  -> level-1 closed form over the ascending
 //                                   list's node s and its (leaf) arcs
-//   column                       -> a materialised distance row (gather)
+//   up index u (ascending arcs)  -> a row of the compact up store (gather)
+//   column (down-sweep)          -> a final distance row (gather)
 constexpr uint32_t kLeafBit = 0x80000000u;
 constexpr uint32_t kL1Bit = 0x40000000u;
 constexpr uint32_t kIdxMask = 0x3FFFFFFFu;
@@ -141,8 +142,10 @@ __device__ __forceinline__ uint4 arc_val(const uint4* __restrict__ d4, const uin
 // targets (group g = l4 / 64, wave-uniform) share one u32 base per column and
 // hold u16 offsets from it, 0xFFFF = unreachable.  A lane's 4 targets are one
 // 8-B access (512 B per wave instruction), half the wide row's bytes.  A group
-// row whose finite spread does not fit is stored wide instead, in `dist`, and
-// its base says so (kWideRow): readers branch on the (wave-uniform) base.
+// row whose finite spread does not fit is stored wide instead, in a 1-KiB
+// pool row whose index fills its d16 words, and its base says so (kWideRow):
+// readers branch on the (wave-uniform) base and read the pool row at the
+// index their own d16 load brought.
 constexpr uint32_t kNarrowInf = 0xFFFFu;
 constexpr uint32_t kWideRow = 0xFFFFFFFEu;  // > every finite distance (cpd_graph_create)
 
@@ -168,11 +171,15 @@ __device__ __forceinline__ NLoad nl_issue(const NarrowRows& nr, uint32_t col, ui
                  reinterpret_cast<const uint2*>(nr.d16)[(size_t)col * B4 + l4]};
 }
 
-__device__ __forceinline__ uint4 nl_finish(const NLoad& p, const uint4* __restrict__ d4,
-                                           uint32_t col, uint32_t B4, uint32_t l4) {
+// pool row of a wide group row, as uint4 (64 per 256 targets)
+__device__ __forceinline__ const uint4* pool_row(const NarrowRows& nr, uint32_t idx) {
+    return reinterpret_cast<const uint4*>(nr.pool) + (size_t)idx * 64u;
+}
+
+__device__ __forceinline__ uint4 nl_finish(const NLoad& p, const NarrowRows& nr, uint32_t l4) {
     uint4 r = make_uint4(dec16(p.b, p.q.x & 0xFFFFu), dec16(p.b, p.q.x >> 16),
                          dec16(p.b, p.q.y & 0xFFFFu), dec16(p.b, p.q.y >> 16));
-    if (p.b == kWideRow) r = d4[(size_t)col * B4 + l4];  // wave-uniform, rare
+    if (p.b == kWideRow) r = pool_row(nr, p.q.x)[l4 & 63u];  // wave-uniform, rare
     return r;
 }
 
@@ -185,12 +192,14 @@ __device__ __forceinline__ uint32_t enc16(uint32_t d, uint32_t b, bool& bad) {
 
 // One CH sweep level, dense.  Logical block = (slot in the level, 1024-target
 // slab), slots fastest, XCD-remapped (remap != 0): node v = nodes[slot]; its
-// arcs (col, w) are wave-uniform (scalar loads); each lane owns 4 consecutive
-// targets.  ASCEND: upward sweep, init 0 at the lane's own target else INF
-// (used only when skipping is off, CPD_LIVE=0).  !ASCEND: downward sweep, init
-// = current dist (the upward value — INF outside live[v] when live != null —
-// or its closed form for levels 0/1).  Then acc = min(acc, w + d[arc]) over the
-// arcs, eight gathers in flight per wave.
+// arcs (ref, w) are wave-uniform (scalar loads); each lane owns 4 consecutive
+// targets.  ASCEND: upward sweep into the up store (row slot - ubase), init 0
+// at the lane's own target else INF (used only when skipping is off,
+// CPD_LIVE=0), gathers from up rows.  !ASCEND: downward sweep into the dense
+// final rows `dist`, init = the node's up row uidx[slot] (INF outside
+// live[u] when live != null) or its closed form for levels 0/1; gathers
+// from final rows.  acc = min(acc, w + d[arc]) over the arcs, eight gathers
+// in flight per wave.
 //
 // Leaf first moves (lf.out != null, 4-bit sets): a leaf (no down-arcs) has
 // only higher-ranked out-neighbours, all final when the down-sweep reaches
@@ -212,6 +221,8 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
                                                    const uint2* __restrict__ arcs,
                                                    uint32_t slot0, uint32_t count, uint32_t remap,
                                                    uint32_t* __restrict__ dist,
+                                                   uint32_t* __restrict__ up, uint32_t ubase,
+                                                   const uint32_t* __restrict__ uidx,
                                                    const uint4* __restrict__ tgt4,
                                                    uint32_t B4, Closed cf,
                                                    const uint32_t* __restrict__ live, LeafFm lf) {
@@ -220,13 +231,17 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
     const uint32_t slot = slot0 + (L - slab * count);
     const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t vraw = nodes[slot];
-    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    uint4* __restrict__ u4 = reinterpret_cast<uint4*>(up);
+    // rows written and gathered: up rows (ASCEND), final rows (!ASCEND)
+    uint4* __restrict__ d4 = ASCEND ? u4 : reinterpret_cast<uint4*>(dist);
+    uint32_t row;  // the row this slot writes
 
     const uint4 t = tgt4[l4];
     uint32_t v;
     uint4 acc;
     if (ASCEND) {
         v = vraw;
+        row = slot - ubase;
         acc = leaf4(t, v, 0u);
     } else if (vraw & kLeafBit) {
         v = vraw & kIdxMask;
@@ -270,9 +285,11 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
         acc = l1_val(cf, vraw & kIdxMask, t);
     } else {
         v = vraw;
-        const bool own = !live || ((live[v] >> (l4 >> 8)) & 1u);  // live bits: 1024 targets
-        acc = own ? d4[(size_t)v * B4 + l4] : make_uint4(INF, INF, INF, INF);
+        const uint32_t u = uidx[slot];
+        const bool own = !live || ((live[u] >> (l4 >> 8)) & 1u);  // live bits: 1024 targets
+        acc = own ? u4[(size_t)u * B4 + l4] : make_uint4(INF, INF, INF, INF);
     }
+    if (!ASCEND) row = v;
     const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
     uint32_t a = a0;
     for (; a + 8 <= a1; a += 8) {
@@ -289,7 +306,7 @@ __global__ __launch_bounds__(256) void sweep_level(const uint32_t* __restrict__ 
         const uint2 e = arcs[a];
         min4(acc, arc_val(d4, t, e, B4, l4, cf, true), e.y);
     }
-    d4[(size_t)v * B4 + l4] = acc;
+    d4[(size_t)row * B4 + l4] = acc;
 }
 
 // Down-sweep into narrow rows, 8 targets per lane.  The narrow rows halve the
@@ -332,21 +349,25 @@ __device__ __forceinline__ NLoad8 nl8_issue(const NarrowRows& nr, uint32_t col, 
                   reinterpret_cast<const uint4*>(nr.d16)[(size_t)col * B8 + l8]};
 }
 
-__device__ __forceinline__ U8 nl8_finish(const NLoad8& p, const uint4* __restrict__ d4,
-                                         uint32_t col, uint32_t B4, uint32_t l8) {
+__device__ __forceinline__ U8 nl8_finish(const NLoad8& p, const NarrowRows& nr, uint32_t l8) {
     U8 r{make_uint4(dec16(p.b, p.q.x & 0xFFFFu), dec16(p.b, p.q.x >> 16),
                     dec16(p.b, p.q.y & 0xFFFFu), dec16(p.b, p.q.y >> 16)),
          make_uint4(dec16(p.b, p.q.z & 0xFFFFu), dec16(p.b, p.q.z >> 16),
                     dec16(p.b, p.q.w & 0xFFFFu), dec16(p.b, p.q.w >> 16))};
     if (p.b == kWideRow) {  // uniform per half-wave, rare
-        r.a = d4[(size_t)col * B4 + 2u * l8];
-        r.b = d4[(size_t)col * B4 + 2u * l8 + 1u];
+        const uint4* pr = pool_row(nr, p.q.x) + 2u * (l8 & 31u);
+        r.a = pr[0];
+        r.b = pr[1];
     }
     return r;
 }
 
-__device__ __forceinline__ void narrow_store8(const NarrowRows& nr, uint4* __restrict__ d4,
-                                              uint32_t col, uint32_t grp, uint32_t B4,
+// A half-wave (one 256-target group) stores its row narrow, or — when the
+// spread does not fit 16 bits — takes a pool row (the head's atomic on the
+// pool counter) and stores it there, the index in every d16 word.  Past the
+// pool's capacity nothing is stored: the counter tells the host, which
+// rebuilds the batch in pieces the pool holds (readers stay in bounds).
+__device__ __forceinline__ void narrow_store8(const NarrowRows& nr, uint32_t col, uint32_t grp,
                                               uint32_t B8, uint32_t l8, const U8& acc) {
     uint32_t b = min(min(min(acc.a.x, acc.a.y), min(acc.a.z, acc.a.w)),
                      min(min(acc.b.x, acc.b.y), min(acc.b.z, acc.b.w)));
@@ -362,8 +383,17 @@ __device__ __forceinline__ void narrow_store8(const NarrowRows& nr, uint4* __res
     const bool half_bad = ((lane < 32u ? m : (m >> 32)) & 0xFFFFFFFFull) != 0;
     const bool head = (lane & 31u) == 0;
     if (half_bad) {
-        d4[(size_t)col * B4 + 2u * l8] = acc.a;
-        d4[(size_t)col * B4 + 2u * l8 + 1u] = acc.b;
+        uint32_t p = 0;
+        if (head) p = atomicAdd(nr.ovf, 1u);
+        p = (uint32_t)__shfl((int)p, (int)(lane & 32u), 64);
+        const bool fits = p < nr.cap;
+        p = fits ? p : nr.cap - 1u;
+        if (fits) {
+            uint4* pr = reinterpret_cast<uint4*>(nr.pool) + (size_t)p * 64u + 2u * (l8 & 31u);
+            pr[0] = acc.a;
+            pr[1] = acc.b;
+        }
+        reinterpret_cast<uint4*>(nr.d16)[(size_t)col * B8 + l8] = make_uint4(p, p, p, p);
         if (head) nr.base[(size_t)grp * nr.n + col] = kWideRow;
         return;
     }
@@ -419,14 +449,13 @@ __device__ __forceinline__ uint32_t fm_wild4(const uint4& t, const uint4& acc, u
 
 __device__ __forceinline__ void leaf_finish8(const uint2* e, const NLoad8 (&pl)[kDescArcs],
                                              uint32_t v, U8& acc, const U8& t, uint32_t l8,
-                                             uint32_t grp, uint32_t B4, uint32_t B8,
-                                             uint4* __restrict__ d4,
+                                             uint32_t grp, uint32_t B8,
                                              uint16_t* __restrict__ fmleaf, const NarrowRows& nr) {
     uint32_t ba = 0, bb = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         if (e[k].x == kNoEdge || e[k].x == v) continue;
-        const U8 x = nl8_finish(pl[k], d4, e[k].x, B4, l8);
+        const U8 x = nl8_finish(pl[k], nr, l8);
         const uint32_t w = e[k].y;
         argmin_fold<0>(acc.a.x, ba, sat_add(x.a.x, w), k);
         argmin_fold<1>(acc.a.y, ba, sat_add(x.a.y, w), k);
@@ -444,23 +473,22 @@ __device__ __forceinline__ void leaf_finish8(const uint2* e, const NLoad8 (&pl)[
             bb |= 0x1111u << k;
         }
     const uint32_t sets = fm_wild4(t.a, acc.a, v, ba) | (fm_wild4(t.b, acc.b, v, bb) << 16);
-    narrow_store8(nr, d4, v, grp, B4, B8, l8, acc);
+    narrow_store8(nr, v, grp, B8, l8, acc);
     reinterpret_cast<uint32_t*>(fmleaf)[(size_t)v * B8 + l8] = sets;  // 8 nibbles
 }
 
 __device__ __forceinline__ void leaf_slot8(const uint2* e, uint32_t v, U8& acc, const U8& t,
-                                           uint32_t l8, uint32_t grp, uint32_t B4, uint32_t B8,
-                                           uint4* __restrict__ d4, uint16_t* __restrict__ fmleaf,
-                                           const NarrowRows& nr) {
+                                           uint32_t l8, uint32_t grp, uint32_t B8,
+                                           uint16_t* __restrict__ fmleaf, const NarrowRows& nr) {
     NLoad8 pl[kDescArcs];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (e[k].x != kNoEdge && e[k].x != v) pl[k] = nl8_issue(nr, e[k].x, grp, B8, l8);
-    leaf_finish8(e, pl, v, acc, t, l8, grp, B4, B8, d4, fmleaf, nr);
+    leaf_finish8(e, pl, v, acc, t, l8, grp, B8, fmleaf, nr);
 }
 
 // A down-sweep slot's descriptor (see down_desc_arcs): the 64-B head (node
-// word, arc range, first kDescArcs arcs) and, for a level-1 node, the
+// word, arc range, up index, first kDescArcs arcs) and, for a level-1 node, the
 // closed-form part (c0..c2), all loaded together (one 128-B scalar fetch).
 struct Desc8 {
     uint4 h, i0, i1, i2, c0, c1, c2;
@@ -481,13 +509,13 @@ constexpr int kLong = CPD_DOWN8_LONG;
 
 // One slot of the narrow down-sweep for the lane's 8 targets t.
 __device__ __forceinline__ void down8_slot(const Desc8& D, const U8& t, uint32_t l8, uint32_t grp,
-                                           uint32_t B4, uint32_t B8, uint4* __restrict__ d4,
+                                           uint32_t B4, uint32_t B8, const uint4* __restrict__ u4,
                                            const uint2* __restrict__ arcs, const Closed& cf,
                                            const uint32_t* __restrict__ live,
                                            uint16_t* __restrict__ fmleaf, const NarrowRows& nr) {
-    // (node word, first arc, end arc, -) + its first kDescArcs arcs (a leaf's
-    // out-edges in file order); for a level-1 node also its column and its
-    // <= 4 leaf arcs (closed form)
+    // (node word, first arc, end arc, up index) + its first kDescArcs arcs (a
+    // leaf's out-edges in file order); for a level-1 node also its column and
+    // its <= 4 leaf arcs (closed form)
     const uint4 i0 = D.i0, i1 = D.i1, i2 = D.i2;
     const uint2 all6[6] = {make_uint2(i0.x, i0.y), make_uint2(i0.z, i0.w),
                            make_uint2(i1.x, i1.y), make_uint2(i1.z, i1.w),
@@ -502,7 +530,7 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const U8& t, uint32_t
         v = vraw & kIdxMask;
         acc = U8{leaf4(t.a, v, 0u), leaf4(t.b, v, 0u)};
         if (fmleaf) {  // out-degree <= 4 (4-bit sets): all inline
-            leaf_slot8(inl, v, acc, t, l8, grp, B4, B8, d4, fmleaf, nr);
+            leaf_slot8(inl, v, acc, t, l8, grp, B8, fmleaf, nr);
             return;
         }
     } else if (vraw & kL1Bit) {  // closed form from the descriptor
@@ -527,8 +555,9 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const U8& t, uint32_t
         }
     } else {
         v = vraw;
-        const bool own = !live || ((live[v] >> (l8 >> 7)) & 1u);  // live bits: 1024 targets
-        acc = own ? U8{d4[(size_t)v * B4 + 2u * l8], d4[(size_t)v * B4 + 2u * l8 + 1u]} : inf8();
+        const uint32_t u = D.h.w;  // its row in the up store
+        const bool own = !live || ((live[u] >> (l8 >> 7)) & 1u);  // live bits: 1024 targets
+        acc = own ? U8{u4[(size_t)u * B4 + 2u * l8], u4[(size_t)u * B4 + 2u * l8 + 1u]} : inf8();
     }
     {  // the inline arcs (kNoEdge past the list), gathers in flight together
         NLoad8 pl[kDescArcs];
@@ -537,7 +566,7 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const U8& t, uint32_t
             if (inl[i].x != kNoEdge) pl[i] = nl8_issue(nr, inl[i].x, grp, B8, l8);
 #pragma unroll
         for (int i = 0; i < (int)kDescArcs; ++i)
-            if (inl[i].x != kNoEdge) min8(acc, nl8_finish(pl[i], d4, inl[i].x, B4, l8), inl[i].y);
+            if (inl[i].x != kNoEdge) min8(acc, nl8_finish(pl[i], nr, l8), inl[i].y);
     }
     uint32_t a = a0 + kDescArcs;  // the rest of a long list (rare), kLong gathers at a time
     for (; a + kLong <= a1; a += kLong) {
@@ -548,13 +577,13 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const U8& t, uint32_t
 #pragma unroll
         for (int i = 0; i < kLong; ++i) pl[i] = nl8_issue(nr, e[i].x, grp, B8, l8);
 #pragma unroll
-        for (int i = 0; i < kLong; ++i) min8(acc, nl8_finish(pl[i], d4, e[i].x, B4, l8), e[i].y);
+        for (int i = 0; i < kLong; ++i) min8(acc, nl8_finish(pl[i], nr, l8), e[i].y);
     }
     for (; a < a1; ++a) {
         const uint2 e = arcs[a];
-        min8(acc, nl8_finish(nl8_issue(nr, e.x, grp, B8, l8), d4, e.x, B4, l8), e.y);
+        min8(acc, nl8_finish(nl8_issue(nr, e.x, grp, B8, l8), nr, l8), e.y);
     }
-    narrow_store8(nr, d4, v, grp, B4, B8, l8, acc);
+    narrow_store8(nr, v, grp, B8, l8, acc);
 }
 
 
@@ -566,7 +595,7 @@ __device__ __forceinline__ void down8_slot(const Desc8& D, const U8& t, uint32_t
 __global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ desc,
                                                    const uint2* __restrict__ arcs,
                                                    uint32_t slot0, uint32_t count, uint32_t remap,
-                                                   uint32_t* __restrict__ dist,
+                                                   const uint32_t* __restrict__ up,
                                                    const uint4* __restrict__ tgt4, uint32_t B4,
                                                    Closed cf, const uint32_t* __restrict__ live,
                                                    uint16_t* __restrict__ fmleaf, NarrowRows nr) {
@@ -576,22 +605,9 @@ __global__ __launch_bounds__(256) void sweep_down8(const uint4* __restrict__ des
     const uint32_t l8 = blk * blockDim.x + threadIdx.x;  // targets 8 l8 .. 8 l8 + 7
     const uint32_t grp = l8 >> 5;                        // uniform per half-wave
     const uint32_t B8 = B4 / 2u;
-    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    const uint4* __restrict__ u4 = reinterpret_cast<const uint4*>(up);
     const U8 t{tgt4[2u * l8], tgt4[2u * l8 + 1u]};
-    down8_slot(load_desc8(desc, s0), t, l8, grp, B4, B8, d4, arcs, cf, live, fmleaf, nr);
-}
-
-// Group rows stored wide (timing runs only): *out += #{base[i] == kWideRow}.
-__global__ __launch_bounds__(256) void count_wide_rows(const uint32_t* __restrict__ base,
-                                                       size_t total,
-                                                       unsigned int* __restrict__ out) {
-    uint32_t c = 0;
-    for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < total;
-         i += (size_t)gridDim.x * 256u)
-        c += base[i] == kWideRow ? 1u : 0u;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63u) == 0 && c) atomicAdd(out, c);
+    down8_slot(load_desc8(desc, s0), t, l8, grp, B4, B8, u4, arcs, cf, live, fmleaf, nr);
 }
 
 // Slab mask of an arc's source row (see "Up-sweep sparsity").
@@ -615,27 +631,38 @@ __device__ __forceinline__ uint32_t arc_mask(uint32_t ex, const uint32_t* __rest
 // live slab: 256 threads x 4 targets as in sweep_level, gathers only from
 // arcs live in that slab.  live[v] = the node's mask (every split writes the
 // same value); nothing else of a dead slab is read or written.
-__global__ __launch_bounds__(256) void sweep_up_sparse(
+// The up-sweep runs on its own stream beside the down-sweep and the first
+// moves, so its kernels are one-wave workgroups of <= 64 VGPRs: a workgroup
+// of four 96-VGPR waves needed four SIMDs of one CU to free room at once
+// while the main stream's 58-VGPR waves refilled every hole first — the up
+// levels waited 200-450 us each (round 6, profiles/up_store_ab/); one wave
+// of <= 64 VGPRs fits the slot any retiring down-sweep wave leaves.  A wave
+// covers a quarter slab (256 targets, 4 per lane): q = its quarter.
+constexpr uint32_t kUpQ = 4;  // waves (quarters) per 1024-target slab
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sweep_up_sparse(
     const uint32_t* __restrict__ nodes, const uint32_t* __restrict__ arc_off,
     const uint2* __restrict__ arcs, uint32_t slot0, uint32_t count, uint32_t nsplit,
-    uint32_t remap, uint32_t* __restrict__ dist, const uint4* __restrict__ tgt4, uint32_t B4,
-    Closed cf, uint32_t* __restrict__ live, const uint32_t* __restrict__ tmask,
+    uint32_t remap, uint32_t* __restrict__ up, uint32_t ubase, const uint4* __restrict__ tgt4,
+    uint32_t B4, Closed cf, uint32_t* __restrict__ live, const uint32_t* __restrict__ tmask,
     uint32_t active) {
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t j = L / count;
-    const uint32_t slot = slot0 + (L - j * count);
-    const uint32_t v = nodes[slot];
+    const uint32_t jq = L / count;
+    const uint32_t slot = slot0 + (L - jq * count);
+    const uint32_t j = jq / kUpQ, q = jq - j * kUpQ;
+    const uint32_t v = nodes[slot];   // column: the target test and tmask
+    const uint32_t u = slot - ubase;  // row in the up store
     const uint32_t a0 = arc_off[slot], a1 = arc_off[slot + 1];
     const uint32_t* __restrict__ live_in = live;  // rows of finished levels only
     uint32_t m = tmask[v];
     for (uint32_t a = a0; a < a1; ++a) m |= arc_mask(arcs[a].x, live_in, tmask, cf);
     m &= active;
-    if (threadIdx.x == 0 && j == 0) live[v] = m;
-    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dist);
+    if (threadIdx.x == 0 && j == 0 && q == 0) live[u] = m;
+    uint4* __restrict__ d4 = reinterpret_cast<uint4*>(up);
     for (uint32_t mm = m; mm; mm &= mm - 1u) {
         const uint32_t slab = (uint32_t)__builtin_ctz(mm);
         if (slab % nsplit != j) continue;
-        const uint32_t l4 = slab * 256u + threadIdx.x;
+        const uint32_t l4 = slab * 256u + q * 64u + threadIdx.x;
         const uint4 t = tgt4[l4];
         uint4 acc = leaf4(t, v, 0u);
         uint32_t a = a0;
@@ -656,7 +683,7 @@ __global__ __launch_bounds__(256) void sweep_up_sparse(
             min4(acc, arc_val(d4, t, e, B4, l4, cf, (arc_mask(e.x, live_in, tmask, cf) >> slab) & 1u),
                  e.y);
         }
-        d4[(size_t)v * B4 + l4] = acc;
+        d4[(size_t)u * B4 + l4] = acc;
     }
 }
 
@@ -667,37 +694,40 @@ __global__ __launch_bounds__(256) void sweep_up_sparse(
 // folds its partial minimum into the row with atomicMin; the rows start as the
 // leaf form (sweep_up_init, once per batch) and live[v] collects the chunks'
 // masks with atomicOr.
-constexpr int kChunk = 16;
+constexpr int kChunk = 8;
 
 // Grid-stride over (column, slab) rows with a small grid: the init runs on the
 // early up-sweep stream beside the previous batch's first moves, and one block
 // per 4-KiB row (~240k blocks at 1M nodes) would be dispatched round-robin
 // with first_moves' blocks and end with it, holding back every up level.
-__global__ __launch_bounds__(256) void sweep_up_init(const uint32_t* __restrict__ cols,
-                                                     uint32_t ncols, uint32_t total,
-                                                     uint32_t* __restrict__ dist,
+__global__ __launch_bounds__(64) void sweep_up_init(const uint32_t* __restrict__ slots,
+                                                     uint32_t nslots, uint32_t total,
+                                                     const uint32_t* __restrict__ nodes,
+                                                     uint32_t* __restrict__ up, uint32_t ubase,
                                                      const uint4* __restrict__ tgt4, uint32_t B4,
                                                      uint32_t* __restrict__ live,
                                                      const uint32_t* __restrict__ tmask,
                                                      uint32_t active) {
-    for (uint32_t L = blockIdx.x; L < total; L += gridDim.x) {
-        const uint32_t slab = L / ncols;
-        const uint32_t v = cols[L - slab * ncols];
-        const uint32_t l4 = slab * 256u + threadIdx.x;
-        reinterpret_cast<uint4*>(dist)[(size_t)v * B4 + l4] = leaf4(tgt4[l4], v, 0u);
-        if (slab == 0 && threadIdx.x == 0) live[v] = tmask[v] & active;
+    for (uint32_t L = blockIdx.x; L < total; L += gridDim.x) {  // (slot, quarter slab)
+        const uint32_t sq = L / nslots;
+        const uint32_t s = slots[L - sq * nslots];
+        const uint32_t v = nodes[s], u = s - ubase;
+        const uint32_t l4 = sq * 64u + threadIdx.x;
+        reinterpret_cast<uint4*>(up)[(size_t)u * B4 + l4] = leaf4(tgt4[l4], v, 0u);
+        if (sq == 0 && threadIdx.x == 0) live[u] = tmask[v] & active;
     }
 }
 
-__global__ __launch_bounds__(256) void sweep_up_chunks(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sweep_up_chunks(
     const uint4* __restrict__ items, uint32_t nitems, uint32_t remap,
-    const uint32_t* __restrict__ nodes, const uint2* __restrict__ arcs,
-    uint32_t* __restrict__ dist, const uint4* __restrict__ tgt4, uint32_t B4, Closed cf,
+    const uint2* __restrict__ arcs, uint32_t* __restrict__ up, uint32_t ubase,
+    const uint4* __restrict__ tgt4, uint32_t B4, Closed cf,
     uint32_t* __restrict__ live, const uint32_t* __restrict__ tmask, uint32_t active) {
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t slab = L / nitems;
-    const uint4 it = items[L - slab * nitems];  // (slot, first arc, end arc, -)
-    const uint32_t v = nodes[it.x];
+    const uint32_t sq = L / nitems;  // (slab, quarter)
+    const uint32_t slab = sq / kUpQ, q = sq - slab * kUpQ;
+    const uint4 it = items[L - sq * nitems];  // (slot, first arc, end arc, -)
+    const uint32_t v = it.x - ubase;              // its row in the up store
     const uint32_t* __restrict__ live_in = live;  // lower levels' masks only
     uint2 e[kChunk];
     uint32_t mk[kChunk], pm = 0;
@@ -708,29 +738,109 @@ __global__ __launch_bounds__(256) void sweep_up_chunks(
         mk[i] = it.y + i < it.z ? arc_mask(e[i].x, live_in, tmask, cf) & active : 0u;
         pm |= mk[i];
     }
-    if (slab == 0 && threadIdx.x == 0 && pm) atomicOr(&live[v], pm);
+    if (sq == 0 && threadIdx.x == 0 && pm) atomicOr(&live[v], pm);
     if (!((pm >> slab) & 1u)) return;
-    const uint32_t l4 = slab * 256u + threadIdx.x;
+    const uint32_t l4 = slab * 256u + q * 64u + threadIdx.x;
     const uint4 t = tgt4[l4];
-    const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
+    const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(up);
     uint4 x[kChunk];
 #pragma unroll
     for (int i = 0; i < kChunk; ++i) x[i] = arc_val(d4, t, e[i], B4, l4, cf, (mk[i] >> slab) & 1u);
     uint4 acc = make_uint4(INF, INF, INF, INF);
 #pragma unroll
     for (int i = 0; i < kChunk; ++i) min4(acc, x[i], e[i].y);
-    uint32_t* row = dist + ((size_t)v * B4 + l4) * 4u;
+    uint32_t* row = up + ((size_t)v * B4 + l4) * 4u;
     if (acc.x != INF) atomicMin(row + 0, acc.x);
     if (acc.y != INF) atomicMin(row + 1, acc.y);
     if (acc.z != INF) atomicMin(row + 2, acc.z);
     if (acc.w != INF) atomicMin(row + 3, acc.w);
 }
 
+// The up-sweep's top: a run of narrow levels in ONE launch (round 6).  As
+// separate launches (sweep_up_chunks) each of these ~140 levels costs a
+// launch and a dispatch: 65 us alone, and 200-450 us beside the other
+// streams' large launches, where the chain of them became the step's
+// critical path.  Slabs are independent (a target's up row reads only
+// lower rows of the same target), so G resident one-wave workgroups per
+// quarter slab walk the levels together: each takes every G-th chunk item
+// of the level, then the quarter's G waves meet at a barrier (an atomic
+// counter per quarter slab, zeroed by the caller) before the next level.  Everything a
+// later level reads was written by atomics (rows: atomicMin, masks:
+// atomicOr) before the barrier's release; the acquire after it invalidates
+// the CU's L1, and the masks (live words of several nodes share a line) are
+// read with coherent loads.  A wave sets only its own slab's live bit (each
+// quarter computes the same bits from the same inputs).  The grid is slabs
+// x 4 x G one-wave workgroups, small enough to be resident at once beside
+// other kernels (each waits only for the others' waves to retire); every
+// workgroup runs every level, so all reach each barrier and the end.
+__device__ __forceinline__ uint32_t coherent_u32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t arc_bit(uint32_t ex, const uint32_t* __restrict__ live,
+                                            const uint32_t* __restrict__ tmask, const Closed& cf,
+                                            uint32_t slab) {
+    if (ex & (kLeafBit | kL1Bit)) return (arc_mask(ex, live, tmask, cf) >> slab) & 1u;
+    return (coherent_u32(live + ex) >> slab) & 1u;
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sweep_up_narrow(
+    const uint4* __restrict__ items, const uint32_t* __restrict__ item_first, uint32_t l0,
+    uint32_t l1, uint32_t G, const uint2* __restrict__ arcs, uint32_t* __restrict__ up,
+    uint32_t ubase, const uint4* __restrict__ tgt4, uint32_t B4, Closed cf,
+    uint32_t* __restrict__ live, const uint32_t* __restrict__ tmask, uint32_t* __restrict__ bar) {
+    const uint32_t sq = blockIdx.x / G, g = blockIdx.x - sq * G;  // (slab, quarter), member
+    const uint32_t slab = sq / kUpQ;
+    const uint32_t l4 = sq * 64u + threadIdx.x;
+    const uint4 t = tgt4[l4];
+    const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(up);
+    for (uint32_t l = l0; l < l1; ++l) {
+        const uint32_t i1 = item_first[l + 1];
+        for (uint32_t i = item_first[l] + g; i < i1; i += G) {
+            const uint4 it = items[i];  // (slot, first arc, end arc, -)
+            const uint32_t v = it.x - ubase;
+            uint2 e[kChunk];
+            uint32_t mk = 0;
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j)
+                e[j] = it.y + j < it.z ? arcs[it.y + j] : make_uint2(0u, 0u);
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j)
+                if (it.y + j < it.z) mk |= arc_bit(e[j].x, live, tmask, cf, slab) << j;
+            if (!mk) continue;  // no live input in this slab
+            if (threadIdx.x == 0) atomicOr(&live[v], 1u << slab);
+            uint4 x[kChunk];
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j) x[j] = arc_val(d4, t, e[j], B4, l4, cf, (mk >> j) & 1u);
+            uint4 acc = make_uint4(INF, INF, INF, INF);
+#pragma unroll
+            for (int j = 0; j < kChunk; ++j) min4(acc, x[j], e[j].y);
+            uint32_t* row = up + ((size_t)v * B4 + l4) * 4u;
+            if (acc.x != INF) atomicMin(row + 0, acc.x);
+            if (acc.y != INF) atomicMin(row + 1, acc.y);
+            if (acc.z != INF) atomicMin(row + 2, acc.z);
+            if (acc.w != INF) atomicMin(row + 3, acc.w);
+        }
+        if (l + 1 == l1) break;  // the launch's end orders the rest
+        // release: the wave's atomics complete at agent scope before its
+        // arrival (the explicit wait: the compiler may drop the fence's own,
+        // MI355X_MICROARCH.md "Compiler hazard")
+        __threadfence();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) {
+            atomicAdd(&bar[sq], 1u);
+            const uint32_t want = (l - l0 + 1u) * G;
+            while (coherent_u32(bar + sq) < want) __builtin_amdgcn_s_sleep(1);
+        }
+        __threadfence();  // acquire: the CU's L1 invalidated before the next level's loads
+    }
+}
+
 // tmask[col] |= 1 << slab for every target lane (4 per thread) of the batch;
 // the caller zeroes tmask first.
-__global__ __launch_bounds__(256) void target_mask(const uint32_t* __restrict__ tgt, uint32_t B,
-                                                   uint32_t* __restrict__ tmask) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+__global__ __launch_bounds__(64) void target_mask(const uint32_t* __restrict__ tgt, uint32_t B,
+                                                  uint32_t* __restrict__ tmask) {
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
     if (i < B) atomicOr(&tmask[tgt[i]], 1u << (i >> 10));
 }
 
@@ -748,7 +858,8 @@ __global__ __launch_bounds__(256) void live_stats(const uint32_t* __restrict__ n
                                                   const uint32_t* __restrict__ arc_off,
                                                   const uint2* __restrict__ arcs,
                                                   const uint32_t* __restrict__ lvl_of,
-                                                  uint32_t slot0, uint32_t slot1,
+                                                  uint32_t slot0, uint32_t slot1, uint32_t ubase,
+                                                  const uint32_t* __restrict__ uidx,
                                                   const uint32_t* __restrict__ live,
                                                   unsigned int* __restrict__ stat) {
     const uint32_t slot = slot0 + blockIdx.x * 256u + threadIdx.x;
@@ -756,7 +867,8 @@ __global__ __launch_bounds__(256) void live_stats(const uint32_t* __restrict__ n
     if (slot < slot1) {
         lvl = lvl_of[slot];
         const uint32_t v = nodes[slot];
-        if (ASCEND || !(v & (kLeafBit | kL1Bit))) own = __builtin_popcount(live[v]);
+        if (ASCEND) own = __builtin_popcount(live[slot - ubase]);
+        else if (!(v & (kLeafBit | kL1Bit))) own = __builtin_popcount(live[uidx[slot]]);
         if (ASCEND)
             for (uint32_t a = arc_off[slot]; a < arc_off[slot + 1]; ++a) {
                 const uint32_t c = arcs[a].x;
@@ -856,7 +968,7 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
 #pragma unroll
             for (int j = 0; j < G; ++j) {
                 const uint32_t c = c0 + (uint32_t)(cg + j);
-                dn[j] = c < n && !((lbits >> (cg + j)) & 1u) ? nl_finish(pn[j], d4, c, B4, l4)
+                dn[j] = c < n && !((lbits >> (cg + j)) & 1u) ? nl_finish(pn[j], nr, l4)
                                                              : make_uint4(INF, INF, INF, INF);
             }
             dn_done = true;
@@ -882,7 +994,7 @@ __global__ __launch_bounds__(256) void first_moves(const uint2* __restrict__ adj
 #pragma unroll
                     for (int k = 0; k < KC; ++k)
                         if (e[j][kb + k].x != kNoEdge)
-                            dv[j][k] = nl_finish(pv[j][k], d4, e[j][kb + k].x, B4, l4);
+                            dv[j][k] = nl_finish(pv[j][k], nr, l4);
             } else {
 #pragma unroll
                 for (int j = 0; j < G; ++j)
@@ -1000,7 +1112,6 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
     const uint32_t cb = (seg_order ? seg_order[sl] : sl) * kSeg;
     const uint32_t lane = threadIdx.x & 63u;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
-    const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(dist);
     const uint32_t grp = wave_group(l4);
     // each row word is staged in LDS (64 B per lane, dynamic shared memory) as
     // soon as its 8 columns are done, so only the current word of each row is
@@ -1053,7 +1164,7 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                 for (int k = 0; k < 4; ++k) {
                     const uint2 e = edge(cc, k);
                     if (e.x == kNoEdge) continue;
-                    const uint4 dv = nl_finish(g.nb[j][k], d4, e.x, B4, l4);
+                    const uint4 dv = nl_finish(g.nb[j][k], nr, l4);
                     argmin_fold<0>(dn.x, bits, sat_add(dv.x, e.y), k);
                     argmin_fold<1>(dn.y, bits, sat_add(dv.y, e.y), k);
                     argmin_fold<2>(dn.z, bits, sat_add(dv.z, e.y), k);
@@ -1325,11 +1436,12 @@ __device__ __forceinline__ void store_cols32(uint32_t* __restrict__ row, uint32_
 
 // store_cols32 by a whole wave whose lane l holds segment g0 + l: the packed
 // widths' 8-B (2-bit) and 4-B (1-bit) pieces gathered into 16-B stores by
-// every second / fourth lane (CPD_EMIT_WIDE=0: per-lane stores, A/B)
+// every second / fourth lane (per-lane 8-B / 4-B stores measured 378.7k
+// against 380.7k rows/s and were removed in round 6)
 __device__ __forceinline__ void store_cols32_wave(uint32_t* __restrict__ row, uint32_t g,
                                                   uint32_t lb, const uint32_t (&o)[4],
-                                                  uint32_t lane, uint32_t wide) {
-    if (lb == 2u || !wide) {
+                                                  uint32_t lane) {
+    if (lb == 2u) {
         store_cols32(row, g, lb, o);
     } else if (lb == 1u) {
         const uint32_t a = nib_to2(o[0]) | (nib_to2(o[1]) << 16);
@@ -1499,8 +1611,8 @@ __global__ __launch_bounds__(256) void rle_moves(const uint32_t* __restrict__ fm
     }
 }
 
-// rle_moves for 4-bit sets on the packed nibbles (CPD_MOVES_SWAR, default
-// on; =0 runs the per-column kernel above — identical tables).  Per lane:
+// rle_moves for 4-bit sets on the packed nibbles (the per-column kernel
+// above serves 8- and 16-bit sets; identical tables).  Per lane:
 //   forward: only the running sets S_k (one nibble insert per column);
 //   breaks:  a run starts at column k iff S_{k-1} & f_k == 0 — the running
 //            sets shifted up a nibble (the entry set at nibble 0) AND the
@@ -1557,7 +1669,7 @@ __device__ __forceinline__ uint32_t seg4_entry_set(const Seg4& r) {
 // it belongs to, the move = that set's lowest bit.
 __device__ __forceinline__ void fill_tile4(const Seg4& r, uint32_t& carry,
                                            uint32_t* __restrict__ orow, uint32_t seg,
-                                           uint32_t lb, uint32_t lane, uint32_t emit_wide) {
+                                           uint32_t lb, uint32_t lane) {
     const bool any = (r.Z[0] | r.Z[1] | r.Z[2] | r.Z[3]) != 0u;
     const uint32_t fl = seg4_entry_set(r);
     const uint64_t m = __ballot(any);
@@ -1621,7 +1733,7 @@ __device__ __forceinline__ void fill_tile4(const Seg4& r, uint32_t& carry,
         const uint32_t b2 = ~(X[i] >> 2) & b1;
         o[i] = b0 + b1 + b2;
     }
-    store_cols32_wave(orow, seg, lb, o, lane, emit_wide);
+    store_cols32_wave(orow, seg, lb, o, lane);
     if (m) carry = (uint32_t)__shfl((int)fl, (int)__builtin_ctzll(m), 64);
 }
 
@@ -1670,7 +1782,7 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
         const uint32_t seg = t * 64u + lane;
         uint32_t v[4];
         load(seg, v);
-        fill_tile4(seg4_scan(v, strow[seg] & 0xFu), carry, orow, seg, lb, lane, 1u);
+        fill_tile4(seg4_scan(v, strow[seg] & 0xFu), carry, orow, seg, lb, lane);
     }
 }
 
@@ -1732,7 +1844,7 @@ __device__ __forceinline__ uint32_t scan32_breaks(const uint32_t (&v)[4], uint32
 __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uint32_t nseg,
                                 uint32_t ntiles, uint32_t t0, uint32_t t1, uint32_t Sin,
                                 uint8_t* ent, uint32_t* __restrict__ orow, uint32_t lb,
-                                uint32_t lane, uint32_t& breaks, uint32_t wide) {
+                                uint32_t lane, uint32_t& breaks) {
     auto load = [&](uint32_t seg, uint32_t (&v)[4]) {
         const uint4 q = f4[fm4_piece(brow, nseg, seg)];
         v[0] = q.x;
@@ -1832,7 +1944,7 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
     carry = close;
     for (uint32_t t = t1; t-- > t0;) {
         fill_tile4(seg4_scan(C[kEmitTiles - 1], ent[(t - t0) * 64u + lane]), carry, orow,
-                   t * 64u + lane, lb, lane, wide);
+                   t * 64u + lane, lb, lane);
 #pragma unroll
         for (int i = (int)kEmitTiles - 1; i >= 1; --i)
 #pragma unroll
@@ -1845,7 +1957,7 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
 __global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm, uint32_t npad,
                                                  uint32_t nrows, const uint32_t* __restrict__ out_row,
                                                  uint32_t lb, uint32_t* __restrict__ dense,
-                                                 EmitChunks ck, uint32_t wide) {
+                                                 EmitChunks ck) {
     __shared__ uint8_t ent_all[4 * 64 * kEmitTiles];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t brow = blockIdx.y * 4u + wv;
@@ -1873,7 +1985,7 @@ __global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm
     uint32_t* __restrict__ orow = dense + (size_t)out_row[brow] * (npad >> (5u - lb));
     uint32_t breaks = 0;
     const uint32_t xs = emit_chunk4(f4, brow, nseg, ntiles, t0, t1, Sin, ent_all + wv * 64u * kEmitTiles,
-                                    orow, lb, lane, breaks, wide);
+                                    orow, lb, lane, breaks);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) breaks += (uint32_t)__shfl_xor((int)breaks, o, 64);
     if (lane == 0) {
@@ -1892,8 +2004,7 @@ __global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm
 __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ fm, uint32_t npad,
                                                    uint32_t nrows, const uint32_t* __restrict__ out_row,
                                                    uint32_t lb, uint32_t* __restrict__ dense,
-                                                   EmitChunks ck, uint32_t* __restrict__ counts,
-                                                   uint32_t wide) {
+                                                   EmitChunks ck, uint32_t* __restrict__ counts) {
     __shared__ uint8_t ent[64 * kEmitTiles];
     const uint32_t row = blockIdx.x;
     if (row >= nrows) return;
@@ -1920,7 +2031,7 @@ __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ 
             const uint32_t t0 = (b + j) * kEmitTiles;
             uint32_t br = 0;
             const uint32_t xj = emit_chunk4(f4, row, nseg, ntiles, t0, min(ntiles, t0 + kEmitTiles), Sj,
-                                            ent, orow, lb, lane, br, wide);
+                                            ent, orow, lb, lane, br);
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) br += (uint32_t)__shfl_xor((int)br, o, 64);
             if (lane == j) {
@@ -2360,8 +2471,7 @@ __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
 //
 // Work is cut by RUNS, not columns: chunks of kExpandRuns consecutive runs of
 // one row (chunk_first[row] = the row's first chunk, a prefix over rows of
-// ceil(R / kExpandRuns)); a wave takes cpw consecutive chunks (CPD_EXP_CPW,
-// default kExpandCpw), loads each plus the next 8 runs (coalesced, into LDS)
+// ceil(R / kExpandRuns)); a wave takes kExpandCpw consecutive chunks, loads each plus the next 8 runs (coalesced, into LDS)
 // and writes the output words whose first column lies in the chunk:
 // [ceil(start(r0) / 8), ceil(start(r1) / 8)) — the first chunk of a row from
 // word 0, the last to the end of the row — a lane per word (the last staged
@@ -2770,124 +2880,6 @@ __device__ void wave_stats(uint64_t cost, uint32_t hops, uint32_t fin,
     }
 }
 
-// Suffix sharing between the walks of one wave (the
-// experiment behind CPD_TS_SHARE=1, dense rows, 4-slot adjacency): a wave's
-// chunk is target-sorted, and walks to one target follow one tree of CPD
-// moves, so a walk that reaches a column an earlier walk to the same target
-// passed can add that walk's remaining (cost, moves) and stop — bit-exact,
-// both being sums along one deterministic path.  Per wave, in LDS: a lossy
-// table of (column -> walk, its cost and moves so far), overwritten by every
-// hop, and the totals of the walks that finished.  A walk looks its column
-// up before each hop; a hit on a finished walk of the same row ends it.
-constexpr uint32_t kShareCols = 1024, kShareFin = 256;
-
-__global__ __launch_bounds__(64) void table_walk_share(
-    const uint2* __restrict__ adj, DenseRows rows, const uint32_t* __restrict__ qs,
-    const uint32_t* __restrict__ qt, const uint32_t* __restrict__ qrow, uint32_t nq,
-    uint32_t chunk, uint32_t limit, uint64_t* __restrict__ cost_out,
-    uint32_t* __restrict__ hops_out, uint8_t* __restrict__ fin_out,
-    unsigned long long* __restrict__ agg, unsigned long long* __restrict__ saved) {
-    __shared__ uint4 col_tab[kShareCols];  // column, walk (query) + 1, cost so far (lo, hi)
-    __shared__ uint32_t col_hops[kShareCols];
-    __shared__ uint4 fin_tab[kShareFin];   // walk + 1, row, total cost lo, hi
-    __shared__ uint32_t fin_hops[kShareFin];
-    const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t i = lane; i < kShareCols; i += 64u) col_tab[i] = make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t i = lane; i < kShareFin; i += 64u) fin_tab[i] = make_uint4(0u, 0u, 0u, 0u);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t wave = blockIdx.x;
-    const uint64_t q0l = wave * chunk;
-    const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
-    const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
-    uint64_t sum_cost = 0;
-    uint32_t sum_hops = 0, sum_fin = 0;
-    unsigned long long skipped = 0;
-    WalkState w;
-    w.q = kIdleQ;
-    w.cur = 0;
-    w.t = 0;
-    w.hops = 0;
-    w.bad = false;
-    w.cost = 0;
-    w.row = rows.dense;
-    uint32_t myrow = 0;
-    uint32_t next = q0;
-    if (q0 + lane < q1) {
-        walk_begin(w, q0 + lane, qs, qt, qrow, rows);
-        myrow = qrow[q0 + lane];
-    }
-    next = min(q1, q0 + 64u);
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    for (;;) {
-        const bool idle = w.q == kIdleQ;
-        // a column an earlier finished walk to this row passed: its suffix
-        if (!idle && w.cur != w.t && !w.bad) {
-            const uint32_t h = (w.cur * 0x9E3779B1u) >> 22;  // kShareCols = 2^10
-            const uint4 e = col_tab[h];
-            if (e.x == w.cur && e.y) {
-                const uint32_t fq = e.y - 1u;
-                const uint4 fe = fin_tab[fq & (kShareFin - 1u)];
-                if (fe.x == e.y && fe.y == myrow) {
-                    const uint32_t rest = fin_hops[fq & (kShareFin - 1u)] - col_hops[h];
-                    if (w.hops + rest <= limit) {
-                        w.cost += (((uint64_t)fe.w << 32) | fe.z) - (((uint64_t)e.w << 32) | e.z);
-                        w.hops += rest;
-                        w.cur = w.t;
-                        skipped += rest;
-                    }
-                }
-            }
-        }
-        const bool done = !idle && (w.cur == w.t || w.hops >= limit || w.bad);
-        const uint64_t m = __ballot(done);
-        if (m) {
-            if (done) {
-                const uint32_t fin = w.cur == w.t ? 1u : 0u;
-                cost_out[w.q] = w.cost;
-                hops_out[w.q] = w.hops;
-                fin_out[w.q] = (uint8_t)fin;
-                sum_cost += w.cost;
-                sum_hops += w.hops;
-                sum_fin += fin;
-                if (fin) {
-                    const uint32_t fi = w.q & (kShareFin - 1u);
-                    fin_tab[fi] = make_uint4(w.q + 1u, myrow, (uint32_t)w.cost, (uint32_t)(w.cost >> 32));
-                    fin_hops[fi] = w.hops;
-                }
-                const uint32_t nqi = next + (uint32_t)__builtin_popcountll(m & lt_mask);
-                if (nqi < q1) {
-                    walk_begin(w, nqi, qs, qt, qrow, rows);
-                    myrow = qrow[nqi];
-                } else {
-                    w.q = kIdleQ;
-                }
-            }
-            next = min(q1, next + (uint32_t)__builtin_popcountll(m));
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (!__any(w.q != kIdleQ)) break;
-        if (w.q != kIdleQ && w.cur != w.t) {  // record this column, then one hop
-            const uint32_t h = (w.cur * 0x9E3779B1u) >> 22;
-            col_tab[h] = make_uint4(w.cur, w.q + 1u, (uint32_t)w.cost, (uint32_t)(w.cost >> 32));
-            col_hops[h] = w.hops;
-        }
-        WalkState one[1] = {w};
-        walk_hops<2, 1>(one, adj, rows);
-        w = one[0];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    wave_stats(sum_cost, sum_hops, sum_fin, agg);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) skipped += __shfl_xor(skipped, o, 64);
-    if (lane == 0 && saved) atomicAdd(saved, skipped);
-}
-
 // ---------------------------------------------------------------------------
 // CPD-heuristic search (semantics restated in
 // oracle/cpd_oracle.c ora_cpd_search, [U]).
@@ -3011,17 +3003,13 @@ __global__ __launch_bounds__(256) void jump_final(JumpState a, const uint32_t* _
 
 
 struct SearchWs {
-    uint4* ent;     // [slots][2C]
-    uint4* memo;    // [slots][2C]
-    uint2* aux;     // [slots][2C]
-    uint4* hk;      // [slots][C + K] heap: f lo, f hi, column, hash slot
-    uint4* stk;     // [slots][C] walk stack: hash slot, w free, w selected, -
     uint32_t cap;   // C (power of 2)
-    // lane-major (stride != 0): slot s's arrays lie together in one block at
-    // base + s * stride (heap, ent, aux, then memo and stk with walks), so
-    // a search touches one contiguous region of a few MB instead of six
-    // regions spread over the whole workspace (fewer pages in flight per
-    // lane for the address translation); array-major above when 0
+    // slot s's arrays lie together in one block at base + s * stride: the
+    // heap (C + K entries: f lo, f hi, column, hash slot), ent and aux (2C
+    // each), then with walks memo (2C) and the walk stack (C: hash slot, w
+    // free, w selected, -) — a search touches one contiguous region of a few
+    // MB, not six spread over the workspace (array-major blocks measured
+    // 1-5% slower in round 5 and were removed in round 6)
     char* base;
     uint64_t stride;
     uint32_t lpw;  // lanes per wave that search (64 / 32 / 16 / 8)
@@ -3451,22 +3439,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const uint32_t q0 = q0l < nq ? (uint32_t)q0l : nq;
     const uint32_t q1 = (uint32_t)min((uint64_t)nq, q0l + chunk);
     const uint32_t C = ws.cap;
-    // lane-major (stride != 0): the slot's block = the heap (C + K entries),
-    // ent, aux, then memo and stk with walks; array-major: each array over
-    // all slots.  The heap pointer starts K - 1 entries in (aligned child
-    // groups).
+    // the slot's block = the heap (C + K entries), ent, aux, then memo and
+    // stk with walks.  The heap pointer starts K - 1 entries in (aligned
+    // child groups).
     char* const lb0 = ws.base + slot * ws.stride;
     const uint64_t C2 = 2ull * C, CH = (uint64_t)C + kHeapK;
-    const LaneWs W = ws.stride
-        ? LaneWs{reinterpret_cast<uint4*>(lb0 + CH * 16ull),
-                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 16ull + C2 * 24ull),
-                 reinterpret_cast<uint2*>(lb0 + CH * 16ull + C2 * 16ull),
-                 reinterpret_cast<uint4*>(lb0) + (kHeapK - 1u),
-                 TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 16ull + C2 * 40ull), C,
-                 2u * C - 1u, Tbl{lb}}
-        : LaneWs{ws.ent + slot * C2, TABLES ? nullptr : ws.memo + slot * C2, ws.aux + slot * C2,
-                 ws.hk + slot * CH + (kHeapK - 1u), TABLES ? nullptr : ws.stk + slot * C, C,
-                 2u * C - 1u, Tbl{lb}};
+    const LaneWs W{reinterpret_cast<uint4*>(lb0 + CH * 16ull),
+                   TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 16ull + C2 * 24ull),
+                   reinterpret_cast<uint2*>(lb0 + CH * 16ull + C2 * 16ull),
+                   reinterpret_cast<uint4*>(lb0) + (kHeapK - 1u),
+                   TABLES ? nullptr : reinterpret_cast<uint4*>(lb0 + CH * 16ull + C2 * 40ull), C,
+                   2u * C - 1u, Tbl{lb}};
     unsigned long long s_exp = 0, s_ins = 0, s_tou = 0, s_upd = 0, s_sur = 0, s_len = 0,
                        s_fin = 0, s_ovf = 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -3985,14 +3968,14 @@ uint32_t fm_wpb() {
     static const uint32_t v = env_u32("CPD_FM_WPB", 2);
     return v;
 }
-uint32_t fm_n4() {  // CPD_FM_N4=0: narrow first moves by the generic kernel
-    static const uint32_t v = env_u32("CPD_FM_N4", 1);
-    return v;
-}
+// narrow rows, 4-slot adjacency: first_moves_n4 (the generic
+// first_moves<4, 2, true> measured slower and is not launched)
+uint32_t fm_n4() { return 1u; }
 
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                   const uint32_t* arcs32, uint32_t slot0, uint32_t count, uint32_t* dist,
-                  const uint32_t* tgt, uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
+                  uint32_t* up, uint32_t ubase, const uint32_t* uidx, const uint32_t* tgt,
+                  uint32_t B, uint32_t slabs, const uint32_t* asc_nodes,
                   const uint32_t* asc_off, const uint32_t* asc_arcs, uint32_t* live,
                   const uint32_t* tmask, const uint32_t* adj, uint32_t shift, uint16_t* fmleaf,
                   NarrowRows nr, const uint32_t* desc, hipStream_t s) {
@@ -4004,11 +3987,12 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
         // one block per node on wide levels; narrow levels split the slabs
         const uint32_t nsplit = std::max(1u, std::min(slabs, 2048u / std::max(count, 1u)));
         const uint32_t active = slabs >= 32 ? 0xFFFFFFFFu : ((1u << slabs) - 1u);
-        launch(kern::sweep_up_sparse, dim3(count * nsplit), dim3(256), s, nodes, arc_off, arcs,
-               slot0, count, nsplit, xcd_remap(), dist, t4, B / 4u, cf, live, tmask, active);
+        launch(kern::sweep_up_sparse, dim3(count * nsplit * kern::kUpQ), dim3(64), s, nodes, arc_off, arcs,
+               slot0, count, nsplit, xcd_remap(), up, ubase, t4, B / 4u, cf, live, tmask, active);
     } else if (ascend) {
         launch(kern::sweep_level<true>, dim3(count * slabs), dim3(256), s, nodes, arc_off, arcs,
-               slot0, count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)nullptr, lf);
+               slot0, count, xcd_remap(), dist, up, ubase, uidx, t4, B / 4u, cf,
+               (const uint32_t*)nullptr, lf);
     } else {
         const uint32_t tpb = 64u * down_wpb();  // a workgroup covers 4 * tpb targets
         const dim3 grid(count * slabs * (256u / tpb)), blk(tpb);
@@ -4020,66 +4004,79 @@ void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
             const uint32_t tpb8 = 64u * wpb8;
             const dim3 g8(count * slabs * 2u / wpb8), b8(tpb8);
             launch(kern::sweep_down8, g8, b8, s, reinterpret_cast<const uint4*>(desc), arcs, slot0,
-                   count, xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live, fmleaf, nr);
+                   count, xcd_remap(), (const uint32_t*)up, t4, B / 4u, cf, (const uint32_t*)live,
+                   fmleaf, nr);
         } else
             launch(kern::sweep_level<false>, grid, blk, s, nodes, arc_off, arcs, slot0, count,
-                   xcd_remap(), dist, t4, B / 4u, cf, (const uint32_t*)live, lf);
+                   xcd_remap(), dist, up, ubase, uidx, t4, B / 4u, cf, (const uint32_t*)live, lf);
     }
 }
 
-static uint32_t up_init_blocks() {  // CPD_UP_INIT_BLOCKS: the init's grid (grid-stride)
-    static const uint32_t v = std::max(1u, env_u32("CPD_UP_INIT_BLOCKS", 512));
-    return v;
-}
+static uint32_t up_init_blocks() { return 2048u; }  // the init's grid (grid-stride, one wave each)
 
-void launch_sweep_up_init(const uint32_t* cols, uint32_t ncols, uint32_t* dist,
-                          const uint32_t* tgt, uint32_t B, uint32_t slabs, uint32_t* live,
-                          const uint32_t* tmask, hipStream_t s) {
-    if (!ncols) return;
+void launch_sweep_up_init(const uint32_t* slots, uint32_t nslots, const uint32_t* nodes,
+                          uint32_t* up, uint32_t ubase, const uint32_t* tgt, uint32_t B,
+                          uint32_t slabs, uint32_t* live, const uint32_t* tmask, hipStream_t s) {
+    if (!nslots) return;
     const uint32_t active = slabs >= 32 ? 0xFFFFFFFFu : ((1u << slabs) - 1u);
-    const uint32_t total = ncols * slabs;
-    launch(kern::sweep_up_init, dim3(std::min(total, up_init_blocks())), dim3(256), s, cols, ncols,
-           total, dist, reinterpret_cast<const uint4*>(tgt), B / 4u, live, tmask, active);
+    const uint32_t total = nslots * slabs * kern::kUpQ;
+    launch(kern::sweep_up_init, dim3(std::min(total, up_init_blocks())), dim3(64), s, slots,
+           nslots, total, nodes, up, ubase, reinterpret_cast<const uint4*>(tgt), B / 4u, live,
+           tmask, active);
 }
 
-void launch_sweep_up_chunks(const uint32_t* items, uint32_t nitems, const uint32_t* nodes,
-                            const uint32_t* arcs32, uint32_t* dist, const uint32_t* tgt, uint32_t B,
+void launch_sweep_up_chunks(const uint32_t* items, uint32_t nitems, const uint32_t* arcs32,
+                            uint32_t* up, uint32_t ubase, const uint32_t* tgt, uint32_t B,
                             uint32_t slabs, const uint32_t* asc_nodes, const uint32_t* asc_off,
                             const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
                             hipStream_t s) {
     if (!nitems) return;
     const uint32_t active = slabs >= 32 ? 0xFFFFFFFFu : ((1u << slabs) - 1u);
     const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
-    launch(kern::sweep_up_chunks, dim3(nitems * slabs), dim3(256), s,
-           reinterpret_cast<const uint4*>(items), nitems, xcd_remap(), nodes,
-           reinterpret_cast<const uint2*>(arcs32), dist, reinterpret_cast<const uint4*>(tgt),
+    launch(kern::sweep_up_chunks, dim3(nitems * slabs * kern::kUpQ), dim3(64), s,
+           reinterpret_cast<const uint4*>(items), nitems, xcd_remap(),
+           reinterpret_cast<const uint2*>(arcs32), up, ubase, reinterpret_cast<const uint4*>(tgt),
            B / 4u, cf, live, tmask, active);
+}
+
+void launch_sweep_up_narrow(const uint32_t* items, const uint32_t* item_first, uint32_t l0,
+                            uint32_t l1, const uint32_t* arcs32, uint32_t* up, uint32_t ubase,
+                            const uint32_t* tgt, uint32_t B, uint32_t slabs,
+                            const uint32_t* asc_nodes, const uint32_t* asc_off,
+                            const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
+                            uint32_t* bar, hipStream_t s) {
+    if (l1 <= l0 || !slabs) return;
+    // one-wave workgroups per quarter slab: ~1024 waves in all (an eighth
+    // of the chip's wave slots), 4 to 16 per quarter
+    const uint32_t G = std::min(16u, std::max(4u, 256u / slabs));
+    const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
+    (void)hipMemsetAsync(bar, 0, slabs * kern::kUpQ * sizeof(uint32_t), s);
+    launch(kern::sweep_up_narrow, dim3(slabs * kern::kUpQ * G), dim3(64), s,
+           reinterpret_cast<const uint4*>(items), item_first, l0, l1, G,
+           reinterpret_cast<const uint2*>(arcs32), up, ubase, reinterpret_cast<const uint4*>(tgt),
+           B / 4u, cf, live, tmask, bar);
 }
 
 uint32_t sweep_chunk_arcs() { return (uint32_t)kern::kChunk; }
 uint32_t down_desc_arcs() { return kern::kDescArcs; }
 
-void launch_count_wide_rows(const uint32_t* base, size_t total, unsigned int* out,
-                            hipStream_t s) {
-    launch(kern::count_wide_rows, dim3(2048), dim3(256), s, base, total, out);
-}
-
 void launch_target_mask(const uint32_t* tgt, uint32_t B, uint32_t* tmask, hipStream_t s) {
-    launch(kern::target_mask, dim3((B + 255u) / 256u), dim3(256), s, tgt, B, tmask);
+    launch(kern::target_mask, dim3((B + 63u) / 64u), dim3(64), s, tgt, B, tmask);
 }
 
 void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                        const uint32_t* arcs32, const uint32_t* lvl_of, uint32_t slot0,
-                       uint32_t slot1, const uint32_t* live, unsigned int* stat, hipStream_t s) {
+                       uint32_t slot1, uint32_t ubase, const uint32_t* uidx,
+                       const uint32_t* live, unsigned int* stat, hipStream_t s) {
     if (slot1 <= slot0) return;
     const dim3 grid((slot1 - slot0 + 255u) / 256u);
     const uint2* arcs = reinterpret_cast<const uint2*>(arcs32);
     if (ascend)
         launch(kern::live_stats<true>, grid, dim3(256), s, nodes, arc_off, arcs, lvl_of, slot0,
-               slot1, live, stat);
+               slot1, ubase, uidx, live, stat);
     else
         launch(kern::live_stats<false>, grid, dim3(256), s, nodes, arc_off, arcs, lvl_of, slot0,
-               slot1, live, stat);
+               slot1, ubase, uidx, live, stat);
 }
 
 uint32_t fm_bits(uint32_t shift) { return shift <= 2 ? 4u : (1u << shift); }
@@ -4108,11 +4105,7 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
     const dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u) * (256u / tpb)), blk(tpb);
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     if (nr.d16 && shift == 2 && fm_n4()) {
-        // CPD_FM_LDS (A/B): more LDS per workgroup than the stage needs caps
-        // the first moves' workgroups per CU, leaving wave slots free
-        static const uint32_t lds_min = env_u32("CPD_FM_LDS", 0);
-        launch_shm(kern::first_moves_n4<2>, grid, blk, std::max(64u * tpb, lds_min), s, adj, dist,
-                   tgt, B, n, npad,
+        launch_shm(kern::first_moves_n4<2>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n, npad,
                    xcd_remap(), fm, leafbits, fmleaf, nr, seg_order);
     } else if (nr.d16)
         launch_first_moves_t<true>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
@@ -4139,12 +4132,8 @@ void launch_rle_count(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
     }
 }
 
-uint32_t rle_ch() {  // CPD_RLE_CH=0: count with rle_scan instead of the chunked count (32 segments)
-    static const uint32_t v = env_u32("CPD_RLE_CH", 32) == 0 ? 0u : 32u;
-    return v;
-}
-
-uint32_t rle_count_chunks(uint32_t npad) { return rle_ch() ? npad / kern::kSeg / rle_ch() : 0u; }
+// the chunked count's chunks: 32 segments each (rle_count_ch<32>)
+uint32_t rle_count_chunks(uint32_t npad) { return npad / kern::kSeg / 32u; }
 
 void launch_rle_count_ch(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
                          uint8_t* rc, uint32_t* xs, uint32_t* cc, hipStream_t s) {
@@ -4174,14 +4163,10 @@ void launch_rle_emit(const uint32_t* fm, uint32_t npad, uint32_t nrows, const ui
                      uint32_t* counts, hipStream_t s) {
     if (!nrows) return;
     const kern::EmitChunks ck{xe, xs, cc};
-    static const uint32_t wide = env_u32("CPD_EMIT_WIDE", 1) ? 1u : 0u;  // 16-B table stores
-    // CPD_EMIT_LDS (A/B): extra LDS per workgroup, capping the emit's
-    // workgroups per CU so that it takes less from the sweeps beside it
-    static const uint32_t xlds = env_u32("CPD_EMIT_LDS", 0);
-    launch_shm(kern::rle_emit4, dim3(rle_emit_chunks(npad), (nrows + 3u) / 4u), dim3(256), xlds, s,
-               fm, npad, nrows, out_row, lb, dense, ck, wide);
+    launch(kern::rle_emit4, dim3(rle_emit_chunks(npad), (nrows + 3u) / 4u), dim3(256), s, fm, npad,
+           nrows, out_row, lb, dense, ck);
     launch(kern::rle_emit_fix, dim3(nrows), dim3(64), s, fm, npad, nrows, out_row, lb, dense, ck,
-           counts, wide);
+           counts);
 }
 
 void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t nrows,
@@ -4191,12 +4176,8 @@ void launch_rle_moves(const uint32_t* fm, uint32_t fmb, uint32_t npad, uint32_t 
     const uint32_t ntiles = npad / kern::kTile;
     const dim3 grid((ntiles + kern::kMoveTiles - 1u) / kern::kMoveTiles, (nrows + 3u) / 4u),
         block(256);
-    static const bool swar = env_u32("CPD_MOVES_SWAR", 1) != 0;
     switch (fmb) {
-        case 4:
-            if (swar) launch(kern::rle_moves4, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense);
-            else launch(kern::rle_moves<4>, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense);
-            break;
+        case 4: launch(kern::rle_moves4, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense); break;
         case 8: launch(kern::rle_moves<8>, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense); break;
         default: launch(kern::rle_moves<16>, grid, block, s, fm, npad, nrows, st, rc, out_row, lb, dense); break;
     }
@@ -4240,7 +4221,7 @@ void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, const uin
                         uint32_t nrows, uint32_t total_chunks, uint32_t npad, uint32_t* dense,
                         hipStream_t s) {
     if (!nrows || !total_chunks) return;
-    static const uint32_t cpw = std::max(1u, env_u32("CPD_EXP_CPW", kern::kExpandCpw));
+    constexpr uint32_t cpw = kern::kExpandCpw;
     const uint32_t waves = (total_chunks + cpw - 1u) / cpw;
     launch(kern::expand_rows, dim3((waves + 3u) / 4u), dim3(256), s, offsets, runs, chunk_first,
            nrows, total_chunks, npad / 8u, cpw, dense);
@@ -4248,7 +4229,7 @@ void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, const uin
 
 // Table-search chunking (launch parameters only; results are identical under
 // every setting): the batch is cut into chunks of ceil(nq / waves) queries (a
-// multiple of 64, at most CPD_TS_CHUNK_MAX for dense rows), CPD_TS_WAVES
+// multiple of 64, at most 1024 for dense rows), CPD_TS_WAVES
 // overriding the wave count.  Measured on the 1M-node bench (1M queries,
 // MI355X, tools_scripts/query_ab.py): dense walks want few waves that each
 // refill their lanes ~16 times (waves 1024: 88M q/s; 8192 waves, i.e. no
@@ -4258,10 +4239,6 @@ void launch_expand_rows(const uint64_t* offsets, const uint32_t* runs, const uin
 // kernels were removed in round 3.
 uint32_t ts_waves(uint32_t dflt) {
     static const uint32_t v = env_u32("CPD_TS_WAVES", 0);
-    return v ? v : dflt;
-}
-uint32_t ts_chunk_max(uint32_t dflt) {
-    static const uint32_t v = env_u32("CPD_TS_CHUNK_MAX", 0);
     return v ? v : dflt;
 }
 
@@ -4308,19 +4285,8 @@ void launch_table_search_dense(const uint32_t* adj, uint32_t shift, const uint32
                                uint32_t* hops, uint8_t* fin, unsigned long long* agg,
                                hipStream_t s) {
     const kern::DenseRows rows{dense, npad >> (5u - lb), kern::Tbl{lb}};
-    static const bool share = env_u32("CPD_TS_SHARE", 0) != 0;  // experiment
-    if (share && shift == 2 && nq) {
-        const uint64_t chunk = std::max<uint64_t>(
-            64u, std::min<uint64_t>(ts_chunk_max(1024), ((uint64_t)nq + ts_waves(1024) - 1u) /
-                                                            ts_waves(1024) + 63u) / 64u * 64u);
-        const uint32_t waves = (uint32_t)(((uint64_t)nq + chunk - 1u) / chunk);
-        launch(kern::table_walk_share, dim3(waves), dim3(64), s, reinterpret_cast<const uint2*>(adj),
-               rows, qs, qt, qrow, nq, (uint32_t)chunk, walk_limit(kmoves, n), cost, hops, fin, agg,
-               agg + 3);
-        return;
-    }
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, rows, qs, qt, qrow, nq,
-                walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(1024), ts_chunk_max(1024), s,
+                walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(1024), 1024u, s,
                 1u);
 }
 
@@ -4331,13 +4297,9 @@ void launch_table_search(const uint32_t* adj, uint32_t shift, const uint32_t* ro
                          unsigned long long* agg, hipStream_t s) {
     launch_walk(reinterpret_cast<const uint2*>(adj), shift, kern::RleRows{offsets, runs}, qs, qt,
                 qrow, nq, walk_limit(kmoves, n), cost, hops, fin, agg, ts_waves(8192),
-                ts_chunk_max(1u << 30), s, 4u);
+                1u << 30, s, 4u);
 }
 
-static bool search_lane_major() {
-    static const bool on = env_u32("CPD_SEARCH_LANE_MAJOR", 1) != 0;
-    return on;
-}
 
 // Lane slots for nq searches: at most CPD_SEARCH_WAVES (1024) one-wave
 // workgroups (64k lanes: 3,389 q/s at fscale 0 on the 1M graph against
@@ -4401,37 +4363,19 @@ void launch_cpd_search(const uint32_t* adj_f, const uint32_t* adj_w, uint32_t sh
     // r05aj: fscale 0 5.51-5.69k against 5.03k q/s)
     static const uint32_t lpw_min = std::max(8u, std::min(64u, env_u32("CPD_SEARCH_LPW_MIN", 8)));
     // (the fewest lanes, a multiple of 8, at which the slots' waves still fit
-    // one per SIMD: 1024 one-wave workgroups)
-    // (CPD_SEARCH_RESIDENT, A/B: more waves than SIMDs queue behind the
-    // resident ones)
-    static const uint32_t resident = std::max(64u, env_u32("CPD_SEARCH_RESIDENT", 1024));
+    // one per SIMD: 1024 one-wave workgroups; more waves queued behind the
+    // resident ones lost their A/B in round 5, profiles/search_resident_ab/)
+    constexpr uint32_t resident = 1024u;
     const uint32_t fit = (uint32_t)(((uint64_t)slots + resident - 1u) / resident);
     const uint32_t lpw = std::max(lpw_min, std::min(64u, (fit + 7u) / 8u * 8u));
     const uint32_t waves = slots / lpw;  // waves x lpw <= slots workspaces
-    char* p = static_cast<char*>(ws);
-    const size_t h2 = (size_t)slots * 2u * cap;
     kern::SearchWs w;
     w.cap = cap;
-    // lane-major blocks (CPD_SEARCH_LANE_MAJOR=0: array-major, A/B):
-    // search_ws_bytes_per_slot each, 128-B aligned; the heap first
+    // lane-major blocks: search_ws_bytes_per_slot each, 128-B aligned; the
+    // heap first
     w.base = static_cast<char*>(ws);
-    w.stride = search_lane_major() ? search_ws_bytes_per_slot(cap, tables) : 0u;
+    w.stride = search_ws_bytes_per_slot(cap, tables);
     w.lpw = lpw;
-    const size_t hk = (size_t)slots * (cap + kern::kHeapK);
-    w.hk = reinterpret_cast<uint4*>(p);
-    p += hk * 16u;
-    w.ent = reinterpret_cast<uint4*>(p);
-    p += h2 * 16u;
-    w.aux = reinterpret_cast<uint2*>(p);
-    p += h2 * 8u;
-    if (!tables) {
-        w.memo = reinterpret_cast<uint4*>(p);
-        p += h2 * 16u;
-        w.stk = reinterpret_cast<uint4*>(p);
-    } else {
-        w.memo = nullptr;
-        w.stk = nullptr;
-    }
     const kern::SearchOpt o{hscale, fscale, kmoves, itrs, time_ns, tick_ns};
     const kern::SearchTables tb{hrow, crow, lrow, n};
     const kern::SearchSpill sp{spill.resume, spill.rin, spill.at, spill.rout, spill.top,

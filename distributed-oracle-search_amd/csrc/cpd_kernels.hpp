@@ -16,16 +16,29 @@ void set_launch_events(hipEvent_t start, hipEvent_t stop);
 // 0xFFFF = unreachable.  Halves the bytes of the two dominant kernels.  (The
 // group-major base layout lets neighbouring slots, which gather neighbouring
 // columns, share base lines; column-major, which puts a wave's two groups in
-// one line, measured 6% slower in the down-sweep: 31.0 vs 29.1 ms/step.)  A group row whose finite spread reaches 0xFFFF is
-// stored in `dist` (32-bit) instead, with base 0xFFFFFFFE (counted by
-// launch_count_wide_rows into *ovf in timing runs).  Every finite distance
-// must stay below 0xFFFFFFFE.  d16 == nullptr: every row in `dist`.
+// one line, measured 6% slower in the down-sweep: 31.0 vs 29.1 ms/step.)  A
+// group row whose finite spread reaches 0xFFFF is stored 32-bit in a pool
+// row instead (1 KiB: the group's 256 distances), with base 0xFFFFFFFE and
+// the pool row's index in every u32 word of its d16 group row; *ovf (zeroed
+// before the down-sweep) counts the pool rows taken — past `cap` they were
+// not stored and the batch must be rebuilt narrower.  Every finite distance
+// must stay below 0xFFFFFFFE.  d16 == nullptr: every row in the dense `dist`.
 struct NarrowRows {
     uint16_t* d16;
     uint32_t* base;
     uint32_t n;
     uint32_t* ovf;
+    uint32_t* pool;
+    uint32_t cap;
 };
+
+// The up-sweep's rows live in their own compact store, up[u][B] u32 (and
+// live[u]), u = ascending slot - ubase: only nodes of upward level >= 2 (the
+// levels below are closed forms) own a row there.  Ascending arcs into such
+// nodes carry u (not the column); the down-sweep reads a node's own up row
+// at the index its descriptor word 3 (narrow) or uidx[slot] (dense) holds
+// (~0: none).  Two stores, one per batch slot, so batch k+1's up-sweep runs
+// beside batch k's down-sweep.
 
 // One CH sweep level: `count` node slots starting at `slot0` of the
 // level-ordered node list; count * slabs workgroups of 256 threads, one slab =
@@ -39,15 +52,18 @@ struct NarrowRows {
 // (launch_target_mask); B <= 32768 so that a mask fits in 32 bits.
 // fmleaf (may be null; down-sweep, 4-bit sets, shift <= 2): leaf slots take
 // their out-edges from adj and also store their first-move sets there.
+// up / ubase / uidx: the compact up store (above); dist: the dense final rows
+// (down-sweep without narrow rows only).
 void launch_sweep(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
-                  const uint32_t* arcs /* (col, w) pairs */, uint32_t slot0, uint32_t count,
-                  uint32_t* dist, const uint32_t* tgt, uint32_t B, uint32_t slabs,
+                  const uint32_t* arcs /* (col or up index, w) pairs */, uint32_t slot0,
+                  uint32_t count, uint32_t* dist, uint32_t* up, uint32_t ubase,
+                  const uint32_t* uidx, const uint32_t* tgt, uint32_t B, uint32_t slabs,
                   const uint32_t* asc_nodes, const uint32_t* asc_off, const uint32_t* asc_arcs,
                   uint32_t* live, const uint32_t* tmask, const uint32_t* adj, uint32_t shift,
                   uint16_t* fmleaf, NarrowRows nr, const uint32_t* desc, hipStream_t s);
 
 // Down-sweep slot descriptors for the narrow down-sweep (desc arg of
-// launch_sweep): 32 u32 per slot = node word, first arc, end arc, 0, then the
+// launch_sweep): 32 u32 per slot = node word, first arc, end arc, up index, then the
 // slot's first down_desc_arcs() arcs as (column, weight), (kNoEdge, 0) past
 // the end of its list; words 16.. for a level-1 node (kL1Bit): its column,
 // its number of (leaf) down-arcs, then the first 4 of them as (column,
@@ -57,22 +73,27 @@ uint32_t down_desc_arcs();
 // Narrow upward levels, chunked: items (slot, first arc, end arc, 0) of at
 // most sweep_chunk_arcs() arcs each, nitems x slabs workgroups, partial
 // minima folded in with atomicMin.  The rows of every node handled this way
-// must first be set to their leaf form by launch_sweep_up_init (cols: their
-// columns), which also seeds live[col] = tmask[col].
-void launch_sweep_up_init(const uint32_t* cols, uint32_t ncols, uint32_t* dist,
-                          const uint32_t* tgt, uint32_t B, uint32_t slabs, uint32_t* live,
-                          const uint32_t* tmask, hipStream_t s);
+// must first be set to their leaf form by launch_sweep_up_init (slots: their
+// ascending slots), which also seeds live[u] = tmask[col].
+void launch_sweep_up_init(const uint32_t* slots, uint32_t nslots, const uint32_t* nodes,
+                          uint32_t* up, uint32_t ubase, const uint32_t* tgt, uint32_t B,
+                          uint32_t slabs, uint32_t* live, const uint32_t* tmask, hipStream_t s);
 void launch_sweep_up_chunks(const uint32_t* items /* uint4 each */, uint32_t nitems,
-                            const uint32_t* nodes, const uint32_t* arcs, uint32_t* dist,
+                            const uint32_t* arcs, uint32_t* up, uint32_t ubase,
                             const uint32_t* tgt, uint32_t B, uint32_t slabs,
                             const uint32_t* asc_nodes, const uint32_t* asc_off,
                             const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
                             hipStream_t s);
+// A run of chunked levels [l0, l1) in one launch (cpd_kernels.hip
+// sweep_up_narrow): items as above, level l's at [item_first[l],
+// item_first[l + 1]); bar: slabs u32 of barrier counters (zeroed here, on s).
+void launch_sweep_up_narrow(const uint32_t* items, const uint32_t* item_first, uint32_t l0,
+                            uint32_t l1, const uint32_t* arcs, uint32_t* up, uint32_t ubase,
+                            const uint32_t* tgt, uint32_t B, uint32_t slabs,
+                            const uint32_t* asc_nodes, const uint32_t* asc_off,
+                            const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
+                            uint32_t* bar, hipStream_t s);
 uint32_t sweep_chunk_arcs();
-
-// *out += number of the `total` narrow-row bases that mark a wide row.
-void launch_count_wide_rows(const uint32_t* base, size_t total, unsigned int* out,
-                            hipStream_t s);
 
 // tmask[tgt[i]] |= 1 << (i / 1024) for i < B; tmask must be zeroed first.
 void launch_target_mask(const uint32_t* tgt, uint32_t B, uint32_t* tmask, hipStream_t s);
@@ -80,10 +101,12 @@ void launch_target_mask(const uint32_t* tgt, uint32_t B, uint32_t* tmask, hipStr
 // Row counts behind the live masks for the bytes model (timing runs): over
 // node slots [slot0, slot1) of one sweep direction, stat[2 * lvl_of[slot]]
 // += rows stored (up) / own rows read (down), stat[2 * lvl + 1] += rows
-// gathered (up).  stat must be zeroed by the caller.
+// gathered (up).  stat must be zeroed by the caller.  live is indexed by up
+// index: slot - ubase (ascending), uidx[slot] (descending).
 void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_off,
                        const uint32_t* arcs, const uint32_t* lvl_of, uint32_t slot0,
-                       uint32_t slot1, const uint32_t* live, unsigned int* stat, hipStream_t s);
+                       uint32_t slot1, uint32_t ubase, const uint32_t* uidx,
+                       const uint32_t* live, unsigned int* stat, hipStream_t s);
 
 // Bits per first-move set for a packed adjacency of 2^shift slots per column:
 // max(4, 2^shift) (>= the max out-degree); sets are stored 32/bits per u32.
@@ -160,7 +183,7 @@ void launch_moves_runs(const uint32_t* dense, uint32_t stride, uint32_t lb, uint
 // are too long for that to be cheap: the caller then runs launch_rle_count
 // on the batch instead.  cc: nrows x rle_count_chunks(npad) u32; xs: twice
 // that (the chunks' exit states, then their guessed entry states).
-// rle_count_chunks = 0: off (CPD_RLE_CH=0), use launch_rle_count.
+// (8- and 16-bit sets use launch_rle_count.)
 uint32_t rle_count_chunks(uint32_t npad);
 void launch_rle_count_ch(const uint32_t* fm, uint32_t npad, uint32_t nrows, uint32_t* st,
                          uint8_t* rc, uint32_t* xs, uint32_t* cc, hipStream_t s);

@@ -1,5 +1,7 @@
 // Host utilities behind the C ABI: error channel, partitioner, DFS column
 // order, CSR validation, distance bound, synthetic road graphs.
+#include <sys/statvfs.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -344,6 +346,34 @@ int cpd_partition(uint32_t nodenum, uint32_t maxworker, int method, uint32_t key
     *bidx = i;
     *wid = b % maxworker;
     return CPD_OK;
+}
+
+int cpd_bucket_bytes(uint32_t n, uint32_t bits, uint64_t nrows, uint32_t nbuckets,
+                     uint32_t stripes, uint64_t* bytes) {
+    return guarded([&] {
+        CPD_REQUIRE(bytes && (bits == 1 || bits == 2 || bits == 4) && stripes >= 1, CPD_E_ARG,
+                    "bucket bytes: bits must be 1, 2 or 4, stripes >= 1");
+        // rows at ceil(n bits / 32) words, 8 B of target + count per row, a
+        // header per bucket file (rounded to 4 KiB; DOSCPD02 pads its rows to
+        // 4 KiB) and per part file a block of slack
+        const uint64_t words = ((uint64_t)n * bits + 31u) / 32u;
+        *bytes = nrows * (4ull * words + 8ull) + (uint64_t)nbuckets * (1ull + stripes) * 4096ull;
+    });
+}
+
+int cpd_space_check(const char* dir, uint64_t bytes, uint64_t* avail) {
+    return guarded([&] {
+        CPD_REQUIRE(dir, CPD_E_ARG, "space check: null directory");
+        struct statvfs sv {};
+        if (::statvfs(dir, &sv) != 0)
+            throw Error(CPD_E_IO, std::string("cannot stat the file system of ") + dir);
+        const uint64_t have = (uint64_t)sv.f_bavail * (uint64_t)sv.f_frsize;
+        if (avail) *avail = have;
+        if (have < bytes)
+            throw Error(CPD_E_IO, std::string(dir) + " has " + std::to_string(have >> 20) +
+                                      " MiB free, the worker's bucket files need " +
+                                      std::to_string((bytes + (1u << 20) - 1) >> 20) + " MiB");
+    });
 }
 
 int cpd_dfs_preorder(uint32_t n, const uint32_t* row_ptr, const uint32_t* dst,

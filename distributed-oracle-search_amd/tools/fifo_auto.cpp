@@ -230,7 +230,13 @@ int main(int argc, char** argv) {
                 if (all_compact && !targets.empty() && move_bits) {
                     const uint64_t npad = (n0 + 2047ull) / 2048ull * 2048ull;
                     const uint64_t bytes = (uint64_t)targets.size() * (npad * move_bits / 32ull) * 4ull;
-                    arena = cpd_device_arena(device, bytes + (1ull << 20), 0) == CPD_OK;
+                    // only for an index that will be dense (--index rle keeps
+                    // runs; auto takes tables when the runs weigh more — the
+                    // index's own test): an unused arena would hold HBM the
+                    // search workspace is sized from
+                    const std::string im0 = a.str("index", "auto");
+                    const bool dense = im0 == "dense" || (im0 != "rle" && 4ull * total_runs > bytes);
+                    if (dense) arena = cpd_device_arena(device, bytes + (1ull << 20), 0) == CPD_OK;
                 }
             }
             if (dev_rc != CPD_OK) dev_err = cpd_last_error();

@@ -401,6 +401,58 @@ int main(int argc, char** argv) {
         uint64_t fp = cpd::io::graph_fingerprint(g.n, g.row_ptr.data(), g.dst.data(), g.w.data());
         double t_read = now() - t_start;
 
+        // owned buckets
+        uint32_t nb = 0;
+        cli::check(cpd_partition_nbuckets(g.n, mcode, (uint32_t)key, &nb), "buckets");
+        std::vector<uint32_t> owned;
+        for (uint32_t b = 0; b < nb; ++b)
+            if (b % (uint32_t)W == (uint32_t)wid) owned.push_back(b);
+        uint32_t chunk = (uint32_t)(((uint64_t)g.n + key - 1) / key);
+        // --targets-from SCEN: only the rows some query of the scenario needs
+        // (its "q s t" targets; process_query.py:56-57 routes by t), so a
+        // partial CPD for a known workload stays small on disk
+        std::vector<char> wanted;
+        if (a.has("targets-from")) {
+            wanted.assign(g.n, 0);
+            for (const auto& q : cpd::io::read_scen(a.str("targets-from"))) {
+                if (q.second >= g.n) throw std::runtime_error("scenario target out of range");
+                wanted[q.second] = 1;
+            }
+        }
+        auto bucket_nodes = [&](uint32_t b) {
+            std::vector<uint32_t> v;
+            auto keep = [&](uint64_t x) {
+                if (wanted.empty() || wanted[x]) v.push_back((uint32_t)x);
+            };
+            if (mcode == CPD_PART_MOD) {
+                for (uint64_t x = b; x < g.n; x += (uint64_t)key) keep(x);
+            } else {
+                for (uint64_t x = (uint64_t)b * chunk; x < std::min<uint64_t>(g.n, (uint64_t)(b + 1) * chunk); ++x)
+                    keep(x);
+            }
+            return v;
+        };
+
+        // Disk preflight: every owned row's bucket files must fit --outdir
+        // before the plan and the GPU work start (eight `div 8` workers of the
+        // 1M graph write 250 GB at once; a full disk would otherwise surface
+        // as a write error minutes in).  The rle layout's size depends on the
+        // runs, unknown before the build: not checked.
+        if (moves && !a.has("discard") && !a.has("plan-only")) {
+            uint64_t nrows = 0;
+            for (uint32_t b : owned) nrows += bucket_nodes(b).size();
+            uint32_t maxdeg = 1;
+            for (uint32_t v = 0; v < g.n; ++v) maxdeg = std::max(maxdeg, g.row_ptr[v + 1] - g.row_ptr[v]);
+            const uint32_t bits = maxdeg <= 2 ? 1u : maxdeg <= 4 ? 2u : 4u;
+            uint64_t need = 0, have = 0;
+            cli::check(cpd_bucket_bytes(g.n, bits, nrows, (uint32_t)owned.size(), stripes, &need),
+                       "bucket bytes");
+            if (cpd_space_check(outdir.c_str(), need, &have) != CPD_OK) {
+                std::fprintf(stderr, "make_cpd_auto: %s\n", cpd_last_error());
+                return 3;
+            }
+        }
+
         // host preprocessing (column order + hierarchy), cached per graph
         char fph[32];
         std::snprintf(fph, sizeof fph, "%016llx", (unsigned long long)fp);
@@ -493,38 +545,6 @@ int main(int argc, char** argv) {
         cli::check(cpd_plan_info_get(plan, &info), "plan info");
         std::vector<uint32_t> order(g.n);
         cli::check(cpd_plan_order(plan, order.data()), "order");
-
-        // owned buckets
-        uint32_t nb = 0;
-        cli::check(cpd_partition_nbuckets(g.n, mcode, (uint32_t)key, &nb), "buckets");
-        std::vector<uint32_t> owned;
-        for (uint32_t b = 0; b < nb; ++b)
-            if (b % (uint32_t)W == (uint32_t)wid) owned.push_back(b);
-        uint32_t chunk = (uint32_t)(((uint64_t)g.n + key - 1) / key);
-        // --targets-from SCEN: only the rows some query of the scenario needs
-        // (its "q s t" targets; process_query.py:56-57 routes by t), so a
-        // partial CPD for a known workload stays small on disk
-        std::vector<char> wanted;
-        if (a.has("targets-from")) {
-            wanted.assign(g.n, 0);
-            for (const auto& q : cpd::io::read_scen(a.str("targets-from"))) {
-                if (q.second >= g.n) throw std::runtime_error("scenario target out of range");
-                wanted[q.second] = 1;
-            }
-        }
-        auto bucket_nodes = [&](uint32_t b) {
-            std::vector<uint32_t> v;
-            auto keep = [&](uint64_t x) {
-                if (wanted.empty() || wanted[x]) v.push_back((uint32_t)x);
-            };
-            if (mcode == CPD_PART_MOD) {
-                for (uint64_t x = b; x < g.n; x += (uint64_t)key) keep(x);
-            } else {
-                for (uint64_t x = (uint64_t)b * chunk; x < std::min<uint64_t>(g.n, (uint64_t)(b + 1) * chunk); ++x)
-                    keep(x);
-            }
-            return v;
-        };
 
         if (ndev == 0) {
             std::fprintf(stderr, "make_cpd_auto: no GPU visible (this build has no CPU path)\n");

@@ -78,6 +78,17 @@ int cpd_partition(uint32_t nodenum, uint32_t maxworker, int method,
 int cpd_partition_nbuckets(uint32_t nodenum, int method, uint32_t key,
                            uint32_t* nbuckets);
 
+/* [host] Disk preflight of a make_cpd_auto worker (make_cpds.py:58-60 starts
+ * every worker at once, each writing its buckets into one --outdir; VERDICT
+ * r05 item 2).  cpd_bucket_bytes: bytes of nrows compact rows at `bits` per
+ * column (DOSCPD02/03) in nbuckets bucket files of `stripes` parts, headers
+ * included.  cpd_space_check: CPD_E_IO (the numbers in cpd_last_error) when
+ * the file system holding `dir` has fewer than `bytes` bytes available to
+ * this user; *avail (may be NULL) = what it has.                             */
+int cpd_bucket_bytes(uint32_t n, uint32_t bits, uint64_t nrows, uint32_t nbuckets,
+                     uint32_t stripes, uint64_t* bytes);
+int cpd_space_check(const char* dir, uint64_t bytes, uint64_t* avail);
+
 /* [host] DFS-preorder column order — replaces warthog
  * cpd::compute_dfs_preorder [U]: iterative DFS from node 0 (then from every
  * still-unvisited node in id order), out-edges pushed in file order, so the

@@ -136,7 +136,7 @@ def test_move_naming_no_edge_stops_walk(env, mode):
     r = runs[: int(off[1])].copy()
     r = (r & ~np.uint32(0xF)) | np.uint32(15)   # every move = 15: no such edge
     ix = cpd.Index.streamed(dev, targets[:1], len(r), mode=mode)
-    if mode == "dense" and dev.move_bits() < 4 and os.environ.get("CPD_TABLE_BITS") != "4":
+    if mode == "dense" and dev.move_bits() < 4:
         # this graph's tables hold 1- or 2-bit moves: such a row is refused,
         # never truncated into a move that names a real edge
         with pytest.raises(cpd.CpdError) as ei:
@@ -190,7 +190,7 @@ def test_compact_rows_wider_than_tables(env, mode):
     out-degree <= 4): valid rows are repacked bit-exact; a row carrying a move
     the tables cannot hold is refused (never truncated)."""
     g, plan, dev, targets, off, runs = env[:6]
-    if dev.move_bits() == 4 or os.environ.get("CPD_TABLE_BITS") == "4":
+    if dev.move_bits() == 4:
         pytest.skip("this graph's tables are 4-bit")
     k = 5
     mv4 = oracle.moves_from_runs(off[:k + 1], runs, g.n, 4)

@@ -113,6 +113,9 @@ def test_search_overflow_is_counted_tables(env):
     np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small])
     assert (fin[rs[:, 1] > cap] == 2).all()  # stopped on the workspace, not unfinished
     assert int((fin == 2).sum()) == st["overflow"]
+    # the sums hold every query's counters, overflowed ones included
+    assert st["expanded"] == int(cnt[:, 0].astype(np.uint64).sum())
+    assert st["inserted"] == int(cnt[:, 1].astype(np.uint64).sum())
 
 
 def test_search_overflow_is_counted_walks(env):
@@ -133,6 +136,8 @@ def test_search_overflow_is_counted_walks(env):
     np.testing.assert_array_equal(cnt[small].astype(np.uint64), rs[small, :5])
     assert (fin[rs[:, 5] > cap] == 2).all()
     assert int((fin == 2).sum()) == st["overflow"]
+    assert st["expanded"] == int(cnt[:, 0].astype(np.uint64).sum())
+    assert st["inserted"] == int(cnt[:, 1].astype(np.uint64).sum())
 
 
 @pytest.mark.parametrize("form", ["tables", "walks"])
@@ -160,9 +165,10 @@ def test_search_capacity_escalation(env, form):
     assert st["expanded"] == int(rs[:, 0].sum()) and st["inserted"] == int(rs[:, 1].sum())
     assert st["finished"] == int(rf.sum()) and st["plen"] == int(rp[rf == 1].sum())
     # a capacity_max that still leaves some overflowing: those report 2
-    _, _, fin3, _, st3 = ix.search(s, t, capacity=64, capacity_max=256, tables=form)
+    _, _, fin3, cnt3, st3 = ix.search(s, t, capacity=64, capacity_max=256, tables=form)
     assert int((fin3 == 2).sum()) == st3["overflow"] <= st1["overflow"]
     assert not (fin3 == 3).any()
+    assert st3["expanded"] == int(cnt3[:, 0].astype(np.uint64).sum())
 
 
 @pytest.mark.parametrize("form", ["tables", "walks"])
@@ -197,6 +203,8 @@ def test_search_capacity_max_beyond_hbm(env):
                                          workspace_frac=2e-5)
     assert st["capacity_last"] < (1 << 24)
     assert int((fin == 2).sum()) == st["overflow"]
+    assert st["expanded"] == int(cnt[:, 0].astype(np.uint64).sum())
+    assert st["touched"] == int(cnt[:, 2].astype(np.uint64).sum())
     ok = fin != 2
     assert ok.sum() > 100
     np.testing.assert_array_equal(cost[ok], rc[ok])

@@ -201,3 +201,48 @@ def test_tools_roundtrip_and_fail_loudly(tmp_path):
                             "--maxworker", "2", "--outdir", str(tmp_path / "idx")],
                            capture_output=True, text=True)
         assert p.returncode != 0 and "no GPU" in p.stderr
+
+
+def test_space_preflight_library():
+    """cpd_bucket_bytes / cpd_space_check (make_cpd_auto's disk preflight):
+    the row bytes of a worker's compact buckets, and CPD_E_IO with the numbers
+    when a tmpfs cannot hold them."""
+    # 1M nodes at 2 bits: 62500 words per row; + target and count per row
+    b = cpd.bucket_bytes(1_000_000, 2, 125_000, nbuckets=1, stripes=16)
+    assert b == 125_000 * (4 * 62_500 + 8) + 17 * 4096
+    assert cpd.bucket_bytes(10, 1, 0, nbuckets=2, stripes=1) == 2 * 2 * 4096
+    free = cpd.space_check("/dev/shm", 1)
+    assert free > 0
+    with pytest.raises(cpd.CpdError) as e:
+        cpd.space_check("/dev/shm", free + (1 << 40))
+    assert "error -6" in str(e.value) and "MiB free" in str(e.value)
+    with pytest.raises(cpd.CpdError):
+        cpd.space_check("/no/such/dir/for/cpd", 1)
+
+
+def test_make_cpd_auto_refuses_a_disk_too_small(tmp_path):
+    """A worker whose bucket files outgrow --outdir (a tmpfs here) exits with
+    status 3 and a one-line message before any plan or GPU work — not with a
+    write error minutes in."""
+    shm = "/dev/shm"
+    free = os.statvfs(shm).f_bavail * os.statvfs(shm).f_frsize
+    # one worker owning every row: n^2 / 4 bytes at 2 bits per column
+    width = int(np.ceil(np.sqrt(np.sqrt(6.0 * free))))
+    if width > 1400:
+        pytest.skip(f"{shm} has {free >> 30} GiB free: the graph would be too large")
+    prefix = str(tmp_path / "big")
+    subprocess.run([os.path.join(ROOT, "bin", "gen_synth"), "--width", str(width), "--height",
+                    str(width), "--seed", "4", "--out", prefix], check=True,
+                   capture_output=True, timeout=300)
+    out = os.path.join(shm, f"cpd_preflight_{os.getpid()}")
+    try:
+        p = subprocess.run([os.path.join(ROOT, "bin", "make_cpd_auto"), "--input", prefix + ".xy",
+                            "--partmethod", "div", "--partkey", "1", "--workerid", "0",
+                            "--maxworker", "1", "--outdir", out],
+                           capture_output=True, text=True, timeout=120)
+        assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+        msg = p.stderr.strip().splitlines()
+        assert len(msg) == 1 and "MiB free" in msg[0] and "need" in msg[0], p.stderr
+        assert not [f for f in os.listdir(out) if f.endswith(".plan") or ".cpd" in f]
+    finally:
+        subprocess.run(["rm", "-rf", out])
