@@ -437,7 +437,7 @@ def step_pmc(traffic, step_s):
 
 
 # libcpd reports these counters through the timing table (launches = count)
-_COUNTERS = ("wide_rows", "group_rows", "emit_sets")
+_COUNTERS = ("wide_rows", "group_rows", "emit_sets", "pool_rebuilds")
 
 
 # --------------------------------------------------------------------------

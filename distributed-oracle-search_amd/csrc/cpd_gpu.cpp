@@ -366,8 +366,9 @@ struct cpd_graph {
     // lane of the caller's target i; stat: per-level sweep counters (timing
     // runs; 2 per launch: stored / own rows, gathered rows), stat_h its host
     // copy; up_late: (level, arcs, nodes) of the up levels whose bytes wait
-    // for it.  ev_fm[slot] marks the end of the slot's batch (its first moves
-    // are the last reader of its targets, up store and stats).
+    // for it.  ev_fm[slot] marks the end of the slot's batch (its first
+    // moves); its down-sweep is the last reader of its up store, live and
+    // target masks and stats, and first moves read the targets from fm_tgt.
     struct BatchSlot {
         DevBuf<uint32_t> tgt;
         std::vector<uint32_t> pos_of, tgt_col;
@@ -377,6 +378,7 @@ struct cpd_graph {
         std::vector<std::array<double, 3>> up_late;
     };
     BatchSlot bs[2];
+    DevBuf<uint32_t> fm_tgt;  // the targets of the batch whose first moves are queued
     // Timing runs: a batch's sweep bytes that depend on its live-row counts
     // (stat_h, copied out after its first moves), folded into agg once those
     // have landed — at the end of the next batch, or at timing_get / reset.
@@ -620,6 +622,7 @@ struct cpd_graph {
             b.tgt.alloc(B);
             b.tgt_h.alloc(B);
         }
+        fm_tgt.alloc(B);
         counts.alloc(B);
         rle_hard_h.alloc(1);
         ovf_hb.alloc(1);
@@ -1083,7 +1086,9 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         int ncu = 0;
         HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
         create_cu_stream(&g->stream, q, ncu, false);
-        // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step)
+        // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step
+        // in round 5, 374.6-375.9k against 375.2-375.9k rows/s with the
+        // one-wave emit, profiles/up_store_ab/r06k_*)
         create_cu_stream(&g->estream, q, ncu, false);
         if (q) {
             create_cu_stream(&g->ustream, q, ncu, true);
@@ -1601,6 +1606,13 @@ void launch_down(cpd_graph* g, uint32_t k, bool narrow, uint32_t slot) {
                               stat + 2 * nasc, g->stream);
         });
     }
+    // the slot is free for the batch after next once these land: its targets
+    // copied for the first moves, the stats copied out
+    HIP_CHECK(hipMemcpyAsync(g->fm_tgt.p, S.tgt.p, (size_t)B * sizeof(uint32_t),
+                             hipMemcpyDeviceToDevice, g->stream));
+    if (stat)
+        HIP_CHECK(hipMemcpyAsync(S.stat_h.p, stat, S.stat.n * sizeof(unsigned int),
+                                 hipMemcpyDeviceToHost, g->stream));
     HIP_CHECK(hipEventRecord(g->ev_down, g->stream));
 }
 
@@ -1608,10 +1620,8 @@ void launch_down(cpd_graph* g, uint32_t k, bool narrow, uint32_t slot) {
 // down-sweep on g->stream), then ev_fm[slot]; the timing stats' copy.
 void launch_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slot) {
     const uint32_t B = g->B, n = g->n;
-    auto& S = g->bs[slot];
     const NarrowRows nr = g->narrow_rows(narrow);
     const double drow = narrow ? 2.0 + 4.0 / 256.0 : 4.0;
-    unsigned int* stat = g->timing ? S.stat.p : nullptr;
     // per row: own distance 4n (kernels that read it) + neighbour distances
     // 4m + first-move write npad * fmb / 8; the packed adjacency (8 B per
     // slot) is read once per 1024-target slab.  Leaf columns (leaf_fm) read
@@ -1624,13 +1634,10 @@ void launch_fm(cpd_graph* g, uint32_t k, bool narrow, uint32_t* fm, uint32_t slo
             (fslabs * 1024.0) +
         8.0 * (double)(n - nl) * (double)(1u << g->adj_shift) * fslabs + 4.0 * g->npad / 32.0;
     g->timed("first_moves", fbytes, [&] {
-        launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, S.tgt.p, B, k, n, g->npad,
+        launch_first_moves(g->adj.p, g->adj_shift, g->dist.p, g->fm_tgt.p, B, k, n, g->npad,
                            fm, g->leaf_fm ? g->leafbits.p : nullptr,
                            g->leaf_fm ? g->fmleaf.p : nullptr, nr, g->stream, g->seg_order.p);
     });
-    if (stat)
-        HIP_CHECK(hipMemcpyAsync(S.stat_h.p, stat, S.stat.n * sizeof(unsigned int),
-                                 hipMemcpyDeviceToHost, g->stream));
     HIP_CHECK(hipEventRecord(g->ev_fm[slot], g->stream));
 }
 
@@ -1703,11 +1710,14 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t 
 }
 
 
-// CPD_UP_PERSIST=0: every chunked up level its own launch (A/B; identical
-// rows).  Default: runs of levels of at most kPersistItems chunk items in
-// one launch (sweep_up_narrow).
+// CPD_UP_PERSIST=1 (A/B): runs of chunked up levels of at most
+// kPersistItems items in one persistent launch (sweep_up_narrow) instead of
+// a launch each (identical rows).
 bool up_persist_on() {
-    static const bool on = env_on("CPD_UP_PERSIST");
+    static const bool on = [] {
+        const char* e = std::getenv("CPD_UP_PERSIST");
+        return e && *e == '1';
+    }();
     return on;
 }
 
@@ -1753,15 +1763,20 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
     const double st_row = 5.0 * npad / 32.0;
     const bool narrow = g->narrow;
     // The next batch's up-sweep (ustream, high priority) into the other slot,
-    // after that slot's last batch (its first moves: the last reader of the
-    // slot's targets and up store).  Queued before this down-sweep, so that
-    // the host's launch latency never delays it: its wide levels run beside
-    // this down-sweep's narrow top levels, its narrow latency-bound levels
-    // beside the wide ones.
+    // after that slot's last batch's down-sweep (the last reader of the
+    // slot's targets, up store, masks and stats; its first moves read the
+    // targets from fm_tgt).  The host queues it as soon as this batch starts:
+    // it runs beside the previous batch's first moves, ahead of this
+    // down-sweep, which the host's launch latency then never delays.
     const uint32_t ns = slot ^ 1u;
     if (next && next_k && overlap_on()) {
         prepare_targets(g, next, next_k, ns);
-        HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_fm[ns], 0));
+        // after the other slot's last batch: its down-sweep (ev_down, not yet
+        // re-recorded for this batch), so this up-sweep runs beside its first
+        // moves (after them, ev_fm[ns], it ran beside this down-sweep: the
+        // same rows/s within noise, 371.9-376.9k against 374.6-377.1k, and
+        // the down-sweep's launches 9% longer, profiles/up_store_ab/r06k_*)
+        HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
         upload_targets(g, next, next_k, ns, g->ustream, true);
         launch_up(g, next_k, ns, g->ustream);
         HIP_CHECK(hipEventRecord(g->ev_up, g->ustream));
@@ -1806,6 +1821,7 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         // of pool_cap / (4 n) slabs, whose group rows all fit the pool.
         HIP_CHECK(hipStreamSynchronize(g->stream));
         g->drop_prep();
+        if (g->timing) g->agg["pool_rebuilds"].launches += 1;
         if (trace_on())
             std::fprintf(stderr, "[cpd] batch of %u rows: %u wide group rows past the pool's %u, rebuilt\n",
                          k, g->ovf_h(), g->pool_cap);

@@ -1376,7 +1376,7 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
 // tile: a wave writes 1 KiB contiguous.
 constexpr uint32_t kMoveTiles = 16;
 #ifndef CPD_EMIT_TILES
-#define CPD_EMIT_TILES 16
+#define CPD_EMIT_TILES 2
 #endif
 // tiles per chunk of the fused emit (its chunk lives in 4 * kEmitTiles VGPRs)
 constexpr uint32_t kEmitTiles = CPD_EMIT_TILES;
@@ -1953,19 +1953,28 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
     return exitS;
 }
 
-// wave per (row, chunk of kEmitTiles tiles); 4 waves per workgroup = 4 rows
-__global__ __launch_bounds__(256) void rle_emit4(const uint32_t* __restrict__ fm, uint32_t npad,
-                                                 uint32_t nrows, const uint32_t* __restrict__ out_row,
-                                                 uint32_t lb, uint32_t* __restrict__ dense,
-                                                 EmitChunks ck) {
-    __shared__ uint8_t ent_all[4 * 64 * kEmitTiles];
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t brow = blockIdx.y * 4u + wv;
-    const uint32_t lane = threadIdx.x & 63u;
-    if (brow >= nrows) return;  // wave-uniform
+// A one-wave workgroup per (row, chunk of kEmitTiles tiles).  The emit runs
+// beside the next batches' sweeps on its own stream; as four-wave workgroups
+// of 129-VGPR waves it waited for four SIMDs of a CU to free room at once
+// while the sweeps' smaller waves refilled every hole, and one launch
+// stretched over 70-90 ms (round 6 traces).  Logical blocks: row group
+// (4 rows sharing the 64-B sectors of the interleaved layout) outermost,
+// then chunk, then the group's 4 rows, XCD-remapped so that the 4 waves of
+// one (group, chunk) run together on one XCD and share its L2 lines.
+__global__ __launch_bounds__(64) void rle_emit4(const uint32_t* __restrict__ fm, uint32_t npad,
+                                                uint32_t nrows, const uint32_t* __restrict__ out_row,
+                                                uint32_t lb, uint32_t* __restrict__ dense,
+                                                EmitChunks ck, uint32_t remap) {
+    __shared__ uint8_t ent_all[64 * kEmitTiles];
     const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
     const uint32_t nch = (ntiles + kEmitTiles - 1u) / kEmitTiles;
-    const uint32_t ch = blockIdx.x;
+    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t rg = L / (4u * nch), rest = L - rg * 4u * nch;
+    const uint32_t ch = rest >> 2;
+    const uint32_t brow = rg * 4u + (rest & 3u);
+    const uint32_t lane = threadIdx.x & 63u;
+    constexpr uint32_t wv = 0;
+    if (brow >= nrows) return;  // wave-uniform
     const uint32_t t0 = ch * kEmitTiles;
     if (t0 >= ntiles) return;
     const uint32_t t1 = min(ntiles, t0 + kEmitTiles);
@@ -2047,6 +2056,311 @@ __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ 
         carry = (uint32_t)__shfl((int)ex, 63, 64);
     }
     if (lane == 0) counts[row] = total + 1u;  // + the row's first run
+}
+
+// ---------------------------------------------------------------------------
+// The fused emit, eight rows per wave (round 6).  rle_emit4's wave scanned
+// one row, so each greedy step moved one 4-bit set: ~17 VALU instructions
+// per (row, column), and the emit, ALU-bound, took 15 ms of every step's
+// CUs.  Here a lane holds one COLUMN of eight rows per 32-bit word (nibble i
+// = row 8·oct + i; the 64-B sectors of the two row groups transposed in
+// registers, three byte/nibble swap stages per 8x8 block), and one step of
+// the scan — T = S & F, a zero-nibble test, S = T, or F where T is empty —
+// advances all eight rows in nine instructions.  Lane L owns the 64 columns
+// [c0 + 64 L, c0 + 64 L + 64) of a 4096-column chunk (kEmitTiles tiles: the
+// chunk of rle_emit_fix and emit_chunk4):
+//   guess    the running sets entering the lane: the 16 columns before it
+//            scanned from a wildcard (lane 0: the previous chunk's last 16,
+//            the chunk's guessed entry; a wildcard for chunk 0);
+//   forward  its 64 columns from that entry, each running set to LDS (16 KiB
+//            per wave); a lane whose entry differs from lane L-1's exit scans
+//            again from that exit (lane 0 keeps the chunk's entry) until no
+//            lane changes;
+//   ahead    the closing sets of the runs open at the chunk's right edge:
+//            the following columns one per lane, a prefix-AND from the
+//            chunk's exit, the first empty set per row;
+//   backward right to left, each column's closing set (the set at the last
+//            column of its run; a run ends before a break: S_c & S_c+1 is
+//            empty), the breaks counted; the lane's trailing run is left
+//            empty;
+//   tails    the trailing run closes where the first lane to the right has,
+//            per row, a break: at its column 0 with the lane's entry set,
+//            else with that lane's first run's closing set; past the last
+//            lane with the ahead set (a suffix scan over the lanes);
+//   store    the lowest set bit per nibble, neighbouring columns merged to
+//            the table's 1/2/4-bit fields and transposed back to rows: one
+//            8-, 16- or 32-B store per row and lane, a wave writing 0.5-2
+//            KiB contiguous per row.
+// It records per (row, chunk) what rle_emit4 recorded (guessed entry, exit,
+// breaks), so rle_emit_fix repairs a wrong chunk guess as before.
+__device__ __forceinline__ uint32_t zero_nib(uint32_t a) {  // bit 3 of nibble k: nibble k is 0
+    return ~(((a & 0x77777777u) + 0x77777777u) | a) & 0x88888888u;
+}
+__device__ __forceinline__ uint32_t nib_mask(uint32_t z) {  // bit-3 flags -> whole nibbles
+    return z | (z - (z >> 3));
+}
+__device__ __forceinline__ uint32_t step8(uint32_t S, uint32_t F) {  // one column, 8 rows
+    const uint32_t T = S & F;
+    return T | (F & nib_mask(zero_nib(T)));
+}
+// 8x8 nibble transpose: nibble k of a[r] <-> nibble r of a[k] (the index bits
+// 2, 1, 0 of word and nibble swapped in turn: half words, bytes, nibbles)
+__device__ __forceinline__ void tr8(uint32_t (&a)[8]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t x = a[r], y = a[r + 4];
+        a[r] = __builtin_amdgcn_perm(y, x, 0x05040100u);
+        a[r + 4] = __builtin_amdgcn_perm(y, x, 0x07060302u);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = (i & 1) | ((i & 2) << 1);  // 0, 1, 4, 5
+        const uint32_t x = a[r], y = a[r + 2];
+        a[r] = __builtin_amdgcn_perm(y, x, 0x06020400u);
+        a[r + 2] = __builtin_amdgcn_perm(y, x, 0x07030501u);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) {
+        const uint32_t x = a[r], y = a[r + 1];
+        a[r] = (x & 0x0F0F0F0Fu) | ((y << 4) & 0xF0F0F0F0u);
+        a[r + 1] = ((x >> 4) & 0x0F0F0F0Fu) | (y & 0xF0F0F0F0u);
+    }
+}
+__device__ __forceinline__ uint32_t low_bits8(uint32_t X) {  // lowest set bit of every nibble
+    const uint32_t b0 = ~X & 0x11111111u;
+    const uint32_t b1 = ~(X >> 1) & b0;
+    const uint32_t b2 = ~(X >> 2) & b1;
+    return b0 + b1 + b2;
+}
+
+constexpr uint32_t kE8Cols = 64;  // columns per lane
+static_assert(kEmitTiles * kTile == 64u * kE8Cols, "a chunk is 64 lanes x kE8Cols columns");
+
+template <uint32_t LB>
+__global__ __launch_bounds__(64) void rle_emit8(const uint32_t* __restrict__ fm, uint32_t npad,
+                                                uint32_t nrows, const uint32_t* __restrict__ out_row,
+                                                uint32_t* __restrict__ dense, EmitChunks ck,
+                                                uint32_t remap) {
+    __shared__ uint32_t run_set[kE8Cols * 64u];  // [column][lane]
+    const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
+    const uint32_t nch = (ntiles + kEmitTiles - 1u) / kEmitTiles;
+    const uint32_t Lb = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t oct = Lb / nch, ch = Lb - oct * nch;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t r0 = oct * 8u;
+    if (r0 >= nrows) return;  // wave-uniform
+    const uint32_t c0 = ch * kEmitTiles * kTile;
+    const uint32_t cl = c0 + lane * kE8Cols;   // the lane's first column
+    const bool have = cl < npad;               // (a short last chunk: lanes past the row)
+    const uint32_t last = min(63u, (npad - c0) / kE8Cols - 1u);  // the chunk's last lane
+    const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
+    uint32_t F[kE8Cols];  // column words (the running sets go to run_set, then the closing sets)
+    {
+        uint32_t R[8][8];  // [row][8-column group]
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const uint4 q = have ? f4[fm4_piece(r0 + 4u * g + p, nseg, cl / kSeg + h)]
+                                         : make_uint4(~0u, ~0u, ~0u, ~0u);
+                    R[4 * g + p][4 * h + 0] = q.x;
+                    R[4 * g + p][4 * h + 1] = q.y;
+                    R[4 * g + p][4 * h + 2] = q.z;
+                    R[4 * g + p][4 * h + 3] = q.w;
+                }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t a[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) a[r] = R[r][j];
+            tr8(a);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) F[8 * j + k] = a[k];
+        }
+    }
+    // guess: the 16 columns before the lane from a wildcard
+    uint32_t in = ~0u;
+    if (cl > 0u && have) {
+        const uint2* __restrict__ f2 = reinterpret_cast<const uint2*>(fm);
+        const uint32_t sp = cl / kSeg - 1u;
+        uint32_t a[8], b[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint2 q = f2[fm4_piece(r0 + (uint32_t)r, nseg, sp) * 2u + 1u];  // columns 16..31
+            a[r] = q.x;
+            b[r] = q.y;
+        }
+        tr8(a);
+        tr8(b);
+        uint32_t S = a[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) S = step8(S, a[k]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) S = step8(S, b[k]);
+        in = S;
+    }
+    const uint32_t guess0 = (uint32_t)__shfl((int)in, 0, 64);  // the chunk's guessed entry
+    // forward, until every lane's entry is its left neighbour's exit
+    uint32_t ex;
+    for (;;) {
+        uint32_t S = in;
+#pragma unroll
+        for (int c = 0; c < (int)kE8Cols; ++c) {
+            S = step8(S, F[c]);
+            run_set[(uint32_t)c * 64u + lane] = S;
+            // (written as it goes: held back to the end, the 64 sets took 64 VGPRs more)
+            if (c & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t pe = (uint32_t)__shfl_up((int)S, 1, 64);
+        if (lane == 0) pe = in;
+        const bool fix = have && pe != in;
+        if (!__any(fix)) {
+            ex = S;
+            break;
+        }
+        if (fix) in = pe;
+    }
+    const uint32_t E = (uint32_t)__shfl((int)ex, (int)last, 64);  // the chunk's exit
+    // ahead: per row, the set before the first break right of the chunk
+    uint32_t A = 0u, open = ~0u, P = E;
+    for (uint32_t cb = c0 + (last + 1u) * kE8Cols; cb < npad && open; cb += 64u) {
+        const uint32_t col = cb + lane;
+        uint32_t w = ~0u;
+        if (col < npad) {
+            const uint32_t seg = col / kSeg, wd = (col % kSeg) / 8u, sh = 4u * (col % 8u);
+            w = 0u;
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                w |= ((fm[fm4_piece(r0 + (uint32_t)r, nseg, seg) * 4u + wd] >> sh) & 0xFu) << (4 * r);
+        }
+        uint32_t incl = w;  // prefix-AND over the lanes
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= (uint32_t)d) incl &= y;
+        }
+        const uint32_t Rs = P & incl;             // the running set, no break since the edge
+        const uint32_t z = zero_nib(Rs) & open;   // broken by this column
+        uint32_t zp = (uint32_t)__shfl_up((int)z, 1, 64);
+        uint32_t Rp = (uint32_t)__shfl_up((int)Rs, 1, 64);
+        if (lane == 0) {
+            zp = 0u;
+            Rp = P;
+        }
+        const uint32_t first = z & ~zp;
+        uint32_t got = Rp & nib_mask(first), res = first;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            got |= (uint32_t)__shfl_xor((int)got, o, 64);
+            res |= (uint32_t)__shfl_xor((int)res, o, 64);
+        }
+        A |= got;
+        open &= ~nib_mask(res);
+        P = (uint32_t)__shfl((int)Rs, 63, 64);
+    }
+    A |= P & open;  // no break up to the row's end: the set there
+    // backward: closing sets (the trailing run left 0), breaks counted
+    uint32_t c4 = 0u, ce = 0u, co = 0u;  // nibble counters; even / odd rows' byte counters
+    uint32_t W;                          // the run entering from the left: its closing set or 0
+    {
+        uint32_t Sn = run_set[(kE8Cols - 1u) * 64u + lane];
+        uint32_t X = 0u;
+        run_set[(kE8Cols - 1u) * 64u + lane] = 0u;
+#pragma unroll
+        for (int c = (int)kE8Cols - 2; c >= 0; --c) {
+            const uint32_t Sc = run_set[(uint32_t)c * 64u + lane];
+            const uint32_t z = zero_nib(Sc & Sn);  // a break at column c + 1
+            const uint32_t m = nib_mask(z);
+            X = (Sc & m) | (X & ~m);
+            run_set[(uint32_t)c * 64u + lane] = X;
+            if (c & 1) __builtin_amdgcn_sched_barrier(0);
+            c4 += z >> 3;
+            if (((int)kE8Cols - 2 - c) % 15 == 14) {
+                ce += c4 & 0x0F0F0F0Fu;
+                co += (c4 >> 4) & 0x0F0F0F0Fu;
+                c4 = 0u;
+            }
+            Sn = Sc;
+        }
+        const uint32_t z0 = zero_nib(in & Sn);  // a break at column 0 (Sn = S_0)
+        c4 += z0 >> 3;
+        ce += c4 & 0x0F0F0F0Fu;
+        co += (c4 >> 4) & 0x0F0F0F0Fu;
+        const uint32_t m0 = nib_mask(z0);
+        W = (in & m0) | (X & ~m0);
+    }
+    // tails: the first lane to the right with a closing set, per row
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = (uint32_t)__shfl_down((int)W, d, 64);
+        if (lane + (uint32_t)d >= 64u) y = A;
+        W |= nib_mask(zero_nib(W)) & y;
+    }
+    uint32_t tail = (uint32_t)__shfl_down((int)W, 1, 64);
+    if (lane == 63u) tail = A;
+    for (int c = (int)kE8Cols - 1; c >= 0; --c) {  // the trailing run: right to left, short
+        const uint32_t x = run_set[(uint32_t)c * 64u + lane];
+        const uint32_t z = zero_nib(x);
+        if (!__any(z != 0u)) break;
+        run_set[(uint32_t)c * 64u + lane] = x | (nib_mask(z) & tail);
+    }
+    // per-row breaks summed over the wave (16-bit halves: rows 0,4 / 2,6 / 1,5 / 3,7)
+    uint32_t s0 = ce & 0x00FF00FFu, s1 = (ce >> 8) & 0x00FF00FFu;
+    uint32_t s2 = co & 0x00FF00FFu, s3 = (co >> 8) & 0x00FF00FFu;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += (uint32_t)__shfl_xor((int)s0, o, 64);
+        s1 += (uint32_t)__shfl_xor((int)s1, o, 64);
+        s2 += (uint32_t)__shfl_xor((int)s2, o, 64);
+        s3 += (uint32_t)__shfl_xor((int)s3, o, 64);
+    }
+    if (have) {
+        const size_t wpr = npad >> (5u - LB);
+        constexpr int kWords = 2 << LB;  // table words per row and lane
+        uint32_t out[8][kWords];
+#pragma unroll
+        for (int q = 0; q < kWords; ++q) {
+            uint32_t a[8];
+            constexpr int per = 4 >> LB;  // columns per nibble
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                uint32_t v = 0u;
+#pragma unroll
+                for (int b = 0; b < per; ++b)
+                    v |= (low_bits8(run_set[(uint32_t)(q * 8 * per + j * per + b) * 64u + lane]) &
+                          (LB == 0 ? 0x11111111u : 0x33333333u))
+                         << ((1 << LB) * b);
+                a[j] = v;
+            }
+            tr8(a);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) out[r][q] = a[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            if (r0 + (uint32_t)r >= nrows) continue;
+            uint32_t* __restrict__ orow = dense + (size_t)out_row[r0 + r] * wpr;
+            if constexpr (LB == 2) {
+                uint4* o4 = reinterpret_cast<uint4*>(orow) + cl / 32u;
+                o4[0] = make_uint4(out[r][0], out[r][1], out[r][2], out[r][3]);
+                o4[1] = make_uint4(out[r][4], out[r][5], out[r][6], out[r][7]);
+            } else if constexpr (LB == 1) {
+                reinterpret_cast<uint4*>(orow)[cl / 64u] =
+                    make_uint4(out[r][0], out[r][1], out[r][2], out[r][3]);
+            } else {
+                reinterpret_cast<uint2*>(orow)[cl / 64u] = make_uint2(out[r][0], out[r][1]);
+            }
+        }
+    }
+    if (lane < 8u && r0 + lane < nrows) {
+        const uint32_t w = (lane & 1u) ? ((lane & 2u) ? s3 : s2) : ((lane & 2u) ? s1 : s0);
+        const size_t at = (size_t)(r0 + lane) * nch + ch;
+        ck.xe[at] = (guess0 >> (4u * lane)) & 0xFu;
+        ck.xs[at] = (E >> (4u * lane)) & 0xFu;
+        ck.cc[at] = (lane & 4u) ? w >> 16 : w & 0xFFFFu;
+    }
 }
 
 // The compact form on the wire and on disk: a move per column in `bits` =
@@ -4163,8 +4477,13 @@ void launch_rle_emit(const uint32_t* fm, uint32_t npad, uint32_t nrows, const ui
                      uint32_t* counts, hipStream_t s) {
     if (!nrows) return;
     const kern::EmitChunks ck{xe, xs, cc};
-    launch(kern::rle_emit4, dim3(rle_emit_chunks(npad), (nrows + 3u) / 4u), dim3(256), s, fm, npad,
-           nrows, out_row, lb, dense, ck);
+    const dim3 grid(rle_emit_chunks(npad) * ((nrows + 7u) / 8u));
+    if (lb == 2u)
+        launch(kern::rle_emit8<2>, grid, dim3(64), s, fm, npad, nrows, out_row, dense, ck, xcd_remap());
+    else if (lb == 1u)
+        launch(kern::rle_emit8<1>, grid, dim3(64), s, fm, npad, nrows, out_row, dense, ck, xcd_remap());
+    else
+        launch(kern::rle_emit8<0>, grid, dim3(64), s, fm, npad, nrows, out_row, dense, ck, xcd_remap());
     launch(kern::rle_emit_fix, dim3(nrows), dim3(64), s, fm, npad, nrows, out_row, lb, dense, ck,
            counts);
 }

@@ -341,3 +341,45 @@ def test_long_runs_chunk_seams(n):
     np.testing.assert_array_equal(off, ref_off)
     np.testing.assert_array_equal(runs, ref_runs)
     assert int(off[-1]) < 8 * len(targets)  # a handful of runs per row
+
+
+def test_narrow_pool_overflow_rebuilds_exact():
+    """Narrow rows keep the wide 256-target group rows (spread >= 0xFFFF) in a
+    pool of an eighth of a full batch's group rows (at least every group row
+    of one 1024-target slab).  A batch whose wide rows outgrow it is built
+    again in pieces the pool holds.  Weights scaled here so that about half of
+    a 4-slab batch's group rows are wide (the pool holds a quarter): the rows
+    stay bit-exact, the timing counters show the rebuild, and narrow rows are
+    kept (a partial batch never runs the probe that switches them off)."""
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import dijkstra
+    g0 = cpd.synth_road_graph(60, 60, seed=21)
+    plan0 = cpd.Plan(g0)
+    order = plan0.order()
+    n = g0.n
+    targets = np.random.default_rng(21).permutation(n).astype(np.uint32)  # k = n = 3600: 4 slabs
+    B = 8192
+    # lanes as the build orders them without coordinates: by column, the
+    # active slabs' tail padded with the first lane's target
+    lanes = targets[np.argsort(order[targets], kind="stable")]
+    lanes = np.concatenate([lanes, np.full(4096 - n, lanes[0], np.uint32)])
+    rows = np.repeat(np.arange(n), np.diff(g0.row_ptr))
+    rev = csr_matrix((g0.w.astype(np.float64), (g0.dst, rows)), shape=(n, n))
+    d = dijkstra(rev, indices=lanes)            # d[lane, node] = dist(node -> target)
+    d[np.isinf(d)] = np.nan
+    grp = d.reshape(16, 256, n)
+    spread = np.nanmax(grp, axis=1) - np.nanmin(grp, axis=1)  # [group, column]
+    scale = int(np.ceil(65535.0 / np.nanmedian(spread)))
+    assert 2 <= scale <= 5000, scale
+    g = cpd.RoadGraph(g0.row_ptr, g0.dst, (g0.w.astype(np.int64) * scale).astype(np.uint32),
+                      g0.x, g0.y)
+    plan = cpd.Plan(g)
+    dev = make_graph(plan, B, True)
+    dev.timing(True)
+    off, runs = dev.build_rows(targets).export()
+    kt = dev.timing_get()
+    ref_off, ref_runs = oracle.build_rows(g.row_ptr, g.dst, g.w, plan.order(), targets)
+    np.testing.assert_array_equal(off, ref_off)
+    np.testing.assert_array_equal(runs, ref_runs)
+    assert kt.get("pool_rebuilds", {}).get("launches", 0) >= 1, kt
+    assert "group_rows" in kt  # narrow rows still on
