@@ -991,6 +991,9 @@ def main():
     gpu = 0 if share else local
     if share and args.batch == 0:  # ranks sized from one card's free HBM would overcommit it
         args.batch = 4096
+    # the search workspaces' share of free HBM: ranks sharing one card split it
+    # (the library's default share per rank would overcommit it)
+    wf = 0.6 / world if share else 0.0
     traffic = None
     if rank == 0 and local == 0 and not args.no_pmc:
         traffic = pmc_traffic(args)
@@ -1157,6 +1160,7 @@ def main():
     # 1024 search waves: 820k, profiles/r04ar_bench_sq64k.json)
     search = None
     if args.sample is None and not args.no_search:
+        log(f"rank {rank}: cpd-search legs")
         srows = last_targets[:256]
         sr = dev.build_rows(srows)
         six = cpd.Index.streamed(dev, srows, sr.count()[1], mode="dense")
@@ -1169,8 +1173,8 @@ def main():
         sq = 65536  # as many searches as the 1024 search waves have lanes
         ss = rng.integers(0, g.n, sq).astype(np.uint32)
         st_ = srows[rng.integers(0, len(srows), sq)]
-        wst = six.search(ss[:256], st_[:256], fscale=0.1)[4]  # warm: tables built here
-        _, _, sfin, scnt, sst = six.search(ss, st_, fscale=0.1)
+        wst = six.search(ss[:256], st_[:256], fscale=0.1, workspace_frac=wf)[4]  # warm: tables built here
+        _, _, sfin, scnt, sst = six.search(ss, st_, fscale=0.1, workspace_frac=wf)
         tot = comm.reduce([float(sq), sst["kernel_ms"]], "SUM")
         (smax,) = comm.reduce([sst["kernel_ms"]], "MAX")
 
@@ -1197,7 +1201,7 @@ def main():
         # (profiles/search_lanes_ab/).  Ranks sharing one card in a rehearsal
         # split its HBM.
         # the fscale-0.1 queries with the memoised-walk form: the headline
-        _, _, wfin, wcnt, wsst = six.search(ss, st_, fscale=0.1, tables="walks")
+        _, _, wfin, wcnt, wsst = six.search(ss, st_, fscale=0.1, tables="walks", workspace_frac=wf)
         wtot = comm.reduce([float(sq)], "SUM")
         (wmax,) = comm.reduce([wsst["kernel_ms"]], "MAX")
         search = {"queries_per_s": round(wtot[0] / (wmax / 1e3), 1) if wmax else 0.0,
@@ -1211,8 +1215,8 @@ def main():
         zq = 65536
         zs = rng.integers(0, g.n, zq).astype(np.uint32)
         zt = srows[rng.integers(0, len(srows), zq)]
-        six.search(zs[:64], zt[:64])  # warm
-        _, _, zfin, zcnt, zst = six.search(zs, zt, workspace_frac=0.6 / world if share else 0.0)
+        six.search(zs[:64], zt[:64], workspace_frac=wf)  # warm
+        _, _, zfin, zcnt, zst = six.search(zs, zt, workspace_frac=wf)
         ztot = comm.reduce([float(zq), zst["kernel_ms"]], "SUM")
         (zmax,) = comm.reduce([zst["kernel_ms"]], "MAX")
         search["fscale0"] = {
@@ -1316,7 +1320,7 @@ def main():
             rc, rp, rf, rs = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, order, srows,
                                                sref[0], sref[1], ss2, st2, fscale=0.1,
                                                threads=threads)
-            gcs, gps, gfs, gcnt, _ = six.search(ss2, st2, fscale=0.1)
+            gcs, gps, gfs, gcnt, _ = six.search(ss2, st2, fscale=0.1, workspace_frac=wf)
             search["parity_2000_bit_exact"] = bool(
                 np.array_equal(gcs, rc) and np.array_equal(gps, rp) and np.array_equal(gfs, rf)
                 and np.array_equal(gcnt.astype(np.uint64), rs))
@@ -1325,7 +1329,7 @@ def main():
             rc, rp, rf, rs = oracle.cpd_search(g.row_ptr, g.dst, g.w, w_cong, order, srows,
                                                sref[0], sref[1], ss2[:64], st2[:64],
                                                threads=threads)
-            gcs, gps, gfs, gcnt, _ = six.search(ss2[:64], st2[:64])
+            gcs, gps, gfs, gcnt, _ = six.search(ss2[:64], st2[:64], workspace_frac=wf)
             search["fscale0"]["parity_64_bit_exact"] = bool(
                 np.array_equal(gcs, rc) and np.array_equal(gps, rp) and np.array_equal(gfs, rf)
                 and np.array_equal(gcnt.astype(np.uint64), rs))

@@ -1096,7 +1096,9 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
             // the highest priority: its small, latency-bound level kernels
             // must get CUs while the other streams' workgroups are queued (at
             // equal priority they waited for all of them to be dispatched:
-            // 15 ms for a 0.7-ms init kernel)
+            // 15 ms for a 0.7-ms init kernel; beside the first moves, as now,
+            // normal priority measured the same: 419.1k against 413.2-419.1k
+            // rows/s, profiles/up_store_ab/r06o_*)
             int least = 0, greatest = 0;
             HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             HIP_CHECK(hipStreamCreateWithPriority(&g->ustream, hipStreamNonBlocking, greatest));
@@ -1773,9 +1775,11 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         prepare_targets(g, next, next_k, ns);
         // after the other slot's last batch: its down-sweep (ev_down, not yet
         // re-recorded for this batch), so this up-sweep runs beside its first
-        // moves (after them, ev_fm[ns], it ran beside this down-sweep: the
-        // same rows/s within noise, 371.9-376.9k against 374.6-377.1k, and
-        // the down-sweep's launches 9% longer, profiles/up_store_ab/r06k_*)
+        // moves (after them, ev_fm[ns], it ran beside this down-sweep: with
+        // the one-row emit the same rows/s within noise, 371.9-376.9k against
+        // 374.6-377.1k, profiles/up_store_ab/r06k_*; with the eight-row emit
+        // 414.2-415.1k against 413.2-423.4k, the down-sweep's launches 12%
+        // longer, r06o_*)
         HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
         upload_targets(g, next, next_k, ns, g->ustream, true);
         launch_up(g, next_k, ns, g->ustream);

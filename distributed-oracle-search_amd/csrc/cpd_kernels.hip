@@ -1098,18 +1098,14 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
                                                       const uint32_t* __restrict__ leafbits,
                                                       const uint16_t* __restrict__ fmleaf,
                                                       NarrowRows nr,
-                                                      const uint32_t* __restrict__ seg_order) {
+                                                      const uint32_t* __restrict__ seg_order,
+                                                      uint32_t spw) {
     static_assert(kSeg % G == 0, "group size");
-    const uint32_t nseg = npad / kSeg;
+    const uint32_t nseg = npad / kSeg, ngrp = nseg / spw;
     const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t slab = L / nseg;
+    const uint32_t slab = L / ngrp;
     const uint32_t l4 = slab * blockDim.x + threadIdx.x;  // slab = blockDim.x x 4 targets
     const uint32_t B4 = B / 4u;
-    // segments in the order seg_order gives (spatially compact runs: the
-    // neighbour rows one XCD's blocks gather at once overlap in its L2), else
-    // in column order
-    const uint32_t sl = L - slab * nseg;
-    const uint32_t cb = (seg_order ? seg_order[sl] : sl) * kSeg;
     const uint32_t lane = threadIdx.x & 63u;
     const uint4 tc = reinterpret_cast<const uint4*>(tgt)[l4];
     const uint32_t grp = wave_group(l4);
@@ -1117,6 +1113,13 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
     // soon as its 8 columns are done, so only the current word of each row is
     // live in registers
     extern __shared__ uint32_t fm_stage[];
+    // spw segments one after another (a neighbour row shared by the end of one
+    // and the start of the next is read again while it is still in L2),
+    // in the order seg_order gives (spatially compact runs), else in column
+    // order
+    for (uint32_t it = 0; it < spw; ++it) {
+    const uint32_t sl = (L - slab * ngrp) * spw + it;
+    const uint32_t cb = (seg_order ? seg_order[sl] : sl) * kSeg;
     uint32_t pk[4][4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) pk[0][p] = pk[1][p] = pk[2][p] = pk[3][p] = 0xFFFFFFFFu;
@@ -1202,6 +1205,7 @@ __global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ 
     const uint4* st = reinterpret_cast<const uint4*>(fm_stage) + threadIdx.x * 4u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = st[i];
+    }
 }
 
 // One lane's greedy pass over its 32 columns (warthog graph_oracle::add_row
@@ -4393,6 +4397,19 @@ void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_o
                slot1, ubase, uidx, live, stat);
 }
 
+// segments per first_moves_n4 workgroup, one after another (CPD_FM_SPW: 1,
+// 2, 4, ..., 64; 8 measured 418.6-423.4k rows/s against 413.2-419.1k for one,
+// the kernel 26.2-26.6 against 26.8-27.3 ms beside the up-sweep,
+// profiles/up_store_ab/r06n_*, r06o_*)
+static uint32_t fm_spw() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("CPD_FM_SPW");
+        const uint32_t x = e && *e ? (uint32_t)std::atoi(e) : 8u;
+        return (x && x <= 64u && !(x & (x - 1u))) ? x : 1u;
+    }();
+    return v;
+}
+
 uint32_t fm_bits(uint32_t shift) { return shift <= 2 ? 4u : (1u << shift); }
 
 template <bool NARROW>
@@ -4419,8 +4436,9 @@ void launch_first_moves(const uint32_t* adj32, uint32_t shift, const uint32_t* d
     const dim3 grid((npad / kern::kSeg) * ((rows + 1023u) / 1024u) * (256u / tpb)), blk(tpb);
     const uint2* adj = reinterpret_cast<const uint2*>(adj32);
     if (nr.d16 && shift == 2 && fm_n4()) {
-        launch_shm(kern::first_moves_n4<2>, grid, blk, 64u * tpb, s, adj, dist, tgt, B, n, npad,
-                   xcd_remap(), fm, leafbits, fmleaf, nr, seg_order);
+        const uint32_t spw = fm_spw();
+        launch_shm(kern::first_moves_n4<2>, dim3(grid.x / spw), blk, 64u * tpb, s, adj, dist, tgt,
+                   B, n, npad, xcd_remap(), fm, leafbits, fmleaf, nr, seg_order, spw);
     } else if (nr.d16)
         launch_first_moves_t<true>(adj, shift, dist, tgt, B, n, npad, fm, leafbits, fmleaf, nr,
                                    grid, blk, s);
