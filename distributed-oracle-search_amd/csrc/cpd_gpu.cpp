@@ -1085,6 +1085,8 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         const uint32_t q = up_cus();
         int ncu = 0;
         HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
+        // (the up-sweep alone confined to q of 8 CUs, the other streams on all:
+        // 397.3-420.4k against 420.0-421.5k rows/s, profiles/up_store_ab/r06s_*)
         create_cu_stream(&g->stream, q, ncu, false);
         // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step
         // in round 5, 374.6-375.9k against 375.2-375.9k rows/s with the

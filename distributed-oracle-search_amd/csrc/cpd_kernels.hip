@@ -1379,11 +1379,10 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
 // is the lowest bit of the set at the row's end.  One 16-B store per lane per
 // tile: a wave writes 1 KiB contiguous.
 constexpr uint32_t kMoveTiles = 16;
-#ifndef CPD_EMIT_TILES
-#define CPD_EMIT_TILES 2
-#endif
-// tiles per chunk of the fused emit (its chunk lives in 4 * kEmitTiles VGPRs)
-constexpr uint32_t kEmitTiles = CPD_EMIT_TILES;
+// tiles per chunk of the fused emit: 4096 columns, one wave of rle_emit8 (64
+// lanes x 64 columns of eight rows); rle_emit_fix redoes a chunk with
+// emit_chunk4 (4 * kEmitTiles VGPRs of sets)
+constexpr uint32_t kEmitTiles = 2;
 
 // Move tables at 2^lb bits per column (lb = 0, 1, 2: 1, 2 or 4 bits, by the
 // graph's max out-degree — a move indexes its column's out-list, so every
@@ -1795,7 +1794,9 @@ __global__ __launch_bounds__(256) void rle_moves4(const uint32_t* __restrict__ f
 // rle_count_ch + rle_fix + rle_moves4 read every first-move set twice (the
 // count, then the emit) and write and re-read the per-segment entry states:
 // ~50 GB of HBM per 24576-row step for 12.3 GB of sets and 12.3 GB of
-// tables.  Here a wave owns a chunk of kEmitTiles tiles of one row and:
+// tables.  Here a wave owns a chunk of kEmitTiles tiles of one row (round 6:
+// the bulk of the emit is rle_emit8 below, eight rows per wave; this one-row
+// form, emit_chunk4, remains rle_emit_fix's redo of a chunk) and:
 //   forward  resolves every segment's entry set itself: lane L guesses its
 //            entry by scanning lane L-1's last 16 columns from a wildcard
 //            set, scans its 32 columns, and takes lane L-1's exit instead
@@ -1957,58 +1958,6 @@ __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uin
     return exitS;
 }
 
-// A one-wave workgroup per (row, chunk of kEmitTiles tiles).  The emit runs
-// beside the next batches' sweeps on its own stream; as four-wave workgroups
-// of 129-VGPR waves it waited for four SIMDs of a CU to free room at once
-// while the sweeps' smaller waves refilled every hole, and one launch
-// stretched over 70-90 ms (round 6 traces).  Logical blocks: row group
-// (4 rows sharing the 64-B sectors of the interleaved layout) outermost,
-// then chunk, then the group's 4 rows, XCD-remapped so that the 4 waves of
-// one (group, chunk) run together on one XCD and share its L2 lines.
-__global__ __launch_bounds__(64) void rle_emit4(const uint32_t* __restrict__ fm, uint32_t npad,
-                                                uint32_t nrows, const uint32_t* __restrict__ out_row,
-                                                uint32_t lb, uint32_t* __restrict__ dense,
-                                                EmitChunks ck, uint32_t remap) {
-    __shared__ uint8_t ent_all[64 * kEmitTiles];
-    const uint32_t nseg = npad / kSeg, ntiles = npad / kTile;
-    const uint32_t nch = (ntiles + kEmitTiles - 1u) / kEmitTiles;
-    const uint32_t L = remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t rg = L / (4u * nch), rest = L - rg * 4u * nch;
-    const uint32_t ch = rest >> 2;
-    const uint32_t brow = rg * 4u + (rest & 3u);
-    const uint32_t lane = threadIdx.x & 63u;
-    constexpr uint32_t wv = 0;
-    if (brow >= nrows) return;  // wave-uniform
-    const uint32_t t0 = ch * kEmitTiles;
-    if (t0 >= ntiles) return;
-    const uint32_t t1 = min(ntiles, t0 + kEmitTiles);
-    const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
-    // the chunk's entry: a wildcard at column 0, else the guess from the
-    // last 16 columns left of the chunk (one segment, scanned by every lane)
-    uint32_t Sin = 0xFu;
-    if (t0) {
-        const uint4 q = f4[fm4_piece(brow, nseg, t0 * 64u - 1u)];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t f = ((k < 8 ? q.z : q.w) >> (4 * (k & 7))) & 0xFu;
-            const uint32_t T = Sin & f;
-            Sin = T ? T : f;
-        }
-    }
-    uint32_t* __restrict__ orow = dense + (size_t)out_row[brow] * (npad >> (5u - lb));
-    uint32_t breaks = 0;
-    const uint32_t xs = emit_chunk4(f4, brow, nseg, ntiles, t0, t1, Sin, ent_all + wv * 64u * kEmitTiles,
-                                    orow, lb, lane, breaks);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) breaks += (uint32_t)__shfl_xor((int)breaks, o, 64);
-    if (lane == 0) {
-        const size_t at = (size_t)brow * nch + ch;
-        ck.xe[at] = Sin;
-        ck.xs[at] = xs;
-        ck.cc[at] = breaks;
-    }
-}
-
 // The chunks' seams, a wave per row: lane j holds chunk b + j's guessed entry,
 // exit and breaks; the first chunk whose guess differs from its left
 // neighbour's (true) exit is done again from that exit (emit_chunk4, the
@@ -2095,8 +2044,9 @@ __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ 
 //            the table's 1/2/4-bit fields and transposed back to rows: one
 //            8-, 16- or 32-B store per row and lane, a wave writing 0.5-2
 //            KiB contiguous per row.
-// It records per (row, chunk) what rle_emit4 recorded (guessed entry, exit,
-// breaks), so rle_emit_fix repairs a wrong chunk guess as before.
+// It records per (row, chunk) what round 5's one-row rle_emit4 recorded
+// (guessed entry, exit, breaks), so rle_emit_fix repairs a wrong chunk guess
+// with emit_chunk4, the one-row form, as before.
 __device__ __forceinline__ uint32_t zero_nib(uint32_t a) {  // bit 3 of nibble k: nibble k is 0
     return ~(((a & 0x77777777u) + 0x77777777u) | a) & 0x88888888u;
 }
