@@ -1781,7 +1781,8 @@ void build_batch(cpd_graph* g, const uint32_t* targets, uint32_t k, cpd_rows* r,
         // the one-row emit the same rows/s within noise, 371.9-376.9k against
         // 374.6-377.1k, profiles/up_store_ab/r06k_*; with the eight-row emit
         // 414.2-415.1k against 413.2-423.4k, the down-sweep's launches 12%
-        // longer, r06o_*)
+        // longer, r06o_*; with first_moves at 8 waves per SIMD 419.0-420.5k
+        // against 425.2-431.7k, r06z_*)
         HIP_CHECK(hipStreamWaitEvent(g->ustream, g->ev_down, 0));
         upload_targets(g, next, next_k, ns, g->ustream, true);
         launch_up(g, next_k, ns, g->ustream);

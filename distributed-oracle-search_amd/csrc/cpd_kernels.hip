@@ -1089,8 +1089,12 @@ struct FmGroup {  // edges are re-read from the lanes when needed (no SGPR press
 // are gathered G = 2 at a time, the next group issued before the current one
 // is finished (G = 1 measured 16.2 against 15.3 ms; two segments per
 // workgroup, CPD_FM_SEGS = 2, 101 VGPRs and slower: both removed in round 3).
+// Held to 64 VGPRs for 8 waves per SIMD (round 6: 65 VGPRs had given 7; the
+// cap spills 7 rarely-used values to scratch): 22.8-23.0 against 26.6-26.8
+// ms beside the up-sweep, 429.9-430.2k against 419.7-420.8k rows/s
+// (profiles/fm_packed_ab/r06w_*).
 template <int G>
-__global__ __launch_bounds__(512) void first_moves_n4(const uint2* __restrict__ adj,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8, 8))) void first_moves_n4(const uint2* __restrict__ adj,
                                                       const uint32_t* __restrict__ dist,
                                                       const uint32_t* __restrict__ tgt, uint32_t B,
                                                       uint32_t n, uint32_t npad, uint32_t remap,
