@@ -1383,10 +1383,19 @@ __global__ __launch_bounds__(256) void rle_scan(const uint32_t* __restrict__ fm,
 // is the lowest bit of the set at the row's end.  One 16-B store per lane per
 // tile: a wave writes 1 KiB contiguous.
 constexpr uint32_t kMoveTiles = 16;
-// tiles per chunk of the fused emit: 4096 columns, one wave of rle_emit8 (64
-// lanes x 64 columns of eight rows); rle_emit_fix redoes a chunk with
+// tiles per chunk of the fused emit: one wave of rle_emit8 (64 lanes x
+// kE8Cols columns of eight rows); rle_emit_fix redoes a chunk with
 // emit_chunk4 (4 * kEmitTiles VGPRs of sets)
-constexpr uint32_t kEmitTiles = 2;
+// columns per lane of rle_emit8 (32 or 64, build time): 32 measured
+// 431.5-433.3k against 428.3-431.7k rows/s for 64 (the emit 7.6 against 9.7
+// ms beside the down-sweep: 8 instead of 16 KiB of LDS per wave, 81 instead
+// of 113 VGPRs; profiles/emit8_cols_ab/)
+#ifndef CPD_E8_COLS
+#define CPD_E8_COLS 32
+#endif
+constexpr uint32_t kE8Cols = CPD_E8_COLS;
+static_assert(kE8Cols == 32 || kE8Cols == 64, "rle_emit8 lane width");
+constexpr uint32_t kEmitTiles = kE8Cols / 32u;
 
 // Move tables at 2^lb bits per column (lb = 0, 1, 2: 1, 2 or 4 bits, by the
 // graph's max out-degree — a move indexes its column's out-list, so every
@@ -2023,13 +2032,13 @@ __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ 
 // = row 8·oct + i; the 64-B sectors of the two row groups transposed in
 // registers, three byte/nibble swap stages per 8x8 block), and one step of
 // the scan — T = S & F, a zero-nibble test, S = T, or F where T is empty —
-// advances all eight rows in nine instructions.  Lane L owns the 64 columns
-// [c0 + 64 L, c0 + 64 L + 64) of a 4096-column chunk (kEmitTiles tiles: the
-// chunk of rle_emit_fix and emit_chunk4):
+// advances all eight rows in nine instructions.  Lane L owns the kE8Cols = 32
+// columns [c0 + 32 L, c0 + 32 L + 32) of a 2048-column chunk (kEmitTiles
+// tiles: the chunk of rle_emit_fix and emit_chunk4):
 //   guess    the running sets entering the lane: the 16 columns before it
 //            scanned from a wildcard (lane 0: the previous chunk's last 16,
 //            the chunk's guessed entry; a wildcard for chunk 0);
-//   forward  its 64 columns from that entry, each running set to LDS (16 KiB
+//   forward  its columns from that entry, each running set to LDS (8 KiB
 //            per wave); a lane whose entry differs from lane L-1's exit scans
 //            again from that exit (lane 0 keeps the chunk's entry) until no
 //            lane changes;
@@ -2046,7 +2055,7 @@ __global__ __launch_bounds__(64) void rle_emit_fix(const uint32_t* __restrict__ 
 //            lane with the ahead set (a suffix scan over the lanes);
 //   store    the lowest set bit per nibble, neighbouring columns merged to
 //            the table's 1/2/4-bit fields and transposed back to rows: one
-//            8-, 16- or 32-B store per row and lane, a wave writing 0.5-2
+//            4-, 8- or 16-B store per row and lane, a wave writing 256 B-1
 //            KiB contiguous per row.
 // It records per (row, chunk) what round 5's one-row rle_emit4 recorded
 // (guessed entry, exit, breaks), so rle_emit_fix repairs a wrong chunk guess
@@ -2091,7 +2100,6 @@ __device__ __forceinline__ uint32_t low_bits8(uint32_t X) {  // lowest set bit o
     return b0 + b1 + b2;
 }
 
-constexpr uint32_t kE8Cols = 64;  // columns per lane
 static_assert(kEmitTiles * kTile == 64u * kE8Cols, "a chunk is 64 lanes x kE8Cols columns");
 
 template <uint32_t LB>
@@ -2114,11 +2122,12 @@ __global__ __launch_bounds__(64) void rle_emit8(const uint32_t* __restrict__ fm,
     const uint4* __restrict__ f4 = reinterpret_cast<const uint4*>(fm);
     uint32_t F[kE8Cols];  // column words (the running sets go to run_set, then the closing sets)
     {
-        uint32_t R[8][8];  // [row][8-column group]
+        constexpr int NS = (int)kE8Cols / 32;  // segments per lane
+        uint32_t R[8][4 * NS];                 // [row][8-column group]
 #pragma unroll
         for (int g = 0; g < 2; ++g)
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < NS; ++h)
 #pragma unroll
                 for (int p = 0; p < 4; ++p) {
                     const uint4 q = have ? f4[fm4_piece(r0 + 4u * g + p, nseg, cl / kSeg + h)]
@@ -2129,7 +2138,7 @@ __global__ __launch_bounds__(64) void rle_emit8(const uint32_t* __restrict__ fm,
                     R[4 * g + p][4 * h + 3] = q.w;
                 }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < 4 * NS; ++j) {
             uint32_t a[8];
 #pragma unroll
             for (int r = 0; r < 8; ++r) a[r] = R[r][j];
@@ -2276,7 +2285,7 @@ __global__ __launch_bounds__(64) void rle_emit8(const uint32_t* __restrict__ fm,
     }
     if (have) {
         const size_t wpr = npad >> (5u - LB);
-        constexpr int kWords = 2 << LB;  // table words per row and lane
+        constexpr int kWords = (int)(kE8Cols / 32u) << LB;  // table words per row and lane
         uint32_t out[8][kWords];
 #pragma unroll
         for (int q = 0; q < kWords; ++q) {
@@ -2299,16 +2308,17 @@ __global__ __launch_bounds__(64) void rle_emit8(const uint32_t* __restrict__ fm,
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             if (r0 + (uint32_t)r >= nrows) continue;
-            uint32_t* __restrict__ orow = dense + (size_t)out_row[r0 + r] * wpr;
-            if constexpr (LB == 2) {
-                uint4* o4 = reinterpret_cast<uint4*>(orow) + cl / 32u;
-                o4[0] = make_uint4(out[r][0], out[r][1], out[r][2], out[r][3]);
-                o4[1] = make_uint4(out[r][4], out[r][5], out[r][6], out[r][7]);
-            } else if constexpr (LB == 1) {
-                reinterpret_cast<uint4*>(orow)[cl / 64u] =
-                    make_uint4(out[r][0], out[r][1], out[r][2], out[r][3]);
+            // the lane's kWords words at word (cl << LB) / 32 of the row
+            uint32_t* __restrict__ ow = dense + (size_t)out_row[r0 + r] * wpr + ((cl << LB) >> 5);
+            if constexpr (kWords >= 4) {
+#pragma unroll
+                for (int q = 0; q < kWords; q += 4)
+                    reinterpret_cast<uint4*>(ow)[q / 4] =
+                        make_uint4(out[r][q], out[r][q + 1], out[r][q + 2], out[r][q + 3]);
+            } else if constexpr (kWords == 2) {
+                reinterpret_cast<uint2*>(ow)[0] = make_uint2(out[r][0], out[r][1]);
             } else {
-                reinterpret_cast<uint2*>(orow)[cl / 64u] = make_uint2(out[r][0], out[r][1]);
+                ow[0] = out[r][0];
             }
         }
     }

@@ -9,7 +9,9 @@ from collections import defaultdict
 
 def main(d):
     files = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)
-    rows = list(csv.DictReader(open(files[0])))
+    # the bench process's trace (a plan-building child writes its own)
+    f = max(files, key=lambda x: open(x).read().count("first_moves"))
+    rows = list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     tot = defaultdict(lambda: [0, 0.0])
     for r in rows:
@@ -42,6 +44,22 @@ def main(d):
             if i < 25 or i % 10 == 0 or i == len(per) - 1 or us > 300:
                 print(f"  {i:4d} {us:9.1f} {per[i][0][1]:10d}  {cum:8.2f}")
         print(f"  batches seen: {nb}")
+    # the main stream between the down-sweep's levels: gaps from one level's
+    # end to the next one's start, per batch (launch latency + tail drain)
+    gaps, busy, prev = defaultdict(float), defaultdict(float), None
+    b = 0
+    for r in rows:
+        if "first_moves" in r["_n"]:
+            b += 1
+            prev = None
+        elif "sweep_down8" in r["_n"]:
+            s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if prev is not None:
+                gaps[b] += max(0, s0 - prev) / 1e6
+            busy[b] += (e0 - s0) / 1e6
+            prev = e0
+    for k in sorted(gaps):
+        print(f"batch {k}: down-sweep busy {busy[k]:.2f} ms, gaps between its levels {gaps[k]:.2f} ms")
 
 
 if __name__ == "__main__":
