@@ -4362,13 +4362,15 @@ void launch_live_stats(bool ascend, const uint32_t* nodes, const uint32_t* arc_o
 }
 
 // segments per first_moves_n4 workgroup, one after another (CPD_FM_SPW: 1,
-// 2, 4, ..., 64; 8 measured 418.6-423.4k rows/s against 413.2-419.1k for one,
-// the kernel 26.2-26.6 against 26.8-27.3 ms beside the up-sweep,
-// profiles/up_store_ab/r06n_*, r06o_*)
+// 2, 4, ..., 64).  At 7 waves per SIMD 8 measured 418.6-423.4k rows/s
+// against 413.2-419.1k for one (profiles/up_store_ab/r06n_*, r06o_*); at 8
+// waves per SIMD, whose workgroups hold every slot the up-sweep beside them
+// needs, shorter workgroups hand slots over sooner: 2 measured 440.5-441.2k
+// against 435.3-435.4k for 8 and 435.7-436.0k for 1 (r06ee_*)
 static uint32_t fm_spw() {
     static const uint32_t v = [] {
         const char* e = std::getenv("CPD_FM_SPW");
-        const uint32_t x = e && *e ? (uint32_t)std::atoi(e) : 8u;
+        const uint32_t x = e && *e ? (uint32_t)std::atoi(e) : 2u;
         return (x && x <= 64u && !(x & (x - 1u))) ? x : 1u;
     }();
     return v;
