@@ -179,33 +179,6 @@ bool rle_fused_on() {
     return on;
 }
 bool rle_fused(uint32_t fmb) { return fmb == 4 && rle_fused_on(); }
-bool up_persist_on();
-// chunked up levels of at most this many chunk items run together in one
-// persistent launch (larger ones fill the GPU as launches of their own)
-constexpr uint32_t kPersistItems = 256;
-
-// CPD_UP_CUS = q (0..4): q of every 8 CUs kept for the up-sweep stream, the
-// rest for the main and emit streams (0: no masks).  Bit i of a mask is CU
-// i; the reserved set is spread over every XCD whichever way the bit order
-// maps to XCDs (CU i reserved when (i - i / 32) mod 8 < q).
-uint32_t up_cus() {
-    static const uint32_t v = [] {
-        const char* e = std::getenv("CPD_UP_CUS");
-        const unsigned long q = e && *e ? std::strtoul(e, nullptr, 10) : 0ul;
-        return (uint32_t)std::min(q, 4ul);
-    }();
-    return v;
-}
-void create_cu_stream(hipStream_t* st, uint32_t q, int ncu, bool reserved) {
-    if (!q || ncu <= 0) {
-        HIP_CHECK(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
-        return;
-    }
-    std::vector<uint32_t> mask(((size_t)ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu; ++i)
-        if (((uint32_t)((i - i / 32) & 7) < q) == reserved) mask[(size_t)i / 32] |= 1u << (i % 32);
-    HIP_CHECK(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
-}
 
 // Pool rows (1 KiB: one 256-target group row kept 32-bit) of a narrow batch
 // of B targets: an eighth of its group rows, and at least every group row of
@@ -410,9 +383,6 @@ struct cpd_graph {
     // up_init_slots = the ascending slots of all their nodes (leaf-form init)
     std::vector<uint32_t> up_item_first;
     DevBuf<uint32_t> up_items, up_init_slots;
-    // the same offsets on the device, and per batch slot the persistent
-    // narrow-level launch's barrier counters (one per slab)
-    DevBuf<uint32_t> up_item_first_d, ubar[2];
     uint32_t n_init_slots = 0;
     // lane position of each caller target in the current batch (sorted by
     // lane_key when the caller gave coordinates, else by column)
@@ -1075,26 +1045,19 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
         auto g = std::make_unique<cpd_graph>();
         g->device = device;
         g->select();
-        // The up-sweep stream: the next batch's up-sweep runs beside this
-        // batch's down-sweep and first moves.  Its ~150 narrow levels are a
-        // chain of small latency-bound launches: beside the other streams'
-        // large launches each waits for CUs (at the highest priority they
-        // still spanned ~46 ms per step, profiles/up_store_ab/).  With
-        // CPD_UP_CUS = q (1..4), q of every 8 CUs are the up-sweep's own and
-        // the main and emit streams run on the rest (hipExtStreamCreateWithCUMask).
-        const uint32_t q = up_cus();
-        int ncu = 0;
-        HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device));
-        // (the up-sweep alone confined to q of 8 CUs, the other streams on all:
-        // 397.3-420.4k against 420.0-421.5k rows/s, profiles/up_store_ab/r06s_*)
-        create_cu_stream(&g->stream, q, ncu, false);
+        // Three streams: the main one (down-sweep, first moves), the emit
+        // stream and the up-sweep stream, where the next batch's up-sweep runs
+        // beside the previous batch's first moves.  CU masks were measured and
+        // removed: the up-sweep given q of every 8 CUs and the other streams
+        // the rest (rounds 4-6: 350.6k / 324.2k against 366.7k rows/s; r06d:
+        // 355.9k / 310.6k against 380.1k), or the up-sweep alone confined to
+        // q of 8 (397.3-420.4k against 420.0-421.5k, profiles/up_store_ab/r06s_*).
+        HIP_CHECK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
         // (a lowest-priority emit stream measured the same: 65.2-65.7 ms/step
         // in round 5, 374.6-375.9k against 375.2-375.9k rows/s with the
         // one-wave emit, profiles/up_store_ab/r06k_*)
-        create_cu_stream(&g->estream, q, ncu, false);
-        if (q) {
-            create_cu_stream(&g->ustream, q, ncu, true);
-        } else {
+        HIP_CHECK(hipStreamCreateWithFlags(&g->estream, hipStreamNonBlocking));
+        {
             // the highest priority: its small, latency-bound level kernels
             // must get CUs while the other streams' workgroups are queued (at
             // equal priority they waited for all of them to be dispatched:
@@ -1292,8 +1255,6 @@ int cpd_graph_create(const cpd_plan* p, int device, cpd_graph** out) {
                 }
             }
             g->up_item_first.back() = (uint32_t)(items.size() / 4);
-            g->up_item_first_d.upload(g->up_item_first.data(), g->up_item_first.size(), s);
-            for (auto& b : g->ubar) b.alloc(32u * 4u);  // (slab, quarter) barrier counters
             g->up_items.upload(items.data(), items.size(), s);
             g->up_init_slots.upload(slots.data(), slots.size(), s);
             g->n_init_slots = (uint32_t)slots.size();
@@ -1502,21 +1463,6 @@ void launch_up(cpd_graph* g, uint32_t k, uint32_t slot, hipStream_t st) {
         uint32_t s0 = g->asc_lvl[l], cnt = g->asc_lvl[l + 1] - s0;
         if (!cnt) continue;
         const uint32_t i0 = g->up_item_first[l], ni = items_of(l);
-        if (live && ni && ni <= kPersistItems && up_persist_on()) {
-            // a run of chunked levels with few items each: one launch
-            size_t l2 = l;
-            double dense = 0.0;
-            while (l2 + 1 < nasc && items_of(l2) && items_of(l2) <= kPersistItems)
-                dense += level_bytes(l2++);
-            g->timed("sweep_up", dense, [&] {
-                launch_sweep_up_narrow(g->up_items.p, g->up_item_first_d.p, (uint32_t)l,
-                                       (uint32_t)l2, g->asc_arcs.p, up, g->ubase, S.tgt.p, B,
-                                       slabs, g->asc_nodes.p, g->asc_off.p, g->asc_arcs.p, live,
-                                       tmask, g->ubar[slot].p, st);
-            });
-            l = l2 - 1;
-            continue;
-        }
         const double dense = level_bytes(l);
         g->timed("sweep_up", dense, [&] {
             if (live && ni)
@@ -1713,17 +1659,6 @@ void upload_targets(cpd_graph* g, const uint32_t* targets, uint32_t k, uint32_t 
                              hipMemcpyHostToDevice, st));
 }
 
-
-// CPD_UP_PERSIST=1 (A/B): runs of chunked up levels of at most
-// kPersistItems items in one persistent launch (sweep_up_narrow) instead of
-// a launch each (identical rows).
-bool up_persist_on() {
-    static const bool on = [] {
-        const char* e = std::getenv("CPD_UP_PERSIST");
-        return e && *e == '1';
-    }();
-    return on;
-}
 
 // CPD_OVERLAP=0: no early up-sweep of the next batch (A/B; identical rows).
 bool overlap_on() {

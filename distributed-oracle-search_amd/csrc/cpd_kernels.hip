@@ -756,85 +756,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     if (acc.w != INF) atomicMin(row + 3, acc.w);
 }
 
-// The up-sweep's top: a run of narrow levels in ONE launch (round 6).  As
-// separate launches (sweep_up_chunks) each of these ~140 levels costs a
-// launch and a dispatch: 65 us alone, and 200-450 us beside the other
-// streams' large launches, where the chain of them became the step's
-// critical path.  Slabs are independent (a target's up row reads only
-// lower rows of the same target), so G resident one-wave workgroups per
-// quarter slab walk the levels together: each takes every G-th chunk item
-// of the level, then the quarter's G waves meet at a barrier (an atomic
-// counter per quarter slab, zeroed by the caller) before the next level.  Everything a
-// later level reads was written by atomics (rows: atomicMin, masks:
-// atomicOr) before the barrier's release; the acquire after it invalidates
-// the CU's L1, and the masks (live words of several nodes share a line) are
-// read with coherent loads.  A wave sets only its own slab's live bit (each
-// quarter computes the same bits from the same inputs).  The grid is slabs
-// x 4 x G one-wave workgroups, small enough to be resident at once beside
-// other kernels (each waits only for the others' waves to retire); every
-// workgroup runs every level, so all reach each barrier and the end.
-__device__ __forceinline__ uint32_t coherent_u32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint32_t arc_bit(uint32_t ex, const uint32_t* __restrict__ live,
-                                            const uint32_t* __restrict__ tmask, const Closed& cf,
-                                            uint32_t slab) {
-    if (ex & (kLeafBit | kL1Bit)) return (arc_mask(ex, live, tmask, cf) >> slab) & 1u;
-    return (coherent_u32(live + ex) >> slab) & 1u;
-}
-
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sweep_up_narrow(
-    const uint4* __restrict__ items, const uint32_t* __restrict__ item_first, uint32_t l0,
-    uint32_t l1, uint32_t G, const uint2* __restrict__ arcs, uint32_t* __restrict__ up,
-    uint32_t ubase, const uint4* __restrict__ tgt4, uint32_t B4, Closed cf,
-    uint32_t* __restrict__ live, const uint32_t* __restrict__ tmask, uint32_t* __restrict__ bar) {
-    const uint32_t sq = blockIdx.x / G, g = blockIdx.x - sq * G;  // (slab, quarter), member
-    const uint32_t slab = sq / kUpQ;
-    const uint32_t l4 = sq * 64u + threadIdx.x;
-    const uint4 t = tgt4[l4];
-    const uint4* __restrict__ d4 = reinterpret_cast<const uint4*>(up);
-    for (uint32_t l = l0; l < l1; ++l) {
-        const uint32_t i1 = item_first[l + 1];
-        for (uint32_t i = item_first[l] + g; i < i1; i += G) {
-            const uint4 it = items[i];  // (slot, first arc, end arc, -)
-            const uint32_t v = it.x - ubase;
-            uint2 e[kChunk];
-            uint32_t mk = 0;
-#pragma unroll
-            for (int j = 0; j < kChunk; ++j)
-                e[j] = it.y + j < it.z ? arcs[it.y + j] : make_uint2(0u, 0u);
-#pragma unroll
-            for (int j = 0; j < kChunk; ++j)
-                if (it.y + j < it.z) mk |= arc_bit(e[j].x, live, tmask, cf, slab) << j;
-            if (!mk) continue;  // no live input in this slab
-            if (threadIdx.x == 0) atomicOr(&live[v], 1u << slab);
-            uint4 x[kChunk];
-#pragma unroll
-            for (int j = 0; j < kChunk; ++j) x[j] = arc_val(d4, t, e[j], B4, l4, cf, (mk >> j) & 1u);
-            uint4 acc = make_uint4(INF, INF, INF, INF);
-#pragma unroll
-            for (int j = 0; j < kChunk; ++j) min4(acc, x[j], e[j].y);
-            uint32_t* row = up + ((size_t)v * B4 + l4) * 4u;
-            if (acc.x != INF) atomicMin(row + 0, acc.x);
-            if (acc.y != INF) atomicMin(row + 1, acc.y);
-            if (acc.z != INF) atomicMin(row + 2, acc.z);
-            if (acc.w != INF) atomicMin(row + 3, acc.w);
-        }
-        if (l + 1 == l1) break;  // the launch's end orders the rest
-        // release: the wave's atomics complete at agent scope before its
-        // arrival (the explicit wait: the compiler may drop the fence's own,
-        // MI355X_MICROARCH.md "Compiler hazard")
-        __threadfence();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (threadIdx.x == 0) {
-            atomicAdd(&bar[sq], 1u);
-            const uint32_t want = (l - l0 + 1u) * G;
-            while (coherent_u32(bar + sq) < want) __builtin_amdgcn_s_sleep(1);
-        }
-        __threadfence();  // acquire: the CU's L1 invalidated before the next level's loads
-    }
-}
 
 // tmask[col] |= 1 << slab for every target lane (4 per thread) of the batch;
 // the caller zeroes tmask first.
@@ -4321,23 +4242,6 @@ void launch_sweep_up_chunks(const uint32_t* items, uint32_t nitems, const uint32
            B / 4u, cf, live, tmask, active);
 }
 
-void launch_sweep_up_narrow(const uint32_t* items, const uint32_t* item_first, uint32_t l0,
-                            uint32_t l1, const uint32_t* arcs32, uint32_t* up, uint32_t ubase,
-                            const uint32_t* tgt, uint32_t B, uint32_t slabs,
-                            const uint32_t* asc_nodes, const uint32_t* asc_off,
-                            const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
-                            uint32_t* bar, hipStream_t s) {
-    if (l1 <= l0 || !slabs) return;
-    // one-wave workgroups per quarter slab: ~1024 waves in all (an eighth
-    // of the chip's wave slots), 4 to 16 per quarter
-    const uint32_t G = std::min(16u, std::max(4u, 256u / slabs));
-    const kern::Closed cf{asc_nodes, asc_off, reinterpret_cast<const uint2*>(asc_arcs)};
-    (void)hipMemsetAsync(bar, 0, slabs * kern::kUpQ * sizeof(uint32_t), s);
-    launch(kern::sweep_up_narrow, dim3(slabs * kern::kUpQ * G), dim3(64), s,
-           reinterpret_cast<const uint4*>(items), item_first, l0, l1, G,
-           reinterpret_cast<const uint2*>(arcs32), up, ubase, reinterpret_cast<const uint4*>(tgt),
-           B / 4u, cf, live, tmask, bar);
-}
 
 uint32_t sweep_chunk_arcs() { return (uint32_t)kern::kChunk; }
 uint32_t down_desc_arcs() { return kern::kDescArcs; }

@@ -84,15 +84,6 @@ void launch_sweep_up_chunks(const uint32_t* items /* uint4 each */, uint32_t nit
                             const uint32_t* asc_nodes, const uint32_t* asc_off,
                             const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
                             hipStream_t s);
-// A run of chunked levels [l0, l1) in one launch (cpd_kernels.hip
-// sweep_up_narrow): items as above, level l's at [item_first[l],
-// item_first[l + 1]); bar: slabs u32 of barrier counters (zeroed here, on s).
-void launch_sweep_up_narrow(const uint32_t* items, const uint32_t* item_first, uint32_t l0,
-                            uint32_t l1, const uint32_t* arcs, uint32_t* up, uint32_t ubase,
-                            const uint32_t* tgt, uint32_t B, uint32_t slabs,
-                            const uint32_t* asc_nodes, const uint32_t* asc_off,
-                            const uint32_t* asc_arcs, uint32_t* live, const uint32_t* tmask,
-                            uint32_t* bar, hipStream_t s);
 uint32_t sweep_chunk_arcs();
 
 // tmask[tgt[i]] |= 1 << (i / 1024) for i < B; tmask must be zeroed first.

@@ -13,19 +13,18 @@ oracle, walk queries over them dense and RLE.  What each reaches:
   CPD_XCD=0       identity block mapping
   CPD_ASYNC=0     the emit in line (one buffer set)
   CPD_RLE_FUSED=0 the count (rle_count_ch + rle_fix), then rle_moves4, instead
-                  of the one-pass rle_emit4 + rle_emit_fix
+                  of the one-pass rle_emit8 + rle_emit_fix
   CPD_LEAFFM=0    leaf first-move sets recomputed by first_moves
   CPD_OVERLAP=0   each batch's up-sweep on the main stream, after the previous
                   batch's first moves (no second up store in use)
   CPD_FM_ORDER=0  first_moves' segments in column order (not Hilbert order)
-  CPD_UP_PERSIST=0 every chunked up level its own sweep_up_chunks launch
-                  (not the runs of small levels in one sweep_up_narrow launch)
 Round 6 removed the switches whose variants lost their A/Bs (VERDICT r05
 item 7): CPD_FM_N4, CPD_RLE_CH, CPD_MOVES_SWAR, CPD_TABLE_BITS, CPD_TS_SHARE,
 CPD_EMIT_DEFER, CPD_UP_HEAD, CPD_EMIT_WIDE, CPD_ROWS_NIBBLE (and the schedule
 knobs CPD_CU_RESERVE(_MAIN), CPD_FM_LDS, CPD_EMIT_LDS, CPD_UP_PRIO,
 CPD_SEARCH_RESIDENT, CPD_SEARCH_GROW, CPD_SEARCH_LANE_MAJOR, CPD_EXP_CPW,
-CPD_TS_CHUNK_MAX, CPD_UP_INIT_BLOCKS).
+CPD_TS_CHUNK_MAX, CPD_UP_INIT_BLOCKS, CPD_UP_PERSIST with its persistent
+sweep_up_narrow, CPD_UP_CUS with the CU-masked streams).
 """
 import json
 import os
@@ -75,7 +74,7 @@ print(json.dumps(out))
 """
 
 SWITCHES = ["CPD_LIVE", "CPD_SORT", "CPD_LANE_KEY", "CPD_XCD", "CPD_ASYNC", "CPD_RLE_FUSED",
-            "CPD_LEAFFM", "CPD_OVERLAP", "CPD_FM_ORDER", "CPD_UP_PERSIST"]
+            "CPD_LEAFFM", "CPD_OVERLAP", "CPD_FM_ORDER"]
 OFF = {}   # switches whose "off" value is not 0
 WITH = {}  # switches whose path needs another one set
 
