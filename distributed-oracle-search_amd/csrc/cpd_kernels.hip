@@ -1777,9 +1777,10 @@ __device__ __forceinline__ uint32_t scan32_breaks(const uint32_t (&v)[4], uint32
 // lane of the wave calls it with the same arguments).  ent: 64 * kEmitTiles
 // bytes of LDS for this wave.  Writes the chunk's move table; returns the
 // exit set (wave-uniform) and adds the chunk's breaks to `breaks` (per lane).
-// The chunk's sets stay in registers (64 VGPRs a lane), loaded all at once
-// up front: the wave has its whole 16 KiB in flight instead of one tile per
-// dependent scan, and the backward pass reads nothing again.
+// The chunk's sets stay in registers (4 * kEmitTiles VGPRs a lane), loaded
+// all at once up front (round 5, at 16-tile chunks: the wave's whole 16 KiB
+// in flight instead of one tile per dependent scan), and the backward pass
+// reads nothing again.
 __device__ uint32_t emit_chunk4(const uint4* __restrict__ f4, uint32_t brow, uint32_t nseg,
                                 uint32_t ntiles, uint32_t t0, uint32_t t1, uint32_t Sin,
                                 uint8_t* ent, uint32_t* __restrict__ orow, uint32_t lb,
