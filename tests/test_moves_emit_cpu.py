@@ -1,5 +1,7 @@
-"""The move-table emit's algorithm (csrc/cpd_kernels.hip rle_moves4 — packed
-nibbles — and rle_moves<FMB> — per column), restated step for step in Python
+"""The move-table emit's algorithms (csrc/cpd_kernels.hip rle_moves4 — packed
+nibbles —, rle_moves<FMB> — per column —, the one-row chunk emit that the
+seam repair runs and, since round 6, rle_emit8 — eight rows per lane word),
+restated step for step in Python
 (wave = 64 lanes x 32 columns, tiles walked right to left, look-ahead carry)
 and checked on CPU against the greedy RLE rule expanded per column, on random
 first-move rows with short runs, long runs and a single run.  The GPU suite
@@ -405,3 +407,194 @@ def test_fused_emit_matches_greedy():
         assert out == mv and count == len(runs)
         redone += r
     assert redone > 0  # the seam check redid at least one chunk
+
+
+# The eight-row emit (cpd_kernels.hip rle_emit8, round 6), restated lane by
+# lane: a lane holds one column of eight rows per word (nibble r = row r),
+# the 8x8 nibble transposes that build those words from the row-group
+# sectors, the SWAR greedy step, the lane guesses and fixed point, the
+# look-ahead, the backward closing sets with the trailing run left empty,
+# the suffix scan that closes it, and the per-(row, chunk) records that
+# the seam check (emit_chunk4, restated above as _emit_chunk) repairs.
+def _perm(s0, s1, sel):  # v_perm_b32: bytes 0-3 of s1, 4-7 of s0
+    src = (s0 << 32) | s1
+    return sum(((src >> (8 * ((sel >> (8 * i)) & 0xFF))) & 0xFF) << (8 * i) for i in range(4))
+
+
+def tr8(a):
+    a = list(a)
+    for r in range(4):
+        x, y = a[r], a[r + 4]
+        a[r], a[r + 4] = _perm(y, x, 0x05040100), _perm(y, x, 0x07060302)
+    for r in (0, 1, 4, 5):
+        x, y = a[r], a[r + 2]
+        a[r], a[r + 2] = _perm(y, x, 0x06020400), _perm(y, x, 0x07030501)
+    for r in (0, 2, 4, 6):
+        x, y = a[r], a[r + 1]
+        a[r] = (x & 0x0F0F0F0F) | ((y << 4) & 0xF0F0F0F0)
+        a[r + 1] = ((x >> 4) & 0x0F0F0F0F) | (y & 0xF0F0F0F0)
+    return a
+
+
+def zero_nib(a):
+    return ~((((a & 0x77777777) + 0x77777777) & M32) | a) & 0x88888888
+
+
+def nib_mask(z):
+    return (z | ((z - (z >> 3)) & M32)) & M32
+
+
+def step8(S, F):
+    T = S & F
+    return T | (F & nib_mask(zero_nib(T)))
+
+
+def low_bits8(X):
+    b0 = ~X & 0x11111111
+    b1 = ~(X >> 1) & b0
+    b2 = ~(X >> 2) & b1
+    return (b0 + b1 + b2) & M32
+
+
+def test_tr8_transposes():
+    rnd = random.Random(9)
+    for _ in range(200):
+        m = [[rnd.randrange(16) for _ in range(8)] for _ in range(8)]
+        a = [sum(m[r][k] << (4 * k) for k in range(8)) for r in range(8)]
+        b = tr8(a)
+        assert all((b[k] >> (4 * r)) & 0xF == m[r][k] for r in range(8) for k in range(8))
+
+
+def emit8(rows, W=32):
+    """Eight rows' moves and chunk records as rle_emit8 computes them (chunks
+    of 64 lanes x W columns), then rle_emit_fix's seam check per row."""
+    npad = len(rows[0])
+    CH = 64 * W
+    # the column words, built from the rows' 8-column nibble words by tr8
+    F = [0] * npad
+    for g in range(npad // 8):
+        a = [sum(rows[r][g * 8 + k] << (4 * k) for k in range(8)) for r in range(8)]
+        for k, wd in enumerate(tr8(a)):
+            F[g * 8 + k] = wd
+    out = [[0] * npad for _ in range(8)]
+    recs = [[] for _ in range(8)]  # per row: [guessed entry, exit, breaks] per chunk
+    for c0 in range(0, npad, CH):
+        last = min(63, (npad - c0) // W - 1)
+        ins = []
+        for L in range(64):
+            cl = c0 + L * W
+            S = 0xFFFFFFFF
+            if 0 < cl < npad:  # the 16 columns before the lane, from a wildcard
+                S = F[cl - 16]
+                for c in range(cl - 15, cl):
+                    S = step8(S, F[c])
+            ins.append(S)
+        guess0 = ins[0]
+        while True:  # forward, until every entry is the left neighbour's exit
+            runs = []
+            for L in range(64):
+                S, col = ins[L], []
+                for c in range(W):
+                    cc = c0 + L * W + c
+                    S = step8(S, F[cc] if cc < npad else 0xFFFFFFFF)
+                    col.append(S)
+                runs.append(col)
+            pe = [ins[0]] + [runs[L - 1][-1] for L in range(1, 64)]
+            fix = [c0 + L * W < npad and pe[L] != ins[L] for L in range(64)]
+            if not any(fix):
+                break
+            ins = [pe[L] if fix[L] else ins[L] for L in range(64)]
+        E = runs[last][-1]
+        A, opn, P = 0, M32, E  # ahead
+        cb = c0 + (last + 1) * W
+        while cb < npad and opn:
+            w = [F[cb + l] if cb + l < npad else 0xFFFFFFFF for l in range(64)]
+            incl, acc = [], M32
+            for l in range(64):
+                acc &= w[l]
+                incl.append(acc)
+            Rs = [P & incl[l] for l in range(64)]
+            z = [zero_nib(Rs[l]) & opn for l in range(64)]
+            got = res = 0
+            for l in range(64):
+                zp, Rp = (0, P) if l == 0 else (z[l - 1], Rs[l - 1])
+                first = z[l] & ~zp & M32
+                got |= Rp & nib_mask(first)
+                res |= first
+            A |= got
+            opn &= ~nib_mask(res) & M32
+            P = Rs[63]
+            cb += 64
+        A |= P & opn
+        X, Wl, cnt = [], [], [[0] * 8 for _ in range(64)]
+        for L in range(64):  # backward: closing sets, the trailing run left 0
+            col, Sn, x = [0] * W, runs[L][W - 1], 0
+            for c in range(W - 2, -1, -1):
+                Sc = runs[L][c]
+                z = zero_nib(Sc & Sn)
+                m = nib_mask(z)
+                x = (Sc & m) | (x & ~m & M32)
+                col[c] = x
+                for r in range(8):
+                    cnt[L][r] += (z >> (4 * r + 3)) & 1
+                Sn = Sc
+            z0 = zero_nib(ins[L] & Sn)
+            for r in range(8):
+                cnt[L][r] += (z0 >> (4 * r + 3)) & 1
+            m0 = nib_mask(z0)
+            Wl.append((ins[L] & m0) | (col[0] & ~m0 & M32))
+            X.append(col)
+        for d in (1, 2, 4, 8, 16, 32):  # tails: the first closing set to the right
+            y = [Wl[L + d] if L + d < 64 else A for L in range(64)]
+            Wl = [Wl[L] | (nib_mask(zero_nib(Wl[L])) & y[L]) for L in range(64)]
+        tail = [Wl[L + 1] if L < 63 else A for L in range(64)]
+        for c in range(W - 1, -1, -1):  # the trailing runs, right to left
+            z = [zero_nib(X[L][c]) for L in range(64)]
+            if not any(z):
+                break
+            for L in range(64):
+                X[L][c] |= nib_mask(z[L]) & tail[L]
+        for L in range(64):
+            for c in range(W):
+                cc = c0 + L * W + c
+                if cc < npad:
+                    mv = low_bits8(X[L][c])
+                    for r in range(8):
+                        out[r][cc] = (mv >> (4 * r)) & 0xF
+        for r in range(8):
+            recs[r].append([(guess0 >> (4 * r)) & 0xF, (E >> (4 * r)) & 0xF,
+                            sum(cnt[L][r] for L in range(64))])
+    counts, redone, KT = [], 0, W // 32
+    for r in range(8):  # the seam check, a row at a time (one-row redo)
+        vseg, ntiles = _segments(rows[r]), npad // 2048
+        carry, total = 0xF, 0
+        for c, ck in enumerate(recs[r]):
+            if ck[0] != carry:
+                t0 = c * KT
+                ex, br = _emit_chunk(vseg, ntiles, t0, min(ntiles, t0 + KT), carry, out[r])
+                recs[r][c] = [carry, ex, br]
+                redone += 1
+            total += recs[r][c][2]
+            carry = recs[r][c][1]
+        counts.append(total + 1)
+    return out, counts, redone
+
+
+def test_eight_row_emit_matches_greedy():
+    """Tables and run counts of the eight-row emit equal the greedy rule's for
+    every row, at both lane widths, over short runs, long runs, a row that is
+    one run and rows whose chunk guesses fail (seam repairs)."""
+    rnd = random.Random(11)
+    redone = 0
+    for W, npad in ((32, 4096), (64, 4096), (32, 6144)):
+        gen = list(_rows(4, [0, 1, 3, 0, 1, 2, 3, 0], [npad], rnd.randrange(1000)))
+        rows = [fm[:npad] + [0xF] * (npad - len(fm)) for fm in gen]
+        rows[2] = [1] + [0xF] * (npad - 1)  # one run whose set the first column fixes
+        rows[5] = [2, 3] + [0xF] * (npad // 2 - 2) + [4] + [0xF] * (npad // 2 - 1)
+        out, counts, r = emit8(rows, W)
+        redone += r
+        for i in range(8):
+            mv, runs = greedy_moves(rows[i])
+            assert out[i] == mv, (W, npad, i)
+            assert counts[i] == len(runs), (W, npad, i)
+    assert redone > 0  # crafted long runs force seam repairs
